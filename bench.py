@@ -1,0 +1,116 @@
+"""Headline benchmark: ResNet-50 training images/sec, batch 400 per GPU, whole job.
+
+Contract (driver): ``python bench.py --gpus N --steps K --warmup W``; for N>1 it is
+launched by ``torch.distributed.run`` (one rank per GPU, RCCL over xGMI). Each
+step is a full training step on synthetic data (on-device generation of the
+batch, forward, loss, backward with bucketed gradient all-reduce, fused SGD with
+momentum + weight decay), random-init ResNet-50, bf16 compute / fp32 master
+weights. W untimed warm-up steps, then EXACTLY K timed steps bracketed by a
+barrier + device synchronize on both sides; the MAX elapsed over ranks is used.
+Rank 0 prints ONE JSON line.
+
+Reference metric: images/sec whole node at bs 400/GPU; published
+(derived) 717.0 img/s on 1 GPU and 5,546.7 img/s on 8 GPUs (AMP-DDP "Apex").
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+
+BASELINE = {1: 717.0, 8: 5546.7}   # BASELINE.md derived images/sec (other hardware)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--batch", type=int, default=400, help="per-GPU batch")
+    ap.add_argument("--arch", default="resnet50")
+    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp16", "fp32"])
+    ap.add_argument("--engine", default="auto", choices=["auto", "native", "torch"])
+    ap.add_argument("--bucket-mb", type=float, default=32.0)
+    ap.add_argument("--image-size", type=int, default=224)
+    ap.add_argument("--profile-steps", type=int, default=0)
+    return ap.parse_args()
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.gpus != world and world > 1:
+        print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
+    os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    torch.cuda.set_device(local_rank)
+    device = torch.device("cuda", local_rank)
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=device)
+
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    from pytorch_distributed_amd.bench_step import make_trainer
+    dtype = {"bf16": torch.bfloat16, "fp16": torch.float16, "fp32": torch.float32}[args.dtype]
+    tr = make_trainer(args.arch, args.batch, dtype, device, engine=args.engine,
+                      world=world, rank=rank, bucket_mb=args.bucket_mb, image_size=args.image_size)
+
+    for i in range(args.warmup):
+        tr.step(i)
+    torch.cuda.synchronize()
+
+    def barrier():
+        if world > 1:
+            import torch.distributed as dist
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    barrier()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        tr.step(args.warmup + i)
+    barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        import torch.distributed as dist
+        t = torch.tensor([elapsed], device=device, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    loss = tr.last_loss()
+    ms = 1000.0 * elapsed / max(args.steps, 1)
+    value = args.batch * world * args.steps / elapsed
+    base = BASELINE.get(world)
+    if rank == 0:
+        rec = {
+            "metric": "images/sec (whole node) ResNet-50 bs=400",
+            "value": round(value, 2),
+            "unit": "images/sec",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": round(value / base, 3) if base else None,
+            "dtype": args.dtype,
+            "data": "synthetic (on-device generated 3x224x224, random-init weights)",
+            "config": {"model": args.arch, "global_batch": args.batch * world,
+                       "per_gpu_batch": args.batch, "seq_len": None,
+                       "parallelism": f"dp{world}", "engine": tr.engine,
+                       "optimizer": "SGD(lr=0.1, momentum=0.9, wd=1e-4)"},
+            "loss": loss,
+            "max_mem_gb": round(torch.cuda.max_memory_allocated(device) / 1e9, 2),
+        }
+        print(json.dumps(rec), flush=True)
+    if world > 1:
+        import torch.distributed as dist
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

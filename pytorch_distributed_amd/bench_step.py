@@ -1,0 +1,68 @@
+"""One full training step per engine, shared by ``bench.py`` and the GPU tests.
+
+``make_trainer(...).step(i)`` = generate batch ``i`` on device -> forward -> loss
+-> backward (bucketed all-reduce when distributed) -> SGD(momentum, wd) update.
+"""
+from __future__ import annotations
+
+from typing import Optional
+
+import torch
+from torch import nn
+
+from .data.synthetic import SyntheticImageNet
+
+__all__ = ["make_trainer"]
+
+
+class _TorchTrainer:
+    """PyTorch-ROCm reference engine (MIOpen/hipBLASLt) -- oracle and fallback only."""
+
+    engine = "torch"
+
+    def __init__(self, arch, batch, dtype, device, world, rank, bucket_mb, image_size):
+        from .models.resnet import build_model
+        torch.manual_seed(0)
+        self.model = build_model(arch).to(device).to(memory_format=torch.channels_last)
+        self.dtype = dtype
+        self.device = device
+        self.batch = batch
+        self.world, self.rank = world, rank
+        self.ds = SyntheticImageNet("train", seed=0, image_size=image_size)
+        if world > 1:
+            from .parallel.ddp import DistributedDataParallel
+            self.net = DistributedDataParallel(self.model, bucket_cap_mb=bucket_mb)
+        else:
+            self.net = self.model
+        self.opt = torch.optim.SGD(self.model.parameters(), lr=0.1, momentum=0.9,
+                                   weight_decay=1e-4, foreach=True)
+        self.crit = nn.CrossEntropyLoss()
+        self._loss = None
+
+    def step(self, i: int) -> None:
+        ids = torch.arange(self.batch, device=self.device) + (i * self.world + self.rank) * self.batch
+        x, y = self.ds.batch(ids, device=self.device)
+        x = x.contiguous(memory_format=torch.channels_last)
+        with torch.autocast("cuda", dtype=self.dtype, enabled=self.dtype != torch.float32):
+            out = self.net(x)
+        loss = self.crit(out.float(), y)
+        self.opt.zero_grad(set_to_none=False)
+        loss.backward()
+        self.opt.step()
+        self._loss = loss.detach()
+
+    def last_loss(self) -> Optional[float]:
+        return None if self._loss is None else float(self._loss.item())
+
+
+def make_trainer(arch: str, batch: int, dtype: torch.dtype, device: torch.device,
+                 engine: str = "auto", world: int = 1, rank: int = 0, bucket_mb: float = 32.0,
+                 image_size: int = 224):
+    if engine in ("auto", "native"):
+        from .models import native
+        if native.supports(arch, dtype):
+            return native.NativeTrainer(arch, batch, dtype, device, world, rank, bucket_mb,
+                                        image_size)
+        if engine == "native":
+            raise RuntimeError(f"native engine unavailable for {arch}/{dtype}")
+    return _TorchTrainer(arch, batch, dtype, device, world, rank, bucket_mb, image_size)

@@ -1,0 +1,133 @@
+"""Process launch + rendezvous: replacement for ``hfai.multiprocessing.spawn`` and
+the reference's env contract.
+
+Reference contract (``restnet_ddp.py:86-95,153-155``): the script is started
+once per *node* with ``MASTER_IP``, ``MASTER_PORT``, ``WORLD_SIZE`` (= number of
+nodes) and ``RANK`` (= node index); it spawns one process per visible GPU
+(NUMA-bound), and each computes ``world = nodes * gpus`` and
+``rank = node * gpus + local_rank``.
+
+:func:`spawn` keeps that contract (single-node defaults: 127.0.0.1, a free
+port, 1 node, node 0) and additionally pins each child to the CPUs of the NUMA
+node nearest its GPU (read from sysfs). :func:`dist_env` also accepts a
+``torchrun``-style launch (``LOCAL_RANK``/``LOCAL_WORLD_SIZE`` present), which is
+how ``bench.py`` is driven.
+"""
+from __future__ import annotations
+
+import os
+import socket
+from dataclasses import dataclass
+from typing import Callable, Optional, Sequence
+
+import torch
+
+__all__ = ["DistEnv", "dist_env", "spawn", "free_port", "bind_numa", "init_distributed"]
+
+
+@dataclass
+class DistEnv:
+    master_addr: str
+    master_port: int
+    world_size: int
+    rank: int
+    local_rank: int
+    local_world_size: int
+    node_rank: int
+    nnodes: int
+
+
+def free_port() -> int:
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def dist_env(local_rank: Optional[int] = None, nprocs: Optional[int] = None) -> DistEnv:
+    env = os.environ
+    if "LOCAL_RANK" in env and local_rank is None:          # torchrun
+        lr = int(env["LOCAL_RANK"])
+        lws = int(env.get("LOCAL_WORLD_SIZE", env.get("WORLD_SIZE", "1")))
+        world = int(env.get("WORLD_SIZE", "1"))
+        rank = int(env.get("RANK", str(lr)))
+        return DistEnv(env.get("MASTER_ADDR", "127.0.0.1"), int(env.get("MASTER_PORT", "29500")),
+                       world, rank, lr, lws, rank // max(lws, 1), max(world // max(lws, 1), 1))
+    # reference contract: WORLD_SIZE = nodes, RANK = node index
+    addr = env.get("MASTER_IP", env.get("MASTER_ADDR", "127.0.0.1"))
+    port = int(env.get("MASTER_PORT", "29500"))
+    nnodes = int(env.get("WORLD_SIZE", "1"))
+    node = int(env.get("RANK", "0"))
+    lr = 0 if local_rank is None else local_rank
+    gpus = nprocs if nprocs is not None else max(torch.cuda.device_count(), 1)
+    return DistEnv(addr, port, nnodes * gpus, node * gpus + lr, lr, gpus, node, nnodes)
+
+
+def _gpu_numa_cpus(local_rank: int) -> Optional[Sequence[int]]:
+    """CPUs of the NUMA node that hosts GPU ``local_rank`` (KFD topology, sysfs)."""
+    try:
+        root = "/sys/class/kfd/kfd/topology/nodes"
+        gpus = []
+        for n in sorted(os.listdir(root), key=int):
+            props = open(f"{root}/{n}/properties").read().split("\n")
+            kv = dict(l.split(" ", 1) for l in props if " " in l)
+            if int(kv.get("simd_count", "0")) > 0:
+                gpus.append(kv)
+        if local_rank >= len(gpus):
+            return None
+        dom = int(gpus[local_rank].get("domain", "0"))
+        bdf_bus = int(gpus[local_rank].get("location_id", "0"))
+        bdf = f"{dom:04x}:{(bdf_bus >> 8) & 0xff:02x}:{(bdf_bus >> 3) & 0x1f:02x}.{bdf_bus & 7}"
+        numa = int(open(f"/sys/bus/pci/devices/{bdf}/numa_node").read())
+        if numa < 0:
+            return None
+        cpulist = open(f"/sys/devices/system/node/node{numa}/cpulist").read().strip()
+        cpus = []
+        for part in cpulist.split(","):
+            a, _, b = part.partition("-")
+            cpus.extend(range(int(a), int(b or a) + 1))
+        return cpus
+    except (OSError, ValueError, KeyError):
+        return None
+
+
+def bind_numa(local_rank: int) -> bool:
+    cpus = _gpu_numa_cpus(local_rank)
+    if not cpus:
+        return False
+    try:
+        os.sched_setaffinity(0, cpus)
+        return True
+    except OSError:
+        return False
+
+
+def _child(local_rank: int, fn: Callable, args: tuple, numa: bool) -> None:
+    if numa:
+        bind_numa(local_rank)
+    fn(local_rank, *args)
+
+
+def spawn(fn: Callable, args: tuple = (), nprocs: Optional[int] = None, bind_numa: bool = True,
+          join: bool = True):
+    """``hfai.multiprocessing.spawn`` equivalent: ``fn(local_rank, *args)`` in ``nprocs`` procs."""
+    import torch.multiprocessing as mp
+    nprocs = nprocs if nprocs is not None else max(torch.cuda.device_count(), 1)
+    os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    if "MASTER_PORT" not in os.environ:
+        os.environ["MASTER_PORT"] = str(free_port())
+    os.environ.setdefault("MASTER_IP", os.environ.get("MASTER_ADDR", "127.0.0.1"))
+    if nprocs == 1:
+        _child(0, fn, args, bind_numa)
+        return None
+    return mp.spawn(_child, args=(fn, args, bind_numa), nprocs=nprocs, join=join)
+
+
+def init_distributed(env: DistEnv, backend: str, timeout_s: float = 1800.0) -> None:
+    import datetime
+    import torch.distributed as dist
+    if dist.is_initialized():
+        return
+    dist.init_process_group(backend=backend,
+                            init_method=f"tcp://{env.master_addr}:{env.master_port}",
+                            world_size=env.world_size, rank=env.rank,
+                            timeout=datetime.timedelta(seconds=timeout_s))

@@ -1,0 +1,75 @@
+"""Communicator: the collective layer under DDP / DP / validation.
+
+Two implementations behind one interface:
+
+* :class:`RcclCommunicator` -- our C++ RCCL communicator (``csrc/comm/rccl_comm.cpp``):
+  ``ncclGetUniqueId`` exchanged through the ``torch.distributed`` TCPStore,
+  ``ncclCommInitRank``, collectives enqueued on a dedicated HIP stream that
+  waits on an event recorded on the compute stream, completion tracked by a
+  HIP event the compute stream later waits on (no host sync). Used for the
+  gradient buckets on GPU.
+* :class:`ProcessGroupCommunicator` -- any initialised ``torch.distributed``
+  process group (``gloo`` on CPU for the multi-process CPU tests; ``nccl`` = RCCL
+  on ROCm as a fallback when the native extension is unavailable).
+"""
+from __future__ import annotations
+
+from typing import Any, Optional
+
+import torch
+import torch.distributed as dist
+
+__all__ = ["Communicator", "ProcessGroupCommunicator", "make_communicator"]
+
+
+class Communicator:
+    world_size: int = 1
+    rank: int = 0
+
+    def all_reduce_async(self, t: torch.Tensor) -> Any:
+        raise NotImplementedError
+
+    def wait(self, handle: Any) -> None:
+        raise NotImplementedError
+
+    def all_reduce(self, t: torch.Tensor) -> None:
+        self.wait(self.all_reduce_async(t))
+
+    def broadcast(self, t: torch.Tensor, src: int = 0) -> None:
+        raise NotImplementedError
+
+    def barrier(self) -> None:
+        raise NotImplementedError
+
+
+class ProcessGroupCommunicator(Communicator):
+    def __init__(self, group=None) -> None:
+        self.group = group
+        self.world_size = dist.get_world_size(group)
+        self.rank = dist.get_rank(group)
+
+    def all_reduce_async(self, t: torch.Tensor):
+        return dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
+
+    def wait(self, handle) -> None:
+        if handle is not None:
+            handle.wait()
+
+    def broadcast(self, t: torch.Tensor, src: int = 0) -> None:
+        dist.broadcast(t, src=src, group=self.group)
+
+    def barrier(self) -> None:
+        dist.barrier(group=self.group)
+
+
+def make_communicator(device: Optional[torch.device] = None, group=None,
+                      prefer_native: bool = True) -> Communicator:
+    """Native RCCL communicator on GPU when the extension is built, else process group."""
+    if device is not None and device.type == "cuda" and prefer_native:
+        try:
+            from .rccl import RcclCommunicator
+            return RcclCommunicator(device, group=group)
+        except (ImportError, RuntimeError) as e:  # pragma: no cover - GPU only
+            import warnings
+            warnings.warn(f"native RCCL communicator unavailable ({e}); using torch process group")
+    return ProcessGroupCommunicator(group)

@@ -1,0 +1,27 @@
+"""ResNet-50, multi-process DDP (reference: restnet_ddp.py -- file name kept, typo included).
+
+Launch once per node: MASTER_IP, MASTER_PORT, WORLD_SIZE (= #nodes), RANK (= node index);
+one process per visible GPU is spawned (NUMA-bound). torchrun launches also work.
+"""
+import os
+
+from pytorch_distributed_amd.config import config_for
+from pytorch_distributed_amd.launch import spawn
+from pytorch_distributed_amd.trainer import run
+
+
+def main(local_rank, script="ddp", nprocs=None):
+    run(config_for(script), mode=script, local_rank=local_rank, nprocs=nprocs)
+
+
+def launch(script="ddp"):
+    if "LOCAL_RANK" in os.environ:            # started by torchrun
+        main(int(os.environ["LOCAL_RANK"]), script)
+        return
+    import torch
+    nprocs = int(os.environ.get("MX_NPROCS", "0")) or max(torch.cuda.device_count(), 1)
+    spawn(main, args=(script, nprocs), nprocs=nprocs, bind_numa=True)
+
+
+if __name__ == "__main__":
+    launch("ddp")

@@ -1,0 +1,172 @@
+"""T0/T1 tier: pure-Python components with torch CPU oracles."""
+import math
+import os
+
+import pytest
+import torch
+from torch import nn
+
+from pytorch_distributed_amd.config import config_for
+from pytorch_distributed_amd.data import DistributedSampler, SyntheticImageNet, synthetic_images
+from pytorch_distributed_amd.models import resnet18, resnet50
+from pytorch_distributed_amd.parallel.reducer import plan_buckets
+from pytorch_distributed_amd.utils.checkpoint import load_latest, save_best, save_latest
+
+
+def test_config_defaults_match_reference():
+    s = config_for("single", env={})
+    assert (s.epochs, s.batch_size, s.num_workers, s.lr, s.momentum, s.weight_decay) == \
+        (100, 400, 4, 0.1, 0.9, 1e-4)
+    assert s.save_path == "output/resnet_single"
+    assert config_for("dp", env={}).batch_size == 3200
+    assert config_for("ddp", env={}).save_path == "output/resnet_ddp"
+    a = config_for("ddp_amp", env={})
+    assert a.save_path == "output/resnet_ddp_amp" and a.dtype == "fp16"
+    o = config_for("single", env={"MX_EPOCHS": "3", "MX_DTYPE": "bf16"})
+    assert o.epochs == 3 and o.dtype == "bf16"
+    with pytest.raises(ValueError):
+        config_for("single", env={"MX_DTYPE": "int8"})
+
+
+def test_resnet50_census_matches_torchvision():
+    m = resnet50()
+    n = sum(p.numel() for p in m.parameters())
+    assert n == 25_557_032                      # SURVEY §2.7 model census
+    assert len(list(m.parameters())) == 161
+    assert len(list(m.buffers())) == 159
+    sd = m.state_dict()
+    for k in ["conv1.weight", "bn1.running_mean", "layer1.0.downsample.0.weight",
+              "layer4.2.bn3.num_batches_tracked", "fc.weight", "fc.bias", "layer2.3.conv2.weight"]:
+        assert k in sd
+    assert sd["layer2.0.conv2.weight"].shape == (128, 128, 3, 3)
+    # v1.5: stride on the 3x3 conv
+    assert m.layer2[0].conv2.stride == (2, 2) and m.layer2[0].conv1.stride == (1, 1)
+    # kaiming fan_out init: std = sqrt(2 / (cout*k*k))
+    w = m.layer3[0].conv2.weight
+    assert abs(w.std().item() - math.sqrt(2.0 / (256 * 9))) < 0.01 * math.sqrt(2.0 / (256 * 9)) * 10
+    assert torch.all(m.bn1.weight == 1) and torch.all(m.bn1.bias == 0)
+
+
+def test_resnet18_forward_backward_cpu():
+    m = resnet18(num_classes=10)
+    x = torch.randn(2, 3, 64, 64)
+    y = m(x)
+    assert y.shape == (2, 10)
+    y.sum().backward()
+    assert m.conv1.weight.grad is not None
+
+
+def test_sampler_matches_torch():
+    from torch.utils.data.distributed import DistributedSampler as TorchDS
+    ds = list(range(103))
+    for world in (1, 2, 4, 8):
+        for rank in range(world):
+            for epoch in (0, 3):
+                a = DistributedSampler(ds, world, rank, shuffle=True, seed=7)
+                b = TorchDS(ds, world, rank, shuffle=True, seed=7)
+                a.set_epoch(epoch)
+                b.set_epoch(epoch)
+                assert list(a) == list(b)
+                assert len(a) == len(b)
+
+
+def test_synthetic_deterministic_and_learnable():
+    ids = torch.tensor([0, 5, 17, 5])
+    x1, y1 = synthetic_images(ids, 0, "train", 1000, 32)
+    x2, y2 = synthetic_images(ids, 0, "train", 1000, 32)
+    assert torch.equal(x1, x2) and torch.equal(y1, y2)
+    assert torch.equal(x1[1], x1[3])
+    assert not torch.equal(x1[0], x1[1])
+    xv, _ = synthetic_images(ids, 0, "val", 1000, 32)
+    assert not torch.equal(xv, x1)
+    assert x1.shape == (4, 3, 32, 32) and y1.dtype == torch.int64
+    assert 0 <= int(y1.min()) and int(y1.max()) < 1000
+    ds = SyntheticImageNet("train", 1000, 0, 10, 16)
+    xs, ys = ds.batch(torch.arange(200))
+    # class tint makes channel means label-dependent
+    m0 = xs[ys == ys[0]][:, 0].mean()
+    assert len(ds) == 1000 and torch.isfinite(m0)
+
+
+def test_loader_len_and_resume_seek():
+    ds = SyntheticImageNet("train", 1003, 0, 10, 8)
+    ld = ds.loader(100)
+    assert len(ld) == 11
+    all_b = [b for b in ld]
+    assert all_b[-1][0].shape[0] == 3
+    rest = [b for _, b in ld.iter_from(4)]
+    assert len(rest) == 7 and torch.equal(rest[0][1], all_b[4][1])
+
+
+def test_plan_buckets():
+    MiB = 1 << 20
+    g = plan_buckets([MiB // 2, MiB // 2, MiB, 20 * MiB, 20 * MiB, 3 * MiB, MiB], 32 * MiB, MiB,
+                     2 * MiB)
+    assert g[0] == [0, 1]
+    flat = [i for b in g for i in b]
+    assert flat == list(range(7))
+    assert sum([MiB // 2, MiB // 2, MiB, 20 * MiB, 20 * MiB, 3 * MiB, MiB][i] for i in g[-1]) <= 2 * MiB
+
+
+def test_checkpoint_schema(tmp_path):
+    m = resnet18(num_classes=10)
+    opt = torch.optim.SGD(m.parameters(), lr=0.1, momentum=0.9, weight_decay=1e-4)
+    sch = torch.optim.lr_scheduler.StepLR(opt, 30, 0.1)
+    m(torch.randn(2, 3, 32, 32)).sum().backward()
+    opt.step()
+    save_latest(tmp_path, m.state_dict(), opt.state_dict(), sch.state_dict(), 0.5, 3, 17,
+                scaler_sd={"scale": 1024.0})
+    ck = load_latest(tmp_path)
+    assert set(ck) == {"model", "optimizer", "scheduler", "acc", "epoch", "step", "scaler"}
+    assert ck["epoch"] == 3 and ck["step"] == 17
+    m2 = resnet18(num_classes=10)
+    m2.load_state_dict(ck["model"])
+    for a, b in zip(m.state_dict().values(), m2.state_dict().values()):
+        assert torch.equal(a, b)
+    save_best(tmp_path, m.state_dict())
+    assert (tmp_path / "best.pt").exists()
+    assert load_latest(tmp_path / "nothing") is None
+
+
+def test_suspend_monitor_step_trigger(monkeypatch):
+    from pytorch_distributed_amd.utils.suspend import SuspendMonitor
+    mon = SuspendMonitor(signals=(), at_step=3)
+    hits = []
+    for _ in range(5):
+        mon.tick()
+        hits.append(mon.requested())
+    assert hits == [False, False, True, True, True]
+
+
+def test_suspend_monitor_sentinel(tmp_path):
+    from pytorch_distributed_amd.utils.suspend import SuspendMonitor
+    f = tmp_path / "stop"
+    mon = SuspendMonitor(signals=(), sentinel=str(f))
+    assert not mon.requested()
+    f.write_text("")
+    assert mon.requested()
+
+
+def test_loss_scaler_state_machine_matches_gradscaler():
+    from pytorch_distributed_amd.amp import LossScaler
+    p = nn.Parameter(torch.ones(4))
+    opt = torch.optim.SGD([p], lr=0.1)
+    s = LossScaler(init_scale=8.0, growth_interval=2)
+    scales = []
+    for step in range(6):
+        loss = (p * 2).sum()
+        s.scale(loss).backward()
+        if step == 3:
+            p.grad[0] = float("inf")
+        before = p.detach().clone()
+        s.step(opt)
+        if step == 3:
+            assert torch.equal(before, p.detach())      # skipped
+        s.update()
+        opt.zero_grad()
+        scales.append(s.get_scale())
+    assert scales == [8.0, 16.0, 16.0, 8.0, 8.0, 16.0]
+    sd = s.state_dict()
+    s2 = LossScaler()
+    s2.load_state_dict(sd)
+    assert s2.get_scale() == 16.0
