@@ -1,0 +1,572 @@
+// BatchNorm (+ReLU, +residual, +pool) kernels for gfx950, NHWC 16-bit activations, f32 statistics.
+//
+// Replaces cuDNN BatchNorm train fwd/bwd + ATen ReLU/threshold_backward/add/max_pool2d/avg_pool2d
+// of the reference stack. Statistics are computed from the conv
+// epilogue's per-tile partial sums (conv_gemm.hip) or by the column-reduce kernel below; every
+// cross-workgroup sum is a deterministic slab reduction (no float atomics).
+//
+//   bn_finalize_fwd : partial [T][2][C] -> mean, invstd, scale = g*invstd, shift = b - mean*scale,
+//                     running-stat update (momentum, unbiased var), num_batches_tracked += 1
+//   bn_apply        : a = act(y*scale + shift [+ res | + y2*scale2 + shift2]), 16 B / lane
+//   stem_pool       : a = relu(bn(y)) then 3x3/s2/p1 max-pool with a uint8 argmax per output
+//   tail_pool       : a = relu(bn3(y3) + shortcut) then global average pool (head of ResNet)
+//   bn_bwd_reduce   : partials of sum(dz), sum(dz*xhat) [, sum(dz*xhat_ds)] with dz = dA*mask
+//   bn_bwd_finalize : gamma/beta grads into the flat gradient buffer + apply coefficients
+//   bn_bwd_apply    : dy = k1*dz + k2*y + k3 (dz recomputed, or read back from the tail buffer)
+//   maxpool_bwd     : deterministic gather of max-pool gradients through the argmax bytes
+#include "common.h"
+
+namespace {
+
+constexpr int NT = 256;
+
+template <int DT>
+__device__ __forceinline__ void unpack8(const i32x4& v, float* f) {
+  const u16* h = reinterpret_cast<const u16*>(&v);
+#pragma unroll
+  for (int e = 0; e < 8; ++e) f[e] = ld16<DT>(h[e]);
+}
+template <int DT>
+__device__ __forceinline__ i32x4 pack8(const float* f) {
+  i32x4 v;
+  u16* h = reinterpret_cast<u16*>(&v);
+#pragma unroll
+  for (int e = 0; e < 8; ++e) h[e] = st16<DT>(f[e]);
+  return v;
+}
+__device__ __forceinline__ void ld8f(const float* p, float* f) {
+  const f32x4 a = *reinterpret_cast<const f32x4*>(p);
+  const f32x4 b = *reinterpret_cast<const f32x4*>(p + 4);
+  f[0] = a[0]; f[1] = a[1]; f[2] = a[2]; f[3] = a[3];
+  f[4] = b[0]; f[5] = b[1]; f[6] = b[2]; f[7] = b[3];
+}
+
+// ------------------------------------------------------------------ forward finalize
+// part: [T][2][C] (sum, sumsq) partials. One block = 16 channels x 64 partial-lanes.
+__global__ __launch_bounds__(1024) void bn_finalize_fwd_kernel(
+    const float* __restrict__ part, int T, int C, float count, const float* __restrict__ gamma,
+    const float* __restrict__ beta, float eps, float momentum, float* __restrict__ mean_out,
+    float* __restrict__ invstd_out, float* __restrict__ scale, float* __restrict__ shift,
+    float* __restrict__ run_mean, float* __restrict__ run_var, long long* __restrict__ nbt,
+    int update_running) {
+  __shared__ double red[2][64][17];
+  const int cl = threadIdx.x & 15, g = threadIdx.x >> 4;
+  const int c = blockIdx.x * 16 + cl;
+  double s1 = 0.0, s2 = 0.0;
+  if (c < C) {
+    for (int t = g; t < T; t += 64) {
+      s1 += part[(size_t)t * 2 * C + c];
+      s2 += part[(size_t)t * 2 * C + C + c];
+    }
+  }
+  red[0][g][cl] = s1;
+  red[1][g][cl] = s2;
+  __syncthreads();
+  if (g == 0 && c < C) {
+    double a = 0.0, b = 0.0;
+    for (int i = 0; i < 64; ++i) {
+      a += red[0][i][cl];
+      b += red[1][i][cl];
+    }
+    const double mean = a / count;
+    double var = b / count - mean * mean;
+    if (var < 0.0) var = 0.0;
+    const float inv = (float)(1.0 / sqrt(var + (double)eps));
+    const float sc = gamma[c] * inv;
+    mean_out[c] = (float)mean;
+    invstd_out[c] = inv;
+    scale[c] = sc;
+    shift[c] = beta[c] - (float)mean * sc;
+    if (update_running) {
+      const double unb = count > 1.0 ? var * count / (count - 1.0) : var;
+      run_mean[c] = (1.f - momentum) * run_mean[c] + momentum * (float)mean;
+      run_var[c] = (1.f - momentum) * run_var[c] + momentum * (float)unb;
+    }
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0 && update_running && nbt) *nbt += 1;
+}
+
+// eval-mode scale/shift from running statistics
+__global__ void bn_eval_coeffs_kernel(const float* __restrict__ gamma, const float* __restrict__ beta,
+                                      const float* __restrict__ rm, const float* __restrict__ rv,
+                                      float eps, int C, float* __restrict__ scale,
+                                      float* __restrict__ shift) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  const float inv = rsqrtf(rv[c] + eps);
+  scale[c] = gamma[c] * inv;
+  shift[c] = beta[c] - rm[c] * gamma[c] * inv;
+}
+
+// ------------------------------------------------------------------ apply
+// mode: 0 = act(bn(y)); 1 = act(bn(y) + res); 2 = act(bn(y) + bn2(y2))
+template <int DT>
+__global__ __launch_bounds__(NT) void bn_apply_kernel(
+    const u16* __restrict__ y, const float* __restrict__ sc, const float* __restrict__ sh,
+    const u16* __restrict__ r2, const float* __restrict__ sc2, const float* __restrict__ sh2,
+    u16* __restrict__ out, long long n8, int C, int mode, int relu) {
+  for (long long i = blockIdx.x * (long long)NT + threadIdx.x; i < n8; i += (long long)gridDim.x * NT) {
+    const int c0 = (int)((i * 8) % C);
+    float v[8], a[8], b[8];
+    unpack8<DT>(reinterpret_cast<const i32x4*>(y)[i], v);
+    ld8f(sc + c0, a);
+    ld8f(sh + c0, b);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] = v[e] * a[e] + b[e];
+    if (mode) {
+      float w[8];
+      unpack8<DT>(reinterpret_cast<const i32x4*>(r2)[i], w);
+      if (mode == 2) {
+        ld8f(sc2 + c0, a);
+        ld8f(sh2 + c0, b);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) w[e] = w[e] * a[e] + b[e];
+      }
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] += w[e];
+    }
+    if (relu) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = fmaxf(v[e], 0.f);
+    }
+    reinterpret_cast<i32x4*>(out)[i] = pack8<DT>(v);
+  }
+}
+
+// ------------------------------------------------------------------ stem: bn + relu + maxpool 3x3/2/1
+// y: [N,H,W,C], out: [N,Ho,Wo,C], arg: [N,Ho,Wo,C] uint8 window index (0..8)
+template <int DT>
+__global__ __launch_bounds__(NT) void stem_pool_kernel(const u16* __restrict__ y,
+                                                       const float* __restrict__ sc,
+                                                       const float* __restrict__ sh,
+                                                       u16* __restrict__ out,
+                                                       uint8_t* __restrict__ arg, int N, int H,
+                                                       int W, int C, int Ho, int Wo) {
+  const int CK = C / 8;
+  const long long total = (long long)N * Ho * Wo * CK;
+  for (long long i = blockIdx.x * (long long)NT + threadIdx.x; i < total; i += (long long)gridDim.x * NT) {
+    const int ck = (int)(i % CK);
+    long long pix = i / CK;
+    const int xo = (int)(pix % Wo);
+    pix /= Wo;
+    const int yo = (int)(pix % Ho);
+    const int n = (int)(pix / Ho);
+    float a[8], b[8], best[8];
+    int bi[8];
+    ld8f(sc + ck * 8, a);
+    ld8f(sh + ck * 8, b);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) { best[e] = -1.f; bi[e] = 0; }
+    for (int dy = 0; dy < 3; ++dy) {
+      const int yy = yo * 2 - 1 + dy;
+      if ((unsigned)yy >= (unsigned)H) continue;
+      for (int dx = 0; dx < 3; ++dx) {
+        const int xx = xo * 2 - 1 + dx;
+        if ((unsigned)xx >= (unsigned)W) continue;
+        float v[8];
+        unpack8<DT>(*reinterpret_cast<const i32x4*>(y + (((size_t)n * H + yy) * W + xx) * C + ck * 8), v);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const float r = fmaxf(v[e] * a[e] + b[e], 0.f);
+          if (r > best[e]) { best[e] = r; bi[e] = dy * 3 + dx; }
+        }
+      }
+    }
+    reinterpret_cast<i32x4*>(out)[i] = pack8<DT>(best);
+    uint64_t packed = 0;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) packed |= (uint64_t)bi[e] << (8 * e);
+    reinterpret_cast<uint64_t*>(arg)[i] = packed;
+  }
+}
+
+// gradient of relu(bn(y)) through the max-pool: dA[n,y,x,c] = sum over windows whose argmax is here
+template <int DT>
+__global__ __launch_bounds__(NT) void maxpool_bwd_kernel(const u16* __restrict__ dout,
+                                                         const u16* __restrict__ dout2,
+                                                         const uint8_t* __restrict__ arg,
+                                                         u16* __restrict__ din, int N, int H, int W,
+                                                         int C, int Ho, int Wo) {
+  const int CK = C / 8;
+  const long long total = (long long)N * H * W * CK;
+  for (long long i = blockIdx.x * (long long)NT + threadIdx.x; i < total; i += (long long)gridDim.x * NT) {
+    const int ck = (int)(i % CK);
+    long long pix = i / CK;
+    const int x = (int)(pix % W);
+    pix /= W;
+    const int yy = (int)(pix % H);
+    const int n = (int)(pix / H);
+    float g[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) g[e] = 0.f;
+    // outputs whose window covers (yy, x): yo*2-1 <= yy <= yo*2+1
+    for (int yo = yy / 2; yo <= min(Ho - 1, (yy + 1) / 2); ++yo) {
+      const int dy = yy - (yo * 2 - 1);
+      if (dy < 0 || dy > 2) continue;
+      for (int xo = x / 2; xo <= min(Wo - 1, (x + 1) / 2); ++xo) {
+        const int dx = x - (xo * 2 - 1);
+        if (dx < 0 || dx > 2) continue;
+        const size_t o = ((size_t)n * Ho + yo) * Wo + xo;
+        const uint64_t a = reinterpret_cast<const uint64_t*>(arg)[o * CK + ck];
+        float d[8];
+        unpack8<DT>(*reinterpret_cast<const i32x4*>(dout + o * C + ck * 8), d);
+        if (dout2) {
+          float d2[8];
+          unpack8<DT>(*reinterpret_cast<const i32x4*>(dout2 + o * C + ck * 8), d2);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) d[e] += d2[e];
+        }
+        const int me = dy * 3 + dx;
+#pragma unroll
+        for (int e = 0; e < 8; ++e)
+          if ((int)((a >> (8 * e)) & 0xff) == me) g[e] += d[e];
+      }
+    }
+    reinterpret_cast<i32x4*>(din)[i] = pack8<DT>(g);
+  }
+}
+
+// ------------------------------------------------------------------ head: tail + global avg pool
+// out[n][c] = mean_{hw} relu(bn3(y3) + shortcut) ; shortcut: mode 1 = res tensor, 2 = bn_ds(y_ds)
+template <int DT>
+__global__ __launch_bounds__(NT) void tail_pool_kernel(const u16* __restrict__ y,
+                                                       const float* __restrict__ sc,
+                                                       const float* __restrict__ sh,
+                                                       const u16* __restrict__ r2,
+                                                       const float* __restrict__ sc2,
+                                                       const float* __restrict__ sh2,
+                                                       u16* __restrict__ out, int HW, int C,
+                                                       int mode) {
+  const int n = blockIdx.x;
+  const int CK = C / 8;
+  for (int ck = threadIdx.x; ck < CK; ck += NT) {
+    float a[8], b[8], a2[8], b2[8], acc[8];
+    ld8f(sc + ck * 8, a);
+    ld8f(sh + ck * 8, b);
+    if (mode == 2) {
+      ld8f(sc2 + ck * 8, a2);
+      ld8f(sh2 + ck * 8, b2);
+    }
+#pragma unroll
+    for (int e = 0; e < 8; ++e) acc[e] = 0.f;
+    for (int pp = 0; pp < HW; ++pp) {
+      const size_t off = ((size_t)n * HW + pp) * C + ck * 8;
+      float v[8], w[8];
+      unpack8<DT>(*reinterpret_cast<const i32x4*>(y + off), v);
+      unpack8<DT>(*reinterpret_cast<const i32x4*>(r2 + off), w);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        float s = w[e];
+        if (mode == 2) s = s * a2[e] + b2[e];
+        acc[e] += fmaxf(v[e] * a[e] + b[e] + s, 0.f);
+      }
+    }
+    const float inv = 1.f / (float)HW;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) acc[e] *= inv;
+    *reinterpret_cast<i32x4*>(out + (size_t)n * C + ck * 8) = pack8<DT>(acc);
+  }
+}
+
+// ------------------------------------------------------------------ backward reduce
+// dA = g1 (+ g2), or, when pooled (HW > 0), dA[n,p,c] = gp[n][c] / HW.
+// mask mode: 0 = relu on bn(y) (bn1/bn2/stem), 1 = relu on bn(y)+res, 2 = relu on bn(y)+bn2(y2),
+//            3 = no mask (dz given in g1, e.g. downsample branch re-reading the tail's dz)
+// Outputs partials [G][NQ][C]: q0 = sum dz, q1 = sum dz*y, q2 = sum dz*y2 (mode 2); dz stored if dz_out.
+struct BwdArgs {
+  const u16* g1; const u16* g2; const u16* gp; int HW;
+  const u16* y; const float* sc; const float* sh;
+  const u16* y2; const float* sc2; const float* sh2;
+  int mode;
+  u16* dz_out;
+  float* part; int nq;
+  long long rows; int C;
+  long long rows_per_block;
+};
+
+template <int DT>
+__device__ __forceinline__ void load_grad(const BwdArgs& a, long long row, int c0, float* g) {
+  if (a.gp) {
+    const long long n = row / a.HW;
+    unpack8<DT>(*reinterpret_cast<const i32x4*>(a.gp + n * a.C + c0), g);
+    const float inv = 1.f / (float)a.HW;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) g[e] *= inv;
+  } else {
+    unpack8<DT>(*reinterpret_cast<const i32x4*>(a.g1 + row * a.C + c0), g);
+    if (a.g2) {
+      float h[8];
+      unpack8<DT>(*reinterpret_cast<const i32x4*>(a.g2 + row * a.C + c0), h);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) g[e] += h[e];
+    }
+  }
+}
+
+// dz for one 8-channel chunk of row; also returns y (and y2) values for the moment sums
+template <int DT>
+__device__ __forceinline__ void make_dz(const BwdArgs& a, long long row, int c0, float* dz,
+                                        float* yv, float* y2v) {
+  load_grad<DT>(a, row, c0, dz);
+  unpack8<DT>(*reinterpret_cast<const i32x4*>(a.y + row * a.C + c0), yv);
+  if (a.mode == 3) return;
+  float s[8], h[8];
+  ld8f(a.sc + c0, s);
+  ld8f(a.sh + c0, h);
+  float pre[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) pre[e] = yv[e] * s[e] + h[e];
+  if (a.mode >= 1) {
+    unpack8<DT>(*reinterpret_cast<const i32x4*>(a.y2 + row * a.C + c0), y2v);
+    if (a.mode == 2) {
+      ld8f(a.sc2 + c0, s);
+      ld8f(a.sh2 + c0, h);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) pre[e] += y2v[e] * s[e] + h[e];
+    } else {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) pre[e] += y2v[e];
+    }
+  }
+#pragma unroll
+  for (int e = 0; e < 8; ++e) dz[e] = pre[e] > 0.f ? dz[e] : 0.f;
+}
+
+template <int DT>
+__global__ __launch_bounds__(NT) void bn_bwd_reduce_kernel(BwdArgs a) {
+  __shared__ float red[3][NT][8];
+  const int CK = a.C / 8;
+  const int tpr = CK < NT ? CK : NT;       // threads per row
+  const int rpi = NT / tpr;                // rows per iteration
+  const int ck = threadIdx.x % tpr, rsub = threadIdx.x / tpr;
+  const long long r0 = blockIdx.x * a.rows_per_block;
+  const long long r1 = min(a.rows, r0 + a.rows_per_block);
+  for (int cbase = 0; cbase < CK; cbase += tpr) {
+    const int c0 = (cbase + ck) * 8;
+    float q0[8], q1[8], q2[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) { q0[e] = 0.f; q1[e] = 0.f; q2[e] = 0.f; }
+    if (threadIdx.x < tpr * rpi) {
+      for (long long row = r0 + rsub; row < r1; row += rpi) {
+        float dz[8], yv[8], y2v[8];
+        make_dz<DT>(a, row, c0, dz, yv, y2v);
+        if (a.dz_out) *reinterpret_cast<i32x4*>(a.dz_out + row * a.C + c0) = pack8<DT>(dz);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          q0[e] += dz[e];
+          q1[e] += dz[e] * yv[e];
+        }
+        if (a.nq > 2) {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) q2[e] += dz[e] * y2v[e];
+        }
+      }
+    }
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      red[0][threadIdx.x][e] = q0[e];
+      red[1][threadIdx.x][e] = q1[e];
+      red[2][threadIdx.x][e] = q2[e];
+    }
+    __syncthreads();
+    if (threadIdx.x < tpr) {
+      for (int q = 0; q < a.nq; ++q) {
+        float s[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) s[e] = 0.f;
+        for (int r = 0; r < rpi; ++r)
+#pragma unroll
+          for (int e = 0; e < 8; ++e) s[e] += red[q][r * tpr + threadIdx.x][e];
+        float* dst = a.part + ((size_t)blockIdx.x * a.nq + q) * a.C + c0;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) dst[e] = s[e];
+      }
+    }
+    __syncthreads();
+  }
+}
+
+// finalize: for branch b (0: y with q0,q1; 1: y2 with q0,q2) produce gamma/beta grads and
+// coefficients k1,k2,k3 such that dy = k1*dz + k2*y + k3.
+__global__ __launch_bounds__(1024) void bn_bwd_finalize_kernel(
+    const float* __restrict__ part, int G, int nq, int qy, int C, float count,
+    const float* __restrict__ gamma, const float* __restrict__ mean, const float* __restrict__ invstd,
+    float* __restrict__ dgamma, float* __restrict__ dbeta, float* __restrict__ k1,
+    float* __restrict__ k2, float* __restrict__ k3, float gscale, int accumulate) {
+  __shared__ double red[2][64][17];
+  const int cl = threadIdx.x & 15, g = threadIdx.x >> 4;
+  const int c = blockIdx.x * 16 + cl;
+  double s0 = 0.0, s1 = 0.0;
+  if (c < C) {
+    for (int t = g; t < G; t += 64) {
+      s0 += part[((size_t)t * nq + 0) * C + c];
+      s1 += part[((size_t)t * nq + qy) * C + c];
+    }
+  }
+  red[0][g][cl] = s0;
+  red[1][g][cl] = s1;
+  __syncthreads();
+  if (g == 0 && c < C) {
+    double sdz = 0.0, sdzy = 0.0;
+    for (int i = 0; i < 64; ++i) {
+      sdz += red[0][i][cl];
+      sdzy += red[1][i][cl];
+    }
+    const double mu = mean[c], is = invstd[c], ga = gamma[c];
+    const double sdzx = (sdzy - mu * sdz) * is;  // sum dz * xhat
+    dgamma[c] = (float)(sdzx * gscale) + (accumulate ? dgamma[c] : 0.f);
+    dbeta[c] = (float)(sdz * gscale) + (accumulate ? dbeta[c] : 0.f);
+    const double a = ga * is;
+    const double kk2 = -a * is * sdzx / count;
+    k1[c] = (float)a;
+    k2[c] = (float)kk2;
+    k3[c] = (float)(-a * sdz / count - kk2 * mu);
+  }
+}
+
+// dy = k1*dz + k2*y + k3 ; dz recomputed from (g, mask) exactly as in the reduce, or read (dz_in)
+template <int DT>
+__global__ __launch_bounds__(NT) void bn_bwd_apply_kernel(BwdArgs a, const u16* __restrict__ dz_in,
+                                                          const u16* __restrict__ ysel,
+                                                          const float* __restrict__ k1,
+                                                          const float* __restrict__ k2,
+                                                          const float* __restrict__ k3,
+                                                          u16* __restrict__ dy) {
+  const long long n8 = a.rows * (a.C / 8);
+  for (long long i = blockIdx.x * (long long)NT + threadIdx.x; i < n8; i += (long long)gridDim.x * NT) {
+    const long long row = i / (a.C / 8);
+    const int c0 = (int)(i - row * (a.C / 8)) * 8;
+    float dz[8], yv[8], y2v[8];
+    if (dz_in) {
+      unpack8<DT>(reinterpret_cast<const i32x4*>(dz_in)[i], dz);
+    } else {
+      make_dz<DT>(a, row, c0, dz, yv, y2v);
+    }
+    unpack8<DT>(reinterpret_cast<const i32x4*>(ysel)[i], yv);
+    float A[8], B[8], Cc[8], o[8];
+    ld8f(k1 + c0, A);
+    ld8f(k2 + c0, B);
+    ld8f(k3 + c0, Cc);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) o[e] = A[e] * dz[e] + B[e] * yv[e] + Cc[e];
+    reinterpret_cast<i32x4*>(dy)[i] = pack8<DT>(o);
+  }
+}
+
+inline int grid_for(long long n, int cap = 8192) {
+  long long b = (n + NT - 1) / NT;
+  return (int)(b < 1 ? 1 : (b > cap ? cap : b));
+}
+
+}  // namespace
+
+extern "C" {
+
+int pda_bn_finalize_fwd(const float* part, int T, int C, float count, const float* gamma,
+                        const float* beta, float eps, float momentum, float* mean, float* invstd,
+                        float* scale, float* shift, float* rmean, float* rvar, long long* nbt,
+                        int update_running, hipStream_t st) {
+  hipLaunchKernelGGL(bn_finalize_fwd_kernel, dim3((C + 15) / 16), dim3(1024), 0, st, part, T, C, count,
+                     gamma, beta, eps, momentum, mean, invstd, scale, shift, rmean, rvar, nbt,
+                     update_running);
+  return (int)hipGetLastError();
+}
+
+int pda_bn_eval_coeffs(const float* gamma, const float* beta, const float* rm, const float* rv,
+                       float eps, int C, float* scale, float* shift, hipStream_t st) {
+  hipLaunchKernelGGL(bn_eval_coeffs_kernel, dim3((C + 255) / 256), dim3(256), 0, st, gamma, beta, rm,
+                     rv, eps, C, scale, shift);
+  return (int)hipGetLastError();
+}
+
+int pda_bn_apply(const void* y, const float* sc, const float* sh, const void* r2, const float* sc2,
+                 const float* sh2, void* out, long long numel, int C, int mode, int relu, int dt,
+                 hipStream_t st) {
+  const long long n8 = numel / 8;
+  const int g = grid_for(n8);
+#define ARGS (const u16*)y, sc, sh, (const u16*)r2, sc2, sh2, (u16*)out, n8, C, mode, relu
+  if (dt == DT_BF16) hipLaunchKernelGGL(bn_apply_kernel<DT_BF16>, dim3(g), dim3(NT), 0, st, ARGS);
+  else hipLaunchKernelGGL(bn_apply_kernel<DT_F16>, dim3(g), dim3(NT), 0, st, ARGS);
+#undef ARGS
+  return (int)hipGetLastError();
+}
+
+int pda_stem_pool(const void* y, const float* sc, const float* sh, void* out, void* arg, int N,
+                  int H, int W, int C, int Ho, int Wo, int dt, hipStream_t st) {
+  const int g = grid_for((long long)N * Ho * Wo * (C / 8));
+#define ARGS (const u16*)y, sc, sh, (u16*)out, (uint8_t*)arg, N, H, W, C, Ho, Wo
+  if (dt == DT_BF16) hipLaunchKernelGGL(stem_pool_kernel<DT_BF16>, dim3(g), dim3(NT), 0, st, ARGS);
+  else hipLaunchKernelGGL(stem_pool_kernel<DT_F16>, dim3(g), dim3(NT), 0, st, ARGS);
+#undef ARGS
+  return (int)hipGetLastError();
+}
+
+int pda_maxpool_bwd(const void* dout, const void* dout2, const void* arg, void* din, int N, int H,
+                    int W, int C, int Ho, int Wo, int dt, hipStream_t st) {
+  const int g = grid_for((long long)N * H * W * (C / 8));
+#define ARGS (const u16*)dout, (const u16*)dout2, (const uint8_t*)arg, (u16*)din, N, H, W, C, Ho, Wo
+  if (dt == DT_BF16) hipLaunchKernelGGL(maxpool_bwd_kernel<DT_BF16>, dim3(g), dim3(NT), 0, st, ARGS);
+  else hipLaunchKernelGGL(maxpool_bwd_kernel<DT_F16>, dim3(g), dim3(NT), 0, st, ARGS);
+#undef ARGS
+  return (int)hipGetLastError();
+}
+
+int pda_tail_pool(const void* y, const float* sc, const float* sh, const void* r2, const float* sc2,
+                  const float* sh2, void* out, int N, int HW, int C, int mode, int dt,
+                  hipStream_t st) {
+#define ARGS (const u16*)y, sc, sh, (const u16*)r2, sc2, sh2, (u16*)out, HW, C, mode
+  if (dt == DT_BF16) hipLaunchKernelGGL(tail_pool_kernel<DT_BF16>, dim3(N), dim3(NT), 0, st, ARGS);
+  else hipLaunchKernelGGL(tail_pool_kernel<DT_F16>, dim3(N), dim3(NT), 0, st, ARGS);
+#undef ARGS
+  return (int)hipGetLastError();
+}
+
+struct BwdArgsC {  // mirrors ops/ext.py
+  const void* g1; const void* g2; const void* gp; int HW;
+  const void* y; const float* sc; const float* sh;
+  const void* y2; const float* sc2; const float* sh2;
+  int mode; void* dz_out;
+  float* part; int nq; long long rows; int C;
+};
+
+static BwdArgs to_args(const BwdArgsC* c) {
+  BwdArgs a;
+  a.g1 = (const u16*)c->g1; a.g2 = (const u16*)c->g2; a.gp = (const u16*)c->gp; a.HW = c->HW;
+  a.y = (const u16*)c->y; a.sc = c->sc; a.sh = c->sh;
+  a.y2 = (const u16*)c->y2; a.sc2 = c->sc2; a.sh2 = c->sh2;
+  a.mode = c->mode; a.dz_out = (u16*)c->dz_out;
+  a.part = c->part; a.nq = c->nq; a.rows = c->rows; a.C = c->C; a.rows_per_block = 0;
+  return a;
+}
+
+// G = number of partial slabs written (returned through *G_out); part must hold G*nq*C floats.
+int pda_bn_bwd_reduce(const BwdArgsC* c, int G, int dt, hipStream_t st) {
+  BwdArgs a = to_args(c);
+  a.rows_per_block = (a.rows + G - 1) / G;
+#define K(D) hipLaunchKernelGGL(bn_bwd_reduce_kernel<D>, dim3(G), dim3(NT), 0, st, a)
+  if (dt == DT_BF16) K(DT_BF16); else K(DT_F16);
+#undef K
+  return (int)hipGetLastError();
+}
+
+int pda_bn_bwd_finalize(const float* part, int G, int nq, int qy, int C, float count,
+                        const float* gamma, const float* mean, const float* invstd, float* dgamma,
+                        float* dbeta, float* k1, float* k2, float* k3, float gscale, int accumulate,
+                        hipStream_t st) {
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 15) / 16), dim3(1024), 0, st, part, G, nq, qy,
+                     C, count, gamma, mean, invstd, dgamma, dbeta, k1, k2, k3, gscale, accumulate);
+  return (int)hipGetLastError();
+}
+
+int pda_bn_bwd_apply(const BwdArgsC* c, const void* dz_in, const void* ysel, const float* k1,
+                     const float* k2, const float* k3, void* dy, int dt, hipStream_t st) {
+  BwdArgs a = to_args(c);
+  const int g = grid_for(a.rows * (a.C / 8));
+#define K(D) hipLaunchKernelGGL(bn_bwd_apply_kernel<D>, dim3(g), dim3(NT), 0, st, a, (const u16*)dz_in, \
+                                (const u16*)ysel, k1, k2, k3, (u16*)dy)
+  if (dt == DT_BF16) K(DT_BF16); else K(DT_F16);
+#undef K
+  return (int)hipGetLastError();
+}
+
+}  // extern "C"

@@ -1,0 +1,74 @@
+// Shared device helpers for the gfx950 (CDNA4, MI355X) kernels of pytorch_distributed_amd.
+// Wave64 everywhere; 16-bit element types are moved as raw shorts and bit-cast at the MFMA.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+typedef short s16x8 __attribute__((ext_vector_type(8)));
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef int i32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned short u16;
+
+#define LDS_PTR(T, p) ((__attribute__((address_space(3))) T*)(p))
+
+// dtype tags shared with the Python side (ops/ext.py)
+enum DType : int { DT_F32 = 0, DT_BF16 = 1, DT_F16 = 2 };
+
+// ---- 16-bit <-> f32 conversions -------------------------------------------------------------
+__device__ __forceinline__ float bf16_to_f32(u16 v) { return __uint_as_float(((uint32_t)v) << 16); }
+__device__ __forceinline__ u16 f32_to_bf16(float f) {
+  __bf16 b = (__bf16)f;  // v_cvt_pk_bf16_f32: RNE, NaN stays NaN
+  return __builtin_bit_cast(u16, b);
+}
+__device__ __forceinline__ float f16_to_f32(u16 v) { return (float)__builtin_bit_cast(_Float16, v); }
+__device__ __forceinline__ u16 f32_to_f16(float f) { return __builtin_bit_cast(u16, (_Float16)f); }
+
+template <int DT> __device__ __forceinline__ float ld16(u16 v);
+template <> __device__ __forceinline__ float ld16<DT_BF16>(u16 v) { return bf16_to_f32(v); }
+template <> __device__ __forceinline__ float ld16<DT_F16>(u16 v) { return f16_to_f32(v); }
+template <int DT> __device__ __forceinline__ u16 st16(float f);
+template <> __device__ __forceinline__ u16 st16<DT_BF16>(float f) { return f32_to_bf16(f); }
+template <> __device__ __forceinline__ u16 st16<DT_F16>(float f) { return f32_to_f16(f); }
+
+// ---- MFMA 16x16x32 (bf16 / f16 inputs, f32 accumulate) --------------------------------------
+template <int DT> __device__ __forceinline__ f32x4 mfma16(s16x8 a, s16x8 b, f32x4 c);
+template <> __device__ __forceinline__ f32x4 mfma16<DT_BF16>(s16x8 a, s16x8 b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a),
+                                                 __builtin_bit_cast(bf16x8, b), c, 0, 0, 0);
+}
+template <> __device__ __forceinline__ f32x4 mfma16<DT_F16>(s16x8 a, s16x8 b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, a),
+                                                __builtin_bit_cast(f16x8, b), c, 0, 0, 0);
+}
+
+// ---- fast unsigned division by a runtime constant (n < 2^31) --------------------------------
+struct FastDiv {
+  uint32_t d, m, s;
+};
+__device__ __forceinline__ uint32_t fdiv(uint32_t n, const FastDiv& f) {
+  return (__umulhi(n, f.m) + n) >> f.s;
+}
+
+// ---- wave / block reductions ---------------------------------------------------------------
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// XCD-aware bijective remap of a 1-D block index: consecutive *logical* tiles land on the same
+// XCD (blocks b and b+8 share an XCD under round-robin dispatch), so neighbouring tiles that share
+// an operand panel hit the same L2. Speed only -- never correctness (cdna_hip_programming.md T1).
+__device__ __forceinline__ uint32_t xcd_remap(uint32_t bid, uint32_t nwg) {
+  const uint32_t q = nwg >> 3, r = nwg & 7, x = bid & 7;
+  const uint32_t base = x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q;
+  return base + (bid >> 3);
+}

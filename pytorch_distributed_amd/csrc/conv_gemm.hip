@@ -1,0 +1,578 @@
+// Implicit-GEMM convolution for gfx950 (MI355X): forward, data-gradient and weight-gradient,
+// NHWC activations, OHWI ("KRSC") weights, bf16/f16 inputs, MFMA 16x16x32 with f32 accumulation.
+//
+// Replaces cuDNN conv fwd/dgrad/wgrad of the reference stack: every
+// Conv2d of ResNet (all 23 ResNet-50 shapes + the 7x7 stem) and the fc layer (as a 1x1 conv on a
+// 1x1 image) go through this one kernel template:
+//
+//   FWD   : Y[m][n]      = sum_k A[m][k] * B[n][k]     A = im2col(X) gathered per 16-B chunk,
+//                                                       B = W[Cout][R*S*Cin] (K contiguous)
+//   DGRAD : dX[m][n]     = sum_k A[m][k] * B[k][n]     A = gathered dY, B = W rows (Cin contiguous)
+//           stride-2 layers run as 4 parity classes (blockIdx.y) so no MFMA multiplies a
+//           structural zero; each class only visits the taps that land on its pixels.
+//   WGRAD : dW[n1][n2]   = sum_m A[m][n1] * B[m][n2]   A = dY, B = gathered X; split-K over m
+//           (blockIdx.y) into f32 slabs, reduced deterministically by conv_wgrad_reduce.
+//
+// Operand tiles are staged global->VGPR->LDS (register staging: zero-fill for padding taps and
+// ragged M; loads for tile t+1 are issued before the MFMAs of tile t). Two LDS tile layouts:
+//   ROW  [rows][64 k] (128-B rows, 16-B chunks XOR-swizzled by row&7), fragments by ds_read_b128;
+//   COL  [64 k][cols] (k-major), fragments by ds_read_b64_tr_b16 (hardware transpose read) with a
+//        chunk swizzle that makes both the b128 writes and the transposed reads conflict-free.
+// Block = 256 threads = 4 waves (2x2), block tile BM x BN x 64, wave tile (BM/2) x (BN/2).
+// Forward epilogue stages the tile through LDS for 16-B coalesced stores and emits per-channel
+// partial sum / sum-of-squares (BatchNorm statistics) per M-tile -- no extra pass over Y.
+#include "common.h"
+
+namespace {
+
+constexpr int BK = 64;
+constexpr int NT = 256;
+
+enum Pass : int { FWD = 0, DGRAD = 1, WGRAD = 2 };
+
+struct ConvParams {
+  const void* a;      // FWD: X [Nb,H,W,Cin]; DGRAD: dY [Nb,Ho,Wo,Cout]; WGRAD: dY
+  const void* b;      // FWD: W [N][Kpad]; DGRAD: W [Cout][R][S][Cin]; WGRAD: X [Nb,H,W,Cin]
+  void* out;          // FWD/DGRAD: [M][N] 16-bit (or f32 if out_f32); WGRAD: f32 slab [split][M][N]
+  float* stats;       // FWD: [mtiles][2][N] partial sum / sumsq (nullable)
+  const float* bias;  // FWD: [N] (nullable)
+  int M, N, K;        // GEMM sizes (WGRAD: K = total rows, split by k_split)
+  int Kpad;           // FWD: B row pitch
+  int Nb, H, W, Cin;  // input X geometry
+  int Ho, Wo, Cout;   // output Y geometry
+  int R, S, stride, pad;
+  int log2Cin;        // channels of the gathered tensor are a power of two (3 is padded to 8)
+  int out_f32;
+  int relu;           // FWD epilogue relu (fc: 0)
+  int k_chunk;        // WGRAD: rows per split
+  int out_pitch;      // FWD/DGRAD: output row pitch (elements)
+  FastDiv dHoWo, dWo, dS;   // m -> (img, y, x) decode of the *GEMM row* space; tap -> (r, s)
+  int ntaps[4];       // DGRAD: taps per parity class
+  int taps[4][9];     // DGRAD: tap ids (r*S+s) per parity class
+  int Hc, Wc;         // DGRAD: class grid (H/stride, W/stride)
+  FastDiv dHcWc, dWc;
+};
+
+// ---------------------------------------------------------------- LDS addressing
+// ROW tile: BR rows x 64 k (128 B per row).
+__device__ __forceinline__ int row_addr(int row, int chunk) {
+  return row * 128 + ((chunk ^ (row & 7)) << 4);
+}
+// COL tile: 64 k-rows x BC cols.
+template <int BC>
+__device__ __forceinline__ int col_swz(int krow) {
+  if constexpr (BC == 128) return ((krow & 3) << 1) | (((krow >> 3) & 1) << 3);
+  else return (((krow >> 1) & 1) << 1) | (((krow >> 3) & 1) << 2);
+}
+template <int BC>
+__device__ __forceinline__ int col_addr(int krow, int chunk) {
+  return krow * (BC * 2) + ((chunk ^ col_swz<BC>(krow)) << 4);
+}
+
+// fragment loads -------------------------------------------------------------------
+// ROW tile, operand rows [rb, rb+16), k-step s (32 k): lane holds row rb+(l&15), k 8*(l>>4)..+7
+__device__ __forceinline__ s16x8 frag_row(const char* lds, int rb, int s, int lane) {
+  const int row = rb + (lane & 15);
+  const int chunk = s * 4 + (lane >> 4);
+  return *reinterpret_cast<const s16x8*>(lds + row_addr(row, chunk));
+}
+// COL tile, operand cols [cb, cb+16), k-step s: lane holds col cb+(l&15), k 8*(l>>4)..+7
+template <int BC>
+__device__ __forceinline__ s16x8 frag_col(const char* lds, int cb, int s, int lane) {
+  const int g = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3;
+  const int chunk = (cb >> 3) + (p >> 1);
+  const int k0 = s * 32 + 8 * g + q;
+  const int a0 = col_addr<BC>(k0, chunk) + ((p & 1) << 3);
+  const int a1 = col_addr<BC>(k0 + 4, chunk) + ((p & 1) << 3);
+  s16x4 v0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(s16x4, lds + a0));
+  s16x4 v1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(s16x4, lds + a1));
+  s16x8 r;
+  r[0] = v0[0]; r[1] = v0[1]; r[2] = v0[2]; r[3] = v0[3];
+  r[4] = v1[0]; r[5] = v1[1]; r[6] = v1[2]; r[7] = v1[3];
+  return r;
+}
+
+__device__ __forceinline__ i32x4 ld16B(const void* p, bool ok) {
+  i32x4 z = {0, 0, 0, 0};
+  return ok ? *reinterpret_cast<const i32x4*>(p) : z;
+}
+
+// ================================================================= kernel
+template <int PASS, int DT, int BM, int BN>
+__global__ __launch_bounds__(NT, 2) void conv_gemm_kernel(ConvParams p) {
+  // A tile: FWD/DGRAD ROW [BM][64]; WGRAD COL [64][BM]. B tile: FWD ROW [BN][64]; else COL [64][BN]
+  constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2;
+  constexpr int STAGE = A_BYTES + B_BYTES;
+  constexpr int LDS_BYTES = 2 * STAGE;
+  static_assert(BM * BN * 2 <= LDS_BYTES, "C tile must fit in the staging buffers");
+  static_assert(2 * NT * 8 * 4 <= LDS_BYTES, "stats reduction must fit");
+  __shared__ __attribute__((aligned(16))) char smem[LDS_BYTES];
+
+  constexpr bool A_ROW = (PASS != WGRAD);
+  constexpr bool B_ROW = (PASS == FWD);
+  constexpr int AR = BM / 32, BR = BN / 32;  // 16-B chunks per thread per tile
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wr = wid >> 1, wc = wid & 1;
+  const int tiles_n = (p.N + BN - 1) / BN;
+  const int tiles_m = (p.M + BM - 1) / BM;
+  const int ntile = tiles_m * tiles_n;
+  const int t = (int)xcd_remap(blockIdx.x, ntile);
+  const int tm = t / tiles_n, tn = t - tm * tiles_n;
+  const int m0 = tm * BM, n0 = tn * BN;
+  const int split = blockIdx.y;  // WGRAD: K split; DGRAD: parity class
+
+  // ---- K range --------------------------------------------------------------------
+  int kbeg = 0, kend = p.K;
+  int cls_ph = 0, cls_pw = 0, ntap = 0;
+  if constexpr (PASS == WGRAD) {
+    kbeg = split * p.k_chunk;
+    kend = min(p.K, kbeg + p.k_chunk);
+  } else if constexpr (PASS == DGRAD) {
+    cls_ph = split >> 1;
+    cls_pw = split & 1;
+    ntap = p.ntaps[split];
+    kend = ntap * p.Cout;
+  }
+  const int nk = (kend - kbeg + BK - 1) / BK;
+
+  // ---- per-thread loader precompute -------------------------------------------------
+  // A (ROW: FWD gather from X, DGRAD gather from dY): rows tid/8 + 32*i, chunk tid&7
+  int a_img[AR], a_y[AR], a_x[AR];
+  bool a_ok[AR];
+  if constexpr (A_ROW) {
+#pragma unroll
+    for (int i = 0; i < AR; ++i) {
+      const int m = m0 + (tid >> 3) + 32 * i;
+      a_ok[i] = m < p.M;
+      const uint32_t mm = a_ok[i] ? m : 0;
+      if constexpr (PASS == FWD) {
+        const uint32_t img = fdiv(mm, p.dHoWo), rem = mm - img * p.dHoWo.d;
+        const uint32_t yo = fdiv(rem, p.dWo), xo = rem - yo * p.dWo.d;
+        a_img[i] = img;
+        a_y[i] = (int)yo * p.stride - p.pad;
+        a_x[i] = (int)xo * p.stride - p.pad;
+      } else {  // DGRAD: class-grid pixel -> dX pixel (h, w)
+        const uint32_t img = fdiv(mm, p.dHcWc), rem = mm - img * p.dHcWc.d;
+        const uint32_t yi = fdiv(rem, p.dWc), xi = rem - yi * p.dWc.d;
+        a_img[i] = img;
+        a_y[i] = (int)yi * p.stride + cls_ph + p.pad;  // h + pad
+        a_x[i] = (int)xi * p.stride + cls_pw + p.pad;
+      }
+    }
+  }
+  // WGRAD B gather: fixed column chunk per thread -> (tap, c)
+  int wb_r = 0, wb_s = 0, wb_c = 0;
+  bool wb_colok = true;
+  if constexpr (PASS == WGRAD) {
+    constexpr int CPR = BN / 8;
+    const int col = n0 + (tid % CPR) * 8;
+    wb_colok = col < p.N;
+    const int tap = col >> p.log2Cin;
+    wb_c = col & ((1 << p.log2Cin) - 1);
+    wb_r = (int)fdiv(tap, p.dS);
+    wb_s = tap - wb_r * p.S;
+    wb_colok = wb_colok && (tap < p.R * p.S);
+  }
+
+  const u16* __restrict__ A = reinterpret_cast<const u16*>(p.a);
+  const u16* __restrict__ B = reinterpret_cast<const u16*>(p.b);
+
+  i32x4 ra[AR], rb[BR];
+
+  auto load_tile = [&](int kt) {
+    const int k0 = kbeg + kt * BK;
+    // ---------------- A
+    if constexpr (PASS == FWD) {
+      const int k = k0 + (tid & 7) * 8;
+      const int tap = k >> p.log2Cin;
+      const int c = k & ((1 << p.log2Cin) - 1);
+      const int r = (int)fdiv(tap, p.dS), s = tap - r * p.S;
+      const bool tap_ok = tap < p.R * p.S;
+#pragma unroll
+      for (int i = 0; i < AR; ++i) {
+        const int y = a_y[i] + r, x = a_x[i] + s;
+        const bool ok = a_ok[i] && tap_ok && (unsigned)y < (unsigned)p.H && (unsigned)x < (unsigned)p.W;
+        const size_t off = ((size_t)(a_img[i] * p.H + y) * p.W + x) * p.Cin + c;
+        ra[i] = ld16B(A + (ok ? off : 0), ok);
+      }
+    } else if constexpr (PASS == DGRAD) {
+      const int ti = k0 / p.Cout;  // tile lies in one tap (Cout % 64 == 0)
+      const int c = k0 - ti * p.Cout + (tid & 7) * 8;
+      const int tap = p.taps[split][ti < 9 ? ti : 0];
+      const int r = (int)fdiv(tap, p.dS), s = tap - r * p.S;
+#pragma unroll
+      for (int i = 0; i < AR; ++i) {
+        int yy = a_y[i] - r, xx = a_x[i] - s;  // (h + pad - r), divisible by stride
+        bool ok = a_ok[i] && yy >= 0 && xx >= 0;
+        yy = p.stride == 2 ? (yy >> 1) : yy;
+        xx = p.stride == 2 ? (xx >> 1) : xx;
+        ok = ok && yy < p.Ho && xx < p.Wo;
+        const size_t off = ((size_t)(a_img[i] * p.Ho + yy) * p.Wo + xx) * p.Cout + c;
+        ra[i] = ld16B(A + (ok ? off : 0), ok);
+      }
+    } else {  // WGRAD A: dY rows m (k), cols n1 (COL tile [64][BM])
+      constexpr int CPR = BM / 8, RPI = NT / CPR;
+      const int col = m0 + (tid % CPR) * 8;
+#pragma unroll
+      for (int i = 0; i < AR; ++i) {
+        const int krow = tid / CPR + RPI * i;
+        const int m = k0 + krow;
+        const bool ok = m < kend && col < p.M;
+        ra[i] = ld16B(A + (ok ? (size_t)m * p.Cout + col : 0), ok);
+      }
+    }
+    // ---------------- B
+    if constexpr (PASS == FWD) {
+      const int k = k0 + (tid & 7) * 8;
+#pragma unroll
+      for (int i = 0; i < BR; ++i) {
+        const int n = n0 + (tid >> 3) + 32 * i;
+        const bool ok = n < p.N && k < p.Kpad;
+        rb[i] = ld16B(B + (ok ? (size_t)n * p.Kpad + k : 0), ok);
+      }
+    } else if constexpr (PASS == DGRAD) {
+      constexpr int CPR = BN / 8, RPI = NT / CPR;
+      const int ti = k0 / p.Cout;
+      const int tap = p.taps[split][ti < 9 ? ti : 0];
+      const int col = n0 + (tid % CPR) * 8;
+#pragma unroll
+      for (int i = 0; i < BR; ++i) {
+        const int krow = tid / CPR + RPI * i;
+        const int co = k0 - ti * p.Cout + krow;
+        const bool ok = col < p.N;
+        const size_t off = ((size_t)co * (p.R * p.S) + tap) * p.Cin + col;
+        rb[i] = ld16B(B + (ok ? off : 0), ok);
+      }
+    } else {  // WGRAD B: gathered X rows m, cols (tap, c)
+      constexpr int CPR = BN / 8, RPI = NT / CPR;
+#pragma unroll
+      for (int i = 0; i < BR; ++i) {
+        const int krow = tid / CPR + RPI * i;
+        const int m = k0 + krow;
+        bool ok = wb_colok && m < kend;
+        const uint32_t mm = ok ? m : 0;
+        const uint32_t img = fdiv(mm, p.dHoWo), rem = mm - img * p.dHoWo.d;
+        const uint32_t yo = fdiv(rem, p.dWo), xo = rem - yo * p.dWo.d;
+        const int y = (int)yo * p.stride - p.pad + wb_r, x = (int)xo * p.stride - p.pad + wb_s;
+        ok = ok && (unsigned)y < (unsigned)p.H && (unsigned)x < (unsigned)p.W;
+        const size_t off = ((size_t)(img * p.H + y) * p.W + x) * p.Cin + wb_c;
+        rb[i] = ld16B(B + (ok ? off : 0), ok);
+      }
+    }
+  };
+
+  auto store_tile = [&](int buf) {
+    char* sa = smem + buf * STAGE;
+    char* sb = sa + A_BYTES;
+    if constexpr (A_ROW) {
+#pragma unroll
+      for (int i = 0; i < AR; ++i)
+        *reinterpret_cast<i32x4*>(sa + row_addr((tid >> 3) + 32 * i, tid & 7)) = ra[i];
+    } else {
+      constexpr int CPR = BM / 8, RPI = NT / CPR;
+#pragma unroll
+      for (int i = 0; i < AR; ++i)
+        *reinterpret_cast<i32x4*>(sa + col_addr<BM>(tid / CPR + RPI * i, tid % CPR)) = ra[i];
+    }
+    if constexpr (B_ROW) {
+#pragma unroll
+      for (int i = 0; i < BR; ++i)
+        *reinterpret_cast<i32x4*>(sb + row_addr((tid >> 3) + 32 * i, tid & 7)) = rb[i];
+    } else {
+      constexpr int CPR = BN / 8, RPI = NT / CPR;
+#pragma unroll
+      for (int i = 0; i < BR; ++i)
+        *reinterpret_cast<i32x4*>(sb + col_addr<BN>(tid / CPR + RPI * i, tid % CPR)) = rb[i];
+    }
+  };
+
+  constexpr int MI = BM / 32, NI = BN / 32;
+  f32x4 acc[MI][NI];
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < NI; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  if (nk > 0) {
+    load_tile(0);
+    store_tile(0);
+    __syncthreads();
+  }
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1;
+    if (kt + 1 < nk) load_tile(kt + 1);
+    const char* sa = smem + cur * STAGE;
+    const char* sb = sa + A_BYTES;
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      s16x8 fa[MI], fb[NI];
+#pragma unroll
+      for (int i = 0; i < MI; ++i) {
+        const int rbase = wr * (BM / 2) + i * 16;
+        if constexpr (A_ROW) fa[i] = frag_row(sa, rbase, s, lane);
+        else fa[i] = frag_col<BM>(sa, rbase, s, lane);
+      }
+#pragma unroll
+      for (int j = 0; j < NI; ++j) {
+        const int cbase = wc * (BN / 2) + j * 16;
+        if constexpr (B_ROW) fb[j] = frag_row(sb, cbase, s, lane);
+        else fb[j] = frag_col<BN>(sb, cbase, s, lane);
+      }
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int j = 0; j < NI; ++j) acc[i][j] = mfma16<DT>(fa[i], fb[j], acc[i][j]);
+    }
+    if (kt + 1 < nk) store_tile(cur ^ 1);
+    __syncthreads();
+  }
+
+  // ================================================================ epilogue
+  if constexpr (PASS == WGRAD) {
+    float* slab = reinterpret_cast<float*>(p.out) + (size_t)split * p.M * p.N;
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+      for (int j = 0; j < NI; ++j) {
+        const int col = n0 + wc * (BN / 2) + j * 16 + (lane & 15);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int row = m0 + wr * (BM / 2) + i * 16 + 4 * (lane >> 4) + e;
+          if (row < p.M && col < p.N) slab[(size_t)row * p.N + col] = acc[i][j][e];
+        }
+      }
+    return;
+  } else {
+    if (p.out_f32) {  // fc logits: f32 + bias, direct stores
+      float* out = reinterpret_cast<float*>(p.out);
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int j = 0; j < NI; ++j) {
+          const int col = n0 + wc * (BN / 2) + j * 16 + (lane & 15);
+          const float bv = (p.bias && col < p.N) ? p.bias[col] : 0.f;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const int row = m0 + wr * (BM / 2) + i * 16 + 4 * (lane >> 4) + e;
+            if (row < p.M && col < p.N) out[(size_t)row * p.out_pitch + col] = acc[i][j][e] + bv;
+          }
+        }
+      return;
+    }
+    // stage the 16-bit C tile through LDS: [BM][BN], row pitch BN*2 bytes, 16-B chunks swizzled
+    u16* ct = reinterpret_cast<u16*>(smem);
+    constexpr int CPR = BN / 8;
+    auto c_addr = [&](int row, int chunk) { return row * CPR + (chunk ^ (row & (CPR - 1))); };
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+      for (int j = 0; j < NI; ++j) {
+        const int col = wc * (BN / 2) + j * 16 + (lane & 15);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int row = wr * (BM / 2) + i * 16 + 4 * (lane >> 4) + e;
+          float v = acc[i][j][e];
+          if (p.relu) v = fmaxf(v, 0.f);
+          ct[c_addr(row, col >> 3) * 8 + (col & 7)] = st16<DT>(v);
+        }
+      }
+    __syncthreads();
+    // coalesced 16-B stores + per-channel partial statistics
+    const int cc = tid % CPR;          // column chunk
+    const int rg = tid / CPR;          // row group
+    constexpr int RG = NT / CPR;       // row groups
+    float s1[8], s2[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) { s1[e] = 0.f; s2[e] = 0.f; }
+    u16* out = reinterpret_cast<u16*>(p.out);
+    const int gcol = n0 + cc * 8;
+#pragma unroll
+    for (int i = 0; i < BM / RG; ++i) {
+      const int row = rg + RG * i;
+      const int grow = m0 + row;
+      i32x4 v = *reinterpret_cast<const i32x4*>(ct + c_addr(row, cc) * 8);
+      if (grow < p.M && gcol < p.N) {
+        size_t orow;
+        if constexpr (PASS == DGRAD) {
+          const uint32_t img = fdiv(grow, p.dHcWc), rem = grow - img * p.dHcWc.d;
+          const uint32_t yi = fdiv(rem, p.dWc), xi = rem - yi * p.dWc.d;
+          const int h = (int)yi * p.stride + cls_ph, w = (int)xi * p.stride + cls_pw;
+          orow = ((size_t)img * p.H + h) * p.W + w;
+        } else {
+          orow = grow;
+        }
+        *reinterpret_cast<i32x4*>(out + orow * p.out_pitch + gcol) = v;
+        if (PASS == FWD && p.stats) {
+          const u16* h = reinterpret_cast<const u16*>(&v);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            const float f = ld16<DT>(h[e]);
+            s1[e] += f;
+            s2[e] += f * f;
+          }
+        }
+      }
+    }
+    if (PASS == FWD && p.stats) {
+      __syncthreads();
+      float* red = reinterpret_cast<float*>(smem);  // [RG][BN] x 2
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        red[rg * BN + cc * 8 + e] = s1[e];
+        red[RG * BN + rg * BN + cc * 8 + e] = s2[e];
+      }
+      __syncthreads();
+      if (tid < BN) {
+        float a = 0.f, b = 0.f;
+#pragma unroll
+        for (int g = 0; g < RG; ++g) {
+          a += red[g * BN + tid];
+          b += red[RG * BN + g * BN + tid];
+        }
+        const int col = n0 + tid;
+        if (col < p.N) {
+          p.stats[(size_t)tm * 2 * p.N + col] = a;
+          p.stats[(size_t)tm * 2 * p.N + p.N + col] = b;
+        }
+      }
+    }
+  }
+}
+
+// split-K slab reduction for WGRAD, with layout remap + scale, into the f32 gradient buffer:
+// grad[n1 * dst_pitch + (n2 / cin_pad) * cin_real + n2 % cin_pad] = scale * sum_s slab[s][n1][n2]
+// for n2 % cin_pad < cin_real (stem: Cin padded 3 -> 8).
+__global__ void wgrad_reduce_kernel(const float* __restrict__ slab, float* __restrict__ grad,
+                                    int splits, int M, int N, int cin_pad_log2, int cin_real,
+                                    int dst_pitch, float scale, int accumulate) {
+  const int total = M * N;
+  for (int idx = blockIdx.x * blockDim.x + threadIdx.x; idx < total; idx += gridDim.x * blockDim.x) {
+    float s = 0.f;
+    for (int k = 0; k < splits; ++k) s += slab[(size_t)k * total + idx];
+    const int n1 = idx / N, n2 = idx - n1 * N;
+    const int tap = n2 >> cin_pad_log2, c = n2 & ((1 << cin_pad_log2) - 1);
+    if (c < cin_real) {
+      float* d = grad + (size_t)n1 * dst_pitch + tap * cin_real + c;
+      *d = accumulate ? *d + scale * s : scale * s;
+    }
+  }
+}
+
+}  // namespace
+
+// ================================================================= host launchers (C ABI)
+static FastDiv make_div(uint32_t d) {
+  FastDiv f;
+  f.d = d;
+  uint32_t s = 0;
+  while ((1ull << s) < d) ++s;
+  f.s = s;
+  f.m = (uint32_t)(((1ull << 32) * ((1ull << s) - d)) / d + 1);
+  return f;
+}
+
+struct ConvDesc {  // mirrors pytorch_distributed_amd/ops/ext.py ConvDesc
+  int Nb, H, W, Cin, Cout, R, S, stride, pad, Ho, Wo;
+};
+
+template <int PASS, int DT, int BM, int BN>
+static int launch(const ConvParams& p, dim3 grid, hipStream_t st) {
+  hipLaunchKernelGGL((conv_gemm_kernel<PASS, DT, BM, BN>), grid, dim3(NT), 0, st, p);
+  return (int)hipGetLastError();
+}
+
+template <int PASS>
+static int dispatch(int dt, int bm, int bn, const ConvParams& p, dim3 grid, hipStream_t st) {
+#define PDA_CASE(D, M_, N_)                                                    \
+  if (dt == D && bm == M_ && bn == N_) return launch<PASS, D, M_, N_>(p, grid, st);
+  PDA_CASE(DT_BF16, 128, 128) PDA_CASE(DT_BF16, 128, 64) PDA_CASE(DT_BF16, 64, 128)
+  PDA_CASE(DT_BF16, 64, 64)
+  PDA_CASE(DT_F16, 128, 128) PDA_CASE(DT_F16, 128, 64) PDA_CASE(DT_F16, 64, 128)
+  PDA_CASE(DT_F16, 64, 64)
+#undef PDA_CASE
+  return -1;
+}
+
+static void fill_geom(ConvParams& p, const ConvDesc& d) {
+  p.Nb = d.Nb; p.H = d.H; p.W = d.W; p.Cin = d.Cin; p.Cout = d.Cout;
+  p.R = d.R; p.S = d.S; p.stride = d.stride; p.pad = d.pad; p.Ho = d.Ho; p.Wo = d.Wo;
+  int l = 0;
+  while ((1 << l) < d.Cin) ++l;
+  p.log2Cin = l;
+  p.dHoWo = make_div(d.Ho * d.Wo);
+  p.dWo = make_div(d.Wo);
+  p.dS = make_div(d.S);
+}
+
+extern "C" {
+
+// Y[M=Nb*Ho*Wo][Cout] = conv(X, W). W: [Cout][Kpad] 16-bit. stats: [ceil(M/bm)][2][Cout] or null.
+int pda_conv_fwd(const ConvDesc* d, const void* x, const void* w, int Kpad, void* y, int out_f32,
+                 int out_pitch, const float* bias, float* stats, int relu, int dt, int bm, int bn,
+                 hipStream_t st) {
+  ConvParams p{};
+  fill_geom(p, *d);
+  p.a = x; p.b = w; p.out = y; p.stats = stats; p.bias = bias;
+  p.M = d->Nb * d->Ho * d->Wo; p.N = d->Cout; p.Kpad = Kpad; p.K = Kpad;
+  p.out_f32 = out_f32; p.relu = relu; p.out_pitch = out_pitch > 0 ? out_pitch : d->Cout;
+  const int tiles = ((p.M + bm - 1) / bm) * ((p.N + bn - 1) / bn);
+  return dispatch<FWD>(dt, bm, bn, p, dim3(tiles, 1), st);
+}
+
+// dX[Nb,H,W,Cin] = conv_transpose(dY, W). Every dX element is written (zeros where no tap lands).
+int pda_conv_dgrad(const ConvDesc* d, const void* dy, const void* w, void* dx, int dt, int bm,
+                   int bn, hipStream_t st) {
+  ConvParams p{};
+  fill_geom(p, *d);
+  p.a = dy; p.b = w; p.out = dx;
+  p.N = d->Cin; p.out_pitch = d->Cin;
+  const int sd = d->stride;
+  if (sd != 1 && sd != 2) return -2;
+  if ((d->H % sd) || (d->W % sd) || (d->Cout % 64)) return -3;
+  p.Hc = d->H / sd; p.Wc = d->W / sd;
+  p.dHcWc = make_div(p.Hc * p.Wc);
+  p.dWc = make_div(p.Wc);
+  p.M = d->Nb * p.Hc * p.Wc;
+  const int ncls = sd * sd;
+  for (int c = 0; c < 4; ++c) {
+    p.ntaps[c] = 0;
+    if (c >= ncls) continue;
+    const int ph = (sd == 2) ? (c >> 1) : 0, pw = (sd == 2) ? (c & 1) : 0;
+    for (int r = 0; r < d->R; ++r) {
+      if (((ph + d->pad - r) % sd + sd) % sd) continue;
+      for (int s = 0; s < d->S; ++s) {
+        if (((pw + d->pad - s) % sd + sd) % sd) continue;
+        if (p.ntaps[c] < 9) p.taps[c][p.ntaps[c]++] = r * d->S + s;
+      }
+    }
+  }
+  p.K = 0;
+  const int tiles = ((p.M + bm - 1) / bm) * ((p.N + bn - 1) / bn);
+  return dispatch<DGRAD>(dt, bm, bn, p, dim3(tiles, ncls), st);
+}
+
+// slab[splits][Cout][R*S*Cin] partial weight gradients (f32). k_chunk must be a multiple of 64.
+int pda_conv_wgrad(const ConvDesc* d, const void* dy, const void* x, float* slab, int splits,
+                   int k_chunk, int dt, int bm, int bn, hipStream_t st) {
+  ConvParams p{};
+  fill_geom(p, *d);
+  p.a = dy; p.b = x; p.out = slab;
+  p.M = d->Cout; p.N = d->R * d->S * d->Cin;
+  p.K = d->Nb * d->Ho * d->Wo;
+  p.k_chunk = k_chunk;
+  const int tiles = ((p.M + bm - 1) / bm) * ((p.N + bn - 1) / bn);
+  return dispatch<WGRAD>(dt, bm, bn, p, dim3(tiles, splits), st);
+}
+
+int pda_wgrad_reduce(const float* slab, float* grad, int splits, int M, int N, int cin_pad_log2,
+                     int cin_real, int dst_pitch, float scale, int accumulate, hipStream_t st) {
+  const int total = M * N;
+  int blocks = (total + 255) / 256;
+  if (blocks > 4096) blocks = 4096;
+  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(blocks), dim3(256), 0, st, slab, grad, splits, M, N,
+                     cin_pad_log2, cin_real, dst_pitch, scale, accumulate);
+  return (int)hipGetLastError();
+}
+
+}  // extern "C"

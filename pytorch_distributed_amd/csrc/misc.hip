@@ -1,0 +1,341 @@
+// Loss, optimizer, AMP and data kernels for gfx950.
+//
+//   xent_fwd_bwd   : log-softmax + NLL (mean) forward AND its gradient in one pass, one wave per row
+//                    of the [B, classes] f32 logits (replaces ATen log_softmax/nll_loss fwd+bwd, K8);
+//                    dlogits written 16-bit into a zero-padded [B, ld] buffer for the fc dgrad/wgrad
+//   topk_acc       : top-1 / top-5 hit counters (replaces topk/eq/sum of validate, K11)
+//   col_sum        : sum over rows of a 16-bit [rows, C] matrix (fc bias gradient)
+//   sgd_flat       : ONE launch over the whole flat parameter buffer: AMP unscale, weight decay,
+//                    momentum (torch SGD semantics, first step buf = d_p), update, 16-bit shadow
+//                    write; skipped on device when found_inf (no host sync) (K9, K10)
+//   amp_check / amp_update : non-finite scan of the flat gradient; GradScaler state machine
+//   pack_stem      : f32 master [64][7][7][3] -> 16-bit [64][448] (taps x 8 padded channels)
+//   synth_nhwc8    : on-device synthetic ImageNet batch: NHWC, 3 channels padded to 8, 16-bit,
+//                    bit-compatible with data/synthetic.py (label + uniform u) (K12)
+//   nchw_to_nhwc8  : any f32 NCHW image batch -> NHWC8 16-bit model input
+#include "common.h"
+
+namespace {
+
+constexpr int NT = 256;
+
+// ------------------------------------------------------------------ softmax cross-entropy
+__global__ __launch_bounds__(NT) void xent_kernel(const float* __restrict__ logits, int B, int K,
+                                                  int ld_in, const long long* __restrict__ labels,
+                                                  float* __restrict__ loss_rows, u16* __restrict__ dlog,
+                                                  int ld_out, float gscale, const float* __restrict__ gdev, int dt,
+                                                  int want_grad) {
+  const int wave = (blockIdx.x * NT + threadIdx.x) >> 6;
+  const int lane = threadIdx.x & 63;
+  if (wave >= B) return;
+  const float* x = logits + (size_t)wave * ld_in;
+  float m = -INFINITY;
+  for (int k = lane; k < K; k += 64) m = fmaxf(m, x[k]);
+  m = wave_max(m);
+  float s = 0.f;
+  for (int k = lane; k < K; k += 64) s += __expf(x[k] - m);
+  s = wave_sum(s);
+  const float lse = m + __logf(s);
+  const int lab = (int)labels[wave];
+  if (lane == 0) loss_rows[wave] = lse - x[lab];
+  if (!want_grad) return;
+  const float inv = 1.f / s;
+  if (gdev) gscale *= gdev[0];
+  u16* d = dlog + (size_t)wave * ld_out;
+  for (int k = lane; k < ld_out; k += 64) {
+    float g = 0.f;
+    if (k < K) g = (__expf(x[k] - m) * inv - (k == lab ? 1.f : 0.f)) * gscale;
+    d[k] = dt == DT_BF16 ? f32_to_bf16(g) : f32_to_f16(g);
+  }
+}
+
+// loss = mean(loss_rows) (deterministic single block)
+__global__ __launch_bounds__(1024) void mean_kernel(const float* __restrict__ v, int n,
+                                                    float* __restrict__ out) {
+  __shared__ float red[16];
+  float s = 0.f;
+  for (int i = threadIdx.x; i < n; i += 1024) s += v[i];
+  s = wave_sum(s);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float t = 0.f;
+    for (int i = 0; i < 16; ++i) t += red[i];
+    out[0] = t / (float)n;
+  }
+}
+
+// top-1/top-5 hits: out[0] += top1 hits, out[1] += top5 hits (ties broken like torch.topk: lower idx)
+__global__ __launch_bounds__(NT) void topk_kernel(const float* __restrict__ logits, int B, int K,
+                                                  int ld, const long long* __restrict__ labels,
+                                                  float* __restrict__ hits) {
+  const int wave = (blockIdx.x * NT + threadIdx.x) >> 6;
+  const int lane = threadIdx.x & 63;
+  if (wave >= B) return;
+  const float* x = logits + (size_t)wave * ld;
+  const int lab = (int)labels[wave];
+  const float v = x[lab];
+  // rank = number of classes strictly better than the label (ties: lower index first)
+  int better = 0;
+  for (int k = lane; k < K; k += 64) {
+    const float u = x[k];
+    better += (u > v || (u == v && k < lab)) ? 1 : 0;
+  }
+  for (int o = 32; o > 0; o >>= 1) better += __shfl_xor(better, o, 64);
+  if (lane == 0) {
+    if (better < 1) atomicAdd(&hits[0], 1.f);
+    if (better < 5) atomicAdd(&hits[1], 1.f);
+  }
+}
+
+// out[c] = scale * sum_r x[r][c]  (x: 16-bit [rows][ld])
+__global__ void col_sum_kernel(const u16* __restrict__ x, int rows, int C, int ld, float scale,
+                               float* __restrict__ out, int dt, int accumulate) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  float s = 0.f;
+  for (int r = 0; r < rows; ++r) {
+    const u16 h = x[(size_t)r * ld + c];
+    s += dt == DT_BF16 ? bf16_to_f32(h) : f16_to_f32(h);
+  }
+  out[c] = s * scale + (accumulate ? out[c] : 0.f);
+}
+
+// ------------------------------------------------------------------ optimizer
+// flags: bit0 = momentum buffer initialised (else buf = d_p), bit1 = write shadow
+__global__ __launch_bounds__(NT) void sgd_flat_kernel(float* __restrict__ p, float* __restrict__ g,
+                                                      float* __restrict__ buf, u16* __restrict__ shadow,
+                                                      long long n, float lr, float momentum,
+                                                      float wd, const float* __restrict__ inv_scale_src,
+                                                      const float* __restrict__ found_inf, int flags,
+                                                      int dt) {
+  if (found_inf && found_inf[0] != 0.f) return;
+  const float inv = inv_scale_src ? 1.f / inv_scale_src[0] : 1.f;
+  const long long n4 = n >> 2;
+  for (long long i = blockIdx.x * (long long)NT + threadIdx.x; i < n4; i += (long long)gridDim.x * NT) {
+    f32x4 pv = reinterpret_cast<f32x4*>(p)[i];
+    f32x4 gv = reinterpret_cast<f32x4*>(g)[i];
+    f32x4 bv = reinterpret_cast<f32x4*>(buf)[i];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      float d = gv[e] * inv + wd * pv[e];
+      float b = (flags & 1) ? momentum * bv[e] + d : d;
+      bv[e] = b;
+      pv[e] -= lr * b;
+    }
+    reinterpret_cast<f32x4*>(p)[i] = pv;
+    reinterpret_cast<f32x4*>(buf)[i] = bv;
+    if (flags & 2) {
+      u16 h[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) h[e] = dt == DT_BF16 ? f32_to_bf16(pv[e]) : f32_to_f16(pv[e]);
+      reinterpret_cast<uint2*>(shadow)[i] = *reinterpret_cast<uint2*>(h);
+    }
+  }
+  // tail (n % 4)
+  if (blockIdx.x == 0 && threadIdx.x < (n & 3)) {
+    const long long i = (n4 << 2) + threadIdx.x;
+    float d = g[i] * inv + wd * p[i];
+    float b = (flags & 1) ? momentum * buf[i] + d : d;
+    buf[i] = b;
+    p[i] -= lr * b;
+    if (flags & 2) shadow[i] = dt == DT_BF16 ? f32_to_bf16(p[i]) : f32_to_f16(p[i]);
+  }
+}
+
+__global__ __launch_bounds__(NT) void cast_flat_kernel(const float* __restrict__ p, u16* __restrict__ s,
+                                                       long long n, int dt) {
+  for (long long i = blockIdx.x * (long long)NT + threadIdx.x; i < n; i += (long long)gridDim.x * NT)
+    s[i] = dt == DT_BF16 ? f32_to_bf16(p[i]) : f32_to_f16(p[i]);
+}
+
+__global__ __launch_bounds__(NT) void amp_check_kernel(const float* __restrict__ g, long long n,
+                                                       float* __restrict__ found_inf) {
+  bool bad = false;
+  for (long long i = blockIdx.x * (long long)NT + threadIdx.x; i < n; i += (long long)gridDim.x * NT) {
+    const float v = g[i];
+    bad |= !(fabsf(v) <= 3.4028235e38f);
+  }
+  if (__any(bad) && (threadIdx.x & 63) == 0) found_inf[0] = 1.f;
+}
+
+// torch._amp_update_scale_ semantics
+__global__ void amp_update_kernel(float* scale, int* tracker, const float* found_inf, float growth,
+                                  float backoff, int interval) {
+  if (found_inf[0] != 0.f) {
+    scale[0] *= backoff;
+    tracker[0] = 0;
+  } else {
+    const int t = tracker[0] + 1;
+    if (t == interval) {
+      const float ns = scale[0] * growth;
+      if (fabsf(ns) <= 3.4028235e38f) scale[0] = ns;
+      tracker[0] = 0;
+    } else {
+      tracker[0] = t;
+    }
+  }
+}
+
+// stem weight pack: src f32 [Cout][R*S][Cin] (channels-last OHWI) -> dst 16-bit [Cout][Kpad]
+__global__ void pack_stem_kernel(const float* __restrict__ src, u16* __restrict__ dst, int Cout,
+                                 int RS, int Cin, int Cpad, int Kpad, int dt) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= Cout * Kpad) return;
+  const int co = i / Kpad, k = i - co * Kpad;
+  const int tap = k / Cpad, c = k - tap * Cpad;
+  float v = 0.f;
+  if (tap < RS && c < Cin) v = src[((size_t)co * RS + tap) * Cin + c];
+  dst[i] = dt == DT_BF16 ? f32_to_bf16(v) : f32_to_f16(v);
+}
+
+// ------------------------------------------------------------------ data
+__device__ __forceinline__ uint32_t hash32(uint32_t x) {
+  x ^= x >> 16;
+  x *= 0x7FEB352Du;
+  x ^= x >> 15;
+  x *= 0x846CA68Bu;
+  x ^= x >> 16;
+  return x;
+}
+
+__constant__ float c_mean[3] = {0.485f, 0.456f, 0.406f};
+__constant__ float c_istd[3] = {1.f / 0.229f, 1.f / 0.224f, 1.f / 0.225f};
+
+// keys[b] = hash32(id*2654435761 + salt) computed on host-agnostic 32-bit math; labels[b] likewise
+__global__ void synth_labels_kernel(const long long* __restrict__ ids, int B, uint32_t salt,
+                                    int num_classes, uint32_t* __restrict__ keys,
+                                    long long* __restrict__ labels) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= B) return;
+  const uint32_t id = (uint32_t)ids[b];
+  const uint32_t key = hash32(id * 2654435761u + salt);
+  keys[b] = key;
+  labels[b] = hash32(key ^ 0x5BD1E995u) % (uint32_t)num_classes;
+}
+
+// out: [B][S][S][8] 16-bit; pixel (c,y,x) of sample b: u = hash32(key ^ (pos * 0x27D4EB2F)) >> 8
+__global__ __launch_bounds__(NT) void synth_nhwc8_kernel(const uint32_t* __restrict__ keys,
+                                                         const long long* __restrict__ labels,
+                                                         int B, int S, u16* __restrict__ out, int dt) {
+  const long long npix = (long long)B * S * S;
+  const int hw = S * S;
+  for (long long i = blockIdx.x * (long long)NT + threadIdx.x; i < npix; i += (long long)gridDim.x * NT) {
+    const int b = (int)(i / hw);
+    const int pix = (int)(i - (long long)b * hw);
+    const uint32_t key = keys[b];
+    const long long lab = labels[b];
+    u16 h[8];
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+      const uint32_t pos = (uint32_t)(c * hw + pix);
+      const uint32_t u = hash32(key ^ (pos * 0x27D4EB2Fu)) >> 8;
+      const float uf = (float)u * (1.0f / 16777216.0f);
+      const float tint = (float)((lab * (2 * c + 3) + c) % 4) / 3.0f;
+      const float v = (uf * 0.5f + 0.5f * tint - c_mean[c]) * c_istd[c];
+      h[c] = dt == DT_BF16 ? f32_to_bf16(v) : f32_to_f16(v);
+    }
+#pragma unroll
+    for (int c = 3; c < 8; ++c) h[c] = 0;
+    reinterpret_cast<i32x4*>(out)[i] = *reinterpret_cast<i32x4*>(h);
+  }
+}
+
+__global__ __launch_bounds__(NT) void nchw_to_nhwc8_kernel(const float* __restrict__ x, int B, int C,
+                                                           int H, int W, u16* __restrict__ out,
+                                                           int dt) {
+  const long long npix = (long long)B * H * W;
+  const int hw = H * W;
+  for (long long i = blockIdx.x * (long long)NT + threadIdx.x; i < npix; i += (long long)gridDim.x * NT) {
+    const int b = (int)(i / hw);
+    const int pix = (int)(i - (long long)b * hw);
+    u16 h[8];
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+      const float v = c < C ? x[((size_t)b * C + c) * hw + pix] : 0.f;
+      h[c] = dt == DT_BF16 ? f32_to_bf16(v) : f32_to_f16(v);
+    }
+    reinterpret_cast<i32x4*>(out)[i] = *reinterpret_cast<i32x4*>(h);
+  }
+}
+
+inline int grid_for(long long n, int cap = 4096) {
+  long long b = (n + NT - 1) / NT;
+  return (int)(b < 1 ? 1 : (b > cap ? cap : b));
+}
+
+}  // namespace
+
+extern "C" {
+
+int pda_xent(const float* logits, int B, int K, int ld_in, const long long* labels, float* loss_rows,
+             float* loss, void* dlog, int ld_out, float gscale, const float* gdev, int dt,
+             int want_grad, hipStream_t st) {
+  hipLaunchKernelGGL(xent_kernel, dim3((B + 3) / 4), dim3(NT), 0, st, logits, B, K, ld_in, labels,
+                     loss_rows, (u16*)dlog, ld_out, gscale, gdev, dt, want_grad);
+  if (loss) hipLaunchKernelGGL(mean_kernel, dim3(1), dim3(1024), 0, st, loss_rows, B, loss);
+  return (int)hipGetLastError();
+}
+
+int pda_topk(const float* logits, int B, int K, int ld, const long long* labels, float* hits,
+             hipStream_t st) {
+  hipLaunchKernelGGL(topk_kernel, dim3((B + 3) / 4), dim3(NT), 0, st, logits, B, K, ld, labels, hits);
+  return (int)hipGetLastError();
+}
+
+int pda_col_sum(const void* x, int rows, int C, int ld, float scale, float* out, int dt,
+                int accumulate, hipStream_t st) {
+  hipLaunchKernelGGL(col_sum_kernel, dim3((C + 255) / 256), dim3(256), 0, st, (const u16*)x, rows, C, ld,
+                     scale, out, dt, accumulate);
+  return (int)hipGetLastError();
+}
+
+int pda_sgd_flat(float* p, float* g, float* buf, void* shadow, long long n, float lr, float momentum,
+                 float wd, const float* scale, const float* found_inf, int flags, int dt,
+                 hipStream_t st) {
+  hipLaunchKernelGGL(sgd_flat_kernel, dim3(grid_for(n / 4 + 1, 8192)), dim3(NT), 0, st, p, g, buf,
+                     (u16*)shadow, n, lr, momentum, wd, scale, found_inf, flags, dt);
+  return (int)hipGetLastError();
+}
+
+int pda_cast_flat(const float* p, void* s, long long n, int dt, hipStream_t st) {
+  hipLaunchKernelGGL(cast_flat_kernel, dim3(grid_for(n, 8192)), dim3(NT), 0, st, p, (u16*)s, n, dt);
+  return (int)hipGetLastError();
+}
+
+int pda_amp_check(const float* g, long long n, float* found_inf, hipStream_t st) {
+  hipLaunchKernelGGL(amp_check_kernel, dim3(grid_for(n, 4096)), dim3(NT), 0, st, g, n, found_inf);
+  return (int)hipGetLastError();
+}
+
+int pda_amp_update(float* scale, int* tracker, const float* found_inf, float growth, float backoff,
+                   int interval, hipStream_t st) {
+  hipLaunchKernelGGL(amp_update_kernel, dim3(1), dim3(1), 0, st, scale, tracker, found_inf, growth,
+                     backoff, interval);
+  return (int)hipGetLastError();
+}
+
+int pda_pack_stem(const float* src, void* dst, int Cout, int RS, int Cin, int Cpad, int Kpad, int dt,
+                  hipStream_t st) {
+  const int n = Cout * Kpad;
+  hipLaunchKernelGGL(pack_stem_kernel, dim3((n + 255) / 256), dim3(256), 0, st, src, (u16*)dst, Cout,
+                     RS, Cin, Cpad, Kpad, dt);
+  return (int)hipGetLastError();
+}
+
+int pda_synth(const long long* ids, int B, unsigned salt, int num_classes, unsigned* keys,
+              long long* labels, int S, void* out, int dt, hipStream_t st) {
+  hipLaunchKernelGGL(synth_labels_kernel, dim3((B + 255) / 256), dim3(256), 0, st, ids, B, salt,
+                     num_classes, keys, labels);
+  hipLaunchKernelGGL(synth_nhwc8_kernel, dim3(grid_for((long long)B * S * S, 8192)), dim3(NT), 0, st,
+                     keys, labels, B, S, (u16*)out, dt);
+  return (int)hipGetLastError();
+}
+
+int pda_nchw_to_nhwc8(const float* x, int B, int C, int H, int W, void* out, int dt, hipStream_t st) {
+  hipLaunchKernelGGL(nchw_to_nhwc8_kernel, dim3(grid_for((long long)B * H * W, 8192)), dim3(NT), 0, st,
+                     x, B, C, H, W, (u16*)out, dt);
+  return (int)hipGetLastError();
+}
+
+}  // extern "C"

@@ -1,6 +1,740 @@
-"""Native MI355X ResNet engine (placeholder until the HIP kernels land)."""
+"""Native MI355X ResNet training engine (flat buffers + explicit forward/backward schedule).
+
+What it replaces: the reference runs ``torchvision.models.resnet50()`` through
+ATen/cuDNN/cuBLAS with autograd recording ~500 ops per step.
+Here the whole network is ONE coarse autograd node whose forward and backward
+are explicit schedules of our gfx950 kernels (``ops/native_ops.py``):
+
+* activations are NHWC 16-bit (bf16 default, f16 for the AMP script); the input is
+  the 3-channel image padded to 8 channels so the 7x7 stem runs on MFMA too;
+* every conv is the implicit-GEMM MFMA kernel (fwd / dgrad / split-K wgrad); the
+  forward epilogue emits BatchNorm partial statistics, so BN costs one finalize
+  launch plus one fused apply(+ReLU, +residual, +pool) pass;
+* parameters live in ONE flat f32 buffer laid out in *gradient-production order*
+  (fc, layer4.2 ... layer1.0, stem) so DDP buckets are contiguous slices that
+  complete in order during backward; ``.grad`` of every parameter is a view into
+  one flat f32 gradient buffer; a 16-bit shadow of the flat buffer (written by the
+  fused SGD kernel) is what the convs read -- conv weights are stored OHWI
+  (= ``torch.channels_last`` of the torchvision OIHW parameter), so the shadow
+  needs no repacking (only the 9.4k-element stem is packed);
+* BN running stats / counters live in flat buffers (one broadcast each for DDP).
+
+The module keeps torchvision's module tree and ``state_dict`` keys: it adopts the
+children of a :class:`~pytorch_distributed_amd.models.resnet.ResNet` instance and
+re-points their parameters/buffers into the flat storage.
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass, field
+from typing import Callable, Dict, List, Optional, Tuple
+
 import torch
+from torch import nn
+
+from ..ops import ext
+from ..ops import native_ops as K
+from ..ops.native_ops import ConvGeom, Workspace
+from .resnet import BasicBlock, Bottleneck, ResNet
+
+__all__ = ["NativeResNet", "NativeSGD", "NativeCrossEntropy", "NativeTrainer", "supports"]
+
+ALIGN = 64  # elements; keeps every segment 16-B aligned in the 16-bit shadow
 
 
 def supports(arch: str, dtype: torch.dtype) -> bool:
-    return False
+    if dtype not in (torch.bfloat16, torch.float16):
+        return False
+    if arch not in ("resnet18", "resnet34", "resnet50", "resnet101", "resnet152"):
+        return False
+    return torch.cuda.is_available() and ext.available()
+
+
+def _align(n: int) -> int:
+    return (n + ALIGN - 1) // ALIGN * ALIGN
+
+
+# ====================================================================== plan objects
+@dataclass
+class ConvBN:
+    """One conv (+ the BatchNorm after it)."""
+    name: str
+    conv: nn.Conv2d
+    bn: nn.BatchNorm2d
+    cin_store: int            # channels of the stored input (stem: 8)
+    H: int                    # input spatial size
+    W: int
+    w_off: int = 0            # flat offsets
+    w_len: int = 0
+    bn_off: int = 0
+    buf_off: int = 0
+    nbt_idx: int = 0
+    # per-step state (f32 [C] each): mean, invstd, scale, shift
+    state: Optional[torch.Tensor] = None
+
+    @property
+    def cout(self) -> int:
+        return self.conv.out_channels
+
+    def geom(self, Nb: int) -> ConvGeom:
+        c = self.conv
+        return ConvGeom(Nb, self.H, self.W, self.cin_store, c.out_channels, c.kernel_size[0],
+                        c.kernel_size[1], c.stride[0], c.padding[0])
+
+    @property
+    def Ho(self) -> int:
+        return self.geom(1).Ho
+
+
+@dataclass
+class Block:
+    name: str
+    units: List[ConvBN]               # main path; all but the last have ReLU
+    ds: Optional[ConvBN]              # downsample conv+bn, or None (identity shortcut)
+    seg: Tuple[int, int] = (0, 0)     # flat param range of this block
+
+
+class NativeResNet(nn.Module):
+    def __init__(self, ref: ResNet, device=None, dtype: torch.dtype = torch.bfloat16,
+                 image_size: int = 224) -> None:
+        super().__init__()
+        device = torch.device("cuda", torch.cuda.current_device()) if device is None else torch.device(device)
+        if device.type != "cuda":
+            raise RuntimeError("NativeResNet runs on the GPU; use the torch engine on CPU")
+        ext.load(required=True)
+        self.device = device
+        self.dtype = dtype
+        self.image_size = image_size
+        self.num_classes = ref.fc.out_features
+        self.arch_block = ref.block
+        for name, child in ref.named_children():
+            self.add_module(name, child)
+        self.ws = Workspace(device)
+        self._build_plan()
+        self._allocate(ref)
+        self._reducer = None
+        self._grads_zero = True
+        self._fwd_ctx = None
+        self._anchor = torch.zeros((), device=device, requires_grad=True)
+        self.refresh_shadow()
+
+    # ------------------------------------------------------------------ planning
+    def _build_plan(self) -> None:
+        S = self.image_size
+        self.stem = ConvBN("stem", self.conv1, self.bn1, 8, S, S)
+        h = self.stem.Ho
+        h = (h + 2 - 3) // 2 + 1  # maxpool 3x3/2/1
+        self.pool_hw = h
+        self.blocks: List[Block] = []
+        for li in range(1, 5):
+            layer = getattr(self, f"layer{li}")
+            for bi, blk in enumerate(layer):
+                nm = f"layer{li}.{bi}"
+                cin = blk.conv1.in_channels
+                units = []
+                if isinstance(blk, Bottleneck):
+                    u1 = ConvBN(nm + ".conv1", blk.conv1, blk.bn1, cin, h, h)
+                    u2 = ConvBN(nm + ".conv2", blk.conv2, blk.bn2, blk.conv2.in_channels, h, h)
+                    h2 = u2.Ho
+                    u3 = ConvBN(nm + ".conv3", blk.conv3, blk.bn3, blk.conv3.in_channels, h2, h2)
+                    units = [u1, u2, u3]
+                else:
+                    u1 = ConvBN(nm + ".conv1", blk.conv1, blk.bn1, cin, h, h)
+                    h2 = u1.Ho
+                    u2 = ConvBN(nm + ".conv2", blk.conv2, blk.bn2, blk.conv2.in_channels, h2, h2)
+                    units = [u1, u2]
+                ds = None
+                if blk.downsample is not None:
+                    ds = ConvBN(nm + ".downsample", blk.downsample[0], blk.downsample[1], cin, h, h)
+                self.blocks.append(Block(nm, units, ds))
+                h = units[-1].Ho
+        self.final_hw = h
+        self.feat_dim = self.fc.in_features
+        if self.num_classes > 1024 or self.feat_dim % 64:
+            raise ValueError("unsupported head shape")
+        self.fc_rows = _align(self.num_classes) if self.num_classes % 64 else self.num_classes
+        self.fc_rows = int(math.ceil(self.num_classes / 64) * 64)
+
+    def _units_in_grad_order(self):
+        """(block-or-None, [ConvBN...]) groups in backward completion order."""
+        yield None, []  # fc (handled explicitly)
+        for b in reversed(self.blocks):
+            yield b, list(reversed(b.units)) + ([b.ds] if b.ds else [])
+        yield "stem", [self.stem]
+
+    def _allocate(self, ref: ResNet) -> None:
+        dev = self.device
+        off = 0
+        # fc: bias then weight (padded rows)
+        self.fc_b_off = off
+        off += _align(self.num_classes)
+        self.fc_w_off = off
+        off += self.fc_rows * self.feat_dim
+        self.fc_seg_end = off
+        self.block_bounds: List[int] = [off]
+        units: List[ConvBN] = []
+        for b, us in list(self._units_in_grad_order())[1:]:
+            start = off
+            for u in us:
+                u.w_off = off
+                u.w_len = u.conv.weight.numel()
+                off += _align(u.w_len)
+                u.bn_off = off
+                off += 2 * _align(u.cout)   # gamma, beta
+                units.append(u)
+            if isinstance(b, Block):
+                b.seg = (start, off)
+            self.block_bounds.append(off)
+        self.numel = off
+        self.units = units
+        self.flat_params = torch.zeros(off, dtype=torch.float32, device=dev)
+        self.flat_grad = torch.zeros(off, dtype=torch.float32, device=dev)
+        self.flat_shadow = torch.zeros(off, dtype=self.dtype, device=dev)
+        # BN buffers
+        boff = 0
+        for i, u in enumerate(units):
+            u.buf_off = boff
+            boff += 2 * _align(u.cout)
+            u.nbt_idx = i
+        self.flat_buffers = torch.zeros(boff, dtype=torch.float32, device=dev)
+        self.flat_nbt = torch.zeros(len(units), dtype=torch.int64, device=dev)
+        self.stem_packed = torch.zeros(64, 448, dtype=self.dtype, device=dev)
+        self.bn_state = torch.zeros(sum(4 * _align(u.cout) for u in units), dtype=torch.float32,
+                                    device=dev)
+        so = 0
+        for u in units:
+            c = _align(u.cout)
+            u.state = self.bn_state[so:so + 4 * c].view(4, c)[:, :u.cout]
+            so += 4 * c
+        # re-point parameters / buffers into the flat storage
+        with torch.no_grad():
+            for u in units:
+                w = u.conv.weight
+                O, I, R, S_ = w.shape
+                seg = self.flat_params[u.w_off:u.w_off + u.w_len].view(O, R, S_, I)
+                seg.copy_(w.detach().permute(0, 2, 3, 1))
+                gseg = self.flat_grad[u.w_off:u.w_off + u.w_len].view(O, R, S_, I)
+                self._rebind(u.conv, "weight", seg.permute(0, 3, 1, 2), gseg.permute(0, 3, 1, 2))
+                c = u.cout
+                ca = _align(c)
+                for j, pn in enumerate(("weight", "bias")):
+                    p = getattr(u.bn, pn)
+                    s = self.flat_params[u.bn_off + j * ca:u.bn_off + j * ca + c]
+                    s.copy_(p.detach())
+                    self._rebind(u.bn, pn, s, self.flat_grad[u.bn_off + j * ca:u.bn_off + j * ca + c])
+                rm = self.flat_buffers[u.buf_off:u.buf_off + c]
+                rv = self.flat_buffers[u.buf_off + ca:u.buf_off + ca + c]
+                rm.copy_(u.bn.running_mean)
+                rv.copy_(u.bn.running_var)
+                u.bn.running_mean = rm
+                u.bn.running_var = rv
+                nb = self.flat_nbt[u.nbt_idx:u.nbt_idx + 1].view(())
+                nb.copy_(u.bn.num_batches_tracked)
+                u.bn.num_batches_tracked = nb
+            fw = self.flat_params[self.fc_w_off:self.fc_w_off + self.num_classes * self.feat_dim]
+            fw = fw.view(self.num_classes, self.feat_dim)
+            fw.copy_(self.fc.weight.detach())
+            fgw = self.flat_grad[self.fc_w_off:self.fc_w_off + self.num_classes * self.feat_dim]
+            self._rebind(self.fc, "weight", fw, fgw.view(self.num_classes, self.feat_dim))
+            fb = self.flat_params[self.fc_b_off:self.fc_b_off + self.num_classes]
+            fb.copy_(self.fc.bias.detach())
+            self._rebind(self.fc, "bias", fb, self.flat_grad[self.fc_b_off:self.fc_b_off + self.num_classes])
+        self.fc_w16 = self.flat_shadow[self.fc_w_off:self.fc_w_off + self.fc_rows * self.feat_dim].view(
+            self.fc_rows, self.feat_dim)
+        self.fc_wgrad_full = self.flat_grad[self.fc_w_off:self.fc_w_off + self.fc_rows * self.feat_dim]
+
+    @staticmethod
+    def _rebind(mod: nn.Module, name: str, data: torch.Tensor, grad: torch.Tensor) -> None:
+        p = nn.Parameter(data, requires_grad=True)
+        p.grad = grad
+        mod._parameters[name] = p
+
+    # ------------------------------------------------------------------ helpers
+    def w16(self, u: ConvBN) -> torch.Tensor:
+        if u is self.stem:
+            return self.stem_packed
+        O, I, R, S_ = u.conv.weight.shape
+        return self.flat_shadow[u.w_off:u.w_off + u.w_len].view(O, R * S_ * I)
+
+    def w16_ohwi(self, u: ConvBN) -> torch.Tensor:
+        O, I, R, S_ = u.conv.weight.shape
+        return self.flat_shadow[u.w_off:u.w_off + u.w_len].view(O, R, S_, I)
+
+    def gamma(self, u):
+        return self.flat_params[u.bn_off:u.bn_off + u.cout]
+
+    def beta(self, u):
+        ca = _align(u.cout)
+        return self.flat_params[u.bn_off + ca:u.bn_off + ca + u.cout]
+
+    def dgamma(self, u):
+        return self.flat_grad[u.bn_off:u.bn_off + u.cout]
+
+    def dbeta(self, u):
+        ca = _align(u.cout)
+        return self.flat_grad[u.bn_off + ca:u.bn_off + ca + u.cout]
+
+    def rmean(self, u):
+        return self.flat_buffers[u.buf_off:u.buf_off + u.cout]
+
+    def rvar(self, u):
+        ca = _align(u.cout)
+        return self.flat_buffers[u.buf_off + ca:u.buf_off + ca + u.cout]
+
+    def wgrad_view(self, u):
+        return self.flat_grad[u.w_off:u.w_off + u.w_len]
+
+    @torch.no_grad()
+    def refresh_shadow(self) -> None:
+        """16-bit shadow of the flat parameters (the SGD kernel keeps it fresh afterwards)."""
+        K.cast_flat(self.flat_params, self.flat_shadow)
+        self._pack_stem()
+
+    def _pack_stem(self) -> None:
+        K.pack_stem(self.flat_params[self.stem.w_off:self.stem.w_off + self.stem.w_len],
+                    self.stem_packed)
+
+    def _empty(self, *shape, dtype=None) -> torch.Tensor:
+        return torch.empty(*shape, dtype=self.dtype if dtype is None else dtype, device=self.device)
+
+    # ------------------------------------------------------------------ DDP / DP hooks
+    def grad_boundaries(self) -> List[int]:
+        return list(self.block_bounds)
+
+    def attach_reducer(self, reducer) -> None:
+        self._reducer = reducer
+
+    @torch.no_grad()
+    def sync_from_rank0(self, comm) -> None:
+        comm.broadcast(self.flat_params, 0)
+        self.broadcast_buffers_from_rank0(comm)
+        self.refresh_shadow()
+
+    @torch.no_grad()
+    def broadcast_buffers_from_rank0(self, comm) -> None:
+        comm.broadcast(self.flat_buffers, 0)
+        comm.broadcast(self.flat_nbt, 0)
+
+    def zero_grad_flat(self) -> None:
+        self.flat_grad.zero_()
+        self._grads_zero = True
+
+    # ------------------------------------------------------------------ input
+    def input_generator(self, ds) -> Callable:
+        """Loader hook: sample ids -> (NHWC8 16-bit images, int64 labels) made on the device."""
+        S = ds.image_size
+
+        def gen(ids: torch.Tensor):
+            ids_d = ids.to(self.device, non_blocking=True)
+            B = ids_d.numel()
+            x = self._empty(B, S, S, 8)
+            lab = torch.empty(B, dtype=torch.int64, device=self.device)
+            keys = torch.empty(B, dtype=torch.int32, device=self.device)
+            K.synth_batch(ids_d, ds.seed, ds.split, ds.num_classes, S, x, lab, keys)
+            return x, lab
+
+        return gen
+
+    def prepare_input(self, x: torch.Tensor) -> torch.Tensor:
+        if x.dtype == self.dtype and x.dim() == 4 and x.shape[-1] == 8:
+            return x.contiguous()
+        if x.dim() != 4 or x.shape[1] != 3:
+            raise ValueError(f"expected [B,3,H,W] images or NHWC8 {self.dtype} input, got {tuple(x.shape)}")
+        xin = x.to(self.device, torch.float32).contiguous()
+        out = self._empty(x.shape[0], x.shape[2], x.shape[3], 8)
+        K.nchw_to_nhwc8(xin, out)
+        return out
+
+    # ------------------------------------------------------------------ forward
+    def _conv_bn(self, u: ConvBN, x: torch.Tensor, train: bool) -> torch.Tensor:
+        """y = conv(x) and BN coefficients (batch stats in training, running stats in eval)."""
+        Nb = x.shape[0]
+        g = u.geom(Nb)
+        M = Nb * g.Ho * g.Wo
+        y = self._empty(Nb, g.Ho, g.Wo, u.cout)
+        st = u.state
+        if train:
+            T = K.stats_tiles(M, u.cout)
+            part = self.ws.get("fwd_stats", T * 2 * u.cout)
+            K.conv_fwd(x, self.w16(u), g, y, stats=part)
+            K.bn_finalize_fwd(part, T, u.cout, M, self.gamma(u), self.beta(u), u.bn.eps,
+                              u.bn.momentum if u.bn.momentum is not None else 0.1,
+                              st[0], st[1], st[2], st[3], self.rmean(u), self.rvar(u),
+                              self.flat_nbt[u.nbt_idx:u.nbt_idx + 1], update_running=True)
+        else:
+            K.conv_fwd(x, self.w16(u), g, y)
+            K.bn_eval_coeffs(self.gamma(u), self.beta(u), self.rmean(u), self.rvar(u), u.bn.eps,
+                             st[2], st[3])
+        return y
+
+    def _coeffs(self, u: ConvBN, train: bool):
+        """(scale, shift) tensors -- eval needs private copies (state is shared)."""
+        return u.state[2], u.state[3]
+
+    def native_forward(self, x: torch.Tensor, train: bool, save: bool) -> torch.Tensor:
+        x = self.prepare_input(x)
+        Nb = x.shape[0]
+        saved: Dict = {"x0": x} if save else None
+        # stem: conv -> bn -> relu -> maxpool (fused)
+        y0 = self._conv_bn(self.stem, x, train)
+        ph = self.pool_hw
+        p = self._empty(Nb, ph, ph, self.stem.cout)
+        arg = torch.empty(Nb, ph, ph, self.stem.cout, dtype=torch.uint8, device=self.device)
+        sc, sh = self._coeffs(self.stem, train)
+        K.stem_pool(y0, sc, sh, p, arg)
+        if save:
+            saved["y0"], saved["arg"] = y0, arg
+            saved["stem_stats"] = self.stem.state.clone()
+            saved["blocks"] = []
+        h = p
+        feat = None
+        nblk = len(self.blocks)
+        for bi, b in enumerate(self.blocks):
+            last = bi == nblk - 1
+            rec = {"x": h} if save else None
+            a = h
+            ys, acts = [], [h]
+            for j, u in enumerate(b.units):
+                y = self._conv_bn(u, a, train)
+                ys.append(y)
+                if save:
+                    rec[f"s{j}"] = u.state.clone()
+                if j < len(b.units) - 1:
+                    sc, sh = self._coeffs(u, train)
+                    a = self._empty(*y.shape)
+                    K.bn_apply(y, sc, sh, a, relu=True)
+                    acts.append(a)
+            yd = None
+            if b.ds is not None:
+                yd = self._conv_bn(b.ds, h, train)
+                if save:
+                    rec["sd"] = b.ds.state.clone()
+            ul = b.units[-1]
+            sc, sh = self._coeffs(ul, train)
+            if last:
+                feat = self._empty(Nb, ul.cout)
+                if yd is not None:
+                    K.tail_pool(ys[-1], sc, sh, feat, y2=yd, scale2=b.ds.state[2], shift2=b.ds.state[3])
+                else:
+                    K.tail_pool(ys[-1], sc, sh, feat, res=h)
+                out = None
+            else:
+                out = self._empty(*ys[-1].shape)
+                if yd is not None:
+                    K.bn_apply(ys[-1], sc, sh, out, y2=yd, scale2=b.ds.state[2], shift2=b.ds.state[3])
+                else:
+                    K.bn_apply(ys[-1], sc, sh, out, res=h)
+            if save:
+                rec["ys"], rec["acts"], rec["yd"] = ys, acts, yd
+                saved["blocks"].append(rec)
+            h = out
+        logits = torch.empty(Nb, self.num_classes, dtype=torch.float32, device=self.device)
+        g = ConvGeom(Nb, 1, 1, self.feat_dim, self.num_classes, 1, 1, 1, 0)
+        K.conv_fwd(feat, self.fc_w16, g, logits,
+                   bias=self.flat_params[self.fc_b_off:self.fc_b_off + self.num_classes])
+        if save:
+            saved["feat"] = feat
+            saved["logits"] = logits
+        self._fwd_ctx = saved
+        return logits
+
+    # ------------------------------------------------------------------ backward
+    def native_backward(self, dlog16: torch.Tensor) -> None:
+        """dlog16: [B, fc_rows] 16-bit d(loss)/d(logits) (zero padded)."""
+        sv = self._fwd_ctx
+        if sv is None:
+            raise RuntimeError("native backward without a saved forward")
+        acc = not self._grads_zero
+        red = self._reducer
+        if red is not None:
+            red.reset()
+        Nb = dlog16.shape[0]
+        # ---- fc
+        K.col_sum(dlog16, self.num_classes, self.flat_grad[self.fc_b_off:self.fc_b_off + self.num_classes],
+                  accumulate=acc)
+        gfc = ConvGeom(Nb, 1, 1, self.feat_dim, self.fc_rows, 1, 1, 1, 0)
+        K.conv_wgrad(dlog16, sv["feat"], gfc, self.fc_wgrad_full, self.ws, accumulate=acc)
+        dfeat = self._empty(Nb, 1, 1, self.feat_dim)
+        fc_w_ohwi = self.fc_w16.view(self.fc_rows, 1, 1, self.feat_dim)
+        K.conv_dgrad(dlog16.view(Nb, 1, 1, self.fc_rows), fc_w_ohwi, gfc, dfeat)
+        if red is not None:
+            red.grads_ready(self.block_bounds[0])
+        # ---- blocks, last to first
+        g1, g2, gp = None, None, dfeat.view(Nb, self.feat_dim)
+        for bi in range(len(self.blocks) - 1, -1, -1):
+            b = self.blocks[bi]
+            rec = sv["blocks"][bi]
+            g1, g2 = self._block_backward(b, rec, g1, g2, gp, acc)
+            gp = None
+            if red is not None:
+                red.grads_ready(self.block_bounds[len(self.blocks) - bi])
+        # ---- stem
+        x0, y0, arg = sv["x0"], sv["y0"], sv["arg"]
+        st0 = sv["stem_stats"]
+        dA0 = self._empty(*y0.shape)
+        K.maxpool_bwd(g1, arg, dA0, dout2=g2)
+        dy0 = self._empty(*y0.shape)
+        u = self.stem
+        K.bn_bwd(self.ws, y0, st0[0], st0[1], self.gamma(u), st0[2], st0[3], self.dgamma(u),
+                 self.dbeta(u), dy0, g1=dA0, accumulate=acc)
+        K.conv_wgrad(dy0, x0, u.geom(Nb), self.wgrad_view(u), self.ws, cin_real=3, accumulate=acc)
+        if red is not None:
+            red.grads_ready(self.block_bounds[-1])
+            red.finish()
+        self._grads_zero = False
+        self._fwd_ctx = None
+
+    def _block_backward(self, b: Block, rec, g1, g2, gp, acc):
+        x = rec["x"]
+        ys, acts, yd = rec["ys"], rec["acts"], rec["yd"]
+        Nb = x.shape[0]
+        ul = b.units[-1]
+        sl = rec[f"s{len(b.units) - 1}"]
+        dz = self._empty(*ys[-1].shape)
+        dy = self._empty(*ys[-1].shape)
+        dyd = None
+        if b.ds is not None:
+            sd = rec["sd"]
+            dyd = self._empty(*yd.shape)
+            K.bn_bwd(self.ws, ys[-1], sl[0], sl[1], self.gamma(ul), sl[2], sl[3], self.dgamma(ul),
+                     self.dbeta(ul), dy, g1=g1, g2=g2, gp=gp, y2=yd, mean2=sd[0], invstd2=sd[1],
+                     gamma2=self.gamma(b.ds), scale2=sd[2], shift2=sd[3], dgamma2=self.dgamma(b.ds),
+                     dbeta2=self.dbeta(b.ds), dy2_out=dyd, dz_buf=dz, accumulate=acc)
+        else:
+            K.bn_bwd(self.ws, ys[-1], sl[0], sl[1], self.gamma(ul), sl[2], sl[3], self.dgamma(ul),
+                     self.dbeta(ul), dy, g1=g1, g2=g2, gp=gp, res=x, dz_buf=dz, accumulate=acc)
+        n = len(b.units)
+        dx_main = None
+        for j in range(n - 1, -1, -1):
+            u = b.units[j]
+            a_in = acts[j]
+            g = u.geom(Nb)
+            K.conv_wgrad(dy, a_in, g, self.wgrad_view(u), self.ws, accumulate=acc)
+            da = self._empty(*a_in.shape)
+            K.conv_dgrad(dy, self.w16_ohwi(u), g, da)
+            if j > 0:
+                up = b.units[j - 1]
+                sp = rec[f"s{j - 1}"]
+                dyp = self._empty(*ys[j - 1].shape)
+                K.bn_bwd(self.ws, ys[j - 1], sp[0], sp[1], self.gamma(up), sp[2], sp[3],
+                         self.dgamma(up), self.dbeta(up), dyp, g1=da, accumulate=acc)
+                dy = dyp
+            else:
+                dx_main = da
+        if b.ds is not None:
+            g = b.ds.geom(Nb)
+            K.conv_wgrad(dyd, x, g, self.wgrad_view(b.ds), self.ws, accumulate=acc)
+            dxd = self._empty(*x.shape)
+            K.conv_dgrad(dyd, self.w16_ohwi(b.ds), g, dxd)
+            return dx_main, dxd
+        return dx_main, dz
+
+    # ------------------------------------------------------------------ nn.Module API
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        train = self.training
+        if train and torch.is_grad_enabled():
+            return _NativeNetFn.apply(self._anchor, x, self)
+        with torch.no_grad():
+            return self.native_forward(x, train=train, save=False)
+
+    def make_optimizer(self, lr=0.1, momentum=0.9, weight_decay=1e-4) -> "NativeSGD":
+        return NativeSGD(self, lr=lr, momentum=momentum, weight_decay=weight_decay)
+
+    def make_criterion(self) -> "NativeCrossEntropy":
+        return NativeCrossEntropy(self)
+
+    def _apply(self, fn, recurse=True):  # .to()/.cuda()/.half() would break the flat views
+        return self
+
+    def load_state_dict(self, state_dict, strict: bool = True, assign: bool = False):
+        res = super().load_state_dict(state_dict, strict=strict)
+        self.refresh_shadow()
+        return res
+
+
+class _NativeNetFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, anchor, x, model: NativeResNet):
+        ctx.model = model
+        logits = model.native_forward(x, train=True, save=True)
+        ctx.B = logits.shape[0]
+        return logits
+
+    @staticmethod
+    def backward(ctx, dlogits):
+        m: NativeResNet = ctx.model
+        pending = getattr(m, "_pending_dlog16", None)
+        if pending is not None:
+            dlog16 = pending
+            m._pending_dlog16 = None
+        else:  # generic criterion: convert f32 dlogits to the padded 16-bit buffer
+            dlog16 = torch.zeros(ctx.B, m.fc_rows, dtype=m.dtype, device=m.device)
+            dlog16[:, :m.num_classes].copy_(dlogits)
+        m.native_backward(dlog16)
+        return torch.zeros((), device=m.device), None, None
+
+
+class _XentFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, logits, labels, model: NativeResNet):
+        B = logits.shape[0]
+        loss_rows = torch.empty(B, dtype=torch.float32, device=logits.device)
+        loss = torch.empty((), dtype=torch.float32, device=logits.device)
+        K.xent(logits, labels, loss_rows, loss)
+        ctx.save_for_backward(logits, labels)
+        ctx.model = model
+        return loss
+
+    @staticmethod
+    def backward(ctx, g):
+        logits, labels = ctx.saved_tensors
+        m: NativeResNet = ctx.model
+        B = logits.shape[0]
+        dlog16 = torch.empty(B, m.fc_rows, dtype=m.dtype, device=logits.device)
+        gdev = g.reshape(1).to(torch.float32).contiguous()
+        K.xent(logits, labels, torch.empty(B, device=logits.device), None, dlog=dlog16,
+               gscale=1.0 / B, gdev=gdev)
+        m._pending_dlog16 = dlog16
+        # the dlogits handed to the network node are carried by dlog16; return a placeholder
+        return torch.empty_like(logits), None, None
+
+
+class NativeCrossEntropy(nn.Module):
+    """CrossEntropyLoss (mean) fused with its gradient kernel for the native engine."""
+
+    def __init__(self, model: Optional[NativeResNet] = None) -> None:
+        super().__init__()
+        self.model = model
+
+    def forward(self, logits: torch.Tensor, labels: torch.Tensor) -> torch.Tensor:
+        m = self.model
+        if m is None or not logits.is_cuda or logits.dtype != torch.float32:
+            return nn.functional.cross_entropy(logits.float(), labels)
+        if logits.requires_grad:
+            return _XentFn.apply(logits, labels, m)
+        B = logits.shape[0]
+        loss = torch.empty((), dtype=torch.float32, device=logits.device)
+        K.xent(logits.contiguous(), labels, torch.empty(B, device=logits.device), loss)
+        return loss
+
+
+class NativeSGD(torch.optim.Optimizer):
+    """torch.optim.SGD semantics (momentum, dampening 0, weight decay on every parameter -- as the
+    reference, quirk Q12) executed as ONE fused kernel over the flat buffers, which also refreshes
+    the 16-bit weight shadow. ``state_dict()`` has torch SGD's format (per-parameter
+    ``momentum_buffer``), so checkpoints interchange with the reference's optimizer."""
+
+    def __init__(self, model: NativeResNet, lr=0.1, momentum=0.9, weight_decay=1e-4,
+                 dampening=0.0, nesterov=False) -> None:
+        if dampening != 0.0 or nesterov:
+            raise ValueError("NativeSGD implements dampening=0, nesterov=False (reference settings)")
+        defaults = dict(lr=lr, momentum=momentum, dampening=0.0, weight_decay=weight_decay,
+                        nesterov=False, maximize=False, foreach=None, differentiable=False,
+                        fused=None)
+        super().__init__(list(model.parameters()), defaults)
+        self.model = model
+        self.flat_mom = torch.zeros_like(model.flat_params)
+        self._initialized = False
+        # per-parameter momentum views (torch format in state_dict)
+        self._views = {}
+        fp = model.flat_params
+        base = fp.data_ptr()
+        for p in self.param_groups[0]["params"]:
+            off = (p.data_ptr() - base) // 4
+            v = self.flat_mom[off:off + p.numel()]
+            if p.dim() == 4:
+                O, I, R, S_ = p.shape
+                v = v.view(O, R, S_, I).permute(0, 3, 1, 2)
+            else:
+                v = v.view(p.shape)
+            self._views[p] = v
+
+    def zero_grad(self, set_to_none: bool = True) -> None:
+        self.model.zero_grad_flat()
+
+    def _launch(self, scale=None, found_inf=None) -> None:
+        g = self.param_groups[0]
+        m = self.model
+        K.sgd_flat(m.flat_params, m.flat_grad, self.flat_mom, m.flat_shadow, g["lr"], g["momentum"],
+                   g["weight_decay"], self._initialized, scale=scale, found_inf=found_inf)
+        m._pack_stem()
+        if found_inf is None:
+            self._initialized = True
+        else:
+            self._initialized = True  # first finite step initialises; see _mark below
+        for p in g["params"]:
+            self.state[p]["momentum_buffer"] = self._views[p]
+
+    @torch.no_grad()
+    def step(self, closure=None):
+        loss = closure() if closure is not None else None
+        self._launch()
+        return loss
+
+    # AMP: unscale + inf check + conditional step, all on device (no host sync)
+    @torch.no_grad()
+    def step_amp(self, scale: torch.Tensor, found_inf: torch.Tensor):
+        found_inf.zero_()
+        K.amp_check(self.model.flat_grad, found_inf)
+        self._launch(scale=scale, found_inf=found_inf)
+
+    def state_dict(self):
+        sd = super().state_dict()
+        return sd
+
+    def load_state_dict(self, state_dict):
+        super().load_state_dict(state_dict)
+        with torch.no_grad():
+            any_buf = False
+            for p in self.param_groups[0]["params"]:
+                st = self.state.get(p, {})
+                buf = st.get("momentum_buffer")
+                if buf is not None:
+                    self._views[p].copy_(buf)
+                    st["momentum_buffer"] = self._views[p]
+                    any_buf = True
+            self._initialized = any_buf
+
+
+# ====================================================================== bench trainer
+class NativeTrainer:
+    engine = "native"
+
+    def __init__(self, arch, batch, dtype, device, world=1, rank=0, bucket_mb=32.0, image_size=224):
+        from .resnet import build_model
+        from ..data.synthetic import SyntheticImageNet
+        torch.manual_seed(0)
+        ref = build_model(arch)
+        self.model = NativeResNet(ref, device=device, dtype=dtype, image_size=image_size)
+        self.net = self.model
+        if world > 1:
+            from ..parallel.ddp import DistributedDataParallel
+            self.net = DistributedDataParallel(self.model, bucket_cap_mb=bucket_mb)
+        self.opt = self.model.make_optimizer(lr=0.1, momentum=0.9, weight_decay=1e-4)
+        self.crit = self.model.make_criterion()
+        self.ds = SyntheticImageNet("train", seed=0, image_size=image_size)
+        self.gen = self.model.input_generator(self.ds)
+        self.batch, self.world, self.rank, self.device = batch, world, rank, device
+        self.scaler = None
+        if dtype == torch.float16:
+            from ..amp import LossScaler
+            self.scaler = LossScaler()
+        self._loss = None
+
+    def step(self, i: int) -> None:
+        ids = torch.arange(self.batch, dtype=torch.int64) + (i * self.world + self.rank) * self.batch
+        x, y = self.gen(ids)
+        out = self.net(x)
+        loss = self.crit(out, y)
+        if self.scaler is not None:
+            self.scaler.scale(loss).backward()
+            self.scaler.step(self.opt)
+            self.scaler.update()
+        else:
+            loss.backward()
+            self.opt.step()
+        self.opt.zero_grad()
+        self._loss = loss.detach()
+
+    def last_loss(self):
+        return None if self._loss is None else float(self._loss.item())

@@ -1,0 +1,116 @@
+"""ctypes bindings to ``_lib/libpda_kernels.so`` (the gfx950 HIP kernels).
+
+The library exposes a C ABI of launchers that take raw device pointers and a
+``hipStream_t``; no torch headers are compiled, so the build is fast and
+ABI-independent of the PyTorch wheel. Every launcher returns the HIP error
+code of the launch, which :func:`_check` turns into an exception -- ops never
+fall back silently to PyTorch on a GPU box (a missing library raises).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from pathlib import Path
+from typing import Optional
+
+import torch
+
+__all__ = ["load", "available", "lib", "DT", "dt_of", "ConvDesc", "BwdArgs", "stream", "ptr"]
+
+_LIB: Optional[C.CDLL] = None
+_ERR: Optional[str] = None
+LIBPATH = Path(__file__).resolve().parent.parent / "_lib" / "libpda_kernels.so"
+
+DT = {torch.float32: 0, torch.bfloat16: 1, torch.float16: 2}
+
+
+def dt_of(t) -> int:
+    return DT[t if isinstance(t, torch.dtype) else t.dtype]
+
+
+class ConvDesc(C.Structure):
+    _fields_ = [(n, C.c_int) for n in
+                ("Nb", "H", "W", "Cin", "Cout", "R", "S", "stride", "pad", "Ho", "Wo")]
+
+
+class BwdArgs(C.Structure):
+    _fields_ = [("g1", C.c_void_p), ("g2", C.c_void_p), ("gp", C.c_void_p), ("HW", C.c_int),
+                ("y", C.c_void_p), ("sc", C.c_void_p), ("sh", C.c_void_p),
+                ("y2", C.c_void_p), ("sc2", C.c_void_p), ("sh2", C.c_void_p),
+                ("mode", C.c_int), ("dz_out", C.c_void_p),
+                ("part", C.c_void_p), ("nq", C.c_int), ("rows", C.c_longlong), ("C", C.c_int)]
+
+
+_V, _I, _F, _L, _U = C.c_void_p, C.c_int, C.c_float, C.c_longlong, C.c_uint
+_SIGS = {
+    "pda_conv_fwd": [C.POINTER(ConvDesc), _V, _V, _I, _V, _I, _I, _V, _V, _I, _I, _I, _I, _V],
+    "pda_conv_dgrad": [C.POINTER(ConvDesc), _V, _V, _V, _I, _I, _I, _V],
+    "pda_conv_wgrad": [C.POINTER(ConvDesc), _V, _V, _V, _I, _I, _I, _I, _I, _V],
+    "pda_wgrad_reduce": [_V, _V, _I, _I, _I, _I, _I, _I, _F, _I, _V],
+    "pda_bn_finalize_fwd": [_V, _I, _I, _F, _V, _V, _F, _F, _V, _V, _V, _V, _V, _V, _V, _I, _V],
+    "pda_bn_eval_coeffs": [_V, _V, _V, _V, _F, _I, _V, _V, _V],
+    "pda_bn_apply": [_V, _V, _V, _V, _V, _V, _V, _L, _I, _I, _I, _I, _V],
+    "pda_stem_pool": [_V, _V, _V, _V, _V, _I, _I, _I, _I, _I, _I, _I, _V],
+    "pda_maxpool_bwd": [_V, _V, _V, _V, _I, _I, _I, _I, _I, _I, _I, _V],
+    "pda_tail_pool": [_V, _V, _V, _V, _V, _V, _V, _I, _I, _I, _I, _I, _V],
+    "pda_bn_bwd_reduce": [C.POINTER(BwdArgs), _I, _I, _V],
+    "pda_bn_bwd_finalize": [_V, _I, _I, _I, _I, _F, _V, _V, _V, _V, _V, _V, _V, _V, _F, _I, _V],
+    "pda_bn_bwd_apply": [C.POINTER(BwdArgs), _V, _V, _V, _V, _V, _V, _I, _V],
+    "pda_xent": [_V, _I, _I, _I, _V, _V, _V, _V, _I, _F, _V, _I, _I, _V],
+    "pda_topk": [_V, _I, _I, _I, _V, _V, _V],
+    "pda_col_sum": [_V, _I, _I, _I, _F, _V, _I, _I, _V],
+    "pda_sgd_flat": [_V, _V, _V, _V, _L, _F, _F, _F, _V, _V, _I, _I, _V],
+    "pda_cast_flat": [_V, _V, _L, _I, _V],
+    "pda_amp_check": [_V, _L, _V, _V],
+    "pda_amp_update": [_V, _V, _V, _F, _F, _I, _V],
+    "pda_pack_stem": [_V, _V, _I, _I, _I, _I, _I, _I, _V],
+    "pda_synth": [_V, _I, _U, _I, _V, _V, _I, _V, _I, _V],
+    "pda_nchw_to_nhwc8": [_V, _I, _I, _I, _I, _V, _I, _V],
+}
+
+
+def load(required: bool = False) -> Optional[C.CDLL]:
+    global _LIB, _ERR
+    if _LIB is not None:
+        return _LIB
+    if not LIBPATH.exists() and os.environ.get("PDA_NO_BUILD") != "1":
+        try:
+            from .. import _build
+            _build.build_kernels()
+        except Exception as e:  # pragma: no cover
+            _ERR = f"build failed: {e}"
+    try:
+        lib = C.CDLL(str(LIBPATH))
+        for name, argt in _SIGS.items():
+            fn = getattr(lib, name)
+            fn.argtypes = argt
+            fn.restype = C.c_int
+        _LIB = lib
+    except OSError as e:
+        _ERR = str(e)
+        if required:
+            raise RuntimeError(f"native kernels unavailable: {_ERR}") from e
+    return _LIB
+
+
+def available() -> bool:
+    return load() is not None
+
+
+def lib() -> C.CDLL:
+    l = load(required=True)
+    assert l is not None
+    return l
+
+
+def stream(device=None) -> int:
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+def ptr(t: Optional[torch.Tensor]):
+    return None if t is None else t.data_ptr()
+
+
+def check(rc: int, what: str) -> None:
+    if rc != 0:
+        raise RuntimeError(f"{what} failed with HIP error {rc}")

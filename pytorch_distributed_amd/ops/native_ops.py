@@ -1,0 +1,337 @@
+"""Op-level Python API over the gfx950 kernels (torch tensors in, torch tensors out).
+
+Layout conventions: activations are NHWC 16-bit (bf16 or f16) tensors of shape
+``[N, H, W, C]``; conv weights are 16-bit OHWI ``[Cout, R, S, Cin]`` (the stem
+uses a packed ``[64, 448]`` image, see :func:`pack_stem`); statistics, BN
+parameters, gradients and the optimizer state are f32.
+
+These functions are what the native ResNet engine
+(:mod:`pytorch_distributed_amd.models.native`) schedules, and what the GPU
+numerics tests compare against plain PyTorch fp32 references.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import math
+from dataclasses import dataclass
+from typing import Optional, Tuple
+
+import torch
+
+from . import ext
+from .ext import ConvDesc, BwdArgs, check, dt_of, ptr, stream
+
+__all__ = [
+    "ConvGeom", "conv_fwd", "conv_dgrad", "conv_wgrad", "pick_tile", "wgrad_plan",
+    "bn_finalize_fwd", "bn_eval_coeffs", "bn_apply", "stem_pool", "maxpool_bwd", "tail_pool",
+    "bn_bwd", "xent", "topk_hits", "col_sum", "sgd_flat", "cast_flat", "amp_check", "amp_update",
+    "pack_stem", "synth_batch", "nchw_to_nhwc8", "Workspace",
+]
+
+
+@dataclass(frozen=True)
+class ConvGeom:
+    Nb: int
+    H: int
+    W: int
+    Cin: int     # channels of the stored input (stem: 8, padded from 3)
+    Cout: int
+    R: int
+    S: int
+    stride: int
+    pad: int
+
+    @property
+    def Ho(self) -> int:
+        return (self.H + 2 * self.pad - self.R) // self.stride + 1
+
+    @property
+    def Wo(self) -> int:
+        return (self.W + 2 * self.pad - self.S) // self.stride + 1
+
+    def desc(self, Nb: Optional[int] = None) -> ConvDesc:
+        return ConvDesc(self.Nb if Nb is None else Nb, self.H, self.W, self.Cin, self.Cout, self.R,
+                        self.S, self.stride, self.pad, self.Ho, self.Wo)
+
+    def with_batch(self, Nb: int) -> "ConvGeom":
+        return ConvGeom(Nb, self.H, self.W, self.Cin, self.Cout, self.R, self.S, self.stride, self.pad)
+
+
+class Workspace:
+    """Grow-only scratch buffers (split-K slabs, BN partials) reused by every layer on a stream."""
+
+    def __init__(self, device) -> None:
+        self.device = device
+        self._bufs = {}
+
+    def get(self, name: str, numel: int, dtype=torch.float32) -> torch.Tensor:
+        b = self._bufs.get(name)
+        if b is None or b.numel() < numel or b.dtype != dtype:
+            b = torch.empty(max(numel, 1), dtype=dtype, device=self.device)
+            self._bufs[name] = b
+        return b[:numel]
+
+
+_NUM_CU = 256
+
+
+def pick_tile(M: int, N: int) -> Tuple[int, int]:
+    bn = 64 if N <= 64 else 128
+    bm = 128
+    if math.ceil(M / 128) * math.ceil(N / bn) < 2 * _NUM_CU:
+        bm = 64
+    return bm, bn
+
+
+# ------------------------------------------------------------------ conv
+def conv_fwd(x: torch.Tensor, w: torch.Tensor, g: ConvGeom, out: torch.Tensor,
+             stats: Optional[torch.Tensor] = None, bias: Optional[torch.Tensor] = None,
+             relu: bool = False, tile: Optional[Tuple[int, int]] = None) -> torch.Tensor:
+    """out[M, Cout] (16-bit or f32) = conv(x, w). w: [Cout, Kpad] 16-bit, Kpad = w.shape[1].
+    stats (f32, >= ceil(M/bm)*2*Cout) receives per-M-tile (sum, sumsq) partials."""
+    Nb = x.shape[0]
+    M = Nb * g.Ho * g.Wo
+    bm, bn = tile or pick_tile(M, g.Cout)
+    Kpad = w.shape[-1] if w.dim() == 2 else w[0].numel()
+    d = g.desc(Nb)
+    out_f32 = out.dtype == torch.float32
+    pitch = out.stride(0) if out.dim() == 2 else g.Cout
+    rc = ext.lib().pda_conv_fwd(C.byref(d), ptr(x), ptr(w), Kpad, ptr(out), int(out_f32), pitch,
+                                ptr(bias), ptr(stats), int(relu), dt_of(x), bm, bn,
+                                stream(x.device))
+    check(rc, "conv_fwd")
+    return out
+
+
+def stats_tiles(M: int, Cout: int, tile: Optional[Tuple[int, int]] = None) -> int:
+    bm, _ = tile or pick_tile(M, Cout)
+    return math.ceil(M / bm)
+
+
+def conv_dgrad(dy: torch.Tensor, w: torch.Tensor, g: ConvGeom, dx: torch.Tensor,
+               tile: Optional[Tuple[int, int]] = None) -> torch.Tensor:
+    """dx[Nb,H,W,Cin] = conv_transpose(dy[Nb,Ho,Wo,Cout], w[Cout,R,S,Cin])."""
+    Nb = dy.shape[0]
+    M = Nb * (g.H // g.stride) * (g.W // g.stride)
+    bm, bn = tile or pick_tile(M * g.stride * g.stride, g.Cin)
+    d = g.desc(Nb)
+    rc = ext.lib().pda_conv_dgrad(C.byref(d), ptr(dy), ptr(w), ptr(dx), dt_of(dy), bm, bn,
+                                  stream(dy.device))
+    check(rc, "conv_dgrad")
+    return dx
+
+
+def wgrad_plan(g: ConvGeom, Nb: int, tile: Optional[Tuple[int, int]] = None,
+               target_blocks: int = 2 * _NUM_CU, max_slab_bytes: int = 64 << 20):
+    M, N, K = g.Cout, g.R * g.S * g.Cin, Nb * g.Ho * g.Wo
+    bm = 128 if M >= 128 else 64
+    bn = 128 if N >= 128 else 64
+    if tile:
+        bm, bn = tile
+    tiles = math.ceil(M / bm) * math.ceil(N / bn)
+    splits = max(1, min(math.ceil(target_blocks / tiles), math.ceil(K / 256),
+                        max(1, max_slab_bytes // (M * N * 4))))
+    k_chunk = math.ceil(K / splits / 64) * 64
+    splits = math.ceil(K / k_chunk)
+    return bm, bn, splits, k_chunk
+
+
+def conv_wgrad(dy: torch.Tensor, x: torch.Tensor, g: ConvGeom, grad: torch.Tensor, ws: Workspace,
+               cin_real: Optional[int] = None, scale: float = 1.0, accumulate: bool = False,
+               tile: Optional[Tuple[int, int]] = None) -> torch.Tensor:
+    """grad (f32, OHWI with cin_real channels, rows of pitch R*S*cin_real) = scale * dW."""
+    Nb = dy.shape[0]
+    bm, bn, splits, k_chunk = wgrad_plan(g, Nb, tile)
+    M, N = g.Cout, g.R * g.S * g.Cin
+    slab = ws.get("wgrad_slab", splits * M * N)
+    d = g.desc(Nb)
+    st = stream(dy.device)
+    rc = ext.lib().pda_conv_wgrad(C.byref(d), ptr(dy), ptr(x), ptr(slab), splits, k_chunk, dt_of(dy),
+                                  bm, bn, st)
+    check(rc, "conv_wgrad")
+    cr = g.Cin if cin_real is None else cin_real
+    rc = ext.lib().pda_wgrad_reduce(ptr(slab), ptr(grad), splits, M, N, int(math.log2(g.Cin)), cr,
+                                    g.R * g.S * cr, float(scale), int(accumulate), st)
+    check(rc, "wgrad_reduce")
+    return grad
+
+
+# ------------------------------------------------------------------ batchnorm
+def bn_finalize_fwd(part: torch.Tensor, T: int, C_: int, count: int, gamma, beta, eps, momentum,
+                    mean, invstd, scale, shift, rmean=None, rvar=None, nbt=None,
+                    update_running: bool = True) -> None:
+    rc = ext.lib().pda_bn_finalize_fwd(ptr(part), T, C_, float(count), ptr(gamma), ptr(beta),
+                                       float(eps), float(momentum), ptr(mean), ptr(invstd), ptr(scale),
+                                       ptr(shift), ptr(rmean), ptr(rvar), ptr(nbt),
+                                       int(update_running), stream(part.device))
+    check(rc, "bn_finalize_fwd")
+
+
+def bn_eval_coeffs(gamma, beta, rmean, rvar, eps, scale, shift) -> None:
+    rc = ext.lib().pda_bn_eval_coeffs(ptr(gamma), ptr(beta), ptr(rmean), ptr(rvar), float(eps),
+                                      gamma.numel(), ptr(scale), ptr(shift), stream(gamma.device))
+    check(rc, "bn_eval_coeffs")
+
+
+def bn_apply(y, scale, shift, out, res=None, y2=None, scale2=None, shift2=None, relu=True):
+    mode = 2 if y2 is not None else (1 if res is not None else 0)
+    r2 = y2 if y2 is not None else res
+    rc = ext.lib().pda_bn_apply(ptr(y), ptr(scale), ptr(shift), ptr(r2), ptr(scale2), ptr(shift2),
+                                ptr(out), y.numel(), y.shape[-1], mode, int(relu), dt_of(y),
+                                stream(y.device))
+    check(rc, "bn_apply")
+    return out
+
+
+def stem_pool(y, scale, shift, out, arg):
+    N, H, W, C_ = y.shape
+    Ho, Wo = out.shape[1], out.shape[2]
+    rc = ext.lib().pda_stem_pool(ptr(y), ptr(scale), ptr(shift), ptr(out), ptr(arg), N, H, W, C_, Ho,
+                                 Wo, dt_of(y), stream(y.device))
+    check(rc, "stem_pool")
+    return out
+
+
+def maxpool_bwd(dout, arg, din, dout2=None):
+    N, H, W, C_ = din.shape
+    Ho, Wo = dout.shape[1], dout.shape[2]
+    rc = ext.lib().pda_maxpool_bwd(ptr(dout), ptr(dout2), ptr(arg), ptr(din), N, H, W, C_, Ho, Wo,
+                                   dt_of(din), stream(din.device))
+    check(rc, "maxpool_bwd")
+    return din
+
+
+def tail_pool(y, scale, shift, out, res=None, y2=None, scale2=None, shift2=None):
+    N, H, W, C_ = y.shape
+    mode = 2 if y2 is not None else 1
+    r2 = y2 if y2 is not None else res
+    rc = ext.lib().pda_tail_pool(ptr(y), ptr(scale), ptr(shift), ptr(r2), ptr(scale2), ptr(shift2),
+                                 ptr(out), N, H * W, C_, mode, dt_of(y), stream(y.device))
+    check(rc, "tail_pool")
+    return out
+
+
+def _reduce_blocks(rows: int, C_: int) -> int:
+    tpr = min(C_ // 8, 256)
+    rpi = 256 // tpr
+    # aim for ~1024 blocks with >= 4 row iterations each
+    return max(1, min(1024, rows // (rpi * 4) or 1))
+
+
+def bn_bwd(ws: Workspace, y, mean, invstd, gamma, scale, shift, dgamma, dbeta, dy_out,
+           g1=None, g2=None, gp=None, res=None, y2=None, mean2=None, invstd2=None, gamma2=None,
+           scale2=None, shift2=None, dgamma2=None, dbeta2=None, dy2_out=None, dz_buf=None,
+           no_mask: bool = False, gscale: float = 1.0, accumulate: bool = False) -> None:
+    """Backward of  a = relu(bn(y) [+ res | + bn2(y2)])  w.r.t. y (and y2).
+
+    The incoming gradient is ``g1 (+ g2)`` or, for the pooled head, ``gp[n][c] / HW``.
+    Writes dgamma/dbeta (f32, * gscale, optionally accumulated) and dy_out (16-bit).
+    With a residual (``res`` or ``y2``) the masked gradient dz is materialised in ``dz_buf``
+    because it is also the gradient of the shortcut input."""
+    N, H, W, C_ = y.shape
+    rows = N * H * W
+    mode = 3 if no_mask else (2 if y2 is not None else (1 if res is not None else 0))
+    nq = 3 if mode == 2 else 2
+    G = _reduce_blocks(rows, C_)
+    part = ws.get("bn_part", G * nq * C_)
+    a = BwdArgs(ptr(g1), ptr(g2), ptr(gp), H * W if gp is not None else 0,
+                ptr(y), ptr(scale), ptr(shift),
+                ptr(y2 if y2 is not None else res), ptr(scale2), ptr(shift2),
+                mode, ptr(dz_buf), ptr(part), nq, rows, C_)
+    st = stream(y.device)
+    L = ext.lib()
+    dt = dt_of(y)
+    check(L.pda_bn_bwd_reduce(C.byref(a), G, dt, st), "bn_bwd_reduce")
+    k = ws.get("bn_k", 6 * C_)
+    check(L.pda_bn_bwd_finalize(ptr(part), G, nq, 1, C_, float(rows), ptr(gamma), ptr(mean),
+                                ptr(invstd), ptr(dgamma), ptr(dbeta), ptr(k[0:C_]),
+                                ptr(k[C_:2 * C_]), ptr(k[2 * C_:3 * C_]), float(gscale),
+                                int(accumulate), st), "bn_bwd_finalize")
+    if mode == 2:
+        check(L.pda_bn_bwd_finalize(ptr(part), G, nq, 2, C_, float(rows), ptr(gamma2), ptr(mean2),
+                                    ptr(invstd2), ptr(dgamma2), ptr(dbeta2), ptr(k[3 * C_:4 * C_]),
+                                    ptr(k[4 * C_:5 * C_]), ptr(k[5 * C_:6 * C_]), float(gscale),
+                                    int(accumulate), st), "bn_bwd_finalize2")
+    dz_in = dz_buf if mode in (1, 2) else None
+    check(L.pda_bn_bwd_apply(C.byref(a), ptr(dz_in), ptr(y), ptr(k[0:C_]), ptr(k[C_:2 * C_]),
+                             ptr(k[2 * C_:3 * C_]), ptr(dy_out), dt, st), "bn_bwd_apply")
+    if mode == 2:
+        check(L.pda_bn_bwd_apply(C.byref(a), ptr(dz_buf), ptr(y2), ptr(k[3 * C_:4 * C_]),
+                                 ptr(k[4 * C_:5 * C_]), ptr(k[5 * C_:6 * C_]), ptr(dy2_out), dt, st),
+              "bn_bwd_apply2")
+
+
+# ------------------------------------------------------------------ head / loss
+def xent(logits: torch.Tensor, labels: torch.Tensor, loss_rows, loss, dlog=None,
+         gscale: float = 1.0, gdev: Optional[torch.Tensor] = None) -> None:
+    """loss_rows/loss (nullable) = CE(logits, labels); dlog (16-bit [B, ld]) = d(mean CE)/dlogits
+    * gscale * gdev[0] (zero in the padding columns)."""
+    B, K = logits.shape[0], logits.shape[1]
+    ld_out = dlog.shape[1] if dlog is not None else 0
+    dt = dt_of(dlog) if dlog is not None else 1
+    rc = ext.lib().pda_xent(ptr(logits), B, K, logits.stride(0), ptr(labels), ptr(loss_rows), ptr(loss),
+                            ptr(dlog), ld_out, float(gscale), ptr(gdev), dt, int(dlog is not None),
+                            stream(logits.device))
+    check(rc, "xent")
+
+
+def topk_hits(logits, labels, hits) -> None:
+    B, K = logits.shape
+    rc = ext.lib().pda_topk(ptr(logits), B, K, logits.stride(0), ptr(labels), ptr(hits),
+                            stream(logits.device))
+    check(rc, "topk")
+
+
+def col_sum(x, C_: int, out, scale: float = 1.0, accumulate: bool = False) -> None:
+    rc = ext.lib().pda_col_sum(ptr(x), x.shape[0], C_, x.stride(0), float(scale), ptr(out), dt_of(x),
+                               int(accumulate), stream(x.device))
+    check(rc, "col_sum")
+
+
+# ------------------------------------------------------------------ optimizer / amp
+def sgd_flat(p, g, buf, shadow, lr, momentum, wd, initialized: bool, scale=None, found_inf=None):
+    flags = (1 if initialized else 0) | (2 if shadow is not None else 0)
+    dt = dt_of(shadow) if shadow is not None else 1
+    rc = ext.lib().pda_sgd_flat(ptr(p), ptr(g), ptr(buf), ptr(shadow), p.numel(), float(lr),
+                                float(momentum), float(wd), ptr(scale), ptr(found_inf), flags, dt,
+                                stream(p.device))
+    check(rc, "sgd_flat")
+
+
+def cast_flat(p, shadow) -> None:
+    rc = ext.lib().pda_cast_flat(ptr(p), ptr(shadow), p.numel(), dt_of(shadow), stream(p.device))
+    check(rc, "cast_flat")
+
+
+def amp_check(g, found_inf) -> None:
+    check(ext.lib().pda_amp_check(ptr(g), g.numel(), ptr(found_inf), stream(g.device)), "amp_check")
+
+
+def amp_update(scale, tracker, found_inf, growth=2.0, backoff=0.5, interval=2000) -> None:
+    check(ext.lib().pda_amp_update(ptr(scale), ptr(tracker), ptr(found_inf), float(growth),
+                                   float(backoff), int(interval), stream(scale.device)), "amp_update")
+
+
+def pack_stem(src_ohwi, dst, Cout=64, RS=49, Cin=3, Cpad=8) -> None:
+    Kpad = dst.shape[1]
+    check(ext.lib().pda_pack_stem(ptr(src_ohwi), ptr(dst), Cout, RS, Cin, Cpad, Kpad, dt_of(dst),
+                                  stream(dst.device)), "pack_stem")
+
+
+# ------------------------------------------------------------------ data
+def synth_salt(seed: int, split: str) -> int:
+    from ..data.synthetic import SPLIT_ID
+    return ((seed * 97 + SPLIT_ID[split]) * 0x632BE5AB) & 0xFFFFFFFF
+
+
+def synth_batch(ids: torch.Tensor, seed: int, split: str, num_classes: int, S: int, out, labels,
+                keys) -> None:
+    B = ids.numel()
+    check(ext.lib().pda_synth(ptr(ids), B, synth_salt(seed, split), num_classes, ptr(keys),
+                              ptr(labels), S, ptr(out), dt_of(out), stream(out.device)), "synth")
+
+
+def nchw_to_nhwc8(x, out) -> None:
+    B, C_, H, W = x.shape
+    check(ext.lib().pda_nchw_to_nhwc8(ptr(x), B, C_, H, W, ptr(out), dt_of(out), stream(x.device)),
+          "nchw_to_nhwc8")

@@ -1,0 +1,332 @@
+"""T2 tier: numerics of every gfx950 kernel against plain PyTorch fp32 references.
+
+Inputs are asymmetric random data rounded to the kernel's 16-bit dtype first, so the
+reference sees exactly the kernel's inputs; tolerances are relative to the output scale.
+"""
+import math
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+
+
+def _k():
+    from pytorch_distributed_amd.ops import ext
+    ext.load(required=True)
+    from pytorch_distributed_amd.ops import native_ops as K
+    return K
+
+
+def rel_err(a, b):
+    a = a.float()
+    b = b.float()
+    return ((a - b).norm() / (b.norm() + 1e-12)).item()
+
+
+CONV_CASES = [
+    # Nb, H, Cin, Cout, k, stride
+    (2, 8, 64, 64, 1, 1),
+    (2, 8, 64, 128, 3, 1),
+    (3, 9, 64, 64, 3, 1),       # ragged M
+    (2, 8, 128, 64, 3, 2),
+    (2, 8, 64, 256, 1, 2),
+    (2, 14, 256, 128, 1, 1),
+    (1, 7, 512, 2048, 1, 1),
+    (4, 4, 1024, 256, 1, 1),
+]
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("case", CONV_CASES)
+def test_conv_fwd_dgrad_wgrad(case, dtype):
+    K = _k()
+    Nb, H, Cin, Cout, k, s = case
+    pad = k // 2
+    torch.manual_seed(0)
+    x = (torch.randn(Nb, Cin, H, H, device=DEV) + 0.1).to(dtype).float()
+    w = (torch.randn(Cout, Cin, k, k, device=DEV) / math.sqrt(Cin * k * k)).to(dtype).float()
+    y_ref = F.conv2d(x, w, stride=s, padding=pad)
+    g = K.ConvGeom(Nb, H, H, Cin, Cout, k, k, s, pad)
+    x_nhwc = x.permute(0, 2, 3, 1).contiguous().to(dtype)
+    w_ohwi = w.permute(0, 2, 3, 1).contiguous().to(dtype)
+    y = torch.empty(Nb, g.Ho, g.Wo, Cout, device=DEV, dtype=dtype)
+    M = Nb * g.Ho * g.Wo
+    T = K.stats_tiles(M, Cout)
+    stats = torch.zeros(T * 2 * Cout, device=DEV)
+    K.conv_fwd(x_nhwc, w_ohwi.view(Cout, -1), g, y, stats=stats)
+    torch.cuda.synchronize()
+    yr = y_ref.permute(0, 2, 3, 1)
+    assert rel_err(y, yr) < 1e-2
+    st = stats.view(T, 2, Cout).sum(0)
+    yb = y.float().reshape(-1, Cout)
+    torch.testing.assert_close(st[0], yb.sum(0), rtol=1e-3, atol=1e-2)
+    torch.testing.assert_close(st[1], (yb * yb).sum(0), rtol=1e-3, atol=1e-2)
+    # backward
+    dy = torch.randn_like(y_ref).to(dtype).float()
+    xr = x.clone().requires_grad_(True)
+    wr = w.clone().requires_grad_(True)
+    F.conv2d(xr, wr, stride=s, padding=pad).backward(dy)
+    dy_nhwc = dy.permute(0, 2, 3, 1).contiguous().to(dtype)
+    dx = torch.full((Nb, H, H, Cin), float("nan"), device=DEV, dtype=dtype)
+    K.conv_dgrad(dy_nhwc, w_ohwi, g, dx)
+    ws = K.Workspace(DEV)
+    dw = torch.zeros(Cout, k, k, Cin, device=DEV)
+    K.conv_wgrad(dy_nhwc, x_nhwc, g, dw.view(-1), ws)
+    torch.cuda.synchronize()
+    assert rel_err(dx, xr.grad.permute(0, 2, 3, 1)) < 1e-2
+    assert rel_err(dw, wr.grad.permute(0, 2, 3, 1)) < 1e-2
+
+
+def test_conv_stem_padded_cin():
+    K = _k()
+    dtype = torch.bfloat16
+    Nb, H = 2, 32
+    torch.manual_seed(1)
+    x = torch.randn(Nb, 3, H, H, device=DEV).to(dtype).float()
+    w = (torch.randn(64, 3, 7, 7, device=DEV) * 0.05).to(dtype).float()
+    y_ref = F.conv2d(x, w, stride=2, padding=3)
+    x8 = torch.zeros(Nb, H, H, 8, device=DEV, dtype=dtype)
+    x8[..., :3] = x.permute(0, 2, 3, 1).to(dtype)
+    packed = torch.zeros(64, 448, device=DEV, dtype=dtype)
+    K.pack_stem(w.permute(0, 2, 3, 1).contiguous(), packed)
+    g = K.ConvGeom(Nb, H, H, 8, 64, 7, 7, 2, 3)
+    y = torch.empty(Nb, g.Ho, g.Wo, 64, device=DEV, dtype=dtype)
+    K.conv_fwd(x8, packed, g, y)
+    dy = torch.randn_like(y_ref).to(dtype).float()
+    wr = w.clone().requires_grad_(True)
+    F.conv2d(x, wr, stride=2, padding=3).backward(dy)
+    dw = torch.zeros(64, 7, 7, 3, device=DEV)
+    K.conv_wgrad(dy.permute(0, 2, 3, 1).contiguous().to(dtype), x8, g, dw.view(-1), K.Workspace(DEV),
+                 cin_real=3)
+    torch.cuda.synchronize()
+    assert rel_err(y, y_ref.permute(0, 2, 3, 1)) < 1e-2
+    assert rel_err(dw, wr.grad.permute(0, 2, 3, 1)) < 1e-2
+
+
+def test_fc_as_conv():
+    K = _k()
+    dtype = torch.bfloat16
+    B, Fd, Cls, rows = 5, 256, 100, 128
+    x = torch.randn(B, Fd, device=DEV).to(dtype)
+    w = torch.zeros(rows, Fd, device=DEV, dtype=dtype)
+    w[:Cls] = (torch.randn(Cls, Fd, device=DEV) * 0.05).to(dtype)
+    b = torch.randn(Cls, device=DEV)
+    out = torch.empty(B, Cls, device=DEV)
+    g = K.ConvGeom(B, 1, 1, Fd, Cls, 1, 1, 1, 0)
+    K.conv_fwd(x, w, g, out, bias=b)
+    torch.cuda.synchronize()
+    ref = x.float() @ w[:Cls].float().t() + b
+    assert rel_err(out, ref) < 1e-2
+
+
+def _bn_ref(y, gamma, beta, eps=1e-5):
+    mean = y.mean((0, 1, 2))
+    var = y.var((0, 1, 2), unbiased=False)
+    return mean, var, (y - mean) / torch.sqrt(var + eps) * gamma + beta
+
+
+def test_bn_forward_finalize_apply():
+    K = _k()
+    dtype = torch.bfloat16
+    N, H, C = 4, 6, 128
+    y = (torch.randn(N, H, H, C, device=DEV) * 2 + 0.5).to(dtype)
+    gamma = torch.rand(C, device=DEV) + 0.5
+    beta = torch.randn(C, device=DEV)
+    part = y.float().reshape(-1, C)
+    T = 3
+    rows = part.shape[0]
+    chunks = torch.tensor_split(part, T, 0)
+    stats = torch.stack([torch.stack([c.sum(0), (c * c).sum(0)]) for c in chunks]).contiguous()
+    st = torch.zeros(4, C, device=DEV)
+    rm = torch.zeros(C, device=DEV)
+    rv = torch.ones(C, device=DEV)
+    nbt = torch.zeros(1, dtype=torch.int64, device=DEV)
+    K.bn_finalize_fwd(stats, T, C, rows, gamma, beta, 1e-5, 0.1, st[0], st[1], st[2], st[3], rm, rv, nbt)
+    out = torch.empty_like(y)
+    K.bn_apply(y, st[2], st[3], out, relu=True)
+    torch.cuda.synchronize()
+    mean, var, ref = _bn_ref(y.float(), gamma, beta)
+    torch.testing.assert_close(st[0], mean, rtol=1e-4, atol=1e-4)
+    torch.testing.assert_close(st[1], 1 / torch.sqrt(var + 1e-5), rtol=1e-4, atol=1e-4)
+    assert rel_err(out, torch.relu(ref)) < 1e-2
+    torch.testing.assert_close(rm, 0.1 * mean, rtol=1e-4, atol=1e-5)
+    torch.testing.assert_close(rv, 0.9 + 0.1 * var * rows / (rows - 1), rtol=1e-4, atol=1e-5)
+    assert int(nbt.item()) == 1
+
+
+@pytest.mark.parametrize("mode", ["relu", "res", "ds"])
+def test_bn_backward(mode):
+    K = _k()
+    dtype = torch.bfloat16
+    N, H, C = 4, 7, 64
+    torch.manual_seed(3)
+    y = (torch.randn(N, H, H, C, device=DEV) + 0.3).to(dtype)
+    y2 = (torch.randn(N, H, H, C, device=DEV) - 0.2).to(dtype)
+    g_in = torch.randn(N, H, H, C, device=DEV).to(dtype)
+    gamma = torch.rand(C, device=DEV) + 0.5
+    beta = torch.randn(C, device=DEV) * 0.1
+    gamma2 = torch.rand(C, device=DEV) + 0.5
+    beta2 = torch.randn(C, device=DEV) * 0.1
+    # reference with autograd (train-mode batch stats)
+    yr = y.float().requires_grad_(True)
+    y2r = y2.float().requires_grad_(True)
+    gr = gamma.clone().requires_grad_(True)
+    br = beta.clone().requires_grad_(True)
+    g2r = gamma2.clone().requires_grad_(True)
+    b2r = beta2.clone().requires_grad_(True)
+    _, _, z = _bn_ref(yr, gr, br)
+    if mode == "res":
+        z = z + y2r
+    elif mode == "ds":
+        z = z + _bn_ref(y2r, g2r, b2r)[2]
+    torch.relu(z).backward(g_in.float())
+    # kernel
+    ws = K.Workspace(DEV)
+
+    def coeffs(t, ga, be):
+        m = t.float().mean((0, 1, 2))
+        v = t.float().var((0, 1, 2), unbiased=False)
+        inv = 1 / torch.sqrt(v + 1e-5)
+        return m, inv, ga * inv, be - m * ga * inv
+
+    m1, i1, s1, h1 = coeffs(y, gamma, beta)
+    m2, i2, s2, h2 = coeffs(y2, gamma2, beta2)
+    dg = torch.zeros(C, device=DEV)
+    db = torch.zeros(C, device=DEV)
+    dg2 = torch.zeros(C, device=DEV)
+    db2 = torch.zeros(C, device=DEV)
+    dy = torch.empty_like(y)
+    dy2 = torch.empty_like(y)
+    dz = torch.empty_like(y)
+    if mode == "relu":
+        K.bn_bwd(ws, y, m1, i1, gamma, s1, h1, dg, db, dy, g1=g_in)
+    elif mode == "res":
+        K.bn_bwd(ws, y, m1, i1, gamma, s1, h1, dg, db, dy, g1=g_in, res=y2, dz_buf=dz)
+    else:
+        K.bn_bwd(ws, y, m1, i1, gamma, s1, h1, dg, db, dy, g1=g_in, y2=y2, mean2=m2, invstd2=i2,
+                 gamma2=gamma2, scale2=s2, shift2=h2, dgamma2=dg2, dbeta2=db2, dy2_out=dy2, dz_buf=dz)
+    torch.cuda.synchronize()
+    assert rel_err(dy, yr.grad) < 2e-2
+    assert rel_err(dg, gr.grad) < 1e-2
+    assert rel_err(db, br.grad) < 1e-2
+    if mode == "res":
+        assert rel_err(dz, y2r.grad) < 1e-2
+    if mode == "ds":
+        assert rel_err(dy2, y2r.grad) < 2e-2
+        assert rel_err(dg2, g2r.grad) < 1e-2
+
+
+def test_stem_pool_and_backward():
+    K = _k()
+    dtype = torch.bfloat16
+    N, H, C = 2, 12, 64
+    y = torch.randn(N, H, H, C, device=DEV).to(dtype)
+    sc = torch.rand(C, device=DEV) + 0.5
+    sh = torch.randn(C, device=DEV) * 0.1
+    Ho = (H + 2 - 3) // 2 + 1
+    out = torch.empty(N, Ho, Ho, C, device=DEV, dtype=dtype)
+    arg = torch.empty(N, Ho, Ho, C, device=DEV, dtype=torch.uint8)
+    K.stem_pool(y, sc, sh, out, arg)
+    a = torch.relu(y.float() * sc + sh).permute(0, 3, 1, 2).requires_grad_(True)
+    ref = F.max_pool2d(a, 3, 2, 1)
+    torch.cuda.synchronize()
+    assert rel_err(out, ref.permute(0, 2, 3, 1)) < 1e-2
+    g = torch.randn_like(ref).to(dtype)
+    ref.backward(g.float())
+    din = torch.empty_like(y)
+    K.maxpool_bwd(g.permute(0, 2, 3, 1).contiguous(), arg, din)
+    torch.cuda.synchronize()
+    # ties between equal relu outputs (zeros) can route to different windows: compare sums
+    torch.testing.assert_close(din.float().sum((1, 2)), a.grad.permute(0, 2, 3, 1).sum((1, 2)),
+                               rtol=2e-2, atol=2e-1)
+
+
+def test_tail_pool():
+    K = _k()
+    dtype = torch.bfloat16
+    N, H, C = 3, 7, 256
+    y = torch.randn(N, H, H, C, device=DEV).to(dtype)
+    r = torch.randn(N, H, H, C, device=DEV).to(dtype)
+    sc = torch.rand(C, device=DEV)
+    sh = torch.randn(C, device=DEV) * 0.1
+    out = torch.empty(N, C, device=DEV, dtype=dtype)
+    K.tail_pool(y, sc, sh, out, res=r)
+    torch.cuda.synchronize()
+    ref = torch.relu(y.float() * sc + sh + r.float()).mean((1, 2))
+    assert rel_err(out, ref) < 1e-2
+
+
+def test_xent_and_topk():
+    K = _k()
+    B, Cls, ld = 37, 1000, 1024
+    logits = torch.randn(B, Cls, device=DEV) * 3
+    labels = torch.randint(0, Cls, (B,), device=DEV)
+    lr = torch.empty(B, device=DEV)
+    loss = torch.empty((), device=DEV)
+    dlog = torch.empty(B, ld, device=DEV, dtype=torch.bfloat16)
+    K.xent(logits, labels, lr, loss, dlog=dlog, gscale=1.0 / B)
+    lref = logits.clone().requires_grad_(True)
+    ce = F.cross_entropy(lref, labels)
+    ce.backward()
+    torch.cuda.synchronize()
+    torch.testing.assert_close(loss, ce.detach(), rtol=1e-4, atol=1e-4)
+    assert rel_err(dlog[:, :Cls], lref.grad) < 1e-2
+    assert dlog[:, Cls:].abs().max().item() == 0
+    hits = torch.zeros(2, device=DEV)
+    K.topk_hits(logits, labels, hits)
+    _, pred = logits.topk(5, -1, True, True)
+    h = pred.eq(labels[:, None])
+    torch.cuda.synchronize()
+    assert hits[0].item() == h[:, :1].sum().item() and hits[1].item() == h.sum().item()
+
+
+def test_sgd_flat_matches_torch():
+    K = _k()
+    n = 1000003
+    p = torch.randn(n, device=DEV)
+    g = torch.randn(n, device=DEV)
+    buf = torch.zeros(n, device=DEV)
+    sh = torch.empty(n, device=DEV, dtype=torch.bfloat16)
+    pr = torch.nn.Parameter(p.clone())
+    opt = torch.optim.SGD([pr], lr=0.1, momentum=0.9, weight_decay=1e-4)
+    for it in range(3):
+        pr.grad = g.clone()
+        opt.step()
+        K.sgd_flat(p, g, buf, sh, 0.1, 0.9, 1e-4, initialized=it > 0)
+    torch.cuda.synchronize()
+    torch.testing.assert_close(p, pr.detach(), rtol=1e-6, atol=1e-6)
+    torch.testing.assert_close(sh.float(), p.to(torch.bfloat16).float())
+    # AMP: skipped when found_inf is set, unscaled otherwise
+    scale = torch.tensor([4.0], device=DEV)
+    inf = torch.ones(1, device=DEV)
+    before = p.clone()
+    K.sgd_flat(p, g, buf, sh, 0.1, 0.9, 1e-4, True, scale=scale, found_inf=inf)
+    torch.cuda.synchronize()
+    assert torch.equal(before, p)
+    gg = g.clone()
+    gg[5] = float("inf")
+    fi = torch.zeros(1, device=DEV)
+    K.amp_check(gg, fi)
+    torch.cuda.synchronize()
+    assert fi.item() == 1.0
+
+
+def test_synthetic_kernel_matches_torch_generator():
+    K = _k()
+    from pytorch_distributed_amd.data.synthetic import synthetic_images
+    ids = torch.tensor([0, 7, 1281166, 99], device=DEV)
+    S = 32
+    out = torch.empty(4, S, S, 8, device=DEV, dtype=torch.bfloat16)
+    lab = torch.empty(4, dtype=torch.int64, device=DEV)
+    keys = torch.empty(4, dtype=torch.int32, device=DEV)
+    K.synth_batch(ids, 0, "train", 1000, S, out, lab, keys)
+    xr, yr = synthetic_images(ids.cpu(), 0, "train", 1000, S)
+    torch.cuda.synchronize()
+    assert torch.equal(lab.cpu(), yr)
+    torch.testing.assert_close(out[..., :3].float().cpu(), xr.permute(0, 2, 3, 1).to(torch.bfloat16).float(),
+                               rtol=1e-2, atol=2e-2)
+    assert out[..., 3:].abs().max().item() == 0

@@ -1,0 +1,14 @@
+#!/bin/bash
+# GPU-box script: build in-tree, run GPU tests, smoke, short native bench.
+set -o pipefail
+mkdir -p gpurun_out
+export PYTHONUNBUFFERED=1
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.build()" > gpurun_out/build.log 2>&1 || { echo BUILD FAIL; tail -30 gpurun_out/build.log; exit 1; }
+timeout -k 10 900 python -m pytest tests -m gpu -x -q ${PYTEST_ARGS} > gpurun_out/pytest_gpu.log 2>&1
+rc=$?
+tail -40 gpurun_out/pytest_gpu.log
+[ $rc -ne 0 ] && exit $rc
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 || { tail -30 gpurun_out/smoke.log; exit 1; }
+cat gpurun_out/smoke.log | tail -3
+timeout -k 10 600 python bench.py --engine native --steps 10 --warmup 3 > gpurun_out/bench_native.json 2> gpurun_out/bench_native.err || { tail -30 gpurun_out/bench_native.err; exit 1; }
+cat gpurun_out/bench_native.json
