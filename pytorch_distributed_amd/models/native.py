@@ -374,7 +374,10 @@ class NativeResNet(nn.Module):
     def native_forward(self, x: torch.Tensor, train: bool, save: bool) -> torch.Tensor:
         x = self.prepare_input(x)
         Nb = x.shape[0]
-        saved: Dict = {"x0": x} if save else None
+        # per-unit BN state (mean/invstd/scale/shift) is referenced, not copied, by the saved
+        # context; any later forward overwrites it, which the generation check in backward catches
+        self._state_gen = getattr(self, "_state_gen", 0) + 1
+        saved: Dict = {"x0": x, "gen": self._state_gen} if save else None
         # stem: conv -> bn -> relu -> maxpool (fused)
         y0 = self._conv_bn(self.stem, x, train)
         ph = self.pool_hw
@@ -384,7 +387,7 @@ class NativeResNet(nn.Module):
         K.stem_pool(y0, sc, sh, p, arg)
         if save:
             saved["y0"], saved["arg"] = y0, arg
-            saved["stem_stats"] = self.stem.state.clone()
+            saved["stem_stats"] = self.stem.state
             saved["blocks"] = []
         h = p
         feat = None
@@ -398,7 +401,7 @@ class NativeResNet(nn.Module):
                 y = self._conv_bn(u, a, train)
                 ys.append(y)
                 if save:
-                    rec[f"s{j}"] = u.state.clone()
+                    rec[f"s{j}"] = u.state
                 if j < len(b.units) - 1:
                     sc, sh = self._coeffs(u, train)
                     a = self._empty(*y.shape)
@@ -408,7 +411,7 @@ class NativeResNet(nn.Module):
             if b.ds is not None:
                 yd = self._conv_bn(b.ds, h, train)
                 if save:
-                    rec["sd"] = b.ds.state.clone()
+                    rec["sd"] = b.ds.state
             ul = b.units[-1]
             sc, sh = self._coeffs(ul, train)
             if last:
@@ -444,6 +447,9 @@ class NativeResNet(nn.Module):
         sv = self._fwd_ctx
         if sv is None:
             raise RuntimeError("native backward without a saved forward")
+        if sv["gen"] != self._state_gen:
+            raise RuntimeError("another forward ran between this forward and its backward; the native "
+                               "engine keeps one step of saved state (no retain_graph / interleaving)")
         acc = not self._grads_zero
         red = self._reducer
         if red is not None:

@@ -65,7 +65,10 @@ class ProcessGroupCommunicator(Communicator):
 def make_communicator(device: Optional[torch.device] = None, group=None,
                       prefer_native: bool = True) -> Communicator:
     """Native RCCL communicator on GPU when the extension is built, else process group."""
-    if device is not None and device.type == "cuda" and prefer_native:
+    import os
+    prefer_native = prefer_native and os.environ.get("PDA_COMM", "native") == "native"
+    if device is not None and device.type == "cuda" and prefer_native \
+            and dist.get_backend(group) == "nccl":
         try:
             from .rccl import RcclCommunicator
             return RcclCommunicator(device, group=group)

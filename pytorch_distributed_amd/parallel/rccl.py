@@ -1,0 +1,180 @@
+"""Python side of the native RCCL communicator (``csrc/comm/rccl_comm.cpp``).
+
+Multi-process: the ``ncclUniqueId`` of rank 0 is exchanged through the default
+``torch.distributed`` TCPStore, then every rank runs ``ncclCommInitRank``.
+Collectives run on a dedicated high-priority HIP stream: ``all_reduce_async``
+records an event on the compute stream, makes the comm stream wait on it,
+enqueues ``ncclAllReduce`` and returns a completion event; ``wait`` makes the
+*current* stream wait on that event (the host never blocks). This is how DDP
+gradient buckets overlap the rest of backward.
+
+Single-process multi-GPU (DataParallel): :class:`RcclGroup` wraps
+``ncclCommInitAll`` and issues one grouped collective across all devices.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import itertools
+import os
+from pathlib import Path
+from typing import List, Optional, Sequence
+
+import torch
+import torch.distributed as dist
+
+from .comm import Communicator
+
+__all__ = ["RcclCommunicator", "RcclGroup", "load"]
+
+LIBPATH = Path(__file__).resolve().parent.parent / "_lib" / "libpda_comm.so"
+_LIB: Optional[C.CDLL] = None
+_DT = {torch.float32: 0, torch.bfloat16: 1, torch.float16: 2, torch.int64: 3, torch.float64: 4,
+       torch.int32: 5}
+_OPS = {"sum": 0, "avg": 1, "max": 2, "min": 3}
+_gen = itertools.count()
+
+
+def load() -> C.CDLL:
+    global _LIB
+    if _LIB is None:
+        if not LIBPATH.exists() and os.environ.get("PDA_NO_BUILD") != "1":
+            from .. import _build
+            _build.build_comm()
+        lib = C.CDLL(str(LIBPATH))
+        V, I, Z = C.c_void_p, C.c_int, C.c_size_t
+        sigs = {
+            "pda_comm_unique_id": [C.c_char_p],
+            "pda_comm_init_rank": [C.c_char_p, I, I, I, C.POINTER(V)],
+            "pda_comm_init_all": [C.POINTER(I), I, C.POINTER(V)],
+            "pda_comm_destroy": [V, I],
+            "pda_comm_check": [V],
+            "pda_allreduce": [V, V, V, Z, I, I, V],
+            "pda_broadcast": [V, V, V, Z, I, I, V],
+            "pda_reduce": [V, V, V, Z, I, I, I, V],
+            "pda_allgather": [V, V, V, Z, I, V],
+            "pda_reduce_scatter": [V, V, V, Z, I, I, V],
+            "pda_group_allreduce": [V, C.POINTER(V), Z, I, I, C.POINTER(V)],
+            "pda_group_broadcast": [V, C.POINTER(V), Z, I, I, C.POINTER(V)],
+            "pda_group_reduce": [V, C.POINTER(V), Z, I, I, I, C.POINTER(V)],
+        }
+        for n, a in sigs.items():
+            f = getattr(lib, n)
+            f.argtypes = a
+            f.restype = I
+        lib.pda_comm_error_string.argtypes = [I]
+        lib.pda_comm_error_string.restype = C.c_char_p
+        _LIB = lib
+    return _LIB
+
+
+def _check(rc: int, what: str) -> None:
+    if rc != 0:
+        msg = load().pda_comm_error_string(rc).decode() if rc > 0 else "hip error"
+        raise RuntimeError(f"RCCL {what} failed: {msg} ({rc})")
+
+
+class RcclCommunicator(Communicator):
+    def __init__(self, device: torch.device, group=None, store=None) -> None:
+        if not dist.is_initialized():
+            raise RuntimeError("RcclCommunicator needs an initialised torch.distributed (for the store)")
+        lib = load()
+        self.device = torch.device(device)
+        self.group = group
+        self.rank = dist.get_rank(group)
+        self.world_size = dist.get_world_size(group)
+        store = store if store is not None else dist.distributed_c10d._get_default_store()
+        key = f"pda_rccl_uid_{next(_gen)}"
+        if self.rank == 0:
+            buf = C.create_string_buffer(128)
+            _check(lib.pda_comm_unique_id(buf), "get_unique_id")
+            store.set(key, bytes(buf.raw))
+            uid = bytes(buf.raw)
+        else:
+            uid = store.get(key)
+        self._h = C.c_void_p()
+        _check(lib.pda_comm_init_rank(uid, self.world_size, self.rank, self.device.index,
+                                      C.byref(self._h)), "init_rank")
+        self.stream = torch.cuda.Stream(self.device, priority=-1)
+
+    # async on the comm stream ----------------------------------------------------------
+    def all_reduce_async(self, t: torch.Tensor, op: str = "sum"):
+        cur = torch.cuda.current_stream(self.device)
+        ready = torch.cuda.Event()
+        ready.record(cur)
+        self.stream.wait_event(ready)
+        _check(load().pda_allreduce(self._h, t.data_ptr(), t.data_ptr(), t.numel(), _DT[t.dtype],
+                                    _OPS[op], self.stream.cuda_stream), "allreduce")
+        done = torch.cuda.Event()
+        done.record(self.stream)
+        t.record_stream(self.stream)
+        return done
+
+    def wait(self, handle) -> None:
+        if handle is not None:
+            torch.cuda.current_stream(self.device).wait_event(handle)
+
+    # ordered on the current stream ----------------------------------------------------
+    def broadcast(self, t: torch.Tensor, src: int = 0) -> None:
+        st = torch.cuda.current_stream(self.device).cuda_stream
+        _check(load().pda_broadcast(self._h, t.data_ptr(), t.data_ptr(), t.numel(), _DT[t.dtype], src,
+                                    st), "broadcast")
+
+    def all_reduce(self, t: torch.Tensor, op: str = "sum") -> None:
+        st = torch.cuda.current_stream(self.device).cuda_stream
+        _check(load().pda_allreduce(self._h, t.data_ptr(), t.data_ptr(), t.numel(), _DT[t.dtype],
+                                    _OPS[op], st), "allreduce")
+
+    def reduce(self, t: torch.Tensor, dst: int = 0, op: str = "sum") -> None:
+        st = torch.cuda.current_stream(self.device).cuda_stream
+        _check(load().pda_reduce(self._h, t.data_ptr(), t.data_ptr(), t.numel(), _DT[t.dtype], _OPS[op],
+                                 dst, st), "reduce")
+
+    def all_gather(self, out: torch.Tensor, t: torch.Tensor) -> None:
+        st = torch.cuda.current_stream(self.device).cuda_stream
+        _check(load().pda_allgather(self._h, t.data_ptr(), out.data_ptr(), t.numel(), _DT[t.dtype], st),
+               "allgather")
+
+    def barrier(self) -> None:
+        t = torch.ones(1, device=self.device)
+        self.all_reduce(t)
+        torch.cuda.current_stream(self.device).synchronize()
+
+    def check(self) -> None:
+        """Raise if the communicator saw an asynchronous error (dead peer, network)."""
+        _check(load().pda_comm_check(self._h), "async")
+
+    def close(self, abort: bool = False) -> None:
+        if self._h:
+            load().pda_comm_destroy(self._h, int(abort))
+            self._h = C.c_void_p()
+
+
+class RcclGroup:
+    """In-process communicator over several local GPUs (``ncclCommInitAll``)."""
+
+    def __init__(self, devices: Sequence[int]) -> None:
+        lib = load()
+        self.devices = list(devices)
+        n = len(self.devices)
+        arr = (C.c_int * n)(*self.devices)
+        self._h = C.c_void_p()
+        _check(lib.pda_comm_init_all(arr, n, C.byref(self._h)), "init_all")
+
+    def _streams(self):
+        n = len(self.devices)
+        return (C.c_void_p * n)(*[torch.cuda.current_stream(d).cuda_stream for d in self.devices])
+
+    def _bufs(self, ts: List[torch.Tensor]):
+        return (C.c_void_p * len(ts))(*[t.data_ptr() for t in ts])
+
+    def all_reduce(self, ts: List[torch.Tensor], op: str = "sum") -> None:
+        _check(load().pda_group_allreduce(self._h, self._bufs(ts), ts[0].numel(), _DT[ts[0].dtype],
+                                          _OPS[op], self._streams()), "group_allreduce")
+
+    def broadcast(self, ts: List[torch.Tensor], root: int = 0) -> None:
+        _check(load().pda_group_broadcast(self._h, self._bufs(ts), ts[0].numel(), _DT[ts[0].dtype],
+                                          root, self._streams()), "group_broadcast")
+
+    def reduce(self, ts: List[torch.Tensor], root: int = 0, op: str = "sum") -> None:
+        _check(load().pda_group_reduce(self._h, self._bufs(ts), ts[0].numel(), _DT[ts[0].dtype],
+                                       _OPS[op], root, self._streams()), "group_reduce")

@@ -1,0 +1,53 @@
+"""Summarise a rocprofv3 --kernel-trace CSV: per-step time by kernel family.
+Usage: python tools/prof_summary.py <prof_dir> <num_steps_in_trace>"""
+import csv
+import glob
+import os
+import re
+import sys
+from collections import defaultdict
+
+
+def family(name: str) -> str:
+    n = name
+    m = re.search(r"conv_gemm_kernel<(\d+), (\d+), (\d+), (\d+)>", n) or \
+        re.search(r"conv_gemm_kernelILi(\d+)ELi(\d+)ELi(\d+)ELi(\d+)E", n)
+    if m:
+        p = {"0": "fwd", "1": "dgrad", "2": "wgrad"}[m.group(1)]
+        return f"conv_{p} {m.group(3)}x{m.group(4)}"
+    n = re.sub(r"^void ", "", n)
+    n = n.replace("(anonymous namespace)::", "")
+    if n.startswith("at::native::"):
+        m = re.search(r"at::native::(\w+)<[^,]*, ([\w:]+)", n)
+        return "aten " + (m.group(2).split("::")[-1] if m else n[12:40])
+    n = re.sub(r"[<(].*", "", n)
+    return n[:60]
+
+
+def main():
+    d = sys.argv[1]
+    steps = int(sys.argv[2]) if len(sys.argv) > 2 else 1
+    files = glob.glob(os.path.join(d, "**", "*kernel_trace.csv"), recursive=True)
+    if not files:
+        print("no kernel_trace.csv under", d)
+        return
+    rows = list(csv.DictReader(open(files[0])))
+    tot = defaultdict(float)
+    cnt = defaultdict(int)
+    for r in rows:
+        name = r.get("Kernel_Name") or r.get("KernelName") or ""
+        t = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6
+        f = family(name)
+        tot[f] += t
+        cnt[f] += 1
+    all_ms = sum(tot.values())
+    print(f"# rocprofv3 kernel summary ({files[0].split('/')[-1]})\n")
+    print(f"total GPU kernel time {all_ms:.2f} ms over {steps} steps = {all_ms / steps:.2f} ms/step\n")
+    print("| kernel family | ms/step | % | launches/step |")
+    print("|---|---|---|---|")
+    for f, t in sorted(tot.items(), key=lambda kv: -kv[1]):
+        print(f"| {f} | {t / steps:.3f} | {100 * t / all_ms:.1f} | {cnt[f] / steps:.1f} |")
+
+
+if __name__ == "__main__":
+    main()
