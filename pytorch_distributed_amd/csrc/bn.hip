@@ -453,6 +453,25 @@ __global__ __launch_bounds__(NT) void bn_bwd_apply_kernel(BwdArgs a, const u16* 
   }
 }
 
+// first stage of the statistics reduction: [G][QC] partial slabs -> [S][QC] (S << G), coalesced
+__global__ __launch_bounds__(256) void slab_reduce_kernel(const float* __restrict__ in, int G, int QC,
+                                                          int rows_per, float* __restrict__ out) {
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  if (c >= QC) return;
+  const int g0 = blockIdx.y * rows_per;
+  const int g1 = min(G, g0 + rows_per);
+  float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+  int g = g0;
+  for (; g + 3 < g1; g += 4) {
+    s0 += in[(size_t)g * QC + c];
+    s1 += in[(size_t)(g + 1) * QC + c];
+    s2 += in[(size_t)(g + 2) * QC + c];
+    s3 += in[(size_t)(g + 3) * QC + c];
+  }
+  for (; g < g1; ++g) s0 += in[(size_t)g * QC + c];
+  out[(size_t)blockIdx.y * QC + c] = (s0 + s1) + (s2 + s3);
+}
+
 inline int grid_for(long long n, int cap = 8192) {
   long long b = (n + NT - 1) / NT;
   return (int)(b < 1 ? 1 : (b > cap ? cap : b));
@@ -461,6 +480,14 @@ inline int grid_for(long long n, int cap = 8192) {
 }  // namespace
 
 extern "C" {
+
+int pda_slab_reduce(const float* in, int G, int QC, int S, float* out, hipStream_t st) {
+  const int rows_per = (G + S - 1) / S;
+  const int s = (G + rows_per - 1) / rows_per;
+  hipLaunchKernelGGL(slab_reduce_kernel, dim3((QC + 255) / 256, s), dim3(256), 0, st, in, G, QC, rows_per,
+                     out);
+  return (int)hipGetLastError() ? -1 : s;
+}
 
 int pda_bn_finalize_fwd(const float* part, int T, int C, float count, const float* gamma,
                         const float* beta, float eps, float momentum, float* mean, float* invstd,

@@ -51,6 +51,12 @@ struct ConvParams {
   int taps[4][9];     // DGRAD: tap ids (r*S+s) per parity class
   int Hc, Wc;         // DGRAD: class grid (H/stride, W/stride)
   FastDiv dHcWc, dWc;
+  // DGRAD fused BatchNorm-backward epilogue (emode < 0: plain dX store)
+  int emode, enq;                  // 0 relu(bn(y)), 1 relu(bn(y)+ey2), 2 relu(bn(y)+bn2(ey2))
+  const u16* ey; const float* esc; const float* esh;
+  const u16* ey2; const float* esc2; const float* esh2;
+  const u16* eg2;                  // optional second gradient summed into dA
+  float* epart;                    // [ncls*tiles_m][enq][N] partial sums
 };
 
 // ---------------------------------------------------------------- LDS addressing
@@ -105,7 +111,7 @@ __global__ __launch_bounds__(NT, 2) void conv_gemm_kernel(ConvParams p) {
   constexpr int STAGE = A_BYTES + B_BYTES;
   constexpr int LDS_BYTES = 2 * STAGE;
   static_assert(BM * BN * 2 <= LDS_BYTES, "C tile must fit in the staging buffers");
-  static_assert(2 * NT * 8 * 4 <= LDS_BYTES, "stats reduction must fit");
+  static_assert(3 * NT * 8 * 4 <= LDS_BYTES, "stats reduction must fit");
   __shared__ __attribute__((aligned(16))) char smem[LDS_BYTES];
 
   constexpr bool A_ROW = (PASS != WGRAD);
@@ -377,63 +383,129 @@ __global__ __launch_bounds__(NT, 2) void conv_gemm_kernel(ConvParams p) {
           ct[c_addr(row, col >> 3) * 8 + (col & 7)] = st16<DT>(v);
         }
       }
-    __syncthreads();
-    // coalesced 16-B stores + per-channel partial statistics
+    // coalesced 16-B stores + per-channel partial statistics.
+    //  FWD  (stats): q0 = sum y, q1 = sum y^2 of the written tile (BatchNorm forward statistics).
+    //  DGRAD (emode >= 0): the tile is dA, the gradient of a = relu(bn(y) [+ res | + bn2(y2)]);
+    //        the epilogue adds g2 (second gradient source), applies the ReLU mask recomputed from
+    //        y (and the residual), stores dz instead of dA and emits q0 = sum dz, q1 = sum dz*y,
+    //        q2 = sum dz*y2 -- the BatchNorm-backward reduction, with no extra pass over dA.
+    // The operands of the fused epilogue are prefetched for all of this thread's rows BEFORE the
+    // barrier that publishes the C tile, so their latency overlaps the staging.
     const int cc = tid % CPR;          // column chunk
     const int rg = tid / CPR;          // row group
     constexpr int RG = NT / CPR;       // row groups
-    float s1[8], s2[8];
-#pragma unroll
-    for (int e = 0; e < 8; ++e) { s1[e] = 0.f; s2[e] = 0.f; }
+    constexpr int RPT = BM / RG;       // rows per thread
+    const bool do_stats = (PASS == FWD && p.stats != nullptr);
+    const bool do_bn = (PASS == DGRAD && p.emode >= 0);
+    const int nq = do_bn ? p.enq : 2;
     u16* out = reinterpret_cast<u16*>(p.out);
     const int gcol = n0 + cc * 8;
+    size_t eoff[RPT];
+    bool eok[RPT];
 #pragma unroll
-    for (int i = 0; i < BM / RG; ++i) {
+    for (int i = 0; i < RPT; ++i) {
+      const int grow = m0 + rg + RG * i;
+      eok[i] = grow < p.M && gcol < p.N;
+      size_t orow = grow;
+      if constexpr (PASS == DGRAD) {
+        const uint32_t gg = eok[i] ? grow : 0;
+        const uint32_t img = fdiv(gg, p.dHcWc), rem = gg - img * p.dHcWc.d;
+        const uint32_t yi = fdiv(rem, p.dWc), xi = rem - yi * p.dWc.d;
+        const int h = (int)yi * p.stride + cls_ph, w = (int)xi * p.stride + cls_pw;
+        orow = ((size_t)img * p.H + h) * p.W + w;
+      }
+      eoff[i] = orow * p.out_pitch + gcol;
+    }
+    i32x4 py[RPT], pg2[RPT], py2[RPT];
+    float esc[8], esh[8], esc2[8], esh2[8];
+    if (do_bn) {
+      const i32x4 z = {0, 0, 0, 0};
+#pragma unroll
+      for (int i = 0; i < RPT; ++i) {
+        py[i] = eok[i] ? *reinterpret_cast<const i32x4*>(p.ey + eoff[i]) : z;
+        pg2[i] = (eok[i] && p.eg2) ? *reinterpret_cast<const i32x4*>(p.eg2 + eoff[i]) : z;
+        py2[i] = (eok[i] && p.emode >= 1) ? *reinterpret_cast<const i32x4*>(p.ey2 + eoff[i]) : z;
+      }
+      const int cg = gcol < p.N ? gcol : 0;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        esc[e] = p.esc[cg + e];
+        esh[e] = p.esh[cg + e];
+        esc2[e] = p.emode == 2 ? p.esc2[cg + e] : 0.f;
+        esh2[e] = p.emode == 2 ? p.esh2[cg + e] : 0.f;
+      }
+    }
+    float q0[8], q1[8], q2[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) { q0[e] = 0.f; q1[e] = 0.f; q2[e] = 0.f; }
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < RPT; ++i) {
       const int row = rg + RG * i;
-      const int grow = m0 + row;
       i32x4 v = *reinterpret_cast<const i32x4*>(ct + c_addr(row, cc) * 8);
-      if (grow < p.M && gcol < p.N) {
-        size_t orow;
-        if constexpr (PASS == DGRAD) {
-          const uint32_t img = fdiv(grow, p.dHcWc), rem = grow - img * p.dHcWc.d;
-          const uint32_t yi = fdiv(rem, p.dWc), xi = rem - yi * p.dWc.d;
-          const int h = (int)yi * p.stride + cls_ph, w = (int)xi * p.stride + cls_pw;
-          orow = ((size_t)img * p.H + h) * p.W + w;
-        } else {
-          orow = grow;
-        }
-        *reinterpret_cast<i32x4*>(out + orow * p.out_pitch + gcol) = v;
-        if (PASS == FWD && p.stats) {
+      if (eok[i]) {
+        if (do_bn) {
+          float g[8], yv[8], y2v[8], pre[8];
+          const u16* h = reinterpret_cast<const u16*>(&v);
+          const u16* h2 = reinterpret_cast<const u16*>(&pg2[i]);
+          const u16* hy = reinterpret_cast<const u16*>(&py[i]);
+          const u16* hy2 = reinterpret_cast<const u16*>(&py2[i]);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            g[e] = ld16<DT>(h[e]) + ld16<DT>(h2[e]);
+            yv[e] = ld16<DT>(hy[e]);
+            y2v[e] = ld16<DT>(hy2[e]);
+            pre[e] = yv[e] * esc[e] + esh[e] +
+                     (p.emode == 2 ? y2v[e] * esc2[e] + esh2[e] : (p.emode == 1 ? y2v[e] : 0.f));
+          }
+          u16 dzh[8];
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            const float dz = pre[e] > 0.f ? g[e] : 0.f;
+            dzh[e] = st16<DT>(dz);
+            const float dzr = ld16<DT>(dzh[e]);   // statistics of the stored (rounded) dz
+            q0[e] += dzr;
+            q1[e] += dzr * yv[e];
+            q2[e] += dzr * y2v[e];
+          }
+          v = *reinterpret_cast<const i32x4*>(dzh);
+        } else if (do_stats) {
           const u16* h = reinterpret_cast<const u16*>(&v);
 #pragma unroll
           for (int e = 0; e < 8; ++e) {
             const float f = ld16<DT>(h[e]);
-            s1[e] += f;
-            s2[e] += f * f;
+            q0[e] += f;
+            q1[e] += f * f;
           }
         }
+        *reinterpret_cast<i32x4*>(out + eoff[i]) = v;
       }
     }
-    if (PASS == FWD && p.stats) {
+    if (do_stats || do_bn) {
       __syncthreads();
-      float* red = reinterpret_cast<float*>(smem);  // [RG][BN] x 2
+      float* red = reinterpret_cast<float*>(smem);  // [nq][RG][BN]
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
-        red[rg * BN + cc * 8 + e] = s1[e];
-        red[RG * BN + rg * BN + cc * 8 + e] = s2[e];
+        red[rg * BN + cc * 8 + e] = q0[e];
+        red[RG * BN + rg * BN + cc * 8 + e] = q1[e];
+        if (nq > 2) red[2 * RG * BN + rg * BN + cc * 8 + e] = q2[e];
       }
       __syncthreads();
       if (tid < BN) {
-        float a = 0.f, b = 0.f;
-#pragma unroll
+        float a = 0.f, b = 0.f, c2 = 0.f;
+#pragma unroll 8
         for (int g = 0; g < RG; ++g) {
           a += red[g * BN + tid];
           b += red[RG * BN + g * BN + tid];
+          if (nq > 2) c2 += red[2 * RG * BN + g * BN + tid];
         }
         const int col = n0 + tid;
         if (col < p.N) {
-          p.stats[(size_t)tm * 2 * p.N + col] = a;
-          p.stats[(size_t)tm * 2 * p.N + p.N + col] = b;
+          float* dst = do_bn ? p.epart : p.stats;
+          const size_t slab = do_bn ? (size_t)split * tiles_m + tm : (size_t)tm;
+          dst[(slab * nq + 0) * p.N + col] = a;
+          dst[(slab * nq + 1) * p.N + col] = b;
+          if (nq > 2) dst[(slab * nq + 2) * p.N + col] = c2;
         }
       }
     }
@@ -521,11 +593,25 @@ int pda_conv_fwd(const ConvDesc* d, const void* x, const void* w, int Kpad, void
 }
 
 // dX[Nb,H,W,Cin] = conv_transpose(dY, W). Every dX element is written (zeros where no tap lands).
-int pda_conv_dgrad(const ConvDesc* d, const void* dy, const void* w, void* dx, int dt, int bm,
-                   int bn, hipStream_t st) {
+struct BnEpi {  // mirrors ops/ext.py BnEpi
+  int mode, nq;
+  const void* y; const float* sc; const float* sh;
+  const void* y2; const float* sc2; const float* sh2;
+  const void* g2; float* part;
+};
+
+int pda_conv_dgrad(const ConvDesc* d, const void* dy, const void* w, void* dx, const BnEpi* epi,
+                   int dt, int bm, int bn, hipStream_t st) {
   ConvParams p{};
   fill_geom(p, *d);
   p.a = dy; p.b = w; p.out = dx;
+  p.emode = -1;
+  if (epi) {
+    p.emode = epi->mode; p.enq = epi->nq;
+    p.ey = (const u16*)epi->y; p.esc = epi->sc; p.esh = epi->sh;
+    p.ey2 = (const u16*)epi->y2; p.esc2 = epi->sc2; p.esh2 = epi->sh2;
+    p.eg2 = (const u16*)epi->g2; p.epart = epi->part;
+  }
   p.N = d->Cin; p.out_pitch = d->Cin;
   const int sd = d->stride;
   if (sd != 1 && sd != 2) return -2;

@@ -360,7 +360,8 @@ class NativeResNet(nn.Module):
             K.bn_finalize_fwd(part, T, u.cout, M, self.gamma(u), self.beta(u), u.bn.eps,
                               u.bn.momentum if u.bn.momentum is not None else 0.1,
                               st[0], st[1], st[2], st[3], self.rmean(u), self.rvar(u),
-                              self.flat_nbt[u.nbt_idx:u.nbt_idx + 1], update_running=True)
+                              self.flat_nbt[u.nbt_idx:u.nbt_idx + 1], update_running=True,
+                              ws=self.ws)
         else:
             K.conv_fwd(x, self.w16(u), g, y)
             K.bn_eval_coeffs(self.gamma(u), self.beta(u), self.rmean(u), self.rvar(u), u.bn.eps,
@@ -443,7 +444,14 @@ class NativeResNet(nn.Module):
 
     # ------------------------------------------------------------------ backward
     def native_backward(self, dlog16: torch.Tensor) -> None:
-        """dlog16: [B, fc_rows] 16-bit d(loss)/d(logits) (zero padded)."""
+        """dlog16: [B, fc_rows] 16-bit d(loss)/d(logits) (zero padded).
+
+        Schedule per bottleneck block (last to first): finish the tail BN backward (its reduction
+        was fused into the NEXT block's conv1 dgrad epilogue) -> downsample wgrad/dgrad -> for
+        conv3, conv2: wgrad + dgrad whose epilogue does the ReLU mask and the BN-backward partial
+        sums of the preceding BN -> finish that BN -> conv1 wgrad + dgrad whose epilogue does the
+        PREVIOUS block's tail reduction (adding the shortcut gradient). DDP buckets fire as each
+        block's gradient segment completes."""
         sv = self._fwd_ctx
         if sv is None:
             raise RuntimeError("native backward without a saved forward")
@@ -455,85 +463,131 @@ class NativeResNet(nn.Module):
         if red is not None:
             red.reset()
         Nb = dlog16.shape[0]
+        ws = self.ws
         # ---- fc
         K.col_sum(dlog16, self.num_classes, self.flat_grad[self.fc_b_off:self.fc_b_off + self.num_classes],
                   accumulate=acc)
         gfc = ConvGeom(Nb, 1, 1, self.feat_dim, self.fc_rows, 1, 1, 1, 0)
-        K.conv_wgrad(dlog16, sv["feat"], gfc, self.fc_wgrad_full, self.ws, accumulate=acc)
+        K.conv_wgrad(dlog16, sv["feat"], gfc, self.fc_wgrad_full, ws, accumulate=acc)
         dfeat = self._empty(Nb, 1, 1, self.feat_dim)
         fc_w_ohwi = self.fc_w16.view(self.fc_rows, 1, 1, self.feat_dim)
         K.conv_dgrad(dlog16.view(Nb, 1, 1, self.fc_rows), fc_w_ohwi, gfc, dfeat)
         if red is not None:
             red.grads_ready(self.block_bounds[0])
-        # ---- blocks, last to first
-        g1, g2, gp = None, None, dfeat.view(Nb, self.feat_dim)
-        for bi in range(len(self.blocks) - 1, -1, -1):
+        # ---- last block's tail: standalone reduction of the pooled gradient
+        nblk = len(self.blocks)
+        b = self.blocks[-1]
+        rec = sv["blocks"][-1]
+        tail = self._tail_standalone(b, rec, dfeat.view(Nb, self.feat_dim), acc)
+        shortcut_g = None
+        for bi in range(nblk - 1, -1, -1):
             b = self.blocks[bi]
             rec = sv["blocks"][bi]
-            g1, g2 = self._block_backward(b, rec, g1, g2, gp, acc)
-            gp = None
+            prev = (self.blocks[bi - 1], sv["blocks"][bi - 1]) if bi > 0 else None
+            dx_main, shortcut_g, tail = self._block_backward(b, rec, tail, prev, acc)
             if red is not None:
-                red.grads_ready(self.block_bounds[len(self.blocks) - bi])
-        # ---- stem
+                red.grads_ready(self.block_bounds[nblk - bi])
+        # ---- stem: maxpool backward of (main + shortcut) gradients, BN backward, wgrad
         x0, y0, arg = sv["x0"], sv["y0"], sv["arg"]
         st0 = sv["stem_stats"]
         dA0 = self._empty(*y0.shape)
-        K.maxpool_bwd(g1, arg, dA0, dout2=g2)
+        K.maxpool_bwd(dx_main, arg, dA0, dout2=shortcut_g)
         dy0 = self._empty(*y0.shape)
         u = self.stem
-        K.bn_bwd(self.ws, y0, st0[0], st0[1], self.gamma(u), st0[2], st0[3], self.dgamma(u),
+        K.bn_bwd(ws, y0, st0[0], st0[1], self.gamma(u), st0[2], st0[3], self.dgamma(u),
                  self.dbeta(u), dy0, g1=dA0, accumulate=acc)
-        K.conv_wgrad(dy0, x0, u.geom(Nb), self.wgrad_view(u), self.ws, cin_real=3, accumulate=acc)
+        K.conv_wgrad(dy0, x0, u.geom(Nb), self.wgrad_view(u), ws, cin_real=3, accumulate=acc)
         if red is not None:
             red.grads_ready(self.block_bounds[-1])
             red.finish()
         self._grads_zero = False
         self._fwd_ctx = None
 
-    def _block_backward(self, b: Block, rec, g1, g2, gp, acc):
+    def _tail_args(self, b: Block, rec):
+        """Tensors describing a = relu(bn3(y3) + shortcut) of block b for the BN-backward."""
+        ul = b.units[-1]
+        sl = rec[f"s{len(b.units) - 1}"]
+        d = dict(y=rec["ys"][-1], scale=sl[2], shift=sl[3])
+        if b.ds is not None:
+            sd = rec["sd"]
+            d.update(y2=rec["yd"], scale2=sd[2], shift2=sd[3])
+        else:
+            d.update(res=rec["x"])
+        return d
+
+    def _tail_standalone(self, b: Block, rec, gp, acc):
+        """Tail reduction from the pooled head gradient (no producing dgrad to fuse into)."""
+        ys = rec["ys"]
+        dz = self._empty(*ys[-1].shape)
+        ta = self._tail_args(b, rec)
+        N, H, W, C_ = ys[-1].shape
+        G = K._reduce_blocks(N * H * W, C_)
+        nq = 3 if b.ds is not None else 2
+        part = self.ws.get("bn_part", G * nq * C_)
+        a = ext.BwdArgs(None, None, K.ptr(gp), H * W, K.ptr(ta["y"]), K.ptr(ta["scale"]),
+                        K.ptr(ta["shift"]), K.ptr(ta.get("y2", ta.get("res"))), K.ptr(ta.get("scale2")),
+                        K.ptr(ta.get("shift2")), 2 if b.ds is not None else 1, K.ptr(dz), K.ptr(part), nq,
+                        N * H * W, C_)
+        K.check(ext.lib().pda_bn_bwd_reduce(ext.C.byref(a), G, ext.dt_of(dz), ext.stream(dz.device)),
+                "bn_bwd_reduce")
+        return dz, part, G, nq
+
+    def _block_backward(self, b: Block, rec, tail, prev, acc):
+        """Returns (dx_main, shortcut_grad, prev_tail) -- the last is the fused reduction of the
+        previous block's tail, or None for the first block."""
+        ws = self.ws
         x = rec["x"]
         ys, acts, yd = rec["ys"], rec["acts"], rec["yd"]
         Nb = x.shape[0]
+        n = len(b.units)
         ul = b.units[-1]
-        sl = rec[f"s{len(b.units) - 1}"]
-        dz = self._empty(*ys[-1].shape)
+        sl = rec[f"s{n - 1}"]
+        dz, part, G, nq = tail
         dy = self._empty(*ys[-1].shape)
-        dyd = None
         if b.ds is not None:
             sd = rec["sd"]
             dyd = self._empty(*yd.shape)
-            K.bn_bwd(self.ws, ys[-1], sl[0], sl[1], self.gamma(ul), sl[2], sl[3], self.dgamma(ul),
-                     self.dbeta(ul), dy, g1=g1, g2=g2, gp=gp, y2=yd, mean2=sd[0], invstd2=sd[1],
-                     gamma2=self.gamma(b.ds), scale2=sd[2], shift2=sd[3], dgamma2=self.dgamma(b.ds),
-                     dbeta2=self.dbeta(b.ds), dy2_out=dyd, dz_buf=dz, accumulate=acc)
+            K.bn_bwd_finish(ws, part, G, nq, ys[-1], sl[0], sl[1], self.gamma(ul), self.dgamma(ul),
+                            self.dbeta(ul), dz, dy, y2=yd, mean2=sd[0], invstd2=sd[1],
+                            gamma2=self.gamma(b.ds), dgamma2=self.dgamma(b.ds), dbeta2=self.dbeta(b.ds),
+                            dy2_out=dyd, accumulate=acc)
+            # shortcut branch first: its dX is the second gradient source of the previous tail
+            g = b.ds.geom(Nb)
+            K.conv_wgrad(dyd, x, g, self.wgrad_view(b.ds), ws, accumulate=acc)
+            shortcut_g = self._empty(*x.shape)
+            K.conv_dgrad(dyd, self.w16_ohwi(b.ds), g, shortcut_g)
         else:
-            K.bn_bwd(self.ws, ys[-1], sl[0], sl[1], self.gamma(ul), sl[2], sl[3], self.dgamma(ul),
-                     self.dbeta(ul), dy, g1=g1, g2=g2, gp=gp, res=x, dz_buf=dz, accumulate=acc)
-        n = len(b.units)
+            K.bn_bwd_finish(ws, part, G, nq, ys[-1], sl[0], sl[1], self.gamma(ul), self.dgamma(ul),
+                            self.dbeta(ul), dz, dy, accumulate=acc)
+            shortcut_g = dz
         dx_main = None
+        prev_tail = None
         for j in range(n - 1, -1, -1):
             u = b.units[j]
             a_in = acts[j]
             g = u.geom(Nb)
-            K.conv_wgrad(dy, a_in, g, self.wgrad_view(u), self.ws, accumulate=acc)
-            da = self._empty(*a_in.shape)
-            K.conv_dgrad(dy, self.w16_ohwi(u), g, da)
+            K.conv_wgrad(dy, a_in, g, self.wgrad_view(u), ws, accumulate=acc)
+            out = self._empty(*a_in.shape)
             if j > 0:
                 up = b.units[j - 1]
                 sp = rec[f"s{j - 1}"]
+                Gp = K.dgrad_slabs(g, Nb)
+                epi, part_p, nq_p = K.bn_epilogue(ws, Gp, ys[j - 1], sp[2], sp[3])
+                K.conv_dgrad(dy, self.w16_ohwi(u), g, out, epi=epi)      # out = dz of bn_{j-1}
                 dyp = self._empty(*ys[j - 1].shape)
-                K.bn_bwd(self.ws, ys[j - 1], sp[0], sp[1], self.gamma(up), sp[2], sp[3],
-                         self.dgamma(up), self.dbeta(up), dyp, g1=da, accumulate=acc)
+                K.bn_bwd_finish(ws, part_p, Gp, nq_p, ys[j - 1], sp[0], sp[1], self.gamma(up),
+                                self.dgamma(up), self.dbeta(up), out, dyp, accumulate=acc)
                 dy = dyp
+            elif prev is not None:
+                pb, prec = prev
+                Gp = K.dgrad_slabs(g, Nb)
+                epi, part_p, nq_p = K.bn_epilogue(ws, Gp, g2=shortcut_g, **self._tail_args(pb, prec))
+                K.conv_dgrad(dy, self.w16_ohwi(u), g, out, epi=epi)      # out = dz of prev tail
+                prev_tail = (out, part_p, Gp, nq_p)
             else:
-                dx_main = da
-        if b.ds is not None:
-            g = b.ds.geom(Nb)
-            K.conv_wgrad(dyd, x, g, self.wgrad_view(b.ds), self.ws, accumulate=acc)
-            dxd = self._empty(*x.shape)
-            K.conv_dgrad(dyd, self.w16_ohwi(b.ds), g, dxd)
-            return dx_main, dxd
-        return dx_main, dz
+                K.conv_dgrad(dy, self.w16_ohwi(u), g, out)
+                dx_main = out
+        return dx_main, shortcut_g, prev_tail
 
     # ------------------------------------------------------------------ nn.Module API
     def forward(self, x: torch.Tensor) -> torch.Tensor:

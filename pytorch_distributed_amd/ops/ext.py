@@ -15,7 +15,7 @@ from typing import Optional
 
 import torch
 
-__all__ = ["load", "available", "lib", "DT", "dt_of", "ConvDesc", "BwdArgs", "stream", "ptr"]
+__all__ = ["load", "available", "lib", "DT", "dt_of", "ConvDesc", "BwdArgs", "BnEpi", "stream", "ptr"]
 
 _LIB: Optional[C.CDLL] = None
 _ERR: Optional[str] = None
@@ -41,13 +41,21 @@ class BwdArgs(C.Structure):
                 ("part", C.c_void_p), ("nq", C.c_int), ("rows", C.c_longlong), ("C", C.c_int)]
 
 
+class BnEpi(C.Structure):
+    _fields_ = [("mode", C.c_int), ("nq", C.c_int),
+                ("y", C.c_void_p), ("sc", C.c_void_p), ("sh", C.c_void_p),
+                ("y2", C.c_void_p), ("sc2", C.c_void_p), ("sh2", C.c_void_p),
+                ("g2", C.c_void_p), ("part", C.c_void_p)]
+
+
 _V, _I, _F, _L, _U = C.c_void_p, C.c_int, C.c_float, C.c_longlong, C.c_uint
 _SIGS = {
     "pda_conv_fwd": [C.POINTER(ConvDesc), _V, _V, _I, _V, _I, _I, _V, _V, _I, _I, _I, _I, _V],
-    "pda_conv_dgrad": [C.POINTER(ConvDesc), _V, _V, _V, _I, _I, _I, _V],
+    "pda_conv_dgrad": [C.POINTER(ConvDesc), _V, _V, _V, C.POINTER(BnEpi), _I, _I, _I, _V],
     "pda_conv_wgrad": [C.POINTER(ConvDesc), _V, _V, _V, _I, _I, _I, _I, _I, _V],
     "pda_wgrad_reduce": [_V, _V, _I, _I, _I, _I, _I, _I, _F, _I, _V],
     "pda_bn_finalize_fwd": [_V, _I, _I, _F, _V, _V, _F, _F, _V, _V, _V, _V, _V, _V, _V, _I, _V],
+    "pda_slab_reduce": [_V, _I, _I, _I, _V, _V],
     "pda_bn_eval_coeffs": [_V, _V, _V, _V, _F, _I, _V, _V, _V],
     "pda_bn_apply": [_V, _V, _V, _V, _V, _V, _V, _L, _I, _I, _I, _I, _V],
     "pda_stem_pool": [_V, _V, _V, _V, _V, _I, _I, _I, _I, _I, _I, _I, _V],

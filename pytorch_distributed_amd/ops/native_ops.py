@@ -108,17 +108,45 @@ def stats_tiles(M: int, Cout: int, tile: Optional[Tuple[int, int]] = None) -> in
     return math.ceil(M / bm)
 
 
-def conv_dgrad(dy: torch.Tensor, w: torch.Tensor, g: ConvGeom, dx: torch.Tensor,
-               tile: Optional[Tuple[int, int]] = None) -> torch.Tensor:
-    """dx[Nb,H,W,Cin] = conv_transpose(dy[Nb,Ho,Wo,Cout], w[Cout,R,S,Cin])."""
-    Nb = dy.shape[0]
+def dgrad_tile(g: ConvGeom, Nb: int) -> Tuple[int, int]:
     M = Nb * (g.H // g.stride) * (g.W // g.stride)
-    bm, bn = tile or pick_tile(M * g.stride * g.stride, g.Cin)
+    return pick_tile(M * g.stride * g.stride, g.Cin)
+
+
+def dgrad_slabs(g: ConvGeom, Nb: int, tile: Optional[Tuple[int, int]] = None) -> int:
+    """Number of partial-sum slabs the fused BN epilogue of a dgrad writes (classes x M-tiles)."""
+    bm, _ = tile or dgrad_tile(g, Nb)
+    M = Nb * (g.H // g.stride) * (g.W // g.stride)
+    return g.stride * g.stride * math.ceil(M / bm)
+
+
+def conv_dgrad(dy: torch.Tensor, w: torch.Tensor, g: ConvGeom, dx: torch.Tensor,
+               tile: Optional[Tuple[int, int]] = None, epi: Optional[ext.BnEpi] = None) -> torch.Tensor:
+    """dx[Nb,H,W,Cin] = conv_transpose(dy[Nb,Ho,Wo,Cout], w[Cout,R,S,Cin]).
+
+    With ``epi`` (see :func:`bn_epilogue`) the kernel instead stores dz = dA * relu_mask (dA = the
+    transposed conv result [+ epi.g2]) and writes the BatchNorm-backward partial sums."""
+    Nb = dy.shape[0]
+    bm, bn = tile or dgrad_tile(g, Nb)
     d = g.desc(Nb)
-    rc = ext.lib().pda_conv_dgrad(C.byref(d), ptr(dy), ptr(w), ptr(dx), dt_of(dy), bm, bn,
+    rc = ext.lib().pda_conv_dgrad(C.byref(d), ptr(dy), ptr(w), ptr(dx),
+                                  C.byref(epi) if epi is not None else None, dt_of(dy), bm, bn,
                                   stream(dy.device))
     check(rc, "conv_dgrad")
     return dx
+
+
+def bn_epilogue(ws: "Workspace", G: int, y, scale, shift, res=None, y2=None, scale2=None,
+                shift2=None, g2=None):
+    """Describe the BN-backward reduction a dgrad epilogue performs for a = relu(bn(y) [+res | +bn2(y2)]).
+    Returns (epi, part, nq); ``part`` holds G*nq*C floats after the dgrad."""
+    C_ = y.shape[-1]
+    mode = 2 if y2 is not None else (1 if res is not None else 0)
+    nq = 3 if mode == 2 else 2
+    part = ws.get("bn_part", G * nq * C_)
+    epi = ext.BnEpi(mode, nq, ptr(y), ptr(scale), ptr(shift),
+                    ptr(y2 if y2 is not None else res), ptr(scale2), ptr(shift2), ptr(g2), ptr(part))
+    return epi, part, nq
 
 
 def wgrad_plan(g: ConvGeom, Nb: int, tile: Optional[Tuple[int, int]] = None,
@@ -157,9 +185,26 @@ def conv_wgrad(dy: torch.Tensor, x: torch.Tensor, g: ConvGeom, grad: torch.Tenso
 
 
 # ------------------------------------------------------------------ batchnorm
+_PRE_S = 96
+
+
+def prereduce(part: torch.Tensor, G: int, QC: int, ws: Optional["Workspace"] = None):
+    """[G][QC] partial slabs -> [S][QC] with S <= 96 (coalesced first stage), so the per-channel
+    finalize kernels never walk thousands of slabs serially. Returns (part, G)."""
+    if G <= 2 * _PRE_S:
+        return part, G
+    out = (ws.get("bn_pre", _PRE_S * QC) if ws is not None
+           else torch.empty(_PRE_S * QC, dtype=torch.float32, device=part.device))
+    s = ext.lib().pda_slab_reduce(ptr(part), G, QC, _PRE_S, ptr(out), stream(part.device))
+    if s < 0:
+        raise RuntimeError("slab_reduce launch failed")
+    return out, s
+
+
 def bn_finalize_fwd(part: torch.Tensor, T: int, C_: int, count: int, gamma, beta, eps, momentum,
                     mean, invstd, scale, shift, rmean=None, rvar=None, nbt=None,
-                    update_running: bool = True) -> None:
+                    update_running: bool = True, ws: Optional["Workspace"] = None) -> None:
+    part, T = prereduce(part, T, 2 * C_, ws)
     rc = ext.lib().pda_bn_finalize_fwd(ptr(part), T, C_, float(count), ptr(gamma), ptr(beta),
                                        float(eps), float(momentum), ptr(mean), ptr(invstd), ptr(scale),
                                        ptr(shift), ptr(rmean), ptr(rvar), ptr(nbt),
@@ -242,6 +287,31 @@ def bn_bwd(ws: Workspace, y, mean, invstd, gamma, scale, shift, dgamma, dbeta, d
     L = ext.lib()
     dt = dt_of(y)
     check(L.pda_bn_bwd_reduce(C.byref(a), G, dt, st), "bn_bwd_reduce")
+    _bn_bwd_tail(ws, part, G, nq, mode, a, y, mean, invstd, gamma, dgamma, dbeta, dy_out,
+                 y2, mean2, invstd2, gamma2, dgamma2, dbeta2, dy2_out, dz_buf, gscale, accumulate)
+
+
+def bn_bwd_finish(ws: "Workspace", part, G: int, nq: int, y, mean, invstd, gamma, dgamma, dbeta,
+                  dz, dy_out, y2=None, mean2=None, invstd2=None, gamma2=None, dgamma2=None,
+                  dbeta2=None, dy2_out=None, gscale: float = 1.0, accumulate: bool = False) -> None:
+    """Finalize + apply of a BN backward whose reduction a dgrad epilogue already produced
+    (partials ``part`` [G][nq][C], masked gradient ``dz``)."""
+    N, H, W, C_ = y.shape
+    mode = 2 if nq == 3 else 1   # dz is materialised in both cases
+    a = BwdArgs(None, None, None, 0, ptr(y), None, None, ptr(y2), None, None, mode, None, ptr(part),
+                nq, N * H * W, C_)
+    _bn_bwd_tail(ws, part, G, nq, mode, a, y, mean, invstd, gamma, dgamma, dbeta, dy_out,
+                 y2, mean2, invstd2, gamma2, dgamma2, dbeta2, dy2_out, dz, gscale, accumulate)
+
+
+def _bn_bwd_tail(ws, part, G, nq, mode, a, y, mean, invstd, gamma, dgamma, dbeta, dy_out,
+                 y2, mean2, invstd2, gamma2, dgamma2, dbeta2, dy2_out, dz_buf, gscale, accumulate):
+    C_ = y.shape[-1]
+    rows = y.numel() // C_
+    st = stream(y.device)
+    L = ext.lib()
+    dt = dt_of(y)
+    part, G = prereduce(part, G, nq * C_, ws)
     k = ws.get("bn_k", 6 * C_)
     check(L.pda_bn_bwd_finalize(ptr(part), G, nq, 1, C_, float(rows), ptr(gamma), ptr(mean),
                                 ptr(invstd), ptr(dgamma), ptr(dbeta), ptr(k[0:C_]),

@@ -330,3 +330,67 @@ def test_synthetic_kernel_matches_torch_generator():
     torch.testing.assert_close(out[..., :3].float().cpu(), xr.permute(0, 2, 3, 1).to(torch.bfloat16).float(),
                                rtol=1e-2, atol=2e-2)
     assert out[..., 3:].abs().max().item() == 0
+
+
+@pytest.mark.parametrize("mode", ["relu", "res", "ds"])
+@pytest.mark.parametrize("stride", [1, 2])
+def test_dgrad_fused_bn_backward(mode, stride):
+    """dgrad epilogue (mask + BN-backward partial sums) == plain dgrad followed by the standalone
+    BN-backward reduce/apply."""
+    K = _k()
+    dtype = torch.bfloat16
+    Nb, H, Cin, Cout = 2, 8, 64, 128
+    torch.manual_seed(5)
+    g = K.ConvGeom(Nb, H, H, Cin, Cout, 3, 3, stride, 1)
+    dy = torch.randn(Nb, g.Ho, g.Wo, Cout, device=DEV).to(dtype)
+    w = (torch.randn(Cout, 3, 3, Cin, device=DEV) * 0.05).to(dtype)
+    y = torch.randn(Nb, H, H, Cin, device=DEV).to(dtype)
+    y2 = torch.randn(Nb, H, H, Cin, device=DEV).to(dtype)
+    g2 = torch.randn(Nb, H, H, Cin, device=DEV).to(dtype)
+    sc, sh = torch.rand(Cin, device=DEV) + 0.5, torch.randn(Cin, device=DEV) * 0.1
+    sc2, sh2 = torch.rand(Cin, device=DEV) + 0.5, torch.randn(Cin, device=DEV) * 0.1
+    mean, inv = torch.randn(Cin, device=DEV) * 0.1, torch.rand(Cin, device=DEV) + 0.5
+    mean2, inv2 = torch.randn(Cin, device=DEV) * 0.1, torch.rand(Cin, device=DEV) + 0.5
+    gamma, gamma2 = torch.rand(Cin, device=DEV) + 0.5, torch.rand(Cin, device=DEV) + 0.5
+    ws = K.Workspace(DEV)
+    kw = {}
+    if mode == "res":
+        kw = dict(res=y2)
+    elif mode == "ds":
+        kw = dict(y2=y2, scale2=sc2, shift2=sh2)
+    use_g2 = mode != "relu"
+    # reference: plain dgrad + standalone bn_bwd
+    da = torch.empty(Nb, H, H, Cin, device=DEV, dtype=dtype)
+    K.conv_dgrad(dy, w, g, da)
+    outs_ref = [torch.zeros(Cin, device=DEV) for _ in range(4)]
+    dy_ref = torch.empty_like(y)
+    dy2_ref = torch.empty_like(y)
+    dz_ref = torch.empty_like(y)
+    extra = {}
+    if mode == "ds":
+        extra = dict(mean2=mean2, invstd2=inv2, gamma2=gamma2, dgamma2=outs_ref[2], dbeta2=outs_ref[3],
+                     dy2_out=dy2_ref)
+    K.bn_bwd(ws, y, mean, inv, gamma, sc, sh, outs_ref[0], outs_ref[1], dy_ref, g1=da,
+             g2=g2 if use_g2 else None, dz_buf=dz_ref, **kw, **extra)
+    # fused
+    G = K.dgrad_slabs(g, Nb)
+    epi, part, nq = K.bn_epilogue(ws, G, y, sc, sh, g2=g2 if use_g2 else None, **kw)
+    dz = torch.empty_like(y)
+    K.conv_dgrad(dy, w, g, dz, epi=epi)
+    outs = [torch.zeros(Cin, device=DEV) for _ in range(4)]
+    dyf = torch.empty_like(y)
+    dy2f = torch.empty_like(y)
+    extra = {}
+    if mode == "ds":
+        extra = dict(y2=y2, mean2=mean2, invstd2=inv2, gamma2=gamma2, dgamma2=outs[2], dbeta2=outs[3],
+                     dy2_out=dy2f)
+    K.bn_bwd_finish(ws, part, G, nq, y, mean, inv, gamma, outs[0], outs[1], dz, dyf, **extra)
+    torch.cuda.synchronize()
+    if mode != "relu":
+        assert rel_err(dz, dz_ref) < 1e-2
+    assert rel_err(dyf, dy_ref) < 2e-2
+    for a, b in zip(outs, outs_ref):
+        if b.abs().sum() > 0:
+            assert rel_err(a, b) < 1e-2
+    if mode == "ds":
+        assert rel_err(dy2f, dy2_ref) < 2e-2
