@@ -336,10 +336,17 @@ class NativeResNet(nn.Module):
         return gen
 
     def prepare_input(self, x: torch.Tensor) -> torch.Tensor:
+        """Validate and convert the input BEFORE any kernel runs: every kernel's indexing assumes
+        the plan's geometry, so a mismatched image size must never reach the GPU."""
+        S = self.image_size
         if x.dtype == self.dtype and x.dim() == 4 and x.shape[-1] == 8:
+            if tuple(x.shape[1:3]) != (S, S) or x.device != self.device:
+                raise ValueError(f"NHWC8 input {tuple(x.shape)} on {x.device} does not match the "
+                                 f"planned {S}x{S} on {self.device}")
             return x.contiguous()
-        if x.dim() != 4 or x.shape[1] != 3:
-            raise ValueError(f"expected [B,3,H,W] images or NHWC8 {self.dtype} input, got {tuple(x.shape)}")
+        if x.dim() != 4 or x.shape[1] != 3 or tuple(x.shape[2:]) != (S, S):
+            raise ValueError(f"expected [B,3,{S},{S}] images or NHWC8 {self.dtype} input, "
+                             f"got {tuple(x.shape)}")
         xin = x.to(self.device, torch.float32).contiguous()
         out = self._empty(x.shape[0], x.shape[2], x.shape[3], 8)
         K.nchw_to_nhwc8(xin, out)

@@ -7,15 +7,23 @@ GPU0 every step (13 coalesced 10 MiB broadcasts), runs replicas in Python
 threads, gathers logits on GPU0 and reduce-adds gradients to GPU0 (SURVEY §3.3);
 that is why the reference's DP reaches only 59.8% GPU utilisation.
 
-This implementation keeps the API and the math (replica 0 owns the parameters
-and the optimizer; BN running stats follow replica 0; outputs gathered on
-``output_device``) but:
+This implementation keeps the API and the math (outputs gathered on
+``output_device``; the loss is computed there over the global batch; BN running
+statistics follow replica 0) but is built for a fully connected xGMI node:
 
-* replicas are *persistent* -- created once, refreshed each forward by one
-  broadcast of replica 0's parameters+buffers (a single flat buffer for native
-  models) instead of rebuilding modules;
-* gradients are summed into replica 0 by one reduce over the flat gradient at
-  the end of backward (queued autograd callback), not per-parameter chunks.
+* replicas are *persistent*. For the native engine each GPU holds a full
+  :class:`~pytorch_distributed_amd.models.native.NativeResNet` (flat buffers);
+* after backward the flat gradients are SUM-all-reduced across the local GPUs by
+  ONE grouped in-process RCCL collective (``ncclCommInitAll`` communicator,
+  :class:`~pytorch_distributed_amd.parallel.rccl.RcclGroup`), and every replica
+  runs the fused SGD itself (replicated update: mathematically identical to
+  reduce-to-GPU0 + step + broadcast, with no per-step weight broadcast);
+* BN buffers (213 KB) are broadcast from replica 0 before each training forward,
+  which is what torch's per-step ``replicate`` achieves for them.
+
+For arbitrary (non-native) modules it falls back to persistent deep-copied
+replicas with a parameter refresh before each forward and a gradient
+reduction into replica 0 after backward -- the same math as ``nn.DataParallel``.
 """
 from __future__ import annotations
 
@@ -25,7 +33,7 @@ from typing import List, Optional, Sequence
 import torch
 from torch import nn
 
-__all__ = ["DataParallel"]
+__all__ = ["DataParallel", "ReplicatedSGD"]
 
 
 class _Gather(torch.autograd.Function):
@@ -41,6 +49,51 @@ class _Gather(torch.autograd.Function):
         return (None,) + tuple(p.to(d, non_blocking=True) for p, d in zip(parts, ctx.devices))
 
 
+class ReplicatedSGD(torch.optim.Optimizer):
+    """One fused SGD per replica, stepped after the in-process gradient all-reduce. Exposes
+    replica 0's ``param_groups`` / ``state_dict`` (what schedulers and checkpoints see)."""
+
+    def __init__(self, opts) -> None:
+        super().__init__(opts[0].param_groups[0]["params"], opts[0].defaults)
+        self.opts = opts
+        self.param_groups = opts[0].param_groups
+        self.state = opts[0].state
+
+    def _sync_hparams(self) -> None:
+        for o in self.opts[1:]:
+            for g0, g in zip(self.param_groups, o.param_groups):
+                for k in ("lr", "momentum", "weight_decay"):
+                    g[k] = g0[k]
+
+    def zero_grad(self, set_to_none: bool = True) -> None:
+        for o in self.opts:
+            o.zero_grad(set_to_none)
+
+    def step(self, closure=None):
+        self._sync_hparams()
+        for o in self.opts:
+            with torch.cuda.device(o.model.device):
+                o.step()
+
+    def step_amp(self, scale, found_inf):
+        # every replica holds the same (all-reduced) gradient, so the inf check agrees
+        self._sync_hparams()
+        for o in self.opts:
+            with torch.cuda.device(o.model.device):
+                s = scale.to(o.model.device, non_blocking=True)
+                f = found_inf if o is self.opts[0] else torch.zeros_like(found_inf, device=o.model.device)
+                o.step_amp(s, f)
+
+    def state_dict(self):
+        return self.opts[0].state_dict()
+
+    def load_state_dict(self, sd):
+        for o in self.opts:
+            o.load_state_dict(copy.deepcopy(sd))
+        self.param_groups = self.opts[0].param_groups
+        self.state = self.opts[0].state
+
+
 class DataParallel(nn.Module):
     def __init__(self, module: nn.Module, device_ids: Optional[Sequence[int]] = None,
                  output_device=None, dim: int = 0) -> None:
@@ -52,40 +105,105 @@ class DataParallel(nn.Module):
         elif device_ids is None:
             device_ids = list(range(torch.cuda.device_count()))
         self.device_ids = [int(d) for d in device_ids]
-        self.output_device = self.device_ids[0] if output_device is None and self.device_ids \
+        if self.device_ids and dev.index != self.device_ids[0]:
+            raise ValueError("module must live on device_ids[0]")
+        self.output_device = self.device_ids[0] if (output_device is None and self.device_ids) \
             else output_device
+        self._native = hasattr(module, "flat_params")
         self.replicas: List[nn.Module] = []
+        self.group = None
         for d in self.device_ids[1:]:
-            if hasattr(module, "replicate_to"):
-                self.replicas.append(module.replicate_to(torch.device("cuda", d)))
+            dd = torch.device("cuda", d)
+            if self._native:
+                self.replicas.append(self._native_replica(dd))
             else:
-                self.replicas.append(copy.deepcopy(module).to(torch.device("cuda", d)))
+                self.replicas.append(copy.deepcopy(module).to(dd))
+        if self._native and self.replicas and len(set(self.device_ids)) == len(self.device_ids):
+            from .rccl import RcclGroup
+            self.group = RcclGroup(self.device_ids)
+        # (replicas sharing a device -- used by the 1-GPU tests -- sync through plain copies)
         self._armed = False
 
-    # -- parameter/grad sync -------------------------------------------------------------
+    # ------------------------------------------------------------------ construction
+    def _native_replica(self, dev: torch.device):
+        from ..models.native import NativeResNet
+        from ..models.resnet import ResNet
+        m = self.module
+        ref = ResNet(m.arch_block, [len(getattr(m, f"layer{i}")) for i in range(1, 5)], m.num_classes)
+        with torch.cuda.device(dev):
+            r = NativeResNet(ref, device=dev, dtype=m.dtype, image_size=m.image_size)
+            with torch.no_grad():
+                r.flat_params.copy_(m.flat_params)
+                r.flat_buffers.copy_(m.flat_buffers)
+                r.flat_nbt.copy_(m.flat_nbt)
+            r.refresh_shadow()
+        return r
+
+    @property
+    def all_modules(self) -> List[nn.Module]:
+        return [self.module] + self.replicas
+
+    # ------------------------------------------------------------------ factories
+    def make_optimizer(self, **kw):
+        if self._native:
+            opts = [m.make_optimizer(**kw) for m in self.all_modules]
+            return ReplicatedSGD(opts) if self.replicas else opts[0]
+        return torch.optim.SGD(self.module.parameters(), **kw)
+
+    def make_criterion(self):
+        if not self.replicas and hasattr(self.module, "make_criterion"):
+            return self.module.make_criterion()
+        return nn.CrossEntropyLoss()   # gathered logits: gradient flows back through _Gather
+
+    def input_generator(self, ds):
+        return self.module.input_generator(ds) if hasattr(self.module, "input_generator") else None
+
+    # ------------------------------------------------------------------ sync
     @torch.no_grad()
-    def _broadcast_params(self) -> None:
+    def _broadcast_state(self) -> None:
         if not self.replicas:
+            return
+        if self._native:
+            for name in ("flat_buffers", "flat_nbt"):
+                ts = [getattr(m, name) for m in self.all_modules]
+                if self.group is not None:
+                    self.group.broadcast(ts, 0)
+                else:
+                    for t in ts[1:]:
+                        t.copy_(ts[0], non_blocking=True)
             return
         src = list(self.module.parameters()) + list(self.module.buffers())
         for r in self.replicas:
-            dst = list(r.parameters()) + list(r.buffers())
-            for s, t in zip(src, dst):
+            for s, t in zip(src, list(r.parameters()) + list(r.buffers())):
                 t.copy_(s, non_blocking=True)
 
     @torch.no_grad()
     def _reduce_grads(self) -> None:
         self._armed = False
+        if self._native:
+            ts = [m.flat_grad for m in self.all_modules]
+            if self.group is not None:
+                self.group.all_reduce(ts)
+            else:
+                total = ts[0].clone()
+                for t in ts[1:]:
+                    total.add_(t.to(total.device))
+                for t in ts:
+                    t.copy_(total, non_blocking=True)
+            for m in self.all_modules:
+                m._grads_zero = False
+            return
         for r in self.replicas:
             for p0, pr in zip(self.module.parameters(), r.parameters()):
                 if pr.grad is None:
                     continue
                 g = pr.grad.to(p0.device, non_blocking=True)
-                if p0.grad is None:
-                    p0.grad = g.clone()
-                else:
-                    p0.grad.add_(g)
+                p0.grad = g.clone() if p0.grad is None else p0.grad.add_(g)
                 pr.grad = None
+
+    def zero_grad(self, set_to_none: bool = True) -> None:
+        for m in self.all_modules:
+            m.zero_grad(set_to_none)
 
     def train(self, mode: bool = True):
         super().train(mode)
@@ -93,23 +211,34 @@ class DataParallel(nn.Module):
             r.train(mode)
         return self
 
+    def state_dict(self, *a, **k):
+        return self.module.state_dict(*a, **k)
+
+    def load_state_dict(self, sd, strict: bool = True):
+        res = self.module.load_state_dict(sd, strict=strict)
+        if self._native:
+            for r in self.replicas:
+                r.load_state_dict(sd, strict=strict)
+        return res
+
+    # ------------------------------------------------------------------ forward
     def forward(self, x: torch.Tensor, *args, **kwargs):
         if not self.replicas:
             return self.module(x, *args, **kwargs)
-        self._broadcast_params()
+        self._broadcast_state()
         chunks = torch.chunk(x, len(self.device_ids), 0)
         outs = []
-        mods = [self.module] + self.replicas
-        for m, c, d in zip(mods, chunks, self.device_ids):
+        for m, c, d in zip(self.all_modules, chunks, self.device_ids):
             with torch.cuda.device(d):
                 outs.append(m(c.to(torch.device("cuda", d), non_blocking=True), *args, **kwargs))
-        if torch.is_grad_enabled() and not self._armed:
-            self._armed = True
+        if torch.is_grad_enabled() and outs[0].requires_grad:
             out = _Gather.apply(torch.device("cuda", self.output_device), *outs)
             out.register_hook(self._arm_callback)
             return out
         return torch.cat([o.to(torch.device("cuda", self.output_device)) for o in outs], 0)
 
     def _arm_callback(self, g):
-        torch.autograd.Variable._execution_engine.queue_callback(self._reduce_grads)
+        if not self._armed:
+            self._armed = True
+            torch.autograd.Variable._execution_engine.queue_callback(self._reduce_grads)
         return g

@@ -200,12 +200,17 @@ def build_model(cfg: RunConfig, ctx: Context) -> nn.Module:
     model = build_ref(cfg.arch, cfg.num_classes)
     if ctx.engine == "native":
         from .models.native import NativeResNet
-        return NativeResNet(model, device=ctx.device, dtype=ctx.dtype)
+        return NativeResNet(model, device=ctx.device, dtype=ctx.dtype, image_size=cfg.image_size)
     return model.to(ctx.device)
 
 
+def _factory_owner(model: nn.Module, attr: str):
+    """The wrapper (DataParallel) if it provides ``attr``, else the wrapped module."""
+    return model if hasattr(model, attr) else _unwrap(model)
+
+
 def build_optimizer(cfg: RunConfig, model: nn.Module, ctx: Context):
-    inner = _unwrap(model)
+    inner = _factory_owner(model, "make_optimizer")
     if hasattr(inner, "make_optimizer"):
         return inner.make_optimizer(lr=cfg.lr, momentum=cfg.momentum, weight_decay=cfg.weight_decay)
     return torch.optim.SGD(model.parameters(), lr=cfg.lr, momentum=cfg.momentum,
@@ -213,7 +218,7 @@ def build_optimizer(cfg: RunConfig, model: nn.Module, ctx: Context):
 
 
 def build_criterion(ctx: Context, model: nn.Module):
-    inner = _unwrap(model)
+    inner = _factory_owner(model, "make_criterion")
     if hasattr(inner, "make_criterion"):
         return inner.make_criterion()
     return nn.CrossEntropyLoss()

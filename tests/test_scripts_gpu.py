@@ -1,0 +1,52 @@
+"""T6 tier on the GPU: the entrypoints run the native engine end to end (tiny epochs), including
+preemption -> resume through latest.pt and the fp16 loss-scaled ("Apex") script."""
+import os
+import subprocess
+import sys
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _env(**kw):
+    e = dict(os.environ)
+    e.update({"MX_ARCH": "resnet50", "MX_EPOCHS": "2", "MX_STEPS_PER_EPOCH": "3", "MX_VAL_STEPS": "2",
+              "MX_BATCH": "16", "MX_IMAGE_SIZE": "64", "PYTHONPATH": ROOT, "MASTER_IP": "127.0.0.1",
+              "MX_NPROCS": "1", "MX_LR": "0.01", "MX_METRICS": "1"})
+    e.update(kw)
+    return e
+
+
+def _run(script, tmp_path, **kw):
+    r = subprocess.run([sys.executable, os.path.join(ROOT, script)], cwd=tmp_path, env=_env(**kw),
+                       capture_output=True, text=True, timeout=600)
+    return r
+
+
+@pytest.mark.parametrize("script,outdir", [("resnet_single_gpu.py", "resnet_single"),
+                                           ("restnet_ddp.py", "resnet_ddp"),
+                                           ("resnet_ddp_apex.py", "resnet_ddp_amp"),
+                                           ("resnet_dp.py", "resnet_dp")])
+def test_entrypoint_native(tmp_path, script, outdir):
+    r = _run(script, tmp_path, MASTER_PORT=str(29600 + hash(script) % 200))
+    assert r.returncode == 0, r.stderr[-4000:]
+    assert "Epoch: 1, Loss: " in r.stdout and "cost time per epoch: " in r.stdout
+    m = (tmp_path / "output" / outdir / "metrics.jsonl").read_text()
+    assert '"engine": "native"' in m
+    if script == "resnet_ddp_apex.py":
+        assert "float16" in m
+
+
+def test_suspend_resume_native(tmp_path):
+    from pytorch_distributed_amd.utils.suspend import REQUEUE_EXIT_CODE
+    r = _run("resnet_ddp_apex.py", tmp_path, MX_SUSPEND_AT_STEP="2", MASTER_PORT="29811")
+    assert r.returncode == REQUEUE_EXIT_CODE, r.stderr[-4000:]
+    ck = torch.load(tmp_path / "output/resnet_ddp_amp/latest.pt", weights_only=True)
+    assert ck["step"] == 2 and "scaler" in ck and ck["scaler"]["scale"] > 0
+    assert len(ck["optimizer"]["state"]) == 161
+    r = _run("resnet_ddp_apex.py", tmp_path, MASTER_PORT="29812")
+    assert r.returncode == 0, r.stderr[-4000:]
+    assert "resume: epoch 0 step 2" in r.stdout

@@ -4,7 +4,7 @@ set -o pipefail
 mkdir -p gpurun_out
 export PYTHONUNBUFFERED=1
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.build()" > gpurun_out/build.log 2>&1 || { echo BUILD FAIL; tail -30 gpurun_out/build.log; exit 1; }
-timeout -k 10 900 python -m pytest tests -m gpu -x -q ${PYTEST_ARGS} > gpurun_out/pytest_gpu.log 2>&1
+timeout -k 10 1000 python -m pytest tests -m gpu -x -q --timeout 700 ${PYTEST_ARGS} > gpurun_out/pytest_gpu.log 2>&1
 rc=$?
 tail -40 gpurun_out/pytest_gpu.log
 [ $rc -ne 0 ] && exit $rc
