@@ -104,12 +104,17 @@ __device__ __forceinline__ i32x4 ld16B(const void* p, bool ok) {
 }
 
 // ================================================================= kernel
-template <int PASS, int DT, int BM, int BN>
-__global__ __launch_bounds__(NT, 2) void conv_gemm_kernel(ConvParams p) {
+// STAGES = 2: double-buffered LDS, one barrier per k-tile (deep-K layers).
+// STAGES = 1: single LDS buffer (half the LDS -> one more resident block per CU) for the many
+//             shallow-K layers of ResNet (K = 64..128: nk <= 2), where the per-block
+//             load -> MFMA -> store chain is latency-bound and concurrency matters more.
+template <int PASS, int DT, int BM, int BN, int STAGES>
+__global__ __launch_bounds__(NT, STAGES == 1 ? 3 : 2) void conv_gemm_kernel(ConvParams p) {
   // A tile: FWD/DGRAD ROW [BM][64]; WGRAD COL [64][BM]. B tile: FWD ROW [BN][64]; else COL [64][BN]
   constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2;
   constexpr int STAGE = A_BYTES + B_BYTES;
-  constexpr int LDS_BYTES = 2 * STAGE;
+  constexpr int RED_BYTES = 3 * NT * 8 * 4;
+  constexpr int LDS_BYTES = STAGES * STAGE > RED_BYTES ? STAGES * STAGE : RED_BYTES;
   static_assert(BM * BN * 2 <= LDS_BYTES, "C tile must fit in the staging buffers");
   static_assert(3 * NT * 8 * 4 <= LDS_BYTES, "stats reduction must fit");
   __shared__ __attribute__((aligned(16))) char smem[LDS_BYTES];
@@ -302,11 +307,17 @@ __global__ __launch_bounds__(NT, 2) void conv_gemm_kernel(ConvParams p) {
 
   if (nk > 0) {
     load_tile(0);
-    store_tile(0);
-    __syncthreads();
+    if constexpr (STAGES == 2) {
+      store_tile(0);
+      __syncthreads();
+    }
   }
   for (int kt = 0; kt < nk; ++kt) {
-    const int cur = kt & 1;
+    const int cur = STAGES == 2 ? (kt & 1) : 0;
+    if constexpr (STAGES == 1) {   // registers hold tile kt: publish it, then prefetch kt+1
+      store_tile(0);
+      __syncthreads();
+    }
     if (kt + 1 < nk) load_tile(kt + 1);
     const char* sa = smem + cur * STAGE;
     const char* sb = sa + A_BYTES;
@@ -330,7 +341,9 @@ __global__ __launch_bounds__(NT, 2) void conv_gemm_kernel(ConvParams p) {
 #pragma unroll
         for (int j = 0; j < NI; ++j) acc[i][j] = mfma16<DT>(fa[i], fb[j], acc[i][j]);
     }
-    if (kt + 1 < nk) store_tile(cur ^ 1);
+    if constexpr (STAGES == 2) {
+      if (kt + 1 < nk) store_tile(cur ^ 1);
+    }
     __syncthreads();
   }
 
@@ -548,16 +561,25 @@ struct ConvDesc {  // mirrors pytorch_distributed_amd/ops/ext.py ConvDesc
   int Nb, H, W, Cin, Cout, R, S, stride, pad, Ho, Wo;
 };
 
-template <int PASS, int DT, int BM, int BN>
+template <int PASS, int DT, int BM, int BN, int ST>
 static int launch(const ConvParams& p, dim3 grid, hipStream_t st) {
-  hipLaunchKernelGGL((conv_gemm_kernel<PASS, DT, BM, BN>), grid, dim3(NT), 0, st, p);
+  hipLaunchKernelGGL((conv_gemm_kernel<PASS, DT, BM, BN, ST>), grid, dim3(NT), 0, st, p);
   return (int)hipGetLastError();
 }
 
+// bm < 0 selects the single-buffer (STAGES = 1) variant of tile |bm| x bn (FWD / DGRAD only)
 template <int PASS>
 static int dispatch(int dt, int bm, int bn, const ConvParams& p, dim3 grid, hipStream_t st) {
+  if (bm < 0) {
+#define PDA_CASE1(D, M_, N_)                                                   \
+  if (dt == D && -bm == M_ && bn == N_) return launch<PASS, D, M_, N_, 1>(p, grid, st);
+    PDA_CASE1(DT_BF16, 128, 128) PDA_CASE1(DT_BF16, 128, 64) PDA_CASE1(DT_BF16, 64, 128)
+    PDA_CASE1(DT_F16, 128, 128) PDA_CASE1(DT_F16, 128, 64) PDA_CASE1(DT_F16, 64, 128)
+#undef PDA_CASE1
+    return -1;
+  }
 #define PDA_CASE(D, M_, N_)                                                    \
-  if (dt == D && bm == M_ && bn == N_) return launch<PASS, D, M_, N_>(p, grid, st);
+  if (dt == D && bm == M_ && bn == N_) return launch<PASS, D, M_, N_, 2>(p, grid, st);
   PDA_CASE(DT_BF16, 128, 128) PDA_CASE(DT_BF16, 128, 64) PDA_CASE(DT_BF16, 64, 128)
   PDA_CASE(DT_BF16, 64, 64)
   PDA_CASE(DT_F16, 128, 128) PDA_CASE(DT_F16, 128, 64) PDA_CASE(DT_F16, 64, 128)
@@ -588,7 +610,8 @@ int pda_conv_fwd(const ConvDesc* d, const void* x, const void* w, int Kpad, void
   p.a = x; p.b = w; p.out = y; p.stats = stats; p.bias = bias;
   p.M = d->Nb * d->Ho * d->Wo; p.N = d->Cout; p.Kpad = Kpad; p.K = Kpad;
   p.out_f32 = out_f32; p.relu = relu; p.out_pitch = out_pitch > 0 ? out_pitch : d->Cout;
-  const int tiles = ((p.M + bm - 1) / bm) * ((p.N + bn - 1) / bn);
+  const int abm = bm < 0 ? -bm : bm;
+  const int tiles = ((p.M + abm - 1) / abm) * ((p.N + bn - 1) / bn);
   return dispatch<FWD>(dt, bm, bn, p, dim3(tiles, 1), st);
 }
 
@@ -634,7 +657,8 @@ int pda_conv_dgrad(const ConvDesc* d, const void* dy, const void* w, void* dx, c
     }
   }
   p.K = 0;
-  const int tiles = ((p.M + bm - 1) / bm) * ((p.N + bn - 1) / bn);
+  const int abm = bm < 0 ? -bm : bm;
+  const int tiles = ((p.M + abm - 1) / abm) * ((p.N + bn - 1) / bn);
   return dispatch<DGRAD>(dt, bm, bn, p, dim3(tiles, ncls), st);
 }
 
@@ -647,7 +671,8 @@ int pda_conv_wgrad(const ConvDesc* d, const void* dy, const void* x, float* slab
   p.M = d->Cout; p.N = d->R * d->S * d->Cin;
   p.K = d->Nb * d->Ho * d->Wo;
   p.k_chunk = k_chunk;
-  const int tiles = ((p.M + bm - 1) / bm) * ((p.N + bn - 1) / bn);
+  const int abm = bm < 0 ? -bm : bm;
+  const int tiles = ((p.M + abm - 1) / abm) * ((p.N + bn - 1) / bn);
   return dispatch<WGRAD>(dt, bm, bn, p, dim3(tiles, splits), st);
 }
 

@@ -259,6 +259,96 @@ __global__ __launch_bounds__(NT) void nchw_to_nhwc8_kernel(const float* __restri
   }
 }
 
+// ------------------------------------------------------------------ stem space-to-depth
+// The 7x7/2 stem on a 3-channel image is re-expressed as a 4x4/1 conv (pad 2, output S/2) on the
+// 2x2 space-to-depth image X'[i][j][(p*2+q)*3+c] = x[2i+p][2j+q][c] (12 channels padded to 16):
+// y[o] = sum_{a,b in -2..1} X'[o+a] . W'[a+2][b+2], W'[a+2][b+2][(p,q,c)] = w[2a+p+3][2b+q+3][c].
+// K = 16 taps x 16 channels = 256: whole 16-B chunks, MFMA-aligned, no per-chunk tap decode.
+__global__ __launch_bounds__(NT) void synth_s2d_kernel(const uint32_t* __restrict__ keys,
+                                                       const long long* __restrict__ labels,
+                                                       int B, int S, u16* __restrict__ out, int dt) {
+  const int S2 = S / 2;
+  const long long npix = (long long)B * S2 * S2;
+  const int hw = S * S;
+  for (long long i = blockIdx.x * (long long)NT + threadIdx.x; i < npix; i += (long long)gridDim.x * NT) {
+    const int b = (int)(i / (S2 * S2));
+    const int rem = (int)(i - (long long)b * S2 * S2);
+    const int oi = rem / S2, oj = rem - oi * S2;
+    const uint32_t key = keys[b];
+    const long long lab = labels[b];
+    u16 h[16];
+#pragma unroll
+    for (int pq = 0; pq < 4; ++pq) {
+      const int pix = (2 * oi + (pq >> 1)) * S + 2 * oj + (pq & 1);
+#pragma unroll
+      for (int c = 0; c < 3; ++c) {
+        const uint32_t pos = (uint32_t)(c * hw + pix);
+        const uint32_t u = hash32(key ^ (pos * 0x27D4EB2Fu)) >> 8;
+        const float uf = (float)u * (1.0f / 16777216.0f);
+        const float tint = (float)((lab * (2 * c + 3) + c) % 4) / 3.0f;
+        const float v = (uf * 0.5f + 0.5f * tint - c_mean[c]) * c_istd[c];
+        h[pq * 3 + c] = dt == DT_BF16 ? f32_to_bf16(v) : f32_to_f16(v);
+      }
+    }
+#pragma unroll
+    for (int c = 12; c < 16; ++c) h[c] = 0;
+    reinterpret_cast<i32x4*>(out)[2 * i] = reinterpret_cast<i32x4*>(h)[0];
+    reinterpret_cast<i32x4*>(out)[2 * i + 1] = reinterpret_cast<i32x4*>(h)[1];
+  }
+}
+
+__global__ __launch_bounds__(NT) void nchw_to_s2d_kernel(const float* __restrict__ x, int B, int C,
+                                                         int S, u16* __restrict__ out, int dt) {
+  const int S2 = S / 2;
+  const long long npix = (long long)B * S2 * S2;
+  for (long long i = blockIdx.x * (long long)NT + threadIdx.x; i < npix; i += (long long)gridDim.x * NT) {
+    const int b = (int)(i / (S2 * S2));
+    const int rem = (int)(i - (long long)b * S2 * S2);
+    const int oi = rem / S2, oj = rem - oi * S2;
+    u16 h[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      const int pq = k / 3, c = k - pq * 3;
+      float v = 0.f;
+      if (k < 12 && c < C)
+        v = x[(((size_t)b * C + c) * S + 2 * oi + (pq >> 1)) * S + 2 * oj + (pq & 1)];
+      h[k] = dt == DT_BF16 ? f32_to_bf16(v) : f32_to_f16(v);
+    }
+    reinterpret_cast<i32x4*>(out)[2 * i] = reinterpret_cast<i32x4*>(h)[0];
+    reinterpret_cast<i32x4*>(out)[2 * i + 1] = reinterpret_cast<i32x4*>(h)[1];
+  }
+}
+
+// src f32 OHWI [64][7][7][3] -> dst 16-bit [64][4][4][16]
+__global__ void pack_stem_s2d_kernel(const float* __restrict__ src, u16* __restrict__ dst, int Cout,
+                                     int dt) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= Cout * 256) return;
+  const int co = i >> 8, k = i & 255;
+  const int tap = k >> 4, ch = k & 15;
+  const int ra = tap >> 2, sb = tap & 3;
+  float v = 0.f;
+  if (ch < 12) {
+    const int pq = ch / 3, c = ch - pq * 3;
+    const int r = 2 * ra + (pq >> 1) - 1, s = 2 * sb + (pq & 1) - 1;
+    if (r >= 0 && r < 7 && s >= 0 && s < 7) v = src[(((size_t)co * 7 + r) * 7 + s) * 3 + c];
+  }
+  dst[i] = dt == DT_BF16 ? f32_to_bf16(v) : f32_to_f16(v);
+}
+
+// gradient of the packed weight [64][256] (f32) -> OHWI [64][7][7][3] of the master weight
+__global__ void stem_s2d_grad_kernel(const float* __restrict__ gp, float* __restrict__ g, int Cout,
+                                     int accumulate) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= Cout * 147) return;
+  const int co = i / 147, rem = i - co * 147;
+  const int r = rem / 21, s = (rem / 3) % 7, c = rem % 3;
+  const int p = (r + 1) & 1, q = (s + 1) & 1;
+  const int ra = (r + 1 - p) >> 1, sb = (s + 1 - q) >> 1;
+  const float v = gp[(size_t)co * 256 + (ra * 4 + sb) * 16 + (p * 2 + q) * 3 + c];
+  g[i] = accumulate ? g[i] + v : v;
+}
+
 inline int grid_for(long long n, int cap = 4096) {
   long long b = (n + NT - 1) / NT;
   return (int)(b < 1 ? 1 : (b > cap ? cap : b));
@@ -329,6 +419,33 @@ int pda_synth(const long long* ids, int B, unsigned salt, int num_classes, unsig
                      num_classes, keys, labels);
   hipLaunchKernelGGL(synth_nhwc8_kernel, dim3(grid_for((long long)B * S * S, 8192)), dim3(NT), 0, st,
                      keys, labels, B, S, (u16*)out, dt);
+  return (int)hipGetLastError();
+}
+
+int pda_synth_s2d(const long long* ids, int B, unsigned salt, int num_classes, unsigned* keys,
+                  long long* labels, int S, void* out, int dt, hipStream_t st) {
+  hipLaunchKernelGGL(synth_labels_kernel, dim3((B + 255) / 256), dim3(256), 0, st, ids, B, salt,
+                     num_classes, keys, labels);
+  hipLaunchKernelGGL(synth_s2d_kernel, dim3(grid_for((long long)B * (S / 2) * (S / 2), 8192)), dim3(NT),
+                     0, st, keys, labels, B, S, (u16*)out, dt);
+  return (int)hipGetLastError();
+}
+
+int pda_nchw_to_s2d(const float* x, int B, int C, int S, void* out, int dt, hipStream_t st) {
+  hipLaunchKernelGGL(nchw_to_s2d_kernel, dim3(grid_for((long long)B * (S / 2) * (S / 2), 8192)),
+                     dim3(NT), 0, st, x, B, C, S, (u16*)out, dt);
+  return (int)hipGetLastError();
+}
+
+int pda_pack_stem_s2d(const float* src, void* dst, int Cout, int dt, hipStream_t st) {
+  hipLaunchKernelGGL(pack_stem_s2d_kernel, dim3((Cout * 256 + 255) / 256), dim3(256), 0, st, src,
+                     (u16*)dst, Cout, dt);
+  return (int)hipGetLastError();
+}
+
+int pda_stem_s2d_grad(const float* gp, float* g, int Cout, int accumulate, hipStream_t st) {
+  hipLaunchKernelGGL(stem_s2d_grad_kernel, dim3((Cout * 147 + 255) / 256), dim3(256), 0, st, gp, g,
+                     Cout, accumulate);
   return (int)hipGetLastError();
 }
 

@@ -6,7 +6,8 @@ Here the whole network is ONE coarse autograd node whose forward and backward
 are explicit schedules of our gfx950 kernels (``ops/native_ops.py``):
 
 * activations are NHWC 16-bit (bf16 default, f16 for the AMP script); the input is
-  the 3-channel image padded to 8 channels so the 7x7 stem runs on MFMA too;
+  generated/converted straight into the 2x2 space-to-depth layout (12 of 16 channels used),
+  so the 7x7/2 stem becomes a 4x4/1 MFMA implicit GEMM with K = 256 (whole 16-B chunks);
 * every conv is the implicit-GEMM MFMA kernel (fwd / dgrad / split-K wgrad); the
   forward epilogue emits BatchNorm partial statistics, so BN costs one finalize
   launch plus one fused apply(+ReLU, +residual, +pool) pass;
@@ -61,7 +62,7 @@ class ConvBN:
     name: str
     conv: nn.Conv2d
     bn: nn.BatchNorm2d
-    cin_store: int            # channels of the stored input (stem: 8)
+    cin_store: int            # channels of the stored input (stem: 16, space-to-depth)
     H: int                    # input spatial size
     W: int
     w_off: int = 0            # flat offsets
@@ -78,6 +79,8 @@ class ConvBN:
 
     def geom(self, Nb: int) -> ConvGeom:
         c = self.conv
+        if self.name == "stem":   # 7x7/2 on RGB == 4x4/1 on the 2x2 space-to-depth image
+            return K.stem_s2d_geom(Nb, 2 * self.H)
         return ConvGeom(Nb, self.H, self.W, self.cin_store, c.out_channels, c.kernel_size[0],
                         c.kernel_size[1], c.stride[0], c.padding[0])
 
@@ -121,7 +124,9 @@ class NativeResNet(nn.Module):
     # ------------------------------------------------------------------ planning
     def _build_plan(self) -> None:
         S = self.image_size
-        self.stem = ConvBN("stem", self.conv1, self.bn1, 8, S, S)
+        if S % 2:
+            raise ValueError("image size must be even (space-to-depth stem)")
+        self.stem = ConvBN("stem", self.conv1, self.bn1, 16, S // 2, S // 2)
         h = self.stem.Ho
         h = (h + 2 - 3) // 2 + 1  # maxpool 3x3/2/1
         self.pool_hw = h
@@ -198,7 +203,8 @@ class NativeResNet(nn.Module):
             u.nbt_idx = i
         self.flat_buffers = torch.zeros(boff, dtype=torch.float32, device=dev)
         self.flat_nbt = torch.zeros(len(units), dtype=torch.int64, device=dev)
-        self.stem_packed = torch.zeros(64, 448, dtype=self.dtype, device=dev)
+        self.stem_packed = torch.zeros(64, 256, dtype=self.dtype, device=dev)   # [64][4][4][16]
+        self.stem_wgrad = torch.zeros(64 * 256, dtype=torch.float32, device=dev)
         self.bn_state = torch.zeros(sum(4 * _align(u.cout) for u in units), dtype=torch.float32,
                                     device=dev)
         so = 0
@@ -291,8 +297,8 @@ class NativeResNet(nn.Module):
         self._pack_stem()
 
     def _pack_stem(self) -> None:
-        K.pack_stem(self.flat_params[self.stem.w_off:self.stem.w_off + self.stem.w_len],
-                    self.stem_packed)
+        K.pack_stem_s2d(self.flat_params[self.stem.w_off:self.stem.w_off + self.stem.w_len],
+                        self.stem_packed)
 
     def _empty(self, *shape, dtype=None) -> torch.Tensor:
         return torch.empty(*shape, dtype=self.dtype if dtype is None else dtype, device=self.device)
@@ -321,35 +327,37 @@ class NativeResNet(nn.Module):
 
     # ------------------------------------------------------------------ input
     def input_generator(self, ds) -> Callable:
-        """Loader hook: sample ids -> (NHWC8 16-bit images, int64 labels) made on the device."""
+        """Loader hook: sample ids -> (model-ready input, int64 labels), generated on the device
+        directly in the stem's 2x2 space-to-depth NHWC layout [B, S/2, S/2, 16] (16-bit)."""
         S = ds.image_size
 
         def gen(ids: torch.Tensor):
             ids_d = ids.to(self.device, non_blocking=True)
             B = ids_d.numel()
-            x = self._empty(B, S, S, 8)
+            x = self._empty(B, S // 2, S // 2, 16)
             lab = torch.empty(B, dtype=torch.int64, device=self.device)
             keys = torch.empty(B, dtype=torch.int32, device=self.device)
-            K.synth_batch(ids_d, ds.seed, ds.split, ds.num_classes, S, x, lab, keys)
+            K.synth_batch_s2d(ids_d, ds.seed, ds.split, ds.num_classes, S, x, lab, keys)
             return x, lab
 
         return gen
 
     def prepare_input(self, x: torch.Tensor) -> torch.Tensor:
         """Validate and convert the input BEFORE any kernel runs: every kernel's indexing assumes
-        the plan's geometry, so a mismatched image size must never reach the GPU."""
+        the plan's geometry, so a mismatched image size must never reach the GPU. Accepts NCHW
+        images [B,3,S,S] (any float dtype) or the model-ready s2d layout [B,S/2,S/2,16]."""
         S = self.image_size
-        if x.dtype == self.dtype and x.dim() == 4 and x.shape[-1] == 8:
-            if tuple(x.shape[1:3]) != (S, S) or x.device != self.device:
-                raise ValueError(f"NHWC8 input {tuple(x.shape)} on {x.device} does not match the "
+        if x.dtype == self.dtype and x.dim() == 4 and x.shape[-1] == 16:
+            if tuple(x.shape[1:3]) != (S // 2, S // 2) or x.device != self.device:
+                raise ValueError(f"s2d input {tuple(x.shape)} on {x.device} does not match the "
                                  f"planned {S}x{S} on {self.device}")
             return x.contiguous()
         if x.dim() != 4 or x.shape[1] != 3 or tuple(x.shape[2:]) != (S, S):
-            raise ValueError(f"expected [B,3,{S},{S}] images or NHWC8 {self.dtype} input, "
-                             f"got {tuple(x.shape)}")
+            raise ValueError(f"expected [B,3,{S},{S}] images or [B,{S // 2},{S // 2},16] "
+                             f"{self.dtype} input, got {tuple(x.shape)}")
         xin = x.to(self.device, torch.float32).contiguous()
-        out = self._empty(x.shape[0], x.shape[2], x.shape[3], 8)
-        K.nchw_to_nhwc8(xin, out)
+        out = self._empty(x.shape[0], S // 2, S // 2, 16)
+        K.nchw_to_s2d(xin, out)
         return out
 
     # ------------------------------------------------------------------ forward
@@ -503,7 +511,8 @@ class NativeResNet(nn.Module):
         u = self.stem
         K.bn_bwd(ws, y0, st0[0], st0[1], self.gamma(u), st0[2], st0[3], self.dgamma(u),
                  self.dbeta(u), dy0, g1=dA0, accumulate=acc)
-        K.conv_wgrad(dy0, x0, u.geom(Nb), self.wgrad_view(u), ws, cin_real=3, accumulate=acc)
+        K.conv_wgrad(dy0, x0, u.geom(Nb), self.stem_wgrad, ws)
+        K.stem_s2d_grad(self.stem_wgrad, self.wgrad_view(u), accumulate=acc)
         if red is not None:
             red.grads_ready(self.block_bounds[-1])
             red.finish()

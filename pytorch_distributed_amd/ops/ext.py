@@ -74,6 +74,10 @@ _SIGS = {
     "pda_pack_stem": [_V, _V, _I, _I, _I, _I, _I, _I, _V],
     "pda_synth": [_V, _I, _U, _I, _V, _V, _I, _V, _I, _V],
     "pda_nchw_to_nhwc8": [_V, _I, _I, _I, _I, _V, _I, _V],
+    "pda_synth_s2d": [_V, _I, _U, _I, _V, _V, _I, _V, _I, _V],
+    "pda_nchw_to_s2d": [_V, _I, _I, _I, _V, _I, _V],
+    "pda_pack_stem_s2d": [_V, _V, _I, _I, _V],
+    "pda_stem_s2d_grad": [_V, _V, _I, _I, _V],
 }
 
 

@@ -13,6 +13,7 @@ from __future__ import annotations
 
 import ctypes as C
 import math
+import os
 from dataclasses import dataclass
 from typing import Optional, Tuple
 
@@ -40,21 +41,24 @@ class ConvGeom:
     S: int
     stride: int
     pad: int
+    ho: Optional[int] = None   # explicit output size (asymmetric-padding forms, e.g. the s2d stem)
+    wo: Optional[int] = None
 
     @property
     def Ho(self) -> int:
-        return (self.H + 2 * self.pad - self.R) // self.stride + 1
+        return self.ho if self.ho is not None else (self.H + 2 * self.pad - self.R) // self.stride + 1
 
     @property
     def Wo(self) -> int:
-        return (self.W + 2 * self.pad - self.S) // self.stride + 1
+        return self.wo if self.wo is not None else (self.W + 2 * self.pad - self.S) // self.stride + 1
 
     def desc(self, Nb: Optional[int] = None) -> ConvDesc:
         return ConvDesc(self.Nb if Nb is None else Nb, self.H, self.W, self.Cin, self.Cout, self.R,
                         self.S, self.stride, self.pad, self.Ho, self.Wo)
 
     def with_batch(self, Nb: int) -> "ConvGeom":
-        return ConvGeom(Nb, self.H, self.W, self.Cin, self.Cout, self.R, self.S, self.stride, self.pad)
+        return ConvGeom(Nb, self.H, self.W, self.Cin, self.Cout, self.R, self.S, self.stride, self.pad,
+                        self.ho, self.wo)
 
 
 class Workspace:
@@ -75,11 +79,19 @@ class Workspace:
 _NUM_CU = 256
 
 
-def pick_tile(M: int, N: int) -> Tuple[int, int]:
+_SINGLE_STAGE = os.environ.get("PDA_SINGLE_STAGE", "1") != "0"
+
+
+def pick_tile(M: int, N: int, K: Optional[int] = None) -> Tuple[int, int]:
+    """(bm, bn) for an implicit GEMM; a negative bm selects the single-LDS-buffer variant: half the
+    LDS admits a third resident block per CU, which hides the global-load latency better than
+    double buffering does at two blocks per CU (measured on all 23 ResNet-50 shapes)."""
     bn = 64 if N <= 64 else 128
     bm = 128
     if math.ceil(M / 128) * math.ceil(N / bn) < 2 * _NUM_CU:
         bm = 64
+    if bm == 128 and _SINGLE_STAGE:
+        bm = -128     # measured faster on every ResNet-50 shape (tools/conv_bench.py)
     return bm, bn
 
 
@@ -91,8 +103,8 @@ def conv_fwd(x: torch.Tensor, w: torch.Tensor, g: ConvGeom, out: torch.Tensor,
     stats (f32, >= ceil(M/bm)*2*Cout) receives per-M-tile (sum, sumsq) partials."""
     Nb = x.shape[0]
     M = Nb * g.Ho * g.Wo
-    bm, bn = tile or pick_tile(M, g.Cout)
     Kpad = w.shape[-1] if w.dim() == 2 else w[0].numel()
+    bm, bn = tile or pick_tile(M, g.Cout, Kpad)
     d = g.desc(Nb)
     out_f32 = out.dtype == torch.float32
     pitch = out.stride(0) if out.dim() == 2 else g.Cout
@@ -105,19 +117,27 @@ def conv_fwd(x: torch.Tensor, w: torch.Tensor, g: ConvGeom, out: torch.Tensor,
 
 def stats_tiles(M: int, Cout: int, tile: Optional[Tuple[int, int]] = None) -> int:
     bm, _ = tile or pick_tile(M, Cout)
-    return math.ceil(M / bm)
+    return math.ceil(M / abs(bm))
 
 
 def dgrad_tile(g: ConvGeom, Nb: int) -> Tuple[int, int]:
     M = Nb * (g.H // g.stride) * (g.W // g.stride)
-    return pick_tile(M * g.stride * g.stride, g.Cin)
+    return pick_tile(M * g.stride * g.stride, g.Cin, g.Cout * _max_class_taps(g))
+
+
+def _max_class_taps(g: ConvGeom) -> int:
+    if g.stride == 1:
+        return g.R * g.S
+    return max(sum(1 for r in range(g.R) if (ph + g.pad - r) % 2 == 0) *
+               sum(1 for s in range(g.S) if (pw + g.pad - s) % 2 == 0)
+               for ph in (0, 1) for pw in (0, 1))
 
 
 def dgrad_slabs(g: ConvGeom, Nb: int, tile: Optional[Tuple[int, int]] = None) -> int:
     """Number of partial-sum slabs the fused BN epilogue of a dgrad writes (classes x M-tiles)."""
     bm, _ = tile or dgrad_tile(g, Nb)
     M = Nb * (g.H // g.stride) * (g.W // g.stride)
-    return g.stride * g.stride * math.ceil(M / bm)
+    return g.stride * g.stride * math.ceil(M / abs(bm))
 
 
 def conv_dgrad(dy: torch.Tensor, w: torch.Tensor, g: ConvGeom, dx: torch.Tensor,
@@ -156,7 +176,7 @@ def wgrad_plan(g: ConvGeom, Nb: int, tile: Optional[Tuple[int, int]] = None,
     bn = 128 if N >= 128 else 64
     if tile:
         bm, bn = tile
-    tiles = math.ceil(M / bm) * math.ceil(N / bn)
+    tiles = math.ceil(M / abs(bm)) * math.ceil(N / bn)
     splits = max(1, min(math.ceil(target_blocks / tiles), math.ceil(K / 256),
                         max(1, max_slab_bytes // (M * N * 4))))
     k_chunk = math.ceil(K / splits / 64) * 64
@@ -405,3 +425,31 @@ def nchw_to_nhwc8(x, out) -> None:
     B, C_, H, W = x.shape
     check(ext.lib().pda_nchw_to_nhwc8(ptr(x), B, C_, H, W, ptr(out), dt_of(out), stream(x.device)),
           "nchw_to_nhwc8")
+
+
+# ------------------------------------------------------------------ stem (space-to-depth form)
+def stem_s2d_geom(Nb: int, S: int) -> ConvGeom:
+    """The 7x7/2/3 stem as a 4x4/1 conv with pad 2 on the 2x2 space-to-depth image (16 ch)."""
+    return ConvGeom(Nb, S // 2, S // 2, 16, 64, 4, 4, 1, 2, ho=S // 2, wo=S // 2)
+
+
+def synth_batch_s2d(ids, seed: int, split: str, num_classes: int, S: int, out, labels, keys) -> None:
+    check(ext.lib().pda_synth_s2d(ptr(ids), ids.numel(), synth_salt(seed, split), num_classes,
+                                  ptr(keys), ptr(labels), S, ptr(out), dt_of(out), stream(out.device)),
+          "synth_s2d")
+
+
+def nchw_to_s2d(x, out) -> None:
+    B, C_, S, _ = x.shape
+    check(ext.lib().pda_nchw_to_s2d(ptr(x), B, C_, S, ptr(out), dt_of(out), stream(x.device)),
+          "nchw_to_s2d")
+
+
+def pack_stem_s2d(src_ohwi, dst) -> None:
+    check(ext.lib().pda_pack_stem_s2d(ptr(src_ohwi), ptr(dst), dst.shape[0], dt_of(dst),
+                                      stream(dst.device)), "pack_stem_s2d")
+
+
+def stem_s2d_grad(gpacked, grad_ohwi, accumulate: bool = False) -> None:
+    check(ext.lib().pda_stem_s2d_grad(ptr(gpacked), ptr(grad_ohwi), gpacked.numel() // 256,
+                                      int(accumulate), stream(gpacked.device)), "stem_s2d_grad")
