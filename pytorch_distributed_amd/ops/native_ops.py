@@ -172,8 +172,10 @@ def bn_epilogue(ws: "Workspace", G: int, y, scale, shift, res=None, y2=None, sca
 def wgrad_plan(g: ConvGeom, Nb: int, tile: Optional[Tuple[int, int]] = None,
                target_blocks: int = 2 * _NUM_CU, max_slab_bytes: int = 64 << 20):
     M, N, K = g.Cout, g.R * g.S * g.Cin, Nb * g.Ho * g.Wo
-    bm = 128 if M >= 128 else 64
     bn = 128 if N >= 128 else 64
+    bm = 128 if M >= 128 else 64
+    if _SINGLE_STAGE and (bm == 128 or bn == 128):
+        bm = -bm      # single-LDS-buffer variants (tools/conv_bench.py: best or within 2%)
     if tile:
         bm, bn = tile
     tiles = math.ceil(M / abs(bm)) * math.ceil(N / bn)

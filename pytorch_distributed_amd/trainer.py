@@ -105,6 +105,9 @@ def train(dataloader, model, criterion, optimizer, scheduler, epoch: int, ctx: C
     cfg = ctx.cfg
     steps = 0
     scaler = ctx.scaler
+    from .utils.metrics import StepProfiler
+    prof = StepProfiler(int(os.environ.get("MX_PROFILE", "0") or 0) if epoch == 0 else 0, save_path,
+                        ctx.rank)
     for step, (samples, labels) in dataloader.iter_from(start_step):
         if ctx.cfg.script == "single" and cfg.log_every and step % cfg.log_every == 0:
             print("epoch: {}, step: {}".format(epoch, step), flush=True)
@@ -127,6 +130,7 @@ def train(dataloader, model, criterion, optimizer, scheduler, epoch: int, ctx: C
             optimizer.step()
         _sync_step(ctx)
         steps += 1
+        prof.step()
         if ctx.suspend is not None:
             ctx.suspend.tick()
             if ctx.suspend.requested():
@@ -137,6 +141,7 @@ def train(dataloader, model, criterion, optimizer, scheduler, epoch: int, ctx: C
                     print(f"suspend: saved {save_path / 'latest.pt'} at epoch {epoch} step {step + 1}",
                           flush=True)
                 go_suspend()
+    prof.close()
     return steps
 
 
@@ -174,7 +179,27 @@ def validate(dataloader, model, criterion, epoch: int, ctx: Context) -> float:
     return c1 / total
 
 
+def _make_folder_loaders(cfg: RunConfig, ctx: Context, per_rank_batch: int):
+    from .data.folder import ImageFolder, train_transform, val_transform
+    root = cfg.data.split(":", 1)[1]
+    train_ds = ImageFolder(root, "train", train_transform(cfg.image_size))
+    val_ds = ImageFolder(root, "val", val_transform(cfg.image_size, int(round(cfg.image_size * 256 / 224))))
+    train_sampler = val_sampler = None
+    if ctx.distributed:
+        train_sampler = DistributedSampler(train_ds, ctx.world, ctx.rank, shuffle=True, seed=cfg.seed)
+        val_sampler = DistributedSampler(val_ds, ctx.world, ctx.rank, shuffle=True, seed=cfg.seed)
+    tl = train_ds.loader(per_rank_batch, sampler=train_sampler, num_workers=cfg.num_workers,
+                         max_steps=cfg.steps_per_epoch)
+    vl = val_ds.loader(per_rank_batch, sampler=val_sampler, num_workers=cfg.num_workers,
+                       max_steps=cfg.val_steps)
+    return tl, vl, train_sampler
+
+
 def _make_loaders(cfg: RunConfig, ctx: Context, model: nn.Module, per_rank_batch: int):
+    if cfg.data.startswith("folder:"):
+        return _make_folder_loaders(cfg, ctx, per_rank_batch)
+    if cfg.data != "synthetic":
+        raise ValueError(f"MX_DATA must be 'synthetic' or 'folder:<root>', got {cfg.data!r}")
     train_ds = SyntheticImageNet("train", cfg.train_samples, cfg.seed, cfg.num_classes, cfg.image_size)
     val_ds = SyntheticImageNet("val", cfg.val_samples, cfg.seed, cfg.num_classes, cfg.image_size)
     if ctx.distributed:

@@ -49,6 +49,41 @@ class Throughput:
         return self.images / self.elapsed
 
 
+class StepProfiler:
+    """``MX_PROFILE=<n>``: record the first n training steps with torch.profiler (ROCm kernel
+    names are our HIP kernels) and write a chrome trace to ``<save_path>/profile_rank<r>.json``.
+    For hardware counters use ``tools/gpu_profile.sh`` (rocprofv3) instead."""
+
+    def __init__(self, steps: int, out_dir, rank: int = 0) -> None:
+        self.steps = steps
+        self.n = 0
+        self.out = Path(out_dir) / f"profile_rank{rank}.json"
+        self.prof = None
+        if steps > 0:
+            acts = [torch.profiler.ProfilerActivity.CPU]
+            if torch.cuda.is_available():
+                acts.append(torch.profiler.ProfilerActivity.CUDA)
+            self.prof = torch.profiler.profile(activities=acts)
+            self.prof.__enter__()
+
+    def step(self) -> None:
+        if self.prof is None:
+            return
+        self.n += 1
+        if self.n >= self.steps:
+            self.close()
+
+    def close(self) -> None:
+        if self.prof is None:
+            return
+        if torch.cuda.is_available():
+            torch.cuda.synchronize()
+        self.prof.__exit__(None, None, None)
+        self.out.parent.mkdir(parents=True, exist_ok=True)
+        self.prof.export_chrome_trace(str(self.out))
+        self.prof = None
+
+
 class MetricsLog:
     def __init__(self, path, enabled: bool = True) -> None:
         self.path = Path(path)
