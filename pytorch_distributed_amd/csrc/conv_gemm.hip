@@ -51,8 +51,13 @@ struct ConvParams {
   int taps[4][9];     // DGRAD: tap ids (r*S+s) per parity class
   int Hc, Wc;         // DGRAD: class grid (H/stride, W/stride)
   FastDiv dHcWc, dWc;
+  // fused BatchNorm-apply + ReLU prologue on the gathered activation operand (FWD: A, WGRAD: B):
+  // the conv reads the PRE-BN tensor y and computes relu(y * pro_sc[c] + pro_sh[c]) while
+  // staging the tile (padding stays exactly 0), so the activation is never materialised.
+  const float* pro_sc;
+  const float* pro_sh;
   // DGRAD fused BatchNorm-backward epilogue (emode < 0: plain dX store)
-  int emode, enq;                  // 0 relu(bn(y)), 1 relu(bn(y)+ey2), 2 relu(bn(y)+bn2(ey2))
+  int emode, enq;                 // 0 relu(bn(y)), 1 relu(bn(y)+ey2), 2 relu(bn(y)+bn2(ey2))
   const u16* ey; const float* esc; const float* esh;
   const u16* ey2; const float* esc2; const float* esh2;
   const u16* eg2;                  // optional second gradient summed into dA
@@ -190,6 +195,23 @@ __global__ __launch_bounds__(NT, STAGES == 1 ? 3 : 2) void conv_gemm_kernel(Conv
   const u16* __restrict__ B = reinterpret_cast<const u16*>(p.b);
 
   i32x4 ra[AR], rb[BR];
+  // prologue state: per-chunk validity (padding must stay 0) and the chunk's 8 channel coeffs
+  const bool pro = (PASS == FWD || PASS == WGRAD) && p.pro_sc != nullptr;
+  bool pv[PASS == FWD ? AR : BR];
+  float psc[8], psh[8];
+  if (PASS == WGRAD && pro) {
+    const int cc = wb_colok ? wb_c : 0;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      psc[e] = p.pro_sc[cc + e];
+      psh[e] = p.pro_sh[cc + e];
+    }
+  }
+  auto pro_apply = [&](i32x4& v) {
+    u16* h = reinterpret_cast<u16*>(&v);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) h[e] = st16<DT>(fmaxf(ld16<DT>(h[e]) * psc[e] + psh[e], 0.f));
+  };
 
   auto load_tile = [&](int kt) {
     const int k0 = kbeg + kt * BK;
@@ -206,6 +228,14 @@ __global__ __launch_bounds__(NT, STAGES == 1 ? 3 : 2) void conv_gemm_kernel(Conv
         const bool ok = a_ok[i] && tap_ok && (unsigned)y < (unsigned)p.H && (unsigned)x < (unsigned)p.W;
         const size_t off = ((size_t)(a_img[i] * p.H + y) * p.W + x) * p.Cin + c;
         ra[i] = ld16B(A + (ok ? off : 0), ok);
+        pv[i] = ok;
+      }
+      if (pro) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          psc[e] = p.pro_sc[c + e];
+          psh[e] = p.pro_sh[c + e];
+        }
       }
     } else if constexpr (PASS == DGRAD) {
       const int ti = k0 / p.Cout;  // tile lies in one tap (Cout % 64 == 0)
@@ -269,6 +299,7 @@ __global__ __launch_bounds__(NT, STAGES == 1 ? 3 : 2) void conv_gemm_kernel(Conv
         ok = ok && (unsigned)y < (unsigned)p.H && (unsigned)x < (unsigned)p.W;
         const size_t off = ((size_t)(img * p.H + y) * p.W + x) * p.Cin + wb_c;
         rb[i] = ld16B(B + (ok ? off : 0), ok);
+        if constexpr (PASS == WGRAD) pv[i] = ok;
       }
     }
   };
@@ -278,8 +309,12 @@ __global__ __launch_bounds__(NT, STAGES == 1 ? 3 : 2) void conv_gemm_kernel(Conv
     char* sb = sa + A_BYTES;
     if constexpr (A_ROW) {
 #pragma unroll
-      for (int i = 0; i < AR; ++i)
+      for (int i = 0; i < AR; ++i) {
+        if constexpr (PASS == FWD) {
+          if (pro && pv[i]) pro_apply(ra[i]);
+        }
         *reinterpret_cast<i32x4*>(sa + row_addr((tid >> 3) + 32 * i, tid & 7)) = ra[i];
+      }
     } else {
       constexpr int CPR = BM / 8, RPI = NT / CPR;
 #pragma unroll
@@ -293,8 +328,12 @@ __global__ __launch_bounds__(NT, STAGES == 1 ? 3 : 2) void conv_gemm_kernel(Conv
     } else {
       constexpr int CPR = BN / 8, RPI = NT / CPR;
 #pragma unroll
-      for (int i = 0; i < BR; ++i)
+      for (int i = 0; i < BR; ++i) {
+        if constexpr (PASS == WGRAD) {
+          if (pro && pv[i]) pro_apply(rb[i]);
+        }
         *reinterpret_cast<i32x4*>(sb + col_addr<BN>(tid / CPR + RPI * i, tid % CPR)) = rb[i];
+      }
     }
   };
 
@@ -413,32 +452,12 @@ __global__ __launch_bounds__(NT, STAGES == 1 ? 3 : 2) void conv_gemm_kernel(Conv
     const int nq = do_bn ? p.enq : 2;
     u16* out = reinterpret_cast<u16*>(p.out);
     const int gcol = n0 + cc * 8;
-    size_t eoff[RPT];
-    bool eok[RPT];
-#pragma unroll
-    for (int i = 0; i < RPT; ++i) {
-      const int grow = m0 + rg + RG * i;
-      eok[i] = grow < p.M && gcol < p.N;
-      size_t orow = grow;
-      if constexpr (PASS == DGRAD) {
-        const uint32_t gg = eok[i] ? grow : 0;
-        const uint32_t img = fdiv(gg, p.dHcWc), rem = gg - img * p.dHcWc.d;
-        const uint32_t yi = fdiv(rem, p.dWc), xi = rem - yi * p.dWc.d;
-        const int h = (int)yi * p.stride + cls_ph, w = (int)xi * p.stride + cls_pw;
-        orow = ((size_t)img * p.H + h) * p.W + w;
-      }
-      eoff[i] = orow * p.out_pitch + gcol;
-    }
-    i32x4 py[RPT], pg2[RPT], py2[RPT];
+    // rows are processed in groups of PD; the fused-epilogue operands of a group are loaded
+    // before it is consumed (the first group's before the barrier that publishes the C tile),
+    // which bounds the prefetch registers to PD rows.
+    constexpr int PD = RPT > 4 ? 4 : RPT;
     float esc[8], esh[8], esc2[8], esh2[8];
     if (do_bn) {
-      const i32x4 z = {0, 0, 0, 0};
-#pragma unroll
-      for (int i = 0; i < RPT; ++i) {
-        py[i] = eok[i] ? *reinterpret_cast<const i32x4*>(p.ey + eoff[i]) : z;
-        pg2[i] = (eok[i] && p.eg2) ? *reinterpret_cast<const i32x4*>(p.eg2 + eoff[i]) : z;
-        py2[i] = (eok[i] && p.emode >= 1) ? *reinterpret_cast<const i32x4*>(p.ey2 + eoff[i]) : z;
-      }
       const int cg = gcol < p.N ? gcol : 0;
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
@@ -448,21 +467,52 @@ __global__ __launch_bounds__(NT, STAGES == 1 ? 3 : 2) void conv_gemm_kernel(Conv
         esh2[e] = p.emode == 2 ? p.esh2[cg + e] : 0.f;
       }
     }
+    auto row_off = [&](int i, bool& ok) -> uint32_t {
+      const int grow = m0 + rg + RG * i;
+      ok = grow < p.M && gcol < p.N;
+      uint32_t orow = ok ? grow : 0;
+      if constexpr (PASS == DGRAD) {
+        const uint32_t img = fdiv(orow, p.dHcWc), rem = orow - img * p.dHcWc.d;
+        const uint32_t yi = fdiv(rem, p.dWc), xi = rem - yi * p.dWc.d;
+        const int h = (int)yi * p.stride + cls_ph, w = (int)xi * p.stride + cls_pw;
+        orow = ((uint32_t)img * p.H + h) * p.W + w;
+      }
+      return orow * (uint32_t)p.out_pitch + gcol;
+    };
+    uint32_t eoff[PD];
+    bool eok[PD];
+    i32x4 py[PD], pg2[PD], py2[PD];
+    auto prefetch = [&](int g0) {
+      const i32x4 z = {0, 0, 0, 0};
+#pragma unroll
+      for (int j = 0; j < PD; ++j) {
+        eoff[j] = row_off(g0 + j, eok[j]);
+        if (do_bn) {
+          py[j] = eok[j] ? *reinterpret_cast<const i32x4*>(p.ey + eoff[j]) : z;
+          pg2[j] = (eok[j] && p.eg2) ? *reinterpret_cast<const i32x4*>(p.eg2 + eoff[j]) : z;
+          py2[j] = (eok[j] && p.emode >= 1) ? *reinterpret_cast<const i32x4*>(p.ey2 + eoff[j]) : z;
+        }
+      }
+    };
     float q0[8], q1[8], q2[8];
 #pragma unroll
     for (int e = 0; e < 8; ++e) { q0[e] = 0.f; q1[e] = 0.f; q2[e] = 0.f; }
+    prefetch(0);
     __syncthreads();
 #pragma unroll
-    for (int i = 0; i < RPT; ++i) {
-      const int row = rg + RG * i;
-      i32x4 v = *reinterpret_cast<const i32x4*>(ct + c_addr(row, cc) * 8);
-      if (eok[i]) {
+    for (int g0 = 0; g0 < RPT; g0 += PD) {
+      if (g0 > 0) prefetch(g0);
+#pragma unroll
+      for (int j = 0; j < PD; ++j) {
+        const int row = rg + RG * (g0 + j);
+        i32x4 v = *reinterpret_cast<const i32x4*>(ct + c_addr(row, cc) * 8);
+        if (!eok[j]) continue;
         if (do_bn) {
           float g[8], yv[8], y2v[8], pre[8];
           const u16* h = reinterpret_cast<const u16*>(&v);
-          const u16* h2 = reinterpret_cast<const u16*>(&pg2[i]);
-          const u16* hy = reinterpret_cast<const u16*>(&py[i]);
-          const u16* hy2 = reinterpret_cast<const u16*>(&py2[i]);
+          const u16* h2 = reinterpret_cast<const u16*>(&pg2[j]);
+          const u16* hy = reinterpret_cast<const u16*>(&py[j]);
+          const u16* hy2 = reinterpret_cast<const u16*>(&py2[j]);
 #pragma unroll
           for (int e = 0; e < 8; ++e) {
             g[e] = ld16<DT>(h[e]) + ld16<DT>(h2[e]);
@@ -491,7 +541,7 @@ __global__ __launch_bounds__(NT, STAGES == 1 ? 3 : 2) void conv_gemm_kernel(Conv
             q1[e] += f * f;
           }
         }
-        *reinterpret_cast<i32x4*>(out + eoff[i]) = v;
+        *reinterpret_cast<i32x4*>(out + eoff[j]) = v;
       }
     }
     if (do_stats || do_bn) {
@@ -603,10 +653,11 @@ extern "C" {
 
 // Y[M=Nb*Ho*Wo][Cout] = conv(X, W). W: [Cout][Kpad] 16-bit. stats: [ceil(M/bm)][2][Cout] or null.
 int pda_conv_fwd(const ConvDesc* d, const void* x, const void* w, int Kpad, void* y, int out_f32,
-                 int out_pitch, const float* bias, float* stats, int relu, int dt, int bm, int bn,
-                 hipStream_t st) {
+                 int out_pitch, const float* bias, float* stats, int relu, const float* pro_sc,
+                 const float* pro_sh, int dt, int bm, int bn, hipStream_t st) {
   ConvParams p{};
   fill_geom(p, *d);
+  p.pro_sc = pro_sc; p.pro_sh = pro_sh;
   p.a = x; p.b = w; p.out = y; p.stats = stats; p.bias = bias;
   p.M = d->Nb * d->Ho * d->Wo; p.N = d->Cout; p.Kpad = Kpad; p.K = Kpad;
   p.out_f32 = out_f32; p.relu = relu; p.out_pitch = out_pitch > 0 ? out_pitch : d->Cout;
@@ -664,9 +715,11 @@ int pda_conv_dgrad(const ConvDesc* d, const void* dy, const void* w, void* dx, c
 
 // slab[splits][Cout][R*S*Cin] partial weight gradients (f32). k_chunk must be a multiple of 64.
 int pda_conv_wgrad(const ConvDesc* d, const void* dy, const void* x, float* slab, int splits,
-                   int k_chunk, int dt, int bm, int bn, hipStream_t st) {
+                   int k_chunk, const float* pro_sc, const float* pro_sh, int dt, int bm, int bn,
+                   hipStream_t st) {
   ConvParams p{};
   fill_geom(p, *d);
+  p.pro_sc = pro_sc; p.pro_sh = pro_sh;
   p.a = dy; p.b = x; p.out = slab;
   p.M = d->Cout; p.N = d->R * d->S * d->Cin;
   p.K = d->Nb * d->Ho * d->Wo;

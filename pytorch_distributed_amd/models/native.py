@@ -119,6 +119,9 @@ class NativeResNet(nn.Module):
         self._grads_zero = True
         self._fwd_ctx = None
         self._anchor = torch.zeros((), device=device, requires_grad=True)
+        # BN1/BN2 (+ReLU) applied inside the consumer conv's operand staging (fwd and wgrad)
+        import os
+        self.fuse_prologue = os.environ.get("PDA_FUSE_PROLOGUE", "1") != "0"
         self.refresh_shadow()
 
     # ------------------------------------------------------------------ planning
@@ -361,8 +364,9 @@ class NativeResNet(nn.Module):
         return out
 
     # ------------------------------------------------------------------ forward
-    def _conv_bn(self, u: ConvBN, x: torch.Tensor, train: bool) -> torch.Tensor:
-        """y = conv(x) and BN coefficients (batch stats in training, running stats in eval)."""
+    def _conv_bn(self, u: ConvBN, x: torch.Tensor, train: bool, pro=None) -> torch.Tensor:
+        """y = conv(x) and BN coefficients (batch stats in training, running stats in eval).
+        ``pro=(scale, shift)``: x is the previous PRE-BN tensor; the conv applies BN+ReLU on load."""
         Nb = x.shape[0]
         g = u.geom(Nb)
         M = Nb * g.Ho * g.Wo
@@ -371,14 +375,14 @@ class NativeResNet(nn.Module):
         if train:
             T = K.stats_tiles(M, u.cout)
             part = self.ws.get("fwd_stats", T * 2 * u.cout)
-            K.conv_fwd(x, self.w16(u), g, y, stats=part)
+            K.conv_fwd(x, self.w16(u), g, y, stats=part, pro=pro)
             K.bn_finalize_fwd(part, T, u.cout, M, self.gamma(u), self.beta(u), u.bn.eps,
                               u.bn.momentum if u.bn.momentum is not None else 0.1,
                               st[0], st[1], st[2], st[3], self.rmean(u), self.rvar(u),
                               self.flat_nbt[u.nbt_idx:u.nbt_idx + 1], update_running=True,
                               ws=self.ws)
         else:
-            K.conv_fwd(x, self.w16(u), g, y)
+            K.conv_fwd(x, self.w16(u), g, y, pro=pro)
             K.bn_eval_coeffs(self.gamma(u), self.beta(u), self.rmean(u), self.rvar(u), u.bn.eps,
                              st[2], st[3])
         return y
@@ -413,16 +417,21 @@ class NativeResNet(nn.Module):
             rec = {"x": h} if save else None
             a = h
             ys, acts = [], [h]
+            pro = None
             for j, u in enumerate(b.units):
-                y = self._conv_bn(u, a, train)
+                y = self._conv_bn(u, a, train, pro)
                 ys.append(y)
                 if save:
                     rec[f"s{j}"] = u.state
                 if j < len(b.units) - 1:
                     sc, sh = self._coeffs(u, train)
-                    a = self._empty(*y.shape)
-                    K.bn_apply(y, sc, sh, a, relu=True)
-                    acts.append(a)
+                    if self.fuse_prologue:   # next conv applies BN+ReLU while staging its tiles
+                        a, pro = y, (sc, sh)
+                        acts.append(None)
+                    else:
+                        a, pro = self._empty(*y.shape), None
+                        K.bn_apply(y, sc, sh, a, relu=True)
+                        acts.append(a)
             yd = None
             if b.ds is not None:
                 yd = self._conv_bn(b.ds, h, train)
@@ -582,7 +591,13 @@ class NativeResNet(nn.Module):
             u = b.units[j]
             a_in = acts[j]
             g = u.geom(Nb)
-            K.conv_wgrad(dy, a_in, g, self.wgrad_view(u), ws, accumulate=acc)
+            if a_in is None:   # fused prologue: recompute relu(bn(y_{j-1})) while staging B
+                sp_ = rec[f"s{j - 1}"]
+                K.conv_wgrad(dy, ys[j - 1], g, self.wgrad_view(u), ws, accumulate=acc,
+                             pro=(sp_[2], sp_[3]))
+                a_in = ys[j - 1]
+            else:
+                K.conv_wgrad(dy, a_in, g, self.wgrad_view(u), ws, accumulate=acc)
             out = self._empty(*a_in.shape)
             if j > 0:
                 up = b.units[j - 1]

@@ -50,9 +50,9 @@ class BnEpi(C.Structure):
 
 _V, _I, _F, _L, _U = C.c_void_p, C.c_int, C.c_float, C.c_longlong, C.c_uint
 _SIGS = {
-    "pda_conv_fwd": [C.POINTER(ConvDesc), _V, _V, _I, _V, _I, _I, _V, _V, _I, _I, _I, _I, _V],
+    "pda_conv_fwd": [C.POINTER(ConvDesc), _V, _V, _I, _V, _I, _I, _V, _V, _I, _V, _V, _I, _I, _I, _V],
     "pda_conv_dgrad": [C.POINTER(ConvDesc), _V, _V, _V, C.POINTER(BnEpi), _I, _I, _I, _V],
-    "pda_conv_wgrad": [C.POINTER(ConvDesc), _V, _V, _V, _I, _I, _I, _I, _I, _V],
+    "pda_conv_wgrad": [C.POINTER(ConvDesc), _V, _V, _V, _I, _I, _V, _V, _I, _I, _I, _V],
     "pda_wgrad_reduce": [_V, _V, _I, _I, _I, _I, _I, _I, _F, _I, _V],
     "pda_bn_finalize_fwd": [_V, _I, _I, _F, _V, _V, _F, _F, _V, _V, _V, _V, _V, _V, _V, _I, _V],
     "pda_slab_reduce": [_V, _I, _I, _I, _V, _V],

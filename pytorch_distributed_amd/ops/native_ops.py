@@ -98,9 +98,11 @@ def pick_tile(M: int, N: int, K: Optional[int] = None) -> Tuple[int, int]:
 # ------------------------------------------------------------------ conv
 def conv_fwd(x: torch.Tensor, w: torch.Tensor, g: ConvGeom, out: torch.Tensor,
              stats: Optional[torch.Tensor] = None, bias: Optional[torch.Tensor] = None,
-             relu: bool = False, tile: Optional[Tuple[int, int]] = None) -> torch.Tensor:
+             relu: bool = False, tile: Optional[Tuple[int, int]] = None,
+             pro: Optional[Tuple[torch.Tensor, torch.Tensor]] = None) -> torch.Tensor:
     """out[M, Cout] (16-bit or f32) = conv(x, w). w: [Cout, Kpad] 16-bit, Kpad = w.shape[1].
-    stats (f32, >= ceil(M/bm)*2*Cout) receives per-M-tile (sum, sumsq) partials."""
+    stats (f32, >= ceil(M/bm)*2*Cout) receives per-M-tile (sum, sumsq) partials.
+    pro = (scale, shift): x is a PRE-BatchNorm tensor and the conv consumes relu(x*scale+shift)."""
     Nb = x.shape[0]
     M = Nb * g.Ho * g.Wo
     Kpad = w.shape[-1] if w.dim() == 2 else w[0].numel()
@@ -109,8 +111,8 @@ def conv_fwd(x: torch.Tensor, w: torch.Tensor, g: ConvGeom, out: torch.Tensor,
     out_f32 = out.dtype == torch.float32
     pitch = out.stride(0) if out.dim() == 2 else g.Cout
     rc = ext.lib().pda_conv_fwd(C.byref(d), ptr(x), ptr(w), Kpad, ptr(out), int(out_f32), pitch,
-                                ptr(bias), ptr(stats), int(relu), dt_of(x), bm, bn,
-                                stream(x.device))
+                                ptr(bias), ptr(stats), int(relu), ptr(pro[0] if pro else None),
+                                ptr(pro[1] if pro else None), dt_of(x), bm, bn, stream(x.device))
     check(rc, "conv_fwd")
     return out
 
@@ -188,16 +190,19 @@ def wgrad_plan(g: ConvGeom, Nb: int, tile: Optional[Tuple[int, int]] = None,
 
 def conv_wgrad(dy: torch.Tensor, x: torch.Tensor, g: ConvGeom, grad: torch.Tensor, ws: Workspace,
                cin_real: Optional[int] = None, scale: float = 1.0, accumulate: bool = False,
-               tile: Optional[Tuple[int, int]] = None) -> torch.Tensor:
-    """grad (f32, OHWI with cin_real channels, rows of pitch R*S*cin_real) = scale * dW."""
+               tile: Optional[Tuple[int, int]] = None,
+               pro: Optional[Tuple[torch.Tensor, torch.Tensor]] = None) -> torch.Tensor:
+    """grad (f32, OHWI with cin_real channels, rows of pitch R*S*cin_real) = scale * dW.
+    pro = (scale, shift): x is PRE-BatchNorm; the activation relu(x*scale+shift) is recomputed."""
     Nb = dy.shape[0]
     bm, bn, splits, k_chunk = wgrad_plan(g, Nb, tile)
     M, N = g.Cout, g.R * g.S * g.Cin
     slab = ws.get("wgrad_slab", splits * M * N)
     d = g.desc(Nb)
     st = stream(dy.device)
-    rc = ext.lib().pda_conv_wgrad(C.byref(d), ptr(dy), ptr(x), ptr(slab), splits, k_chunk, dt_of(dy),
-                                  bm, bn, st)
+    rc = ext.lib().pda_conv_wgrad(C.byref(d), ptr(dy), ptr(x), ptr(slab), splits, k_chunk,
+                                  ptr(pro[0] if pro else None), ptr(pro[1] if pro else None),
+                                  dt_of(dy), bm, bn, st)
     check(rc, "conv_wgrad")
     cr = g.Cin if cin_real is None else cin_real
     rc = ext.lib().pda_wgrad_reduce(ptr(slab), ptr(grad), splits, M, N, int(math.log2(g.Cin)), cr,
