@@ -67,9 +67,13 @@ class NativeReducer:
         while self._next < len(self.buckets) and self.buckets[self._next][1] <= upto:
             s, e = self.buckets[self._next]
             view = self.flat[s:e]
-            if self.prescale and self.comm.world_size > 1:
-                view.div_(self.comm.world_size)
-            self._works.append(self.comm.all_reduce_async(view))
+            if getattr(self.comm, "supports_avg", False):
+                # RCCL ncclAvg: the 1/world scaling happens inside the collective (no extra pass)
+                self._works.append(self.comm.all_reduce_async(view, op="avg"))
+            else:
+                if self.prescale and self.comm.world_size > 1:
+                    view.div_(self.comm.world_size)
+                self._works.append(self.comm.all_reduce_async(view))
             self._next += 1
 
     def finish(self) -> None:

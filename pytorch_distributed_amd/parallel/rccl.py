@@ -74,6 +74,8 @@ def _check(rc: int, what: str) -> None:
 
 
 class RcclCommunicator(Communicator):
+    supports_avg = True
+
     def __init__(self, device: torch.device, group=None, store=None) -> None:
         if not dist.is_initialized():
             raise RuntimeError("RcclCommunicator needs an initialised torch.distributed (for the store)")
@@ -110,6 +112,8 @@ class RcclCommunicator(Communicator):
         return done
 
     def wait(self, handle) -> None:
+        if getattr(self, "_watchdog_error", None) is not None:
+            self.check()
         if handle is not None:
             torch.cuda.current_stream(self.device).wait_event(handle)
 
@@ -141,9 +145,37 @@ class RcclCommunicator(Communicator):
 
     def check(self) -> None:
         """Raise if the communicator saw an asynchronous error (dead peer, network)."""
+        err = getattr(self, "_watchdog_error", None)
+        if err is not None:
+            raise RuntimeError(f"RCCL communicator aborted by watchdog: {err}")
         _check(load().pda_comm_check(self._h), "async")
 
+    def start_watchdog(self, interval_s: float = 5.0) -> None:
+        """Poll ``ncclCommGetAsyncError`` from a daemon thread; on an error (e.g. a dead peer)
+        abort the communicator so collectives blocked on it return instead of hanging, and make
+        the next :meth:`check` / :meth:`wait` raise (SURVEY §5.3 failure detection)."""
+        import threading
+
+        def run():
+            while self._h and getattr(self, "_watchdog_on", False):
+                rc = load().pda_comm_check(self._h)
+                if rc != 0:
+                    self._watchdog_error = load().pda_comm_error_string(rc).decode() if rc > 0 else rc
+                    load().pda_comm_destroy(self._h, 1)
+                    self._h = C.c_void_p()
+                    return
+                threading.Event().wait(interval_s)
+
+        self._watchdog_on = True
+        t = threading.Thread(target=run, name="rccl-watchdog", daemon=True)
+        t.start()
+        self._watchdog = t
+
+    def stop_watchdog(self) -> None:
+        self._watchdog_on = False
+
     def close(self, abort: bool = False) -> None:
+        self.stop_watchdog()
         if self._h:
             load().pda_comm_destroy(self._h, int(abort))
             self._h = C.c_void_p()

@@ -90,8 +90,10 @@ def test_rccl_communicator_world1():
     try:
         from pytorch_distributed_amd.parallel.rccl import RcclCommunicator
         c = RcclCommunicator(dev)
+        c.start_watchdog(0.05)
         t = torch.arange(1000, dtype=torch.float32, device=dev)
         h = c.all_reduce_async(t)
+        c.wait(c.all_reduce_async(t, op="avg"))
         c.wait(h)
         c.broadcast(t, 0)
         c.barrier()
