@@ -10,7 +10,7 @@ from collections import defaultdict
 
 def family(name: str) -> str:
     n = name
-    m = re.search(r"conv_gemm_kernel<(\d+), (\d+), (\d+), (\d+)>", n) or \
+    m = re.search(r"conv_gemm_kernel<(\d+), (\d+), (\d+), (\d+)(?:, (\d+))?>", n) or \
         re.search(r"conv_gemm_kernelILi(\d+)ELi(\d+)ELi(\d+)ELi(\d+)E", n)
     if m:
         p = {"0": "fwd", "1": "dgrad", "2": "wgrad"}[m.group(1)]
