@@ -26,6 +26,26 @@ __device__ __forceinline__ u16 f32_to_bf16(float f) {
 __device__ __forceinline__ float f16_to_f32(u16 v) { return (float)__builtin_bit_cast(_Float16, v); }
 __device__ __forceinline__ u16 f32_to_f16(float f) { return __builtin_bit_cast(u16, (_Float16)f); }
 
+// packed pairs: one dword = two 16-bit elements (lo = first). Conversions use the packed
+// instructions (v_cvt_pk_bf16_f32 / v_cvt_pk_f16 RNE) and f32x2 math maps to v_pk_{add,mul,fma}_f32.
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
+template <int DT> __device__ __forceinline__ uint32_t pack2(f32x2 v);
+template <> __device__ __forceinline__ uint32_t pack2<DT_BF16>(f32x2 v) {
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector(v, bf16x2));
+}
+template <> __device__ __forceinline__ uint32_t pack2<DT_F16>(f32x2 v) {
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector(v, f16x2));
+}
+template <int DT> __device__ __forceinline__ f32x2 unpack2(uint32_t w);
+template <> __device__ __forceinline__ f32x2 unpack2<DT_BF16>(uint32_t w) {
+  return f32x2{__uint_as_float(w << 16), __uint_as_float(w & 0xffff0000u)};
+}
+template <> __device__ __forceinline__ f32x2 unpack2<DT_F16>(uint32_t w) {
+  return __builtin_convertvector(__builtin_bit_cast(f16x2, w), f32x2);
+}
+
 template <int DT> __device__ __forceinline__ float ld16(u16 v);
 template <> __device__ __forceinline__ float ld16<DT_BF16>(u16 v) { return bf16_to_f32(v); }
 template <> __device__ __forceinline__ float ld16<DT_F16>(u16 v) { return f16_to_f32(v); }

@@ -30,6 +30,8 @@ constexpr int NT = 256;
 
 enum Pass : int { FWD = 0, DGRAD = 1, WGRAD = 2 };
 
+template <int V> struct IC { static constexpr int value = V; };
+
 struct ConvParams {
   const void* a;      // FWD: X [Nb,H,W,Cin]; DGRAD: dY [Nb,Ho,Wo,Cout]; WGRAD: dY
   const void* b;      // FWD: W [N][Kpad]; DGRAD: W [Cout][R][S][Cin]; WGRAD: X [Nb,H,W,Cin]
@@ -198,19 +200,21 @@ __global__ __launch_bounds__(NT, STAGES == 1 ? 3 : 2) void conv_gemm_kernel(Conv
   // prologue state: per-chunk validity (padding must stay 0) and the chunk's 8 channel coeffs
   const bool pro = (PASS == FWD || PASS == WGRAD) && p.pro_sc != nullptr;
   bool pv[PASS == FWD ? AR : BR];
-  float psc[8], psh[8];
-  if (PASS == WGRAD && pro) {
-    const int cc = wb_colok ? wb_c : 0;
+  f32x2 psc[4], psh[4];
+  auto pro_coeffs = [&](int c) {
 #pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      psc[e] = p.pro_sc[cc + e];
-      psh[e] = p.pro_sh[cc + e];
+    for (int k = 0; k < 4; ++k) {
+      psc[k] = *reinterpret_cast<const f32x2*>(p.pro_sc + c + 2 * k);
+      psh[k] = *reinterpret_cast<const f32x2*>(p.pro_sh + c + 2 * k);
     }
-  }
+  };
+  if (PASS == WGRAD && pro) pro_coeffs(wb_colok ? wb_c : 0);
   auto pro_apply = [&](i32x4& v) {
-    u16* h = reinterpret_cast<u16*>(&v);
 #pragma unroll
-    for (int e = 0; e < 8; ++e) h[e] = st16<DT>(fmaxf(ld16<DT>(h[e]) * psc[e] + psh[e], 0.f));
+    for (int k = 0; k < 4; ++k) {
+      const f32x2 f = unpack2<DT>((uint32_t)v[k]) * psc[k] + psh[k];
+      v[k] = (int)pack2<DT>(f32x2{fmaxf(f.x, 0.f), fmaxf(f.y, 0.f)});
+    }
   };
 
   auto load_tile = [&](int kt) {
@@ -230,13 +234,7 @@ __global__ __launch_bounds__(NT, STAGES == 1 ? 3 : 2) void conv_gemm_kernel(Conv
         ra[i] = ld16B(A + (ok ? off : 0), ok);
         pv[i] = ok;
       }
-      if (pro) {
-#pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          psc[e] = p.pro_sc[c + e];
-          psh[e] = p.pro_sh[c + e];
-        }
-      }
+      if (pro) pro_coeffs(c);
     } else if constexpr (PASS == DGRAD) {
       const int ti = k0 / p.Cout;  // tile lies in one tap (Cout % 64 == 0)
       const int c = k0 - ti * p.Cout + (tid & 7) * 8;
@@ -337,6 +335,11 @@ __global__ __launch_bounds__(NT, STAGES == 1 ? 3 : 2) void conv_gemm_kernel(Conv
     }
   };
 
+  // acc[i][j][e] = C[wr*(BM/2) + i*16 + (lane&15)][wc*(BN/2) + j*16 + 4*(lane>>4) + e].
+  // The MFMA runs with its operands swapped (per 16x16 tile D = Bfrag x Afrag^T = C^T), so every
+  // lane ends up holding 4 consecutive COLUMNS of one row: the epilogue writes the C tile with one
+  // 8-byte packed LDS store per MFMA tile (and the f32 paths with 16-byte stores) instead of
+  // per-element 2-byte stores.
   constexpr int MI = BM / 32, NI = BN / 32;
   f32x4 acc[MI][NI];
 #pragma unroll
@@ -378,7 +381,7 @@ __global__ __launch_bounds__(NT, STAGES == 1 ? 3 : 2) void conv_gemm_kernel(Conv
 #pragma unroll
       for (int i = 0; i < MI; ++i)
 #pragma unroll
-        for (int j = 0; j < NI; ++j) acc[i][j] = mfma16<DT>(fa[i], fb[j], acc[i][j]);
+        for (int j = 0; j < NI; ++j) acc[i][j] = mfma16<DT>(fb[j], fa[i], acc[i][j]);
     }
     if constexpr (STAGES == 2) {
       if (kt + 1 < nk) store_tile(cur ^ 1);
@@ -387,17 +390,24 @@ __global__ __launch_bounds__(NT, STAGES == 1 ? 3 : 2) void conv_gemm_kernel(Conv
   }
 
   // ================================================================ epilogue
+  const int lr = lane & 15, lg = lane >> 4;
   if constexpr (PASS == WGRAD) {
     float* slab = reinterpret_cast<float*>(p.out) + (size_t)split * p.M * p.N;
+    const bool vec = (p.N & 3) == 0;
 #pragma unroll
     for (int i = 0; i < MI; ++i)
 #pragma unroll
       for (int j = 0; j < NI; ++j) {
-        const int col = n0 + wc * (BN / 2) + j * 16 + (lane & 15);
+        const int row = m0 + wr * (BM / 2) + i * 16 + lr;
+        const int col = n0 + wc * (BN / 2) + j * 16 + 4 * lg;
+        if (row >= p.M) continue;
+        float* d = slab + (size_t)row * p.N + col;
+        if (vec) {
+          if (col < p.N) *reinterpret_cast<f32x4*>(d) = acc[i][j];
+        } else {
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const int row = m0 + wr * (BM / 2) + i * 16 + 4 * (lane >> 4) + e;
-          if (row < p.M && col < p.N) slab[(size_t)row * p.N + col] = acc[i][j][e];
+          for (int e = 0; e < 4; ++e)
+            if (col + e < p.N) d[e] = acc[i][j][e];
         }
       }
     return;
@@ -408,65 +418,64 @@ __global__ __launch_bounds__(NT, STAGES == 1 ? 3 : 2) void conv_gemm_kernel(Conv
       for (int i = 0; i < MI; ++i)
 #pragma unroll
         for (int j = 0; j < NI; ++j) {
-          const int col = n0 + wc * (BN / 2) + j * 16 + (lane & 15);
-          const float bv = (p.bias && col < p.N) ? p.bias[col] : 0.f;
+          const int row = m0 + wr * (BM / 2) + i * 16 + lr;
+          const int col = n0 + wc * (BN / 2) + j * 16 + 4 * lg;
+          if (row >= p.M) continue;
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
-            const int row = m0 + wr * (BM / 2) + i * 16 + 4 * (lane >> 4) + e;
-            if (row < p.M && col < p.N) out[(size_t)row * p.out_pitch + col] = acc[i][j][e] + bv;
+            const int c = col + e;
+            if (c < p.N) out[(size_t)row * p.out_pitch + c] = acc[i][j][e] + (p.bias ? p.bias[c] : 0.f);
           }
         }
       return;
     }
-    // stage the 16-bit C tile through LDS: [BM][BN], row pitch BN*2 bytes, 16-B chunks swizzled
-    u16* ct = reinterpret_cast<u16*>(smem);
+    if (p.relu) {
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int j = 0; j < NI; ++j)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) acc[i][j][e] = fmaxf(acc[i][j][e], 0.f);
+    }
+    // stage the 16-bit C tile through LDS: [BM][BN], row pitch BN*2 bytes, 16-B chunks swizzled by
+    // row; one packed 8-byte store (4 columns) per MFMA tile per lane.
     constexpr int CPR = BN / 8;
     auto c_addr = [&](int row, int chunk) { return row * CPR + (chunk ^ (row & (CPR - 1))); };
-#pragma unroll
-    for (int i = 0; i < MI; ++i)
+    {
+      const int sw = lr & (CPR - 1);   // == row & (CPR-1) for every row this lane holds
 #pragma unroll
       for (int j = 0; j < NI; ++j) {
-        const int col = wc * (BN / 2) + j * 16 + (lane & 15);
+        const int col = wc * (BN / 2) + j * 16 + 4 * lg;
+        const int cbyte = (((col >> 3) ^ sw) << 4) + ((col & 4) << 1);
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const int row = wr * (BM / 2) + i * 16 + 4 * (lane >> 4) + e;
-          float v = acc[i][j][e];
-          if (p.relu) v = fmaxf(v, 0.f);
-          ct[c_addr(row, col >> 3) * 8 + (col & 7)] = st16<DT>(v);
+        for (int i = 0; i < MI; ++i) {
+          const int row = wr * (BM / 2) + i * 16 + lr;
+          uint2 pk;
+          pk.x = pack2<DT>(f32x2{acc[i][j][0], acc[i][j][1]});
+          pk.y = pack2<DT>(f32x2{acc[i][j][2], acc[i][j][3]});
+          *reinterpret_cast<uint2*>(smem + row * (BN * 2) + cbyte) = pk;
         }
       }
+    }
+    const u16* ct = reinterpret_cast<const u16*>(smem);
     // coalesced 16-B stores + per-channel partial statistics.
     //  FWD  (stats): q0 = sum y, q1 = sum y^2 of the written tile (BatchNorm forward statistics).
     //  DGRAD (emode >= 0): the tile is dA, the gradient of a = relu(bn(y) [+ res | + bn2(y2)]);
     //        the epilogue adds g2 (second gradient source), applies the ReLU mask recomputed from
     //        y (and the residual), stores dz instead of dA and emits q0 = sum dz, q1 = sum dz*y,
     //        q2 = sum dz*y2 -- the BatchNorm-backward reduction, with no extra pass over dA.
-    // The operands of the fused epilogue are prefetched for all of this thread's rows BEFORE the
-    // barrier that publishes the C tile, so their latency overlaps the staging.
+    // The BN mode and the g2 source are compile-time in the row loop (one uniform dispatch below),
+    // and all per-element math runs on packed pairs (v_pk_fma_f32 / v_cvt_pk_*).
     const int cc = tid % CPR;          // column chunk
     const int rg = tid / CPR;          // row group
     constexpr int RG = NT / CPR;       // row groups
     constexpr int RPT = BM / RG;       // rows per thread
-    const bool do_stats = (PASS == FWD && p.stats != nullptr);
-    const bool do_bn = (PASS == DGRAD && p.emode >= 0);
-    const int nq = do_bn ? p.enq : 2;
-    u16* out = reinterpret_cast<u16*>(p.out);
-    const int gcol = n0 + cc * 8;
     // rows are processed in groups of PD; the fused-epilogue operands of a group are loaded
     // before it is consumed (the first group's before the barrier that publishes the C tile),
     // which bounds the prefetch registers to PD rows.
     constexpr int PD = RPT > 4 ? 4 : RPT;
-    float esc[8], esh[8], esc2[8], esh2[8];
-    if (do_bn) {
-      const int cg = gcol < p.N ? gcol : 0;
-#pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        esc[e] = p.esc[cg + e];
-        esh[e] = p.esh[cg + e];
-        esc2[e] = p.emode == 2 ? p.esc2[cg + e] : 0.f;
-        esh2[e] = p.emode == 2 ? p.esh2[cg + e] : 0.f;
-      }
-    }
+    u16* out = reinterpret_cast<u16*>(p.out);
+    const int gcol = n0 + cc * 8;
     auto row_off = [&](int i, bool& ok) -> uint32_t {
       const int grow = m0 + rg + RG * i;
       ok = grow < p.M && gcol < p.N;
@@ -479,98 +488,118 @@ __global__ __launch_bounds__(NT, STAGES == 1 ? 3 : 2) void conv_gemm_kernel(Conv
       }
       return orow * (uint32_t)p.out_pitch + gcol;
     };
-    uint32_t eoff[PD];
-    bool eok[PD];
-    i32x4 py[PD], pg2[PD], py2[PD];
-    auto prefetch = [&](int g0) {
-      const i32x4 z = {0, 0, 0, 0};
+
+    auto rows = [&](auto mode_c, auto g2_c) {
+      constexpr int MODE = decltype(mode_c)::value;   // -1 plain / FWD stats; 0,1,2 BN-backward
+      constexpr bool G2 = decltype(g2_c)::value != 0;
+      constexpr int NQ = MODE == 2 ? 3 : 2;
+      const bool do_stats = MODE >= 0 || (PASS == FWD && p.stats != nullptr);
+      f32x2 esc[4], esh[4], esc2[4], esh2[4];
+      if constexpr (MODE >= 0) {
+        const int cg = gcol < p.N ? gcol : 0;
 #pragma unroll
-      for (int j = 0; j < PD; ++j) {
-        eoff[j] = row_off(g0 + j, eok[j]);
-        if (do_bn) {
-          py[j] = eok[j] ? *reinterpret_cast<const i32x4*>(p.ey + eoff[j]) : z;
-          pg2[j] = (eok[j] && p.eg2) ? *reinterpret_cast<const i32x4*>(p.eg2 + eoff[j]) : z;
-          py2[j] = (eok[j] && p.emode >= 1) ? *reinterpret_cast<const i32x4*>(p.ey2 + eoff[j]) : z;
+        for (int k = 0; k < 4; ++k) {
+          esc[k] = f32x2{p.esc[cg + 2 * k], p.esc[cg + 2 * k + 1]};
+          esh[k] = f32x2{p.esh[cg + 2 * k], p.esh[cg + 2 * k + 1]};
+          if constexpr (MODE == 2) {
+            esc2[k] = f32x2{p.esc2[cg + 2 * k], p.esc2[cg + 2 * k + 1]};
+            esh2[k] = f32x2{p.esh2[cg + 2 * k], p.esh2[cg + 2 * k + 1]};
+          }
+        }
+      }
+      uint32_t eoff[PD];
+      bool eok[PD];
+      i32x4 py[PD], pg2[PD], py2[PD];
+      auto prefetch = [&](int g0) {
+        const i32x4 z = {0, 0, 0, 0};
+#pragma unroll
+        for (int j = 0; j < PD; ++j) {
+          eoff[j] = row_off(g0 + j, eok[j]);
+          if constexpr (MODE >= 0) py[j] = eok[j] ? *reinterpret_cast<const i32x4*>(p.ey + eoff[j]) : z;
+          if constexpr (G2) pg2[j] = eok[j] ? *reinterpret_cast<const i32x4*>(p.eg2 + eoff[j]) : z;
+          if constexpr (MODE >= 1) py2[j] = eok[j] ? *reinterpret_cast<const i32x4*>(p.ey2 + eoff[j]) : z;
+        }
+      };
+      f32x2 q0[4], q1[4], q2[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) { q0[k] = f32x2{0.f, 0.f}; q1[k] = q0[k]; q2[k] = q0[k]; }
+      prefetch(0);
+      __syncthreads();
+#pragma unroll
+      for (int g0 = 0; g0 < RPT; g0 += PD) {
+        if (g0 > 0) prefetch(g0);
+#pragma unroll
+        for (int j = 0; j < PD; ++j) {
+          const int row = rg + RG * (g0 + j);
+          i32x4 v = *reinterpret_cast<const i32x4*>(ct + c_addr(row, cc) * 8);
+          if (!eok[j]) continue;
+          if constexpr (MODE >= 0) {
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+              f32x2 g = unpack2<DT>((uint32_t)v[k]);
+              if constexpr (G2) g += unpack2<DT>((uint32_t)pg2[j][k]);
+              const f32x2 yv = unpack2<DT>((uint32_t)py[j][k]);
+              f32x2 pre = yv * esc[k] + esh[k];
+              f32x2 y2v = f32x2{0.f, 0.f};
+              if constexpr (MODE >= 1) y2v = unpack2<DT>((uint32_t)py2[j][k]);
+              if constexpr (MODE == 1) pre += y2v;
+              if constexpr (MODE == 2) pre += y2v * esc2[k] + esh2[k];
+              f32x2 dz = f32x2{pre.x > 0.f ? g.x : 0.f, pre.y > 0.f ? g.y : 0.f};
+              const uint32_t o = pack2<DT>(dz);
+              if constexpr (G2) dz = unpack2<DT>(o);   // statistics of the stored (rounded) dz
+              v[k] = (int)o;
+              q0[k] += dz;
+              q1[k] += dz * yv;
+              if constexpr (MODE == 2) q2[k] += dz * y2v;
+            }
+          } else if (do_stats) {
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+              const f32x2 f = unpack2<DT>((uint32_t)v[k]);
+              q0[k] += f;
+              q1[k] += f * f;
+            }
+          }
+          *reinterpret_cast<i32x4*>(out + eoff[j]) = v;
+        }
+      }
+      if (do_stats) {
+        __syncthreads();
+        float* red = reinterpret_cast<float*>(smem);  // [NQ][RG][BN]
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          *reinterpret_cast<f32x2*>(red + rg * BN + cc * 8 + 2 * k) = q0[k];
+          *reinterpret_cast<f32x2*>(red + RG * BN + rg * BN + cc * 8 + 2 * k) = q1[k];
+          if constexpr (NQ > 2) *reinterpret_cast<f32x2*>(red + 2 * RG * BN + rg * BN + cc * 8 + 2 * k) = q2[k];
+        }
+        __syncthreads();
+        if (tid < BN) {
+          float a = 0.f, b = 0.f, c2 = 0.f;
+#pragma unroll 8
+          for (int g = 0; g < RG; ++g) {
+            a += red[g * BN + tid];
+            b += red[RG * BN + g * BN + tid];
+            if constexpr (NQ > 2) c2 += red[2 * RG * BN + g * BN + tid];
+          }
+          const int col = n0 + tid;
+          if (col < p.N) {
+            float* dst = MODE >= 0 ? p.epart : p.stats;
+            const size_t slab = MODE >= 0 ? (size_t)split * tiles_m + tm : (size_t)tm;
+            dst[(slab * NQ + 0) * p.N + col] = a;
+            dst[(slab * NQ + 1) * p.N + col] = b;
+            if constexpr (NQ > 2) dst[(slab * NQ + 2) * p.N + col] = c2;
+          }
         }
       }
     };
-    float q0[8], q1[8], q2[8];
-#pragma unroll
-    for (int e = 0; e < 8; ++e) { q0[e] = 0.f; q1[e] = 0.f; q2[e] = 0.f; }
-    prefetch(0);
-    __syncthreads();
-#pragma unroll
-    for (int g0 = 0; g0 < RPT; g0 += PD) {
-      if (g0 > 0) prefetch(g0);
-#pragma unroll
-      for (int j = 0; j < PD; ++j) {
-        const int row = rg + RG * (g0 + j);
-        i32x4 v = *reinterpret_cast<const i32x4*>(ct + c_addr(row, cc) * 8);
-        if (!eok[j]) continue;
-        if (do_bn) {
-          float g[8], yv[8], y2v[8], pre[8];
-          const u16* h = reinterpret_cast<const u16*>(&v);
-          const u16* h2 = reinterpret_cast<const u16*>(&pg2[j]);
-          const u16* hy = reinterpret_cast<const u16*>(&py[j]);
-          const u16* hy2 = reinterpret_cast<const u16*>(&py2[j]);
-#pragma unroll
-          for (int e = 0; e < 8; ++e) {
-            g[e] = ld16<DT>(h[e]) + ld16<DT>(h2[e]);
-            yv[e] = ld16<DT>(hy[e]);
-            y2v[e] = ld16<DT>(hy2[e]);
-            pre[e] = yv[e] * esc[e] + esh[e] +
-                     (p.emode == 2 ? y2v[e] * esc2[e] + esh2[e] : (p.emode == 1 ? y2v[e] : 0.f));
-          }
-          u16 dzh[8];
-#pragma unroll
-          for (int e = 0; e < 8; ++e) {
-            const float dz = pre[e] > 0.f ? g[e] : 0.f;
-            dzh[e] = st16<DT>(dz);
-            const float dzr = ld16<DT>(dzh[e]);   // statistics of the stored (rounded) dz
-            q0[e] += dzr;
-            q1[e] += dzr * yv[e];
-            q2[e] += dzr * y2v[e];
-          }
-          v = *reinterpret_cast<const i32x4*>(dzh);
-        } else if (do_stats) {
-          const u16* h = reinterpret_cast<const u16*>(&v);
-#pragma unroll
-          for (int e = 0; e < 8; ++e) {
-            const float f = ld16<DT>(h[e]);
-            q0[e] += f;
-            q1[e] += f * f;
-          }
-        }
-        *reinterpret_cast<i32x4*>(out + eoff[j]) = v;
-      }
-    }
-    if (do_stats || do_bn) {
-      __syncthreads();
-      float* red = reinterpret_cast<float*>(smem);  // [nq][RG][BN]
-#pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        red[rg * BN + cc * 8 + e] = q0[e];
-        red[RG * BN + rg * BN + cc * 8 + e] = q1[e];
-        if (nq > 2) red[2 * RG * BN + rg * BN + cc * 8 + e] = q2[e];
-      }
-      __syncthreads();
-      if (tid < BN) {
-        float a = 0.f, b = 0.f, c2 = 0.f;
-#pragma unroll 8
-        for (int g = 0; g < RG; ++g) {
-          a += red[g * BN + tid];
-          b += red[RG * BN + g * BN + tid];
-          if (nq > 2) c2 += red[2 * RG * BN + g * BN + tid];
-        }
-        const int col = n0 + tid;
-        if (col < p.N) {
-          float* dst = do_bn ? p.epart : p.stats;
-          const size_t slab = do_bn ? (size_t)split * tiles_m + tm : (size_t)tm;
-          dst[(slab * nq + 0) * p.N + col] = a;
-          dst[(slab * nq + 1) * p.N + col] = b;
-          if (nq > 2) dst[(slab * nq + 2) * p.N + col] = c2;
-        }
-      }
+    if constexpr (PASS == DGRAD) {
+      const bool g2 = p.eg2 != nullptr;
+      if (p.emode < 0) rows(IC<-1>{}, IC<0>{});
+      else if (p.emode == 0) { if (g2) rows(IC<0>{}, IC<1>{}); else rows(IC<0>{}, IC<0>{}); }
+      else if (p.emode == 1) { if (g2) rows(IC<1>{}, IC<1>{}); else rows(IC<1>{}, IC<0>{}); }
+      else { if (g2) rows(IC<2>{}, IC<1>{}); else rows(IC<2>{}, IC<0>{}); }
+    } else {
+      rows(IC<-1>{}, IC<0>{});
     }
   }
 }
