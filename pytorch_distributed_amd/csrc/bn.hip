@@ -101,35 +101,54 @@ __global__ void bn_eval_coeffs_kernel(const float* __restrict__ gamma, const flo
 // ------------------------------------------------------------------ apply
 // mode: 0 = act(bn(y)); 1 = act(bn(y) + res); 2 = act(bn(y) + bn2(y2))
 template <int DT>
+__device__ __forceinline__ void ld8p(const float* p, f32x2* f) {
+  const f32x4 a = *reinterpret_cast<const f32x4*>(p);
+  const f32x4 b = *reinterpret_cast<const f32x4*>(p + 4);
+  f[0] = f32x2{a[0], a[1]}; f[1] = f32x2{a[2], a[3]};
+  f[2] = f32x2{b[0], b[1]}; f[3] = f32x2{b[2], b[3]};
+}
+
+// Streaming form: 32-bit indices; when the grid stride is a multiple of C/8 (always for
+// power-of-two C <= 2048 with 256-thread blocks) each thread's channel chunk is loop-invariant,
+// so the per-channel coefficients are loaded once, and the math runs on packed pairs.
+template <int DT>
 __global__ __launch_bounds__(NT) void bn_apply_kernel(
     const u16* __restrict__ y, const float* __restrict__ sc, const float* __restrict__ sh,
     const u16* __restrict__ r2, const float* __restrict__ sc2, const float* __restrict__ sh2,
-    u16* __restrict__ out, long long n8, int C, int mode, int relu) {
-  for (long long i = blockIdx.x * (long long)NT + threadIdx.x; i < n8; i += (long long)gridDim.x * NT) {
-    const int c0 = (int)((i * 8) % C);
-    float v[8], a[8], b[8];
-    unpack8<DT>(reinterpret_cast<const i32x4*>(y)[i], v);
-    ld8f(sc + c0, a);
-    ld8f(sh + c0, b);
-#pragma unroll
-    for (int e = 0; e < 8; ++e) v[e] = v[e] * a[e] + b[e];
-    if (mode) {
-      float w[8];
-      unpack8<DT>(reinterpret_cast<const i32x4*>(r2)[i], w);
+    u16* __restrict__ out, int n8, int C, int mode, int relu) {
+  const int C8 = C >> 3;
+  const int stride = gridDim.x * NT;
+  const bool fixed = (stride % C8) == 0;
+  int i = blockIdx.x * NT + threadIdx.x;
+  f32x2 a[4], b[4], a2[4], b2[4];
+  int cprev = -1;
+  for (; i < n8; i += stride) {
+    const int c0 = (i % C8) * 8;
+    if (!fixed || cprev < 0) {
+      ld8p<DT>(sc + c0, a);
+      ld8p<DT>(sh + c0, b);
       if (mode == 2) {
-        ld8f(sc2 + c0, a);
-        ld8f(sh2 + c0, b);
-#pragma unroll
-        for (int e = 0; e < 8; ++e) w[e] = w[e] * a[e] + b[e];
+        ld8p<DT>(sc2 + c0, a2);
+        ld8p<DT>(sh2 + c0, b2);
       }
-#pragma unroll
-      for (int e = 0; e < 8; ++e) v[e] += w[e];
+      cprev = c0;
     }
-    if (relu) {
+    const i32x4 yv = reinterpret_cast<const i32x4*>(y)[i];
+    i32x4 rv = {0, 0, 0, 0};
+    if (mode) rv = reinterpret_cast<const i32x4*>(r2)[i];
+    i32x4 o;
 #pragma unroll
-      for (int e = 0; e < 8; ++e) v[e] = fmaxf(v[e], 0.f);
+    for (int k = 0; k < 4; ++k) {
+      f32x2 v = unpack2<DT>((uint32_t)yv[k]) * a[k] + b[k];
+      if (mode) {
+        f32x2 w = unpack2<DT>((uint32_t)rv[k]);
+        if (mode == 2) w = w * a2[k] + b2[k];
+        v += w;
+      }
+      if (relu) v = f32x2{fmaxf(v.x, 0.f), fmaxf(v.y, 0.f)};
+      o[k] = (int)pack2<DT>(v);
     }
-    reinterpret_cast<i32x4*>(out)[i] = pack8<DT>(v);
+    reinterpret_cast<i32x4*>(out)[i] = o;
   }
 }
 
@@ -141,16 +160,14 @@ __global__ __launch_bounds__(NT) void stem_pool_kernel(const u16* __restrict__ y
                                                        const float* __restrict__ sh,
                                                        u16* __restrict__ out,
                                                        uint8_t* __restrict__ arg, int N, int H,
-                                                       int W, int C, int Ho, int Wo) {
+                                                       int W, int C, int Ho, int Wo, FastDiv dCK,
+                                                       FastDiv dWo, FastDiv dHo) {
   const int CK = C / 8;
-  const long long total = (long long)N * Ho * Wo * CK;
-  for (long long i = blockIdx.x * (long long)NT + threadIdx.x; i < total; i += (long long)gridDim.x * NT) {
-    const int ck = (int)(i % CK);
-    long long pix = i / CK;
-    const int xo = (int)(pix % Wo);
-    pix /= Wo;
-    const int yo = (int)(pix % Ho);
-    const int n = (int)(pix / Ho);
+  const int total = N * Ho * Wo * CK;
+  for (int i = blockIdx.x * NT + threadIdx.x; i < total; i += gridDim.x * NT) {
+    const uint32_t pix = fdiv(i, dCK), ck = i - pix * CK;
+    const uint32_t p2 = fdiv(pix, dWo), xo = pix - p2 * Wo;
+    const uint32_t n = fdiv(p2, dHo), yo = p2 - n * Ho;
     float a[8], b[8], best[8];
     int bi[8];
     ld8f(sc + ck * 8, a);
@@ -164,7 +181,7 @@ __global__ __launch_bounds__(NT) void stem_pool_kernel(const u16* __restrict__ y
         const int xx = xo * 2 - 1 + dx;
         if ((unsigned)xx >= (unsigned)W) continue;
         float v[8];
-        unpack8<DT>(*reinterpret_cast<const i32x4*>(y + (((size_t)n * H + yy) * W + xx) * C + ck * 8), v);
+        unpack8<DT>(*reinterpret_cast<const i32x4*>(y + ((n * H + yy) * W + xx) * C + ck * 8), v);
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
           const float r = fmaxf(v[e] * a[e] + b[e], 0.f);
@@ -186,27 +203,25 @@ __global__ __launch_bounds__(NT) void maxpool_bwd_kernel(const u16* __restrict__
                                                          const u16* __restrict__ dout2,
                                                          const uint8_t* __restrict__ arg,
                                                          u16* __restrict__ din, int N, int H, int W,
-                                                         int C, int Ho, int Wo) {
+                                                         int C, int Ho, int Wo, FastDiv dCK,
+                                                         FastDiv dW, FastDiv dH) {
   const int CK = C / 8;
-  const long long total = (long long)N * H * W * CK;
-  for (long long i = blockIdx.x * (long long)NT + threadIdx.x; i < total; i += (long long)gridDim.x * NT) {
-    const int ck = (int)(i % CK);
-    long long pix = i / CK;
-    const int x = (int)(pix % W);
-    pix /= W;
-    const int yy = (int)(pix % H);
-    const int n = (int)(pix / H);
+  const int total = N * H * W * CK;
+  for (int i = blockIdx.x * NT + threadIdx.x; i < total; i += gridDim.x * NT) {
+    const uint32_t pix = fdiv(i, dCK), ck = i - pix * CK;
+    const uint32_t p2 = fdiv(pix, dW), x = pix - p2 * W;
+    const uint32_t n = fdiv(p2, dH), yy = p2 - n * H;
     float g[8];
 #pragma unroll
     for (int e = 0; e < 8; ++e) g[e] = 0.f;
     // outputs whose window covers (yy, x): yo*2-1 <= yy <= yo*2+1
-    for (int yo = yy / 2; yo <= min(Ho - 1, (yy + 1) / 2); ++yo) {
-      const int dy = yy - (yo * 2 - 1);
+    for (int yo = (int)yy / 2; yo <= min(Ho - 1, ((int)yy + 1) / 2); ++yo) {
+      const int dy = (int)yy - (yo * 2 - 1);
       if (dy < 0 || dy > 2) continue;
-      for (int xo = x / 2; xo <= min(Wo - 1, (x + 1) / 2); ++xo) {
-        const int dx = x - (xo * 2 - 1);
+      for (int xo = (int)x / 2; xo <= min(Wo - 1, ((int)x + 1) / 2); ++xo) {
+        const int dx = (int)x - (xo * 2 - 1);
         if (dx < 0 || dx > 2) continue;
-        const size_t o = ((size_t)n * Ho + yo) * Wo + xo;
+        const uint32_t o = (n * Ho + yo) * Wo + xo;
         const uint64_t a = reinterpret_cast<const uint64_t*>(arg)[o * CK + ck];
         float d[8];
         unpack8<DT>(*reinterpret_cast<const i32x4*>(dout + o * C + ck * 8), d);
@@ -453,6 +468,38 @@ __global__ __launch_bounds__(NT) void bn_bwd_apply_kernel(BwdArgs a, const u16* 
   }
 }
 
+// dz read back (the common case: the consumer conv's dgrad epilogue stored it): pure stream,
+// loop-invariant channel chunk (see bn_apply_kernel), packed math.
+template <int DT>
+__global__ __launch_bounds__(NT) void bn_bwd_apply_dz_kernel(const u16* __restrict__ dz_in,
+                                                             const u16* __restrict__ ysel,
+                                                             const float* __restrict__ k1,
+                                                             const float* __restrict__ k2,
+                                                             const float* __restrict__ k3,
+                                                             u16* __restrict__ dy, int n8, int C) {
+  const int C8 = C >> 3;
+  const int stride = gridDim.x * NT;
+  const bool fixed = (stride % C8) == 0;
+  f32x2 A[4], B[4], K3[4];
+  int cprev = -1;
+  for (int i = blockIdx.x * NT + threadIdx.x; i < n8; i += stride) {
+    const int c0 = (i % C8) * 8;
+    if (!fixed || cprev < 0) {
+      ld8p<DT>(k1 + c0, A);
+      ld8p<DT>(k2 + c0, B);
+      ld8p<DT>(k3 + c0, K3);
+      cprev = c0;
+    }
+    const i32x4 dz = reinterpret_cast<const i32x4*>(dz_in)[i];
+    const i32x4 yv = reinterpret_cast<const i32x4*>(ysel)[i];
+    i32x4 o;
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      o[k] = (int)pack2<DT>(A[k] * unpack2<DT>((uint32_t)dz[k]) + B[k] * unpack2<DT>((uint32_t)yv[k]) + K3[k]);
+    reinterpret_cast<i32x4*>(dy)[i] = o;
+  }
+}
+
 // first stage of the statistics reduction: [G][QC] partial slabs -> [S][QC] (S << G), coalesced
 __global__ __launch_bounds__(256) void slab_reduce_kernel(const float* __restrict__ in, int G, int QC,
                                                           int rows_per, float* __restrict__ out) {
@@ -506,10 +553,21 @@ int pda_bn_eval_coeffs(const float* gamma, const float* beta, const float* rm, c
   return (int)hipGetLastError();
 }
 
+static FastDiv make_div(uint32_t d) {
+  FastDiv f;
+  f.d = d;
+  uint32_t s = 0;
+  while ((1ull << s) < d) ++s;
+  f.s = s;
+  f.m = (uint32_t)(((1ull << 32) * ((1ull << s) - d)) / d + 1);
+  return f;
+}
+
 int pda_bn_apply(const void* y, const float* sc, const float* sh, const void* r2, const float* sc2,
                  const float* sh2, void* out, long long numel, int C, int mode, int relu, int dt,
                  hipStream_t st) {
-  const long long n8 = numel / 8;
+  if (numel / 8 >= (1ll << 31)) return -2;
+  const int n8 = (int)(numel / 8);
   const int g = grid_for(n8);
 #define ARGS (const u16*)y, sc, sh, (const u16*)r2, sc2, sh2, (u16*)out, n8, C, mode, relu
   if (dt == DT_BF16) hipLaunchKernelGGL(bn_apply_kernel<DT_BF16>, dim3(g), dim3(NT), 0, st, ARGS);
@@ -520,8 +578,10 @@ int pda_bn_apply(const void* y, const float* sc, const float* sh, const void* r2
 
 int pda_stem_pool(const void* y, const float* sc, const float* sh, void* out, void* arg, int N,
                   int H, int W, int C, int Ho, int Wo, int dt, hipStream_t st) {
+  if ((long long)N * H * W * (C / 8) >= (1ll << 31)) return -2;
   const int g = grid_for((long long)N * Ho * Wo * (C / 8));
-#define ARGS (const u16*)y, sc, sh, (u16*)out, (uint8_t*)arg, N, H, W, C, Ho, Wo
+#define ARGS (const u16*)y, sc, sh, (u16*)out, (uint8_t*)arg, N, H, W, C, Ho, Wo, make_div(C / 8), \
+             make_div(Wo), make_div(Ho)
   if (dt == DT_BF16) hipLaunchKernelGGL(stem_pool_kernel<DT_BF16>, dim3(g), dim3(NT), 0, st, ARGS);
   else hipLaunchKernelGGL(stem_pool_kernel<DT_F16>, dim3(g), dim3(NT), 0, st, ARGS);
 #undef ARGS
@@ -530,8 +590,10 @@ int pda_stem_pool(const void* y, const float* sc, const float* sh, void* out, vo
 
 int pda_maxpool_bwd(const void* dout, const void* dout2, const void* arg, void* din, int N, int H,
                     int W, int C, int Ho, int Wo, int dt, hipStream_t st) {
+  if ((long long)N * H * W * (C / 8) >= (1ll << 31)) return -2;
   const int g = grid_for((long long)N * H * W * (C / 8));
-#define ARGS (const u16*)dout, (const u16*)dout2, (const uint8_t*)arg, (u16*)din, N, H, W, C, Ho, Wo
+#define ARGS (const u16*)dout, (const u16*)dout2, (const uint8_t*)arg, (u16*)din, N, H, W, C, Ho, Wo, \
+             make_div(C / 8), make_div(W), make_div(H)
   if (dt == DT_BF16) hipLaunchKernelGGL(maxpool_bwd_kernel<DT_BF16>, dim3(g), dim3(NT), 0, st, ARGS);
   else hipLaunchKernelGGL(maxpool_bwd_kernel<DT_F16>, dim3(g), dim3(NT), 0, st, ARGS);
 #undef ARGS
@@ -589,6 +651,14 @@ int pda_bn_bwd_apply(const BwdArgsC* c, const void* dz_in, const void* ysel, con
                      const float* k2, const float* k3, void* dy, int dt, hipStream_t st) {
   BwdArgs a = to_args(c);
   const int g = grid_for(a.rows * (a.C / 8));
+  if (dz_in && a.rows * (a.C / 8) < (1ll << 31)) {
+    const int n8 = (int)(a.rows * (a.C / 8));
+#define K(D) hipLaunchKernelGGL(bn_bwd_apply_dz_kernel<D>, dim3(g), dim3(NT), 0, st, (const u16*)dz_in, \
+                                (const u16*)ysel, k1, k2, k3, (u16*)dy, n8, a.C)
+    if (dt == DT_BF16) K(DT_BF16); else K(DT_F16);
+#undef K
+    return (int)hipGetLastError();
+  }
 #define K(D) hipLaunchKernelGGL(bn_bwd_apply_kernel<D>, dim3(g), dim3(NT), 0, st, a, (const u16*)dz_in, \
                                 (const u16*)ysel, k1, k2, k3, (u16*)dy)
   if (dt == DT_BF16) K(DT_BF16); else K(DT_F16);

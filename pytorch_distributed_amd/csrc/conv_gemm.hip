@@ -623,6 +623,44 @@ __global__ void wgrad_reduce_kernel(const float* __restrict__ slab, float* __res
   }
 }
 
+// Parallel split-K reduction (N % 4 == 0): a block owns EPB consecutive elements and all splits;
+// its 256 threads are SG = 256/(EPB/4) split groups x EPB/4 float4 columns, each group summing
+// splits sg, sg+SG, ... then a fixed-order LDS combine -> deterministic. Small weight tiles with
+// hundreds of splits (e.g. 64x64 1x1 convs) no longer serialise on one thread per element.
+template <int EPB>
+__global__ __launch_bounds__(256) void wgrad_reduce4_kernel(const float* __restrict__ slab,
+                                                            float* __restrict__ grad, int splits,
+                                                            int M, int N, int cin_pad_log2,
+                                                            int cin_real, int dst_pitch, float scale,
+                                                            int accumulate) {
+  constexpr int TPE = EPB / 4, SG = 256 / TPE;
+  __shared__ f32x4 red[256];
+  const int total = M * N;
+  const int t = threadIdx.x, sg = t / TPE, e4 = t - sg * TPE;
+  const int base = blockIdx.x * EPB + e4 * 4;
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  if (base < total) {
+    const float* src = slab + base;
+#pragma unroll 4
+    for (int k = sg; k < splits; k += SG) acc += *reinterpret_cast<const f32x4*>(src + (size_t)k * total);
+  }
+  red[t] = acc;
+  __syncthreads();
+  if (sg != 0 || base >= total) return;
+  f32x4 s = red[e4];
+  for (int g = 1; g < SG; ++g) s += red[g * TPE + e4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int idx = base + q;
+    const int n1 = idx / N, n2 = idx - n1 * N;
+    const int tap = n2 >> cin_pad_log2, c = n2 & ((1 << cin_pad_log2) - 1);
+    if (c < cin_real) {
+      float* d = grad + (size_t)n1 * dst_pitch + tap * cin_real + c;
+      *d = accumulate ? *d + scale * s[q] : scale * s[q];
+    }
+  }
+}
+
 }  // namespace
 
 // ================================================================= host launchers (C ABI)
@@ -761,6 +799,19 @@ int pda_conv_wgrad(const ConvDesc* d, const void* dy, const void* x, float* slab
 int pda_wgrad_reduce(const float* slab, float* grad, int splits, int M, int N, int cin_pad_log2,
                      int cin_real, int dst_pitch, float scale, int accumulate, hipStream_t st) {
   const int total = M * N;
+  if ((N & 3) == 0) {
+    int epb = 256;
+    while (epb > 16 && total / epb < 1024) epb >>= 1;
+    const dim3 grid((total + epb - 1) / epb);
+#define PDA_RED(E)                                                                              \
+  if (epb == E) {                                                                               \
+    hipLaunchKernelGGL(wgrad_reduce4_kernel<E>, grid, dim3(256), 0, st, slab, grad, splits, M, N, \
+                       cin_pad_log2, cin_real, dst_pitch, scale, accumulate);                   \
+    return (int)hipGetLastError();                                                              \
+  }
+    PDA_RED(256) PDA_RED(128) PDA_RED(64) PDA_RED(32) PDA_RED(16)
+#undef PDA_RED
+  }
   int blocks = (total + 255) / 256;
   if (blocks > 4096) blocks = 4096;
   hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(blocks), dim3(256), 0, st, slab, grad, splits, M, N,

@@ -77,6 +77,7 @@ class Workspace:
 
 
 _NUM_CU = 256
+_WGRAD_TARGET = int(os.environ.get("PDA_WGRAD_TARGET", 2 * _NUM_CU))
 
 
 _SINGLE_STAGE = os.environ.get("PDA_SINGLE_STAGE", "1") != "0"
@@ -171,13 +172,36 @@ def bn_epilogue(ws: "Workspace", G: int, y, scale, shift, res=None, y2=None, sca
     return epi, part, nq
 
 
+# Weight-gradient tile / split-K block target per ResNet conv geometry (Cout, R, Cin, stride, Ho),
+# measured with tools/wgrad_sweep.py on MI355X at batch 400 (profiles/wgrad_sweep_r1.txt).
+_WGRAD_TUNED = {
+    (64, 1, 64, 1, 56): ((64, 64), 1024),
+    (64, 3, 64, 1, 56): ((64, 128), 2048),
+    (256, 1, 64, 1, 56): ((-128, 128), 512),
+    (64, 1, 256, 1, 56): ((-128, 128), 512),
+    (128, 1, 256, 1, 56): ((128, 128), 512),
+    (128, 3, 128, 2, 28): ((128, 128), 2048),
+    (128, 3, 128, 1, 28): ((64, 128), 2048),
+    (256, 3, 256, 2, 14): ((128, 128), 2048),
+    (256, 3, 256, 1, 14): ((-128, 128), 2048),
+    (512, 3, 512, 2, 7): ((-128, 128), 4096),
+    (512, 3, 512, 1, 7): ((-128, 128), 1024),
+}
+
+
 def wgrad_plan(g: ConvGeom, Nb: int, tile: Optional[Tuple[int, int]] = None,
-               target_blocks: int = 2 * _NUM_CU, max_slab_bytes: int = 64 << 20):
+               target_blocks: Optional[int] = None, max_slab_bytes: int = 64 << 20):
     M, N, K = g.Cout, g.R * g.S * g.Cin, Nb * g.Ho * g.Wo
+    tuned = _WGRAD_TUNED.get((g.Cout, g.R, g.Cin, g.stride, g.Ho)) if _SINGLE_STAGE else None
     bn = 128 if N >= 128 else 64
     bm = 128 if M >= 128 else 64
     if _SINGLE_STAGE and (bm == 128 or bn == 128):
         bm = -bm      # single-LDS-buffer variants (tools/conv_bench.py: best or within 2%)
+    if tuned and not tile:
+        (bm, bn), tb = tuned
+        target_blocks = target_blocks or tb
+    if target_blocks is None:
+        target_blocks = _WGRAD_TARGET
     if tile:
         bm, bn = tile
     tiles = math.ceil(M / abs(bm)) * math.ceil(N / bn)
@@ -191,11 +215,12 @@ def wgrad_plan(g: ConvGeom, Nb: int, tile: Optional[Tuple[int, int]] = None,
 def conv_wgrad(dy: torch.Tensor, x: torch.Tensor, g: ConvGeom, grad: torch.Tensor, ws: Workspace,
                cin_real: Optional[int] = None, scale: float = 1.0, accumulate: bool = False,
                tile: Optional[Tuple[int, int]] = None,
-               pro: Optional[Tuple[torch.Tensor, torch.Tensor]] = None) -> torch.Tensor:
+               pro: Optional[Tuple[torch.Tensor, torch.Tensor]] = None,
+               target_blocks: Optional[int] = None) -> torch.Tensor:
     """grad (f32, OHWI with cin_real channels, rows of pitch R*S*cin_real) = scale * dW.
     pro = (scale, shift): x is PRE-BatchNorm; the activation relu(x*scale+shift) is recomputed."""
     Nb = dy.shape[0]
-    bm, bn, splits, k_chunk = wgrad_plan(g, Nb, tile)
+    bm, bn, splits, k_chunk = wgrad_plan(g, Nb, tile, target_blocks)
     M, N = g.Cout, g.R * g.S * g.Cin
     slab = ws.get("wgrad_slab", splits * M * N)
     d = g.desc(Nb)
