@@ -12,9 +12,9 @@ from __future__ import annotations
 import dataclasses
 import os
 from dataclasses import dataclass, field
-from typing import Optional
+from typing import Optional, Sequence
 
-__all__ = ["RunConfig", "SCRIPT_DEFAULTS", "config_for"]
+__all__ = ["RunConfig", "SCRIPT_DEFAULTS", "config_for", "parse_cli"]
 
 
 @dataclass(frozen=True)
@@ -84,11 +84,31 @@ _ENV = {
 }
 
 
-def config_for(script: str, env: Optional[dict] = None) -> RunConfig:
-    """Defaults of ``script`` (reference hyper-params) overlaid with ``MX_*`` env."""
+def _flag(var: str) -> str:
+    return "--" + var[3:].lower().replace("_", "-")     # MX_STEPS_PER_EPOCH -> --steps-per-epoch
+
+
+def parse_cli(argv: Sequence[str]) -> dict:
+    """Optional command-line flags mirroring the ``MX_*`` variables (additive: the reference
+    scripts take no arguments, and with none given nothing changes). Returns {env var: value}."""
+    import argparse
+    ap = argparse.ArgumentParser(add_help=True, description="MX_* overrides as flags")
+    for var in _ENV:
+        ap.add_argument(_flag(var), dest=var, default=None, metavar=var,
+                        help=f"same as {var}")
+    ns = ap.parse_args(list(argv))
+    return {k: v for k, v in vars(ns).items() if v is not None}
+
+
+def config_for(script: str, env: Optional[dict] = None,
+               argv: Optional[Sequence[str]] = None) -> RunConfig:
+    """Defaults of ``script`` (reference hyper-params) overlaid with ``MX_*`` env, then with the
+    equivalent command-line flags (``argv``, e.g. ``--epochs 1 --steps-per-epoch 50``)."""
     if script not in SCRIPT_DEFAULTS:
         raise ValueError(f"unknown script {script!r}")
-    env = os.environ if env is None else env
+    env = dict(os.environ if env is None else env)
+    if argv:
+        env.update(parse_cli(argv))
     kw = dict(SCRIPT_DEFAULTS[script])
     kw["script"] = script
     for var, (name, conv) in _ENV.items():

@@ -51,6 +51,7 @@ struct ConvParams {
   FastDiv dHoWo, dWo, dS;   // m -> (img, y, x) decode of the *GEMM row* space; tap -> (r, s)
   int ntaps[4];       // DGRAD: taps per parity class
   int taps[4][9];     // DGRAD: tap ids (r*S+s) per parity class
+  int tdy[4][9], tdx[4][9];   // DGRAD: dY offset of each class tap: (ph + pad - r) / stride, ...
   int Hc, Wc;         // DGRAD: class grid (H/stride, W/stride)
   FastDiv dHcWc, dWc;
   // fused BatchNorm-apply + ReLU prologue on the gathered activation operand (FWD: A, WGRAD: B):
@@ -105,11 +106,6 @@ __device__ __forceinline__ s16x8 frag_col(const char* lds, int cb, int s, int la
   return r;
 }
 
-__device__ __forceinline__ i32x4 ld16B(const void* p, bool ok) {
-  i32x4 z = {0, 0, 0, 0};
-  return ok ? *reinterpret_cast<const i32x4*>(p) : z;
-}
-
 // ================================================================= kernel
 // STAGES = 2: double-buffered LDS, one barrier per k-tile (deep-K layers).
 // STAGES = 1: single LDS buffer (half the LDS -> one more resident block per CU) for the many
@@ -155,33 +151,73 @@ __global__ __launch_bounds__(NT, STAGES == 1 ? 3 : 2) void conv_gemm_kernel(Conv
   const int nk = (kend - kbeg + BK - 1) / BK;
 
   // ---- per-thread loader precompute -------------------------------------------------
+  // Operands are read with buffer loads (32-bit byte offsets, hardware range check): a padding
+  // tap / ragged row / ragged column gets offset OOB and the load returns zeros -- no branch
+  // around the load, no 64-bit address math. Everything that does not change along K is hoisted
+  // here, so a k-tile costs ~1-3 VALU per 16-byte chunk (+ one tap decode per thread).
   // A (ROW: FWD gather from X, DGRAD gather from dY): rows tid/8 + 32*i, chunk tid&7
-  int a_img[AR], a_y[AR], a_x[AR];
-  bool a_ok[AR];
+  constexpr uint32_t OOB = 0x80000000u;
+  int a_base[AR];           // byte offset of the row's tap-(0,0) pixel (FWD/DGRAD), may be < 0
+  uint64_t a_mask[AR];      // bit t: tap t (FWD, R*S <= 64) / class tap t (DGRAD) is inside the image
+  uint32_t a_off[AR];       // WGRAD: byte offset of (krow, col) at k0 = kbeg
+  int a_krow[AR];
   if constexpr (A_ROW) {
 #pragma unroll
     for (int i = 0; i < AR; ++i) {
       const int m = m0 + (tid >> 3) + 32 * i;
-      a_ok[i] = m < p.M;
-      const uint32_t mm = a_ok[i] ? m : 0;
+      const bool okm = m < p.M;
+      const uint32_t mm = okm ? m : 0;
+      uint64_t msk = 0;
       if constexpr (PASS == FWD) {
         const uint32_t img = fdiv(mm, p.dHoWo), rem = mm - img * p.dHoWo.d;
         const uint32_t yo = fdiv(rem, p.dWo), xo = rem - yo * p.dWo.d;
-        a_img[i] = img;
-        a_y[i] = (int)yo * p.stride - p.pad;
-        a_x[i] = (int)xo * p.stride - p.pad;
-      } else {  // DGRAD: class-grid pixel -> dX pixel (h, w)
+        const int y0 = (int)yo * p.stride - p.pad, x0 = (int)xo * p.stride - p.pad;
+        a_base[i] = (((int)img * p.H + y0) * p.W + x0) * p.Cin * 2;
+        for (int r = 0, t = 0; r < p.R; ++r) {
+          const bool yok = (unsigned)(y0 + r) < (unsigned)p.H;
+          for (int q = 0; q < p.S; ++q, ++t)
+            if (yok && (unsigned)(x0 + q) < (unsigned)p.W) msk |= 1ull << t;
+        }
+      } else {  // DGRAD: class-grid pixel (yi, xi); tap t of the class reads dY[yi + dy_t][xi + dx_t]
         const uint32_t img = fdiv(mm, p.dHcWc), rem = mm - img * p.dHcWc.d;
         const uint32_t yi = fdiv(rem, p.dWc), xi = rem - yi * p.dWc.d;
-        a_img[i] = img;
-        a_y[i] = (int)yi * p.stride + cls_ph + p.pad;  // h + pad
-        a_x[i] = (int)xi * p.stride + cls_pw + p.pad;
+        a_base[i] = (((int)img * p.Ho + (int)yi) * p.Wo + (int)xi) * p.Cout * 2;
+        for (int t = 0; t < ntap; ++t) {
+          if ((unsigned)((int)yi + p.tdy[split][t]) < (unsigned)p.Ho &&
+              (unsigned)((int)xi + p.tdx[split][t]) < (unsigned)p.Wo)
+            msk |= 1ull << t;
+        }
       }
+      a_mask[i] = okm ? msk : 0ull;
     }
+  } else {
+    constexpr int CPR = BM / 8, RPI = NT / CPR;
+    const int col = m0 + (tid % CPR) * 8;
+#pragma unroll
+    for (int i = 0; i < AR; ++i) {
+      a_krow[i] = tid / CPR + RPI * i;
+      a_off[i] = col < p.M ? (uint32_t)((kbeg + a_krow[i]) * p.Cout + col) * 2u : OOB;
+    }
+  }
+  // B
+  uint32_t b_off[BR];
+  if constexpr (PASS == FWD) {
+#pragma unroll
+    for (int i = 0; i < BR; ++i) {
+      const int n = n0 + (tid >> 3) + 32 * i;
+      b_off[i] = n < p.N ? (uint32_t)(n * p.Kpad + (tid & 7) * 8) * 2u : OOB;
+    }
+  } else if constexpr (PASS == DGRAD) {
+    constexpr int CPR = BN / 8, RPI = NT / CPR;
+    const int col = n0 + (tid % CPR) * 8;
+#pragma unroll
+    for (int i = 0; i < BR; ++i)
+      b_off[i] = col < p.N ? (uint32_t)((tid / CPR + RPI * i) * p.R * p.S * p.Cin + col) * 2u : OOB;
   }
   // WGRAD B gather: fixed column chunk per thread -> (tap, c)
   int wb_r = 0, wb_s = 0, wb_c = 0;
   bool wb_colok = true;
+  const bool wb_direct = PASS == WGRAD && p.R == 1 && p.S == 1 && p.stride == 1 && p.pad == 0;
   if constexpr (PASS == WGRAD) {
     constexpr int CPR = BN / 8;
     const int col = n0 + (tid % CPR) * 8;
@@ -193,8 +229,25 @@ __global__ __launch_bounds__(NT, STAGES == 1 ? 3 : 2) void conv_gemm_kernel(Conv
     wb_colok = wb_colok && (tap < p.R * p.S);
   }
 
-  const u16* __restrict__ A = reinterpret_cast<const u16*>(p.a);
-  const u16* __restrict__ B = reinterpret_cast<const u16*>(p.b);
+  // buffer resources (wave-uniform: built from kernel arguments only)
+  uint32_t a_bytes, b_bytes;
+  if constexpr (PASS == FWD) {
+    a_bytes = (uint32_t)p.Nb * p.H * p.W * p.Cin * 2u;
+    b_bytes = (uint32_t)p.N * p.Kpad * 2u;
+  } else if constexpr (PASS == DGRAD) {
+    a_bytes = (uint32_t)p.Nb * p.Ho * p.Wo * p.Cout * 2u;
+    b_bytes = (uint32_t)p.Cout * p.R * p.S * p.Cin * 2u;
+  } else {
+    a_bytes = (uint32_t)p.K * p.Cout * 2u;
+    b_bytes = (uint32_t)p.Nb * p.H * p.W * p.Cin * 2u;
+  }
+  const __amdgpu_buffer_rsrc_t rsa = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p.a), (short)0,
+                                                                         (int)a_bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rsb = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p.b), (short)0,
+                                                                         (int)b_bytes, 0x00020000);
+  auto bld = [&](const __amdgpu_buffer_rsrc_t& r, uint32_t off) -> i32x4 {
+    return __builtin_bit_cast(i32x4, __builtin_amdgcn_raw_buffer_load_b128(r, (int)off, 0, 0));
+  };
 
   i32x4 ra[AR], rb[BR];
   // prologue state: per-chunk validity (padding must stay 0) and the chunk's 8 channel coeffs
@@ -209,11 +262,15 @@ __global__ __launch_bounds__(NT, STAGES == 1 ? 3 : 2) void conv_gemm_kernel(Conv
     }
   };
   if (PASS == WGRAD && pro) pro_coeffs(wb_colok ? wb_c : 0);
+  // relu on the packed 16-bit result: bf16/f16 are sign-magnitude, so a signed 16-bit max with 0
+  // zeroes exactly the negative values (and -0) -- one v_pk_max_i16 per pair
+  typedef short s16x2 __attribute__((ext_vector_type(2)));
   auto pro_apply = [&](i32x4& v) {
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
       const f32x2 f = unpack2<DT>((uint32_t)v[k]) * psc[k] + psh[k];
-      v[k] = (int)pack2<DT>(f32x2{fmaxf(f.x, 0.f), fmaxf(f.y, 0.f)});
+      const s16x2 h = __builtin_bit_cast(s16x2, pack2<DT>(f));
+      v[k] = __builtin_bit_cast(int, __builtin_elementwise_max(h, (s16x2){0, 0}));
     }
   };
 
@@ -224,64 +281,50 @@ __global__ __launch_bounds__(NT, STAGES == 1 ? 3 : 2) void conv_gemm_kernel(Conv
       const int k = k0 + (tid & 7) * 8;
       const int tap = k >> p.log2Cin;
       const int c = k & ((1 << p.log2Cin) - 1);
-      const int r = (int)fdiv(tap, p.dS), s = tap - r * p.S;
+      const int r = (int)fdiv(tap, p.dS), q = tap - r * p.S;
+      const int toff = ((r * p.W + q) * p.Cin + c) * 2;
       const bool tap_ok = tap < p.R * p.S;
 #pragma unroll
       for (int i = 0; i < AR; ++i) {
-        const int y = a_y[i] + r, x = a_x[i] + s;
-        const bool ok = a_ok[i] && tap_ok && (unsigned)y < (unsigned)p.H && (unsigned)x < (unsigned)p.W;
-        const size_t off = ((size_t)(a_img[i] * p.H + y) * p.W + x) * p.Cin + c;
-        ra[i] = ld16B(A + (ok ? off : 0), ok);
+        const bool ok = tap_ok && ((a_mask[i] >> (tap & 63)) & 1ull);
+        ra[i] = bld(rsa, ok ? (uint32_t)(a_base[i] + toff) : OOB);
         pv[i] = ok;
       }
       if (pro) pro_coeffs(c);
     } else if constexpr (PASS == DGRAD) {
       const int ti = k0 / p.Cout;  // tile lies in one tap (Cout % 64 == 0)
       const int c = k0 - ti * p.Cout + (tid & 7) * 8;
-      const int tap = p.taps[split][ti < 9 ? ti : 0];
-      const int r = (int)fdiv(tap, p.dS), s = tap - r * p.S;
+      const int tsel = ti < 9 ? ti : 0;
+      const int toff = ((p.tdy[split][tsel] * p.Wo + p.tdx[split][tsel]) * p.Cout + c) * 2;
 #pragma unroll
       for (int i = 0; i < AR; ++i) {
-        int yy = a_y[i] - r, xx = a_x[i] - s;  // (h + pad - r), divisible by stride
-        bool ok = a_ok[i] && yy >= 0 && xx >= 0;
-        yy = p.stride == 2 ? (yy >> 1) : yy;
-        xx = p.stride == 2 ? (xx >> 1) : xx;
-        ok = ok && yy < p.Ho && xx < p.Wo;
-        const size_t off = ((size_t)(a_img[i] * p.Ho + yy) * p.Wo + xx) * p.Cout + c;
-        ra[i] = ld16B(A + (ok ? off : 0), ok);
+        const bool ok = ((uint32_t)a_mask[i] >> ti) & 1u;
+        ra[i] = bld(rsa, ok ? (uint32_t)(a_base[i] + toff) : OOB);
       }
     } else {  // WGRAD A: dY rows m (k), cols n1 (COL tile [64][BM])
-      constexpr int CPR = BM / 8, RPI = NT / CPR;
-      const int col = m0 + (tid % CPR) * 8;
+      const uint32_t koff = (uint32_t)(kt * BK * p.Cout) * 2u;
 #pragma unroll
-      for (int i = 0; i < AR; ++i) {
-        const int krow = tid / CPR + RPI * i;
-        const int m = k0 + krow;
-        const bool ok = m < kend && col < p.M;
-        ra[i] = ld16B(A + (ok ? (size_t)m * p.Cout + col : 0), ok);
-      }
+      for (int i = 0; i < AR; ++i)
+        ra[i] = bld(rsa, (k0 + a_krow[i] < kend) ? a_off[i] + koff : OOB);
     }
     // ---------------- B
     if constexpr (PASS == FWD) {
-      const int k = k0 + (tid & 7) * 8;
 #pragma unroll
-      for (int i = 0; i < BR; ++i) {
-        const int n = n0 + (tid >> 3) + 32 * i;
-        const bool ok = n < p.N && k < p.Kpad;
-        rb[i] = ld16B(B + (ok ? (size_t)n * p.Kpad + k : 0), ok);
-      }
+      for (int i = 0; i < BR; ++i) rb[i] = bld(rsb, b_off[i] + (uint32_t)k0 * 2u);
     } else if constexpr (PASS == DGRAD) {
-      constexpr int CPR = BN / 8, RPI = NT / CPR;
       const int ti = k0 / p.Cout;
       const int tap = p.taps[split][ti < 9 ? ti : 0];
-      const int col = n0 + (tid % CPR) * 8;
+      const uint32_t uoff = (uint32_t)(((k0 - ti * p.Cout) * p.R * p.S + tap) * p.Cin) * 2u;
+#pragma unroll
+      for (int i = 0; i < BR; ++i) rb[i] = bld(rsb, b_off[i] + uoff);
+    } else if (wb_direct) {  // WGRAD B, 1x1 stride-1 conv: X rows ARE the GEMM rows
+      constexpr int CPR = BN / 8, RPI = NT / CPR;
 #pragma unroll
       for (int i = 0; i < BR; ++i) {
-        const int krow = tid / CPR + RPI * i;
-        const int co = k0 - ti * p.Cout + krow;
-        const bool ok = col < p.N;
-        const size_t off = ((size_t)co * (p.R * p.S) + tap) * p.Cin + col;
-        rb[i] = ld16B(B + (ok ? off : 0), ok);
+        const int m = k0 + tid / CPR + RPI * i;
+        const bool ok = wb_colok && m < kend;
+        rb[i] = bld(rsb, ok ? (uint32_t)(m * p.Cin + wb_c) * 2u : OOB);
+        pv[i] = ok;
       }
     } else {  // WGRAD B: gathered X rows m, cols (tap, c)
       constexpr int CPR = BN / 8, RPI = NT / CPR;
@@ -295,8 +338,8 @@ __global__ __launch_bounds__(NT, STAGES == 1 ? 3 : 2) void conv_gemm_kernel(Conv
         const uint32_t yo = fdiv(rem, p.dWo), xo = rem - yo * p.dWo.d;
         const int y = (int)yo * p.stride - p.pad + wb_r, x = (int)xo * p.stride - p.pad + wb_s;
         ok = ok && (unsigned)y < (unsigned)p.H && (unsigned)x < (unsigned)p.W;
-        const size_t off = ((size_t)(img * p.H + y) * p.W + x) * p.Cin + wb_c;
-        rb[i] = ld16B(B + (ok ? off : 0), ok);
+        const int off = ((((int)img * p.H + y) * p.W + x) * p.Cin + wb_c) * 2;
+        rb[i] = bld(rsb, ok ? (uint32_t)off : OOB);
         if constexpr (PASS == WGRAD) pv[i] = ok;
       }
     }
@@ -705,6 +748,12 @@ static int dispatch(int dt, int bm, int bn, const ConvParams& p, dim3 grid, hipS
   return -1;
 }
 
+// the kernels address operands with 32-bit buffer offsets (range-checked, OOB = 0x80000000)
+static bool fits32(long long a, long long b, long long c) {
+  const long long lim = 0x7fffffffll;
+  return a * 2 < lim && b * 2 < lim && c * 4 < lim;
+}
+
 static void fill_geom(ConvParams& p, const ConvDesc& d) {
   p.Nb = d.Nb; p.H = d.H; p.W = d.W; p.Cin = d.Cin; p.Cout = d.Cout;
   p.R = d.R; p.S = d.S; p.stride = d.stride; p.pad = d.pad; p.Ho = d.Ho; p.Wo = d.Wo;
@@ -722,6 +771,9 @@ extern "C" {
 int pda_conv_fwd(const ConvDesc* d, const void* x, const void* w, int Kpad, void* y, int out_f32,
                  int out_pitch, const float* bias, float* stats, int relu, const float* pro_sc,
                  const float* pro_sh, int dt, int bm, int bn, hipStream_t st) {
+  if (!fits32((long long)d->Nb * d->H * d->W * d->Cin, (long long)d->Cout * Kpad,
+              (long long)d->Nb * d->Ho * d->Wo * d->Cout) || d->R * d->S > 64)
+    return -4;
   ConvParams p{};
   fill_geom(p, *d);
   p.pro_sc = pro_sc; p.pro_sh = pro_sh;
@@ -743,6 +795,9 @@ struct BnEpi {  // mirrors ops/ext.py BnEpi
 
 int pda_conv_dgrad(const ConvDesc* d, const void* dy, const void* w, void* dx, const BnEpi* epi,
                    int dt, int bm, int bn, hipStream_t st) {
+  if (!fits32((long long)d->Nb * d->Ho * d->Wo * d->Cout, (long long)d->Cout * d->R * d->S * d->Cin,
+              (long long)d->Nb * d->H * d->W * d->Cin))
+    return -4;
   ConvParams p{};
   fill_geom(p, *d);
   p.a = dy; p.b = w; p.out = dx;
@@ -770,7 +825,11 @@ int pda_conv_dgrad(const ConvDesc* d, const void* dy, const void* w, void* dx, c
       if (((ph + d->pad - r) % sd + sd) % sd) continue;
       for (int s = 0; s < d->S; ++s) {
         if (((pw + d->pad - s) % sd + sd) % sd) continue;
-        if (p.ntaps[c] < 9) p.taps[c][p.ntaps[c]++] = r * d->S + s;
+        if (p.ntaps[c] < 9) {
+          p.tdy[c][p.ntaps[c]] = (ph + d->pad - r) / sd;
+          p.tdx[c][p.ntaps[c]] = (pw + d->pad - s) / sd;
+          p.taps[c][p.ntaps[c]++] = r * d->S + s;
+        }
       }
     }
   }
@@ -784,6 +843,9 @@ int pda_conv_dgrad(const ConvDesc* d, const void* dy, const void* w, void* dx, c
 int pda_conv_wgrad(const ConvDesc* d, const void* dy, const void* x, float* slab, int splits,
                    int k_chunk, const float* pro_sc, const float* pro_sh, int dt, int bm, int bn,
                    hipStream_t st) {
+  if (!fits32((long long)d->Nb * d->Ho * d->Wo * d->Cout, (long long)d->Nb * d->H * d->W * d->Cin,
+              (long long)splits * d->Cout * d->R * d->S * d->Cin))
+    return -4;
   ConvParams p{};
   fill_geom(p, *d);
   p.pro_sc = pro_sc; p.pro_sh = pro_sh;

@@ -241,13 +241,15 @@ _PRE_S = 96
 
 
 def prereduce(part: torch.Tensor, G: int, QC: int, ws: Optional["Workspace"] = None):
-    """[G][QC] partial slabs -> [S][QC] with S <= 96 (coalesced first stage), so the per-channel
-    finalize kernels never walk thousands of slabs serially. Returns (part, G)."""
-    if G <= 2 * _PRE_S:
+    """[G][QC] partial slabs -> [S][QC] with S in [96, 512] (coalesced first stage; narrow layers
+    get more slices so the stage fills the chip), so the per-channel finalize kernels never walk
+    thousands of slabs serially. Returns (part, G)."""
+    S = max(_PRE_S, min(512, 65536 // max(QC, 1)))   # enough blocks for narrow layers
+    if G <= 2 * S:
         return part, G
-    out = (ws.get("bn_pre", _PRE_S * QC) if ws is not None
-           else torch.empty(_PRE_S * QC, dtype=torch.float32, device=part.device))
-    s = ext.lib().pda_slab_reduce(ptr(part), G, QC, _PRE_S, ptr(out), stream(part.device))
+    out = (ws.get("bn_pre", 512 * QC) if ws is not None
+           else torch.empty(S * QC, dtype=torch.float32, device=part.device))
+    s = ext.lib().pda_slab_reduce(ptr(part), G, QC, S, ptr(out), stream(part.device))
     if s < 0:
         raise RuntimeError("slab_reduce launch failed")
     return out, s

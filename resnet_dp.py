@@ -1,14 +1,17 @@
 """ResNet-50, single-process data parallel over all visible GPUs (reference: resnet_dp.py).
 
 Global batch 3200 (= 400 per GPU on 8 GPUs), split across devices by
-pytorch_distributed_amd.parallel.DataParallel. No CLI arguments.
+pytorch_distributed_amd.parallel.DataParallel. No CLI arguments needed; optional flags
+mirror the MX_* env vars (``--help``).
 """
+import sys
+
 from pytorch_distributed_amd.config import config_for
 from pytorch_distributed_amd.trainer import run
 
 
 def main():
-    run(config_for("dp"), mode="dp")
+    run(config_for("dp", argv=sys.argv[1:]), mode="dp")
 
 
 if __name__ == "__main__":

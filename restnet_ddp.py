@@ -4,8 +4,9 @@ Launch once per node: MASTER_IP, MASTER_PORT, WORLD_SIZE (= #nodes), RANK (= nod
 one process per visible GPU is spawned (NUMA-bound). torchrun launches also work.
 """
 import os
+import sys
 
-from pytorch_distributed_amd.config import config_for
+from pytorch_distributed_amd.config import config_for, parse_cli
 from pytorch_distributed_amd.launch import spawn
 from pytorch_distributed_amd.trainer import run
 
@@ -15,6 +16,7 @@ def main(local_rank, script="ddp", nprocs=None):
 
 
 def launch(script="ddp"):
+    os.environ.update(parse_cli(sys.argv[1:]))   # optional flags -> MX_* env (inherited by ranks)
     if "LOCAL_RANK" in os.environ:            # started by torchrun
         main(int(os.environ["LOCAL_RANK"]), script)
         return

@@ -1,0 +1,77 @@
+"""T2 tier: every ResNet-50 conv shape (reduced batch) through
+every compiled tile variant of the implicit-GEMM kernel, fwd / dgrad / wgrad, against a plain
+PyTorch fp32 reference. The split-K weight-gradient path is exercised with several block
+targets, so the parallel slab reduction sees 1..hundreds of splits."""
+import math
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+
+SHAPES = [  # name, H, Cin, Cout, k, stride  
+    ("C1", 56, 64, 64, 1, 1), ("C2", 56, 64, 64, 3, 1), ("C3", 56, 64, 256, 1, 1),
+    ("C4", 56, 256, 64, 1, 1), ("C5", 56, 256, 128, 1, 1), ("C6", 56, 128, 128, 3, 2),
+    ("C7", 28, 128, 512, 1, 1), ("C8", 56, 256, 512, 1, 2), ("C9", 28, 512, 128, 1, 1),
+    ("C10", 28, 128, 128, 3, 1), ("C11", 28, 512, 256, 1, 1), ("C12", 28, 256, 256, 3, 2),
+    ("C13", 14, 256, 1024, 1, 1), ("C14", 28, 512, 1024, 1, 2), ("C15", 14, 1024, 256, 1, 1),
+    ("C16", 14, 256, 256, 3, 1), ("C17", 14, 1024, 512, 1, 1), ("C18", 14, 512, 512, 3, 2),
+    ("C19", 7, 512, 2048, 1, 1), ("C20", 14, 1024, 2048, 1, 2), ("C21", 7, 2048, 512, 1, 1),
+    ("C22", 7, 512, 512, 3, 1),
+]
+TILES = [(128, 128), (128, 64), (64, 128), (64, 64), (-128, 128), (-128, 64), (-64, 128)]
+
+
+def rel_err(a, b):
+    return ((a.float() - b.float()).norm() / (b.float().norm() + 1e-12)).item()
+
+
+@pytest.mark.parametrize("shape", SHAPES, ids=[s[0] for s in SHAPES])
+def test_resnet50_conv_shape_all_tiles(shape):
+    from pytorch_distributed_amd.ops import ext
+    ext.load(required=True)
+    from pytorch_distributed_amd.ops import native_ops as K
+    _, H, Cin, Cout, k, s = shape
+    Nb, pad, dt = 2, k // 2, torch.bfloat16
+    torch.manual_seed(1)
+    x = (torch.randn(Nb, Cin, H, H, device=DEV) + 0.1).to(dt).float()
+    w = (torch.randn(Cout, Cin, k, k, device=DEV) / math.sqrt(Cin * k * k)).to(dt).float()
+    xr = x.clone().requires_grad_(True)
+    wr = w.clone().requires_grad_(True)
+    y_ref = F.conv2d(xr, wr, stride=s, padding=pad)
+    dy = torch.randn_like(y_ref).to(dt).float()
+    y_ref.backward(dy)
+    g = K.ConvGeom(Nb, H, H, Cin, Cout, k, k, s, pad)
+    x_nhwc = x.permute(0, 2, 3, 1).contiguous().to(dt)
+    w_ohwi = w.permute(0, 2, 3, 1).contiguous().to(dt)
+    dy_nhwc = dy.permute(0, 2, 3, 1).contiguous().to(dt)
+    yr = y_ref.detach().permute(0, 2, 3, 1)
+    dxr = xr.grad.permute(0, 2, 3, 1)
+    dwr = wr.grad.permute(0, 2, 3, 1)
+    ws = K.Workspace(DEV)
+    M = Nb * g.Ho * g.Wo
+    bad = []
+    for t in TILES:
+        y = torch.full((Nb, g.Ho, g.Wo, Cout), float("nan"), device=DEV, dtype=dt)
+        stats = torch.zeros(math.ceil(M / 64) * 2 * Cout, device=DEV)
+        K.conv_fwd(x_nhwc, w_ohwi.view(Cout, -1), g, y, stats=stats, tile=t)
+        dx = torch.full((Nb, H, H, Cin), float("nan"), device=DEV, dtype=dt)
+        K.conv_dgrad(dy_nhwc, w_ohwi, g, dx, tile=t)
+        torch.cuda.synchronize()
+        T = math.ceil(M / abs(t[0]))
+        st = stats[:T * 2 * Cout].view(T, 2, Cout).sum(0)
+        for name, e in (("fwd", rel_err(y, yr)), ("dgrad", rel_err(dx, dxr)),
+                        ("stats", rel_err(st[0], y.float().reshape(-1, Cout).sum(0)))):
+            if not e < 1e-2:
+                bad.append((t, name, e))
+        for tb in (64, 512, 4096):
+            dw = torch.full((Cout, k, k, Cin), float("nan"), device=DEV)
+            K.conv_wgrad(dy_nhwc, x_nhwc, g, dw.view(-1), ws, tile=t, target_blocks=tb)
+            torch.cuda.synchronize()
+            e = rel_err(dw, dwr)
+            if not e < 1e-2:
+                bad.append((t, f"wgrad/{tb}", e))
+    assert not bad, bad

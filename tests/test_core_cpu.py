@@ -28,6 +28,16 @@ def test_config_defaults_match_reference():
         config_for("single", env={"MX_DTYPE": "int8"})
 
 
+def test_cli_flags_mirror_env():
+    # no flags -> identical to env-only; flags override env
+    assert config_for("single", env={}, argv=[]) == config_for("single", env={})
+    c = config_for("ddp", env={"MX_EPOCHS": "3"},
+                   argv=["--epochs", "5", "--steps-per-epoch", "7", "--dtype", "bf16"])
+    assert (c.epochs, c.steps_per_epoch, c.dtype) == (5, 7, "bf16")
+    with pytest.raises(SystemExit):
+        config_for("single", env={}, argv=["--no-such-flag", "1"])
+
+
 def test_resnet50_census_matches_torchvision():
     m = resnet50()
     n = sum(p.numel() for p in m.parameters())
