@@ -36,8 +36,14 @@ def _newer(src: Path, obj: Path, deps) -> bool:
     return src.stat().st_mtime > t or any(d.stat().st_mtime > t for d in deps)
 
 
+# per-source flags: the conv kernels keep their operand-prologue math in scalar f32 FMAs, which
+# beside MFMAs issue far cheaper than the v_pk_fma_f32 the SLP vectorizer would form
+FILE_FLAGS = {"conv_gemm.hip": ["-fno-slp-vectorize"]}
+
+
 def _compile(src: Path, obj: Path, extra, verbose: bool) -> None:
-    cmd = [HIPCC, *CFLAGS, *extra, "-I", str(CSRC), "-c", str(src), "-o", str(obj)]
+    cmd = [HIPCC, *CFLAGS, *FILE_FLAGS.get(src.name, []), *extra, "-I", str(CSRC), "-c", str(src),
+           "-o", str(obj)]
     if verbose:
         print(" ".join(cmd), flush=True)
     r = subprocess.run(cmd, capture_output=True, text=True)

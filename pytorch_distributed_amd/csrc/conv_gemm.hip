@@ -67,6 +67,13 @@ struct ConvParams {
   float* epart;                    // [ncls*tiles_m][enq][N] partial sums
 };
 
+// Scalar-f32 pair FMA for the operand prologue, which runs between MFMAs: there a packed
+// v_pk_fma_f32 costs far more issue time than two scalar v_fma_f32 (MI355X_MICROARCH.md, cycle
+// constants). This file is built with -fno-slp-vectorize so the compiler does not re-pack them.
+__device__ __forceinline__ f32x2 fma2(f32x2 a, f32x2 b, f32x2 c) {
+  return f32x2{__builtin_fmaf(a.x, b.x, c.x), __builtin_fmaf(a.y, b.y, c.y)};
+}
+
 // ---------------------------------------------------------------- LDS addressing
 // ROW tile: BR rows x 64 k (128 B per row).
 __device__ __forceinline__ int row_addr(int row, int chunk) {
@@ -75,7 +82,9 @@ __device__ __forceinline__ int row_addr(int row, int chunk) {
 // COL tile: 64 k-rows x BC cols.
 template <int BC>
 __device__ __forceinline__ int col_swz(int krow) {
-  if constexpr (BC == 128) return ((krow & 3) << 1) | (((krow >> 3) & 1) << 3);
+  // BC >= 128: only (address mod 256 B) picks the bank, so the 128-column pattern also makes the
+  // 256-column tile (512-B rows) conflict-free for the b128 writes and the transposed reads
+  if constexpr (BC >= 128) return ((krow & 3) << 1) | (((krow >> 3) & 1) << 3);
   else return (((krow >> 1) & 1) << 1) | (((krow >> 3) & 1) << 2);
 }
 template <int BC>
@@ -112,12 +121,17 @@ __device__ __forceinline__ s16x8 frag_col(const char* lds, int cb, int s, int la
 //             shallow-K layers of ResNet (K = 64..128: nk <= 2), where the per-block
 //             load -> MFMA -> store chain is latency-bound and concurrency matters more.
 template <int PASS, int DT, int BM, int BN, int STAGES>
-__global__ __launch_bounds__(NT, STAGES == 1 ? 3 : 2) void conv_gemm_kernel(ConvParams p) {
+// 256-wide tiles (single-stage only; wave tile 128x64 / 64x128: a quarter less LDS traffic per
+// MFMA) need ~250 registers and 64 KiB of LDS: two blocks per CU.
+__global__ __launch_bounds__(NT, (STAGES == 1 && BM * BN <= 128 * 128) ? 3 : 2) void conv_gemm_kernel(ConvParams p) {
   // A tile: FWD/DGRAD ROW [BM][64]; WGRAD COL [64][BM]. B tile: FWD ROW [BN][64]; else COL [64][BN]
   constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2;
   constexpr int STAGE = A_BYTES + B_BYTES;
   constexpr int RED_BYTES = 3 * NT * 8 * 4;
-  constexpr int LDS_BYTES = STAGES * STAGE > RED_BYTES ? STAGES * STAGE : RED_BYTES;
+  constexpr int C_BYTES = BM * BN * 2;   // staged 16-bit C tile of the epilogue
+  constexpr int LDS_0 = STAGES * STAGE > RED_BYTES ? STAGES * STAGE : RED_BYTES;
+  constexpr int LDS_BYTES = LDS_0 > C_BYTES ? LDS_0 : C_BYTES;
+  static_assert(BN <= NT, "stats reduction: one thread per column");
   static_assert(BM * BN * 2 <= LDS_BYTES, "C tile must fit in the staging buffers");
   static_assert(3 * NT * 8 * 4 <= LDS_BYTES, "stats reduction must fit");
   __shared__ __attribute__((aligned(16))) char smem[LDS_BYTES];
@@ -268,7 +282,8 @@ __global__ __launch_bounds__(NT, STAGES == 1 ? 3 : 2) void conv_gemm_kernel(Conv
   auto pro_apply = [&](i32x4& v) {
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
-      const f32x2 f = unpack2<DT>((uint32_t)v[k]) * psc[k] + psh[k];
+      const f32x2 u = unpack2<DT>((uint32_t)v[k]);
+      const f32x2 f = fma2(u, psc[k], psh[k]);
       const s16x2 h = __builtin_bit_cast(s16x2, pack2<DT>(f));
       v[k] = __builtin_bit_cast(int, __builtin_elementwise_max(h, (s16x2){0, 0}));
     }
@@ -485,14 +500,14 @@ __global__ __launch_bounds__(NT, STAGES == 1 ? 3 : 2) void conv_gemm_kernel(Conv
     constexpr int CPR = BN / 8;
     auto c_addr = [&](int row, int chunk) { return row * CPR + (chunk ^ (row & (CPR - 1))); };
     {
-      const int sw = lr & (CPR - 1);   // == row & (CPR-1) for every row this lane holds
 #pragma unroll
       for (int j = 0; j < NI; ++j) {
         const int col = wc * (BN / 2) + j * 16 + 4 * lg;
-        const int cbyte = (((col >> 3) ^ sw) << 4) + ((col & 4) << 1);
 #pragma unroll
         for (int i = 0; i < MI; ++i) {
           const int row = wr * (BM / 2) + i * 16 + lr;
+          // row & (CPR-1) == lr & (CPR-1) for CPR <= 16 (folded); BN = 256 needs the full row
+          const int cbyte = (((col >> 3) ^ (row & (CPR - 1))) << 4) + ((col & 4) << 1);
           uint2 pk;
           pk.x = pack2<DT>(f32x2{acc[i][j][0], acc[i][j][1]});
           pk.y = pack2<DT>(f32x2{acc[i][j][2], acc[i][j][3]});
@@ -508,7 +523,8 @@ __global__ __launch_bounds__(NT, STAGES == 1 ? 3 : 2) void conv_gemm_kernel(Conv
     //        y (and the residual), stores dz instead of dA and emits q0 = sum dz, q1 = sum dz*y,
     //        q2 = sum dz*y2 -- the BatchNorm-backward reduction, with no extra pass over dA.
     // The BN mode and the g2 source are compile-time in the row loop (one uniform dispatch below),
-    // and all per-element math runs on packed pairs (v_pk_fma_f32 / v_cvt_pk_*).
+    // and all per-element math runs on packed pairs (v_pk_fma_f32 / v_cvt_pk_*); unlike the operand
+    // prologue, the packed form measured faster here.
     const int cc = tid % CPR;          // column chunk
     const int rg = tid / CPR;          // row group
     constexpr int RG = NT / CPR;       // row groups
@@ -734,6 +750,10 @@ static int dispatch(int dt, int bm, int bn, const ConvParams& p, dim3 grid, hipS
 #define PDA_CASE1(D, M_, N_)                                                   \
   if (dt == D && -bm == M_ && bn == N_) return launch<PASS, D, M_, N_, 1>(p, grid, st);
     PDA_CASE1(DT_BF16, 128, 128) PDA_CASE1(DT_BF16, 128, 64) PDA_CASE1(DT_BF16, 64, 128)
+    // 256-wide tiles only where they measured faster (profiles/convbench_r1_v6.txt):
+    // wgrad 256x128 (3x3 layers 3-4), dgrad 128x256 (1x1 with wide Cin)
+    if constexpr (PASS == WGRAD) { PDA_CASE1(DT_BF16, 256, 128) PDA_CASE1(DT_F16, 256, 128) }
+    if constexpr (PASS == DGRAD) { PDA_CASE1(DT_BF16, 128, 256) PDA_CASE1(DT_F16, 128, 256) }
     PDA_CASE1(DT_F16, 128, 128) PDA_CASE1(DT_F16, 128, 64) PDA_CASE1(DT_F16, 64, 128)
 #undef PDA_CASE1
     return -1;

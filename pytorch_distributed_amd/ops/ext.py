@@ -20,6 +20,8 @@ __all__ = ["load", "available", "lib", "DT", "dt_of", "ConvDesc", "BwdArgs", "Bn
 _LIB: Optional[C.CDLL] = None
 _ERR: Optional[str] = None
 LIBPATH = Path(__file__).resolve().parent.parent / "_lib" / "libpda_kernels.so"
+if os.environ.get("PDA_KERNEL_LIB"):   # A/B variants (tools/build_variant.py), relative to _lib/
+    LIBPATH = LIBPATH.parent / os.environ["PDA_KERNEL_LIB"]
 
 DT = {torch.float32: 0, torch.bfloat16: 1, torch.float16: 2}
 

@@ -173,19 +173,31 @@ def bn_epilogue(ws: "Workspace", G: int, y, scale, shift, res=None, y2=None, sca
 
 
 # Weight-gradient tile / split-K block target per ResNet conv geometry (Cout, R, Cin, stride, Ho),
-# measured with tools/wgrad_sweep.py on MI355X at batch 400 (profiles/wgrad_sweep_r1.txt).
+# measured with tools/wgrad_sweep.py on MI355X at batch 400 (profiles/wgrad_sweep_r1_v2.txt; the
+# 256x128 single-stage tile wins on the 3x3 layers 3-4 and the wide strided/narrowing 1x1s).
 _WGRAD_TUNED = {
-    (64, 1, 64, 1, 56): ((64, 64), 1024),
-    (64, 3, 64, 1, 56): ((64, 128), 2048),
-    (256, 1, 64, 1, 56): ((-128, 128), 512),
-    (64, 1, 256, 1, 56): ((-128, 128), 512),
-    (128, 1, 256, 1, 56): ((128, 128), 512),
-    (128, 3, 128, 2, 28): ((128, 128), 2048),
-    (128, 3, 128, 1, 28): ((64, 128), 2048),
-    (256, 3, 256, 2, 14): ((128, 128), 2048),
-    (256, 3, 256, 1, 14): ((-128, 128), 2048),
-    (512, 3, 512, 2, 7): ((-128, 128), 4096),
-    (512, 3, 512, 1, 7): ((-128, 128), 1024),
+    (64, 1, 64, 1, 56): ((64, 64), 1024),       # C1
+    (64, 3, 64, 1, 56): ((64, 128), 512),       # C2
+    (256, 1, 64, 1, 56): ((-128, 128), 512),    # C3
+    (64, 1, 256, 1, 56): ((128, 128), 512),     # C4
+    (128, 1, 256, 1, 56): ((-128, 128), 512),   # C5
+    (128, 3, 128, 2, 28): ((128, 64), 2048),    # C6
+    (512, 1, 128, 1, 28): ((128, 128), 512),    # C7
+    (512, 1, 256, 2, 28): ((-256, 128), 512),   # C8
+    (128, 1, 512, 1, 28): ((-128, 128), 512),   # C9
+    (128, 3, 128, 1, 28): ((64, 128), 2048),    # C10
+    (256, 1, 512, 1, 28): ((-256, 128), 1024),  # C11
+    (256, 3, 256, 2, 14): ((128, 128), 2048),   # C12
+    (1024, 1, 256, 1, 14): ((128, 64), 512),    # C13
+    (1024, 1, 512, 2, 14): ((128, 128), 512),   # C14
+    (256, 1, 1024, 1, 14): ((128, 64), 512),    # C15
+    (256, 3, 256, 1, 14): ((-256, 128), 2048),  # C16
+    (512, 1, 1024, 1, 14): ((128, 128), 512),   # C17
+    (512, 3, 512, 2, 7): ((-256, 128), 4096),   # C18
+    (2048, 1, 512, 1, 7): ((-128, 128), 512),   # C19
+    (2048, 1, 1024, 2, 7): ((-128, 128), 512),  # C20
+    (512, 1, 2048, 1, 7): ((128, 128), 512),    # C21
+    (512, 3, 512, 1, 7): ((-256, 128), 1024),   # C22
 }
 
 

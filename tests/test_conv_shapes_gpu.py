@@ -23,6 +23,7 @@ SHAPES = [  # name, H, Cin, Cout, k, stride  
     ("C22", 7, 512, 512, 3, 1),
 ]
 TILES = [(128, 128), (128, 64), (64, 128), (64, 64), (-128, 128), (-128, 64), (-64, 128)]
+WGRAD_TILES = TILES + [(-256, 128)]   # the 256-row single-stage tile exists for wgrad only
 
 
 def rel_err(a, b):
@@ -54,7 +55,16 @@ def test_resnet50_conv_shape_all_tiles(shape):
     ws = K.Workspace(DEV)
     M = Nb * g.Ho * g.Wo
     bad = []
-    for t in TILES:
+    for t in WGRAD_TILES:
+        if t not in TILES:   # wgrad-only tile
+            for tb in (64, 512, 4096):
+                dw = torch.full((Cout, k, k, Cin), float("nan"), device=DEV)
+                K.conv_wgrad(dy_nhwc, x_nhwc, g, dw.view(-1), ws, tile=t, target_blocks=tb)
+                torch.cuda.synchronize()
+                e = rel_err(dw, dwr)
+                if not e < 1e-2:
+                    bad.append((t, f"wgrad/{tb}", e))
+            continue
         y = torch.full((Nb, g.Ho, g.Wo, Cout), float("nan"), device=DEV, dtype=dt)
         stats = torch.zeros(math.ceil(M / 64) * 2 * Cout, device=DEV)
         K.conv_fwd(x_nhwc, w_ohwi.view(Cout, -1), g, y, stats=stats, tile=t)

@@ -10,11 +10,13 @@ from collections import defaultdict
 
 def family(name: str) -> str:
     n = name
-    m = re.search(r"conv_gemm_kernel<(\d+), (\d+), (\d+), (\d+)(?:, (\d+))?>", n) or \
-        re.search(r"conv_gemm_kernelILi(\d+)ELi(\d+)ELi(\d+)ELi(\d+)E", n)
+    m = re.search(r"conv_gemm_kernel<(\d+), (\d+), (\d+), (\d+)(?:, (\d+))?(?:, (\d+))?>", n) or \
+        re.search(r"conv_gemm_kernelILi(\d+)ELi(\d+)ELi(\d+)ELi(\d+)E(?:Li(\d+)E)?(?:Li(\d+)E)?", n)
     if m:
         p = {"0": "fwd", "1": "dgrad", "2": "wgrad"}[m.group(1)]
-        return f"conv_{p} {m.group(3)}x{m.group(4)}"
+        st = f" st{m.group(5)}" if m.group(5) else ""
+        pro = f" pro{m.group(6)}" if m.group(6) else ""
+        return f"conv_{p} {m.group(3)}x{m.group(4)}{st}{pro}"
     n = re.sub(r"^void ", "", n)
     n = n.replace("(anonymous namespace)::", "")
     if n.startswith("at::native::"):

@@ -11,7 +11,7 @@ from pytorch_distributed_amd.ops import ext  # noqa: E402
 from pytorch_distributed_amd.ops import native_ops as K  # noqa: E402
 from tools.conv_bench import COUNT, SHAPES, timeit  # noqa: E402
 
-TILES = [(64, 64), (128, 64), (64, 128), (-128, 128), (128, 128)]
+TILES = [(64, 64), (128, 64), (64, 128), (-128, 128), (128, 128), (-256, 128)]
 TARGETS = [512, 1024, 2048, 4096]
 
 
