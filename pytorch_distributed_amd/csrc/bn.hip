@@ -41,6 +41,42 @@ __device__ __forceinline__ void ld8f(const float* p, float* f) {
   f[4] = b[0]; f[5] = b[1]; f[6] = b[2]; f[7] = b[3];
 }
 
+// ------------------------------------------------------------------ finalize helpers
+// Sum of slabs t = g, g+64, ... of two per-channel columns (o0, o1) of a [T][pitch] partial buffer
+// in f64, with four independent load chains (the loads pipeline instead of serialising on one
+// accumulator). The summation order depends only on T: deterministic.
+__device__ __forceinline__ void slab_sum2(const float* __restrict__ part, int T, int pitch, int o0,
+                                          int o1, int g, double& s0, double& s1) {
+  double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0, b0 = 0.0, b1 = 0.0, b2 = 0.0, b3 = 0.0;
+  int t = g;
+  for (; t + 192 < T; t += 256) {
+    a0 += part[(size_t)t * pitch + o0];         b0 += part[(size_t)t * pitch + o1];
+    a1 += part[(size_t)(t + 64) * pitch + o0];  b1 += part[(size_t)(t + 64) * pitch + o1];
+    a2 += part[(size_t)(t + 128) * pitch + o0]; b2 += part[(size_t)(t + 128) * pitch + o1];
+    a3 += part[(size_t)(t + 192) * pitch + o0]; b3 += part[(size_t)(t + 192) * pitch + o1];
+  }
+  for (; t < T; t += 64) {
+    a0 += part[(size_t)t * pitch + o0];
+    b0 += part[(size_t)t * pitch + o1];
+  }
+  s0 = (a0 + a1) + (a2 + a3);
+  s1 = (b0 + b1) + (b2 + b3);
+}
+
+// fixed-shape tree over the 64 partial-lanes of red[2][64][17] (1024-thread block: g = tid >> 4,
+// cl = tid & 15); red[q][0][cl] holds the totals afterwards. Replaces a 64-step serial LDS walk.
+__device__ __forceinline__ void tree_reduce2(double (&red)[2][64][17], int g, int cl) {
+  __syncthreads();
+#pragma unroll
+  for (int s = 32; s > 0; s >>= 1) {
+    if (g < s) {
+      red[0][g][cl] += red[0][g + s][cl];
+      red[1][g][cl] += red[1][g + s][cl];
+    }
+    __syncthreads();
+  }
+}
+
 // ------------------------------------------------------------------ forward finalize
 // part: [T][2][C] (sum, sumsq) partials. One block = 16 channels x 64 partial-lanes.
 __global__ __launch_bounds__(1024) void bn_finalize_fwd_kernel(
@@ -53,21 +89,12 @@ __global__ __launch_bounds__(1024) void bn_finalize_fwd_kernel(
   const int cl = threadIdx.x & 15, g = threadIdx.x >> 4;
   const int c = blockIdx.x * 16 + cl;
   double s1 = 0.0, s2 = 0.0;
-  if (c < C) {
-    for (int t = g; t < T; t += 64) {
-      s1 += part[(size_t)t * 2 * C + c];
-      s2 += part[(size_t)t * 2 * C + C + c];
-    }
-  }
+  if (c < C) slab_sum2(part, T, 2 * C, c, C + c, g, s1, s2);
   red[0][g][cl] = s1;
   red[1][g][cl] = s2;
-  __syncthreads();
+  tree_reduce2(red, g, cl);
   if (g == 0 && c < C) {
-    double a = 0.0, b = 0.0;
-    for (int i = 0; i < 64; ++i) {
-      a += red[0][i][cl];
-      b += red[1][i][cl];
-    }
+    const double a = red[0][0][cl], b = red[1][0][cl];
     const double mean = a / count;
     double var = b / count - mean * mean;
     if (var < 0.0) var = 0.0;
@@ -412,21 +439,12 @@ __global__ __launch_bounds__(1024) void bn_bwd_finalize_kernel(
   const int cl = threadIdx.x & 15, g = threadIdx.x >> 4;
   const int c = blockIdx.x * 16 + cl;
   double s0 = 0.0, s1 = 0.0;
-  if (c < C) {
-    for (int t = g; t < G; t += 64) {
-      s0 += part[((size_t)t * nq + 0) * C + c];
-      s1 += part[((size_t)t * nq + qy) * C + c];
-    }
-  }
+  if (c < C) slab_sum2(part, G, nq * C, c, qy * C + c, g, s0, s1);
   red[0][g][cl] = s0;
   red[1][g][cl] = s1;
-  __syncthreads();
+  tree_reduce2(red, g, cl);
   if (g == 0 && c < C) {
-    double sdz = 0.0, sdzy = 0.0;
-    for (int i = 0; i < 64; ++i) {
-      sdz += red[0][i][cl];
-      sdzy += red[1][i][cl];
-    }
+    const double sdz = red[0][0][cl], sdzy = red[1][0][cl];
     const double mu = mean[c], is = invstd[c], ga = gamma[c];
     const double sdzx = (sdzy - mu * sdz) * is;  // sum dz * xhat
     dgamma[c] = (float)(sdzx * gscale) + (accumulate ? dgamma[c] : 0.f);

@@ -88,17 +88,31 @@ __global__ __launch_bounds__(NT) void topk_kernel(const float* __restrict__ logi
   }
 }
 
-// out[c] = scale * sum_r x[r][c]  (x: 16-bit [rows][ld])
-__global__ void col_sum_kernel(const u16* __restrict__ x, int rows, int C, int ld, float scale,
-                               float* __restrict__ out, int dt, int accumulate) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
+// out[c] = scale * sum_r x[r][c]  (x: 16-bit [rows][ld]). Block = 64 columns x 16 row slices
+// (1024 threads): each thread sums every 16th row of its column (independent loads, pipelined),
+// then a fixed-order LDS combine -- deterministic, no serial 400-load chain per column.
+__global__ __launch_bounds__(1024) void col_sum_kernel(const u16* __restrict__ x, int rows, int C,
+                                                       int ld, float scale, float* __restrict__ out,
+                                                       int dt, int accumulate) {
+  __shared__ float red[16][64];
+  const int cl = threadIdx.x & 63, sl = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + cl;
   float s = 0.f;
-  for (int r = 0; r < rows; ++r) {
-    const u16 h = x[(size_t)r * ld + c];
-    s += dt == DT_BF16 ? bf16_to_f32(h) : f16_to_f32(h);
+  if (c < C) {
+#pragma unroll 4
+    for (int r = sl; r < rows; r += 16) {
+      const u16 h = x[(size_t)r * ld + c];
+      s += dt == DT_BF16 ? bf16_to_f32(h) : f16_to_f32(h);
+    }
   }
-  out[c] = s * scale + (accumulate ? out[c] : 0.f);
+  red[sl][cl] = s;
+  __syncthreads();
+  if (sl == 0 && c < C) {
+    float t = 0.f;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) t += red[k][cl];
+    out[c] = t * scale + (accumulate ? out[c] : 0.f);
+  }
 }
 
 // ------------------------------------------------------------------ optimizer
@@ -375,7 +389,7 @@ int pda_topk(const float* logits, int B, int K, int ld, const long long* labels,
 
 int pda_col_sum(const void* x, int rows, int C, int ld, float scale, float* out, int dt,
                 int accumulate, hipStream_t st) {
-  hipLaunchKernelGGL(col_sum_kernel, dim3((C + 255) / 256), dim3(256), 0, st, (const u16*)x, rows, C, ld,
+  hipLaunchKernelGGL(col_sum_kernel, dim3((C + 63) / 64), dim3(1024), 0, st, (const u16*)x, rows, C, ld,
                      scale, out, dt, accumulate);
   return (int)hipGetLastError();
 }
