@@ -428,6 +428,97 @@ __global__ __launch_bounds__(NT) void bn_bwd_reduce_kernel(BwdArgs a) {
   }
 }
 
+// Stem backward, one pass: maxpool gradient gather (as maxpool_bwd_kernel) -> ReLU mask of
+// relu(bn(y0)) -> dz stored -> per-block partials q0 = sum dz, q1 = sum dz*y0. Replaces
+// maxpool_bwd (write dA0) + bn_bwd_reduce (re-read dA0): one full read of the largest activation
+// of the network (400x112x112x64) less, and one launch less. Rows = input pixels (N*H*W).
+template <int DT>
+__global__ __launch_bounds__(NT) void stem_bwd_reduce_kernel(
+    const u16* __restrict__ dout, const u16* __restrict__ dout2, const uint8_t* __restrict__ arg,
+    const u16* __restrict__ y, const float* __restrict__ sc, const float* __restrict__ sh,
+    u16* __restrict__ dz_out, float* __restrict__ part, long long rows, long long rows_per_block,
+    int H, int W, int C, int Ho, int Wo, FastDiv dW, FastDiv dH) {
+  __shared__ float red[2][NT][8];
+  const int CK = C / 8;
+  const int tpr = CK < NT ? CK : NT;
+  const int rpi = NT / tpr;
+  const int ck = threadIdx.x % tpr, rsub = threadIdx.x / tpr;
+  const long long r0 = blockIdx.x * rows_per_block;
+  const long long r1 = min(rows, r0 + rows_per_block);
+  for (int cbase = 0; cbase < CK; cbase += tpr) {
+    const int cc = cbase + ck, c0 = cc * 8;
+    float q0[8], q1[8], s[8], h[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) { q0[e] = 0.f; q1[e] = 0.f; }
+    ld8f(sc + c0, s);
+    ld8f(sh + c0, h);
+    if (threadIdx.x < tpr * rpi) {
+      for (long long row = r0 + rsub; row < r1; row += rpi) {
+        const uint32_t p2 = fdiv((uint32_t)row, dW), x = (uint32_t)row - p2 * W;
+        const uint32_t n = fdiv(p2, dH), yy = p2 - n * H;
+        float g[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) g[e] = 0.f;
+        for (int yo = (int)yy / 2; yo <= min(Ho - 1, ((int)yy + 1) / 2); ++yo) {
+          const int dy = (int)yy - (yo * 2 - 1);
+          if (dy < 0 || dy > 2) continue;
+          for (int xo = (int)x / 2; xo <= min(Wo - 1, ((int)x + 1) / 2); ++xo) {
+            const int dx = (int)x - (xo * 2 - 1);
+            if (dx < 0 || dx > 2) continue;
+            const uint32_t o = (n * Ho + yo) * Wo + xo;
+            const uint64_t am = reinterpret_cast<const uint64_t*>(arg)[o * CK + cc];
+            float d[8];
+            unpack8<DT>(*reinterpret_cast<const i32x4*>(dout + (size_t)o * C + c0), d);
+            if (dout2) {
+              float d2[8];
+              unpack8<DT>(*reinterpret_cast<const i32x4*>(dout2 + (size_t)o * C + c0), d2);
+#pragma unroll
+              for (int e = 0; e < 8; ++e) d[e] += d2[e];
+            }
+            const int me = dy * 3 + dx;
+#pragma unroll
+            for (int e = 0; e < 8; ++e)
+              if ((int)((am >> (8 * e)) & 0xff) == me) g[e] += d[e];
+          }
+        }
+        float yv[8];
+        unpack8<DT>(*reinterpret_cast<const i32x4*>(y + row * C + c0), yv);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) g[e] = yv[e] * s[e] + h[e] > 0.f ? g[e] : 0.f;
+        // statistics of the stored (rounded) dz, as the apply kernel re-reads it
+        const i32x4 pk = pack8<DT>(g);
+        *reinterpret_cast<i32x4*>(dz_out + row * C + c0) = pk;
+        unpack8<DT>(pk, g);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          q0[e] += g[e];
+          q1[e] += g[e] * yv[e];
+        }
+      }
+    }
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      red[0][threadIdx.x][e] = q0[e];
+      red[1][threadIdx.x][e] = q1[e];
+    }
+    __syncthreads();
+    if (threadIdx.x < tpr) {
+      for (int q = 0; q < 2; ++q) {
+        float t[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) t[e] = 0.f;
+        for (int r = 0; r < rpi; ++r)
+#pragma unroll
+          for (int e = 0; e < 8; ++e) t[e] += red[q][r * tpr + threadIdx.x][e];
+        float* dst = part + ((size_t)blockIdx.x * 2 + q) * C + c0;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) dst[e] = t[e];
+      }
+    }
+    __syncthreads();
+  }
+}
+
 // finalize: for branch b (0: y with q0,q1; 1: y2 with q0,q2) produce gamma/beta grads and
 // coefficients k1,k2,k3 such that dy = k1*dz + k2*y + k3.
 __global__ __launch_bounds__(1024) void bn_bwd_finalize_kernel(
@@ -651,6 +742,22 @@ int pda_bn_bwd_reduce(const BwdArgsC* c, int G, int dt, hipStream_t st) {
   BwdArgs a = to_args(c);
   a.rows_per_block = (a.rows + G - 1) / G;
 #define K(D) hipLaunchKernelGGL(bn_bwd_reduce_kernel<D>, dim3(G), dim3(NT), 0, st, a)
+  if (dt == DT_BF16) K(DT_BF16); else K(DT_F16);
+#undef K
+  return (int)hipGetLastError();
+}
+
+// stem backward reduce (maxpool gather + ReLU mask + dz store + partials [G][2][C])
+int pda_stem_bwd_reduce(const void* dout, const void* dout2, const void* arg, const void* y,
+                        const float* sc, const float* sh, void* dz_out, float* part, int G, int N,
+                        int H, int W, int C, int Ho, int Wo, int dt, hipStream_t st) {
+  const long long rows = (long long)N * H * W;
+  if (rows * C >= (1ll << 31) || C % 8) return -2;
+  const long long rpb = (rows + G - 1) / G;
+#define K(D) hipLaunchKernelGGL(stem_bwd_reduce_kernel<D>, dim3(G), dim3(NT), 0, st, (const u16*)dout, \
+                                (const u16*)dout2, (const uint8_t*)arg, (const u16*)y, sc, sh,       \
+                                (u16*)dz_out, part, rows, rpb, H, W, C, Ho, Wo, make_div(W),          \
+                                make_div(H))
   if (dt == DT_BF16) K(DT_BF16); else K(DT_F16);
 #undef K
   return (int)hipGetLastError();

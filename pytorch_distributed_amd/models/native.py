@@ -122,6 +122,7 @@ class NativeResNet(nn.Module):
         # BN1/BN2 (+ReLU) applied inside the consumer conv's operand staging (fwd and wgrad)
         import os
         self.fuse_prologue = os.environ.get("PDA_FUSE_PROLOGUE", "1") != "0"
+        self.fused_stem_bwd = os.environ.get("PDA_FUSED_STEM_BWD", "1") != "0"
         self.refresh_shadow()
 
     # ------------------------------------------------------------------ planning
@@ -514,12 +515,19 @@ class NativeResNet(nn.Module):
         # ---- stem: maxpool backward of (main + shortcut) gradients, BN backward, wgrad
         x0, y0, arg = sv["x0"], sv["y0"], sv["arg"]
         st0 = sv["stem_stats"]
-        dA0 = self._empty(*y0.shape)
-        K.maxpool_bwd(dx_main, arg, dA0, dout2=shortcut_g)
-        dy0 = self._empty(*y0.shape)
         u = self.stem
-        K.bn_bwd(ws, y0, st0[0], st0[1], self.gamma(u), st0[2], st0[3], self.dgamma(u),
-                 self.dbeta(u), dy0, g1=dA0, accumulate=acc)
+        dy0 = self._empty(*y0.shape)
+        if self.fused_stem_bwd:   # maxpool gather + ReLU mask + BN partials in one pass
+            dz0 = self._empty(*y0.shape)
+            part, G, nq = K.stem_bwd_reduce(ws, dx_main, arg, y0, st0[2], st0[3], dz0,
+                                            dout2=shortcut_g)
+            K.bn_bwd_finish(ws, part, G, nq, y0, st0[0], st0[1], self.gamma(u), self.dgamma(u),
+                            self.dbeta(u), dz0, dy0, accumulate=acc)
+        else:
+            dA0 = self._empty(*y0.shape)
+            K.maxpool_bwd(dx_main, arg, dA0, dout2=shortcut_g)
+            K.bn_bwd(ws, y0, st0[0], st0[1], self.gamma(u), st0[2], st0[3], self.dgamma(u),
+                     self.dbeta(u), dy0, g1=dA0, accumulate=acc)
         K.conv_wgrad(dy0, x0, u.geom(Nb), self.stem_wgrad, ws)
         K.stem_s2d_grad(self.stem_wgrad, self.wgrad_view(u), accumulate=acc)
         if red is not None:

@@ -64,6 +64,7 @@ _SIGS = {
     "pda_maxpool_bwd": [_V, _V, _V, _V, _I, _I, _I, _I, _I, _I, _I, _V],
     "pda_tail_pool": [_V, _V, _V, _V, _V, _V, _V, _I, _I, _I, _I, _I, _V],
     "pda_bn_bwd_reduce": [C.POINTER(BwdArgs), _I, _I, _V],
+    "pda_stem_bwd_reduce": [_V, _V, _V, _V, _V, _V, _V, _V, _I, _I, _I, _I, _I, _I, _I, _I, _V],
     "pda_bn_bwd_finalize": [_V, _I, _I, _I, _I, _F, _V, _V, _V, _V, _V, _V, _V, _V, _F, _I, _V],
     "pda_bn_bwd_apply": [C.POINTER(BwdArgs), _V, _V, _V, _V, _V, _V, _I, _V],
     "pda_xent": [_V, _I, _I, _I, _V, _V, _V, _V, _I, _F, _V, _I, _I, _V],
@@ -96,7 +97,9 @@ def load(required: bool = False) -> Optional[C.CDLL]:
     try:
         lib = C.CDLL(str(LIBPATH))
         for name, argt in _SIGS.items():
-            fn = getattr(lib, name)
+            fn = getattr(lib, name, None)
+            if fn is None:   # an older A/B variant library (tools/build_variant.py)
+                continue
             fn.argtypes = argt
             fn.restype = C.c_int
         _LIB = lib

@@ -322,6 +322,21 @@ def tail_pool(y, scale, shift, out, res=None, y2=None, scale2=None, shift2=None)
     return out
 
 
+def stem_bwd_reduce(ws: "Workspace", dout, arg, y, scale, shift, dz_out, dout2=None):
+    """Stem backward, one pass: max-pool gradient gather (``dout`` [+ ``dout2``] through the argmax
+    bytes) -> ReLU mask of relu(bn(y)) -> ``dz_out`` -> BatchNorm-backward partial sums.
+    Returns (part, G, nq) for :func:`bn_bwd_finish`."""
+    N, H, W, C_ = y.shape
+    Ho, Wo = dout.shape[1], dout.shape[2]
+    G = _reduce_blocks(N * H * W, C_)
+    part = ws.get("bn_part", G * 2 * C_)
+    rc = ext.lib().pda_stem_bwd_reduce(ptr(dout), ptr(dout2), ptr(arg), ptr(y), ptr(scale), ptr(shift),
+                                       ptr(dz_out), ptr(part), G, N, H, W, C_, Ho, Wo, dt_of(y),
+                                       stream(y.device))
+    check(rc, "stem_bwd_reduce")
+    return part, G, 2
+
+
 def _reduce_blocks(rows: int, C_: int) -> int:
     tpr = min(C_ // 8, 256)
     rpi = 256 // tpr

@@ -245,6 +245,54 @@ def test_stem_pool_and_backward():
                                rtol=2e-2, atol=2e-1)
 
 
+@pytest.mark.parametrize("with_shortcut", [False, True])
+def test_stem_bwd_reduce_matches_unfused(with_shortcut):
+    """One-pass stem backward (maxpool gather + ReLU mask + BN-backward partials) == maxpool_bwd
+    followed by the standalone BN backward, and both == autograd of relu(bn(y)) -> maxpool."""
+    K = _k()
+    dtype = torch.bfloat16
+    N, H, C = 3, 14, 64
+    torch.manual_seed(7)
+    y = (torch.randn(N, H, H, C, device=DEV) + 0.2).to(dtype)
+    gamma = torch.rand(C, device=DEV) + 0.5
+    beta = torch.randn(C, device=DEV) * 0.1
+    m = y.float().mean((0, 1, 2))
+    v = y.float().var((0, 1, 2), unbiased=False)
+    inv = 1 / torch.sqrt(v + 1e-5)
+    sc, sh = gamma * inv, beta - m * gamma * inv
+    Ho = (H + 2 - 3) // 2 + 1
+    out = torch.empty(N, Ho, Ho, C, device=DEV, dtype=dtype)
+    arg = torch.empty(N, Ho, Ho, C, device=DEV, dtype=torch.uint8)
+    K.stem_pool(y, sc, sh, out, arg)
+    g = torch.randn(N, Ho, Ho, C, device=DEV).to(dtype)
+    g2 = torch.randn(N, Ho, Ho, C, device=DEV).to(dtype) if with_shortcut else None
+    ws = K.Workspace(DEV)
+    # unfused reference path
+    dA = torch.empty_like(y)
+    K.maxpool_bwd(g, arg, dA, dout2=g2)
+    dy_ref = torch.empty_like(y)
+    dg_ref, db_ref = torch.zeros(C, device=DEV), torch.zeros(C, device=DEV)
+    K.bn_bwd(ws, y, m, inv, gamma, sc, sh, dg_ref, db_ref, dy_ref, g1=dA)
+    # fused
+    dz = torch.empty_like(y)
+    part, G, nq = K.stem_bwd_reduce(ws, g, arg, y, sc, sh, dz, dout2=g2)
+    dy = torch.empty_like(y)
+    dg, db = torch.zeros(C, device=DEV), torch.zeros(C, device=DEV)
+    K.bn_bwd_finish(ws, part, G, nq, y, m, inv, gamma, dg, db, dz, dy)
+    torch.cuda.synchronize()
+    assert rel_err(dy, dy_ref) < 1e-2
+    assert rel_err(dg, dg_ref) < 1e-3 and rel_err(db, db_ref) < 1e-3
+    # autograd reference (BN batch statistics + ReLU + max-pool)
+    yr = y.float().requires_grad_(True)
+    gr, br = gamma.clone().requires_grad_(True), beta.clone().requires_grad_(True)
+    _, _, z = _bn_ref(yr, gr, br)
+    ref = F.max_pool2d(torch.relu(z).permute(0, 3, 1, 2), 3, 2, 1)
+    gsum = g.float() + (g2.float() if g2 is not None else 0)
+    ref.backward(gsum.permute(0, 3, 1, 2))
+    assert rel_err(db, br.grad) < 2e-2
+    assert rel_err(dg, gr.grad) < 2e-2
+
+
 def test_tail_pool():
     K = _k()
     dtype = torch.bfloat16
