@@ -456,33 +456,44 @@ __global__ __launch_bounds__(NT) void stem_bwd_reduce_kernel(
       for (long long row = r0 + rsub; row < r1; row += rpi) {
         const uint32_t p2 = fdiv((uint32_t)row, dW), x = (uint32_t)row - p2 * W;
         const uint32_t n = fdiv(p2, dH), yy = p2 - n * H;
-        float g[8];
+        // the (up to) 2x2 pooling windows covering (yy, x): yo in {yy/2, yy/2 + (yy odd)}, same for
+        // x. All four loads are issued unconditionally from clamped (valid) addresses so they
+        // overlap; a window that does not exist gets the impossible argmax id 9 (no match).
+        const int yo0 = (int)yy >> 1, xo0 = (int)x >> 1;
+        const int yo1 = ((yy & 1) && yo0 + 1 < Ho) ? yo0 + 1 : yo0;
+        const int xo1 = ((x & 1) && xo0 + 1 < Wo) ? xo0 + 1 : xo0;
+        i32x4 dv[4], dv2[4];
+        uint64_t am[4];
+        int me[4];
 #pragma unroll
-        for (int e = 0; e < 8; ++e) g[e] = 0.f;
-        for (int yo = (int)yy / 2; yo <= min(Ho - 1, ((int)yy + 1) / 2); ++yo) {
-          const int dy = (int)yy - (yo * 2 - 1);
-          if (dy < 0 || dy > 2) continue;
-          for (int xo = (int)x / 2; xo <= min(Wo - 1, ((int)x + 1) / 2); ++xo) {
-            const int dx = (int)x - (xo * 2 - 1);
-            if (dx < 0 || dx > 2) continue;
-            const uint32_t o = (n * Ho + yo) * Wo + xo;
-            const uint64_t am = reinterpret_cast<const uint64_t*>(arg)[o * CK + cc];
-            float d[8];
-            unpack8<DT>(*reinterpret_cast<const i32x4*>(dout + (size_t)o * C + c0), d);
-            if (dout2) {
-              float d2[8];
-              unpack8<DT>(*reinterpret_cast<const i32x4*>(dout2 + (size_t)o * C + c0), d2);
-#pragma unroll
-              for (int e = 0; e < 8; ++e) d[e] += d2[e];
-            }
-            const int me = dy * 3 + dx;
-#pragma unroll
-            for (int e = 0; e < 8; ++e)
-              if ((int)((am >> (8 * e)) & 0xff) == me) g[e] += d[e];
-          }
+        for (int w = 0; w < 4; ++w) {
+          const int yo = (w & 2) ? yo1 : yo0, xo = (w & 1) ? xo1 : xo0;
+          const bool live = ((w & 2) == 0 || yo1 != yo0) && ((w & 1) == 0 || xo1 != xo0);
+          const uint32_t o = (n * Ho + yo) * Wo + xo;
+          am[w] = reinterpret_cast<const uint64_t*>(arg)[o * CK + cc];
+          dv[w] = *reinterpret_cast<const i32x4*>(dout + (size_t)o * C + c0);
+          if (dout2) dv2[w] = *reinterpret_cast<const i32x4*>(dout2 + (size_t)o * C + c0);
+          me[w] = live ? ((int)yy - (yo * 2 - 1)) * 3 + ((int)x - (xo * 2 - 1)) : 9;
         }
         float yv[8];
         unpack8<DT>(*reinterpret_cast<const i32x4*>(y + row * C + c0), yv);
+        float g[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) g[e] = 0.f;
+#pragma unroll
+        for (int w = 0; w < 4; ++w) {
+          float d[8];
+          unpack8<DT>(dv[w], d);
+          if (dout2) {
+            float d2[8];
+            unpack8<DT>(dv2[w], d2);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) d[e] += d2[e];
+          }
+#pragma unroll
+          for (int e = 0; e < 8; ++e)
+            if ((int)((am[w] >> (8 * e)) & 0xff) == me[w]) g[e] += d[e];
+        }
 #pragma unroll
         for (int e = 0; e < 8; ++e) g[e] = yv[e] * s[e] + h[e] > 0.f ? g[e] : 0.f;
         // statistics of the stored (rounded) dz, as the apply kernel re-reads it

@@ -328,7 +328,7 @@ def stem_bwd_reduce(ws: "Workspace", dout, arg, y, scale, shift, dz_out, dout2=N
     Returns (part, G, nq) for :func:`bn_bwd_finish`."""
     N, H, W, C_ = y.shape
     Ho, Wo = dout.shape[1], dout.shape[2]
-    G = _reduce_blocks(N * H * W, C_)
+    G = max(1, min(4096, (N * H * W) // 512))   # gather-latency bound: more blocks than a plain reduce
     part = ws.get("bn_part", G * 2 * C_)
     rc = ext.lib().pda_stem_bwd_reduce(ptr(dout), ptr(dout2), ptr(arg), ptr(y), ptr(scale), ptr(shift),
                                        ptr(dz_out), ptr(part), G, N, H, W, C_, Ho, Wo, dt_of(y),
