@@ -123,6 +123,13 @@ class NativeResNet(nn.Module):
         import os
         self.fuse_prologue = os.environ.get("PDA_FUSE_PROLOGUE", "1") != "0"
         self.fused_stem_bwd = os.environ.get("PDA_FUSED_STEM_BWD", "1") != "0"
+        # weight gradients on a second HIP stream: nothing in the backward chain consumes them, so
+        # the (compute-bound) wgrad GEMMs fill the CUs left idle by the (HBM-bound) BN-backward
+        # passes and small finalize launches of the dgrad chain on the main stream
+        self._side = (torch.cuda.Stream(device) if os.environ.get("PDA_WGRAD_STREAM", "1") != "0"
+                      else None)
+        self.ws_w = Workspace(device) if self._side is not None else self.ws
+        self._keep: List[torch.Tensor] = []
         self.refresh_shadow()
 
     # ------------------------------------------------------------------ planning
@@ -468,6 +475,29 @@ class NativeResNet(nn.Module):
         return logits
 
     # ------------------------------------------------------------------ backward
+    def _wgrad(self, fn: Callable, *keep: torch.Tensor) -> None:
+        """Enqueue ``fn(workspace)`` (weight-gradient kernels) on the wgrad stream, ordered after
+        everything queued so far on the main stream. Tensors the side stream reads are kept alive
+        until the end-of-backward join, so the caching allocator cannot hand their memory to a
+        main-stream allocation while the side stream may still be reading it."""
+        if self._side is None:
+            fn(self.ws)
+            return
+        self._side.wait_stream(torch.cuda.current_stream(self.device))
+        with torch.cuda.stream(self._side):
+            fn(self.ws_w)
+        self._keep.extend(keep)
+
+    def _grads_ready(self, red, upto: int) -> None:
+        """DDP bucket readiness: the bucket's BN grads come from the main stream, its conv weight
+        grads from the wgrad stream -- launch the all-reduce after both."""
+        if self._side is None:
+            red.grads_ready(upto)
+            return
+        self._side.wait_stream(torch.cuda.current_stream(self.device))
+        with torch.cuda.stream(self._side):
+            red.grads_ready(upto)
+
     def native_backward(self, dlog16: torch.Tensor) -> None:
         """dlog16: [B, fc_rows] 16-bit d(loss)/d(logits) (zero padded).
 
@@ -490,15 +520,18 @@ class NativeResNet(nn.Module):
         Nb = dlog16.shape[0]
         ws = self.ws
         # ---- fc
-        K.col_sum(dlog16, self.num_classes, self.flat_grad[self.fc_b_off:self.fc_b_off + self.num_classes],
-                  accumulate=acc)
         gfc = ConvGeom(Nb, 1, 1, self.feat_dim, self.fc_rows, 1, 1, 1, 0)
-        K.conv_wgrad(dlog16, sv["feat"], gfc, self.fc_wgrad_full, ws, accumulate=acc)
+
+        def fc_wgrad(w):
+            K.col_sum(dlog16, self.num_classes,
+                      self.flat_grad[self.fc_b_off:self.fc_b_off + self.num_classes], accumulate=acc)
+            K.conv_wgrad(dlog16, sv["feat"], gfc, self.fc_wgrad_full, w, accumulate=acc)
+        self._wgrad(fc_wgrad, dlog16, sv["feat"])
         dfeat = self._empty(Nb, 1, 1, self.feat_dim)
         fc_w_ohwi = self.fc_w16.view(self.fc_rows, 1, 1, self.feat_dim)
         K.conv_dgrad(dlog16.view(Nb, 1, 1, self.fc_rows), fc_w_ohwi, gfc, dfeat)
         if red is not None:
-            red.grads_ready(self.block_bounds[0])
+            self._grads_ready(red, self.block_bounds[0])
         # ---- last block's tail: standalone reduction of the pooled gradient
         nblk = len(self.blocks)
         b = self.blocks[-1]
@@ -511,7 +544,7 @@ class NativeResNet(nn.Module):
             prev = (self.blocks[bi - 1], sv["blocks"][bi - 1]) if bi > 0 else None
             dx_main, shortcut_g, tail = self._block_backward(b, rec, tail, prev, acc)
             if red is not None:
-                red.grads_ready(self.block_bounds[nblk - bi])
+                self._grads_ready(red, self.block_bounds[nblk - bi])
         # ---- stem: maxpool backward of (main + shortcut) gradients, BN backward, wgrad
         x0, y0, arg = sv["x0"], sv["y0"], sv["arg"]
         st0 = sv["stem_stats"]
@@ -528,8 +561,15 @@ class NativeResNet(nn.Module):
             K.maxpool_bwd(dx_main, arg, dA0, dout2=shortcut_g)
             K.bn_bwd(ws, y0, st0[0], st0[1], self.gamma(u), st0[2], st0[3], self.dgamma(u),
                      self.dbeta(u), dy0, g1=dA0, accumulate=acc)
-        K.conv_wgrad(dy0, x0, u.geom(Nb), self.stem_wgrad, ws)
-        K.stem_s2d_grad(self.stem_wgrad, self.wgrad_view(u), accumulate=acc)
+        g0 = u.geom(Nb)
+
+        def stem_wgrad(w):
+            K.conv_wgrad(dy0, x0, g0, self.stem_wgrad, w)
+            K.stem_s2d_grad(self.stem_wgrad, self.wgrad_view(u), accumulate=acc)
+        self._wgrad(stem_wgrad, dy0, x0)
+        if self._side is not None:   # join: the optimizer step reads every gradient
+            torch.cuda.current_stream(self.device).wait_stream(self._side)
+            self._keep.clear()
         if red is not None:
             red.grads_ready(self.block_bounds[-1])
             red.finish()
@@ -586,7 +626,8 @@ class NativeResNet(nn.Module):
                             dy2_out=dyd, accumulate=acc)
             # shortcut branch first: its dX is the second gradient source of the previous tail
             g = b.ds.geom(Nb)
-            K.conv_wgrad(dyd, x, g, self.wgrad_view(b.ds), ws, accumulate=acc)
+            self._wgrad(lambda w, u=b.ds, g=g, dyd=dyd: K.conv_wgrad(dyd, x, g, self.wgrad_view(u), w,
+                                                                    accumulate=acc), dyd, x)
             shortcut_g = self._empty(*x.shape)
             K.conv_dgrad(dyd, self.w16_ohwi(b.ds), g, shortcut_g)
         else:
@@ -601,11 +642,13 @@ class NativeResNet(nn.Module):
             g = u.geom(Nb)
             if a_in is None:   # fused prologue: recompute relu(bn(y_{j-1})) while staging B
                 sp_ = rec[f"s{j - 1}"]
-                K.conv_wgrad(dy, ys[j - 1], g, self.wgrad_view(u), ws, accumulate=acc,
-                             pro=(sp_[2], sp_[3]))
                 a_in = ys[j - 1]
+                self._wgrad(lambda w, u=u, g=g, dy=dy, a=a_in, pro=(sp_[2], sp_[3]):
+                            K.conv_wgrad(dy, a, g, self.wgrad_view(u), w, accumulate=acc, pro=pro),
+                            dy, a_in)
             else:
-                K.conv_wgrad(dy, a_in, g, self.wgrad_view(u), ws, accumulate=acc)
+                self._wgrad(lambda w, u=u, g=g, dy=dy, a=a_in:
+                            K.conv_wgrad(dy, a, g, self.wgrad_view(u), w, accumulate=acc), dy, a_in)
             out = self._empty(*a_in.shape)
             if j > 0:
                 up = b.units[j - 1]

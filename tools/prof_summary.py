@@ -49,6 +49,25 @@ def main():
     print("|---|---|---|---|")
     for f, t in sorted(tot.items(), key=lambda kv: -kv[1]):
         print(f"| {f} | {t / steps:.3f} | {100 * t / all_ms:.1f} | {cnt[f] / steps:.1f} |")
+    # device occupancy over the trace's last `steps` steps' window: union of kernel intervals
+    # (kernels of the main and wgrad streams overlap) vs the wall span, and the idle gaps
+    iv = sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"])) for r in rows)
+    n_keep = int(len(iv) * steps / max(steps, 1))
+    iv = iv[len(iv) - n_keep:]
+    busy, gaps, cur_s, cur_e = 0, [], iv[0][0], iv[0][1]
+    for s_, e_ in iv[1:]:
+        if s_ > cur_e:
+            busy += cur_e - cur_s
+            gaps.append(s_ - cur_e)
+            cur_s, cur_e = s_, e_
+        else:
+            cur_e = max(cur_e, e_)
+    busy += cur_e - cur_s
+    span = iv[-1][1] - iv[0][0]
+    print(f"\nwall span {span / 1e6 / steps:.2f} ms/step, device busy (union) {busy / 1e6 / steps:.2f} "
+          f"ms/step, idle {100 * (1 - busy / span):.1f} % in {len(gaps)} gaps "
+          f"(largest {max(gaps or [0]) / 1e3:.1f} us); kernel-time sum / busy = {all_ms * 1e6 / busy:.2f}x "
+          f"(stream concurrency)")
 
 
 if __name__ == "__main__":
