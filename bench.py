@@ -22,7 +22,8 @@ import time
 
 import torch
 
-BASELINE = {1: 717.0, 8: 5546.7}   # BASELINE.md derived images/sec (other hardware)
+BASELINE = {1: 717.0, 8: 5546.7}
+GRAPH_DEFAULT = os.environ.get("PDA_GRAPH", "0") == "1"   # BASELINE.md derived images/sec (other hardware)
 
 
 def parse():
@@ -37,6 +38,8 @@ def parse():
     ap.add_argument("--bucket-mb", type=float, default=32.0)
     ap.add_argument("--image-size", type=int, default=224)
     ap.add_argument("--profile-steps", type=int, default=0)
+    ap.add_argument("--graph", type=int, default=-1,
+                    help="capture the step in a HIP graph (1/0; default: on for 1 GPU, native engine)")
     return ap.parse_args()
 
 
@@ -62,8 +65,10 @@ def main():
     sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
     from pytorch_distributed_amd.bench_step import make_trainer
     dtype = {"bf16": torch.bfloat16, "fp16": torch.float16, "fp32": torch.float32}[args.dtype]
+    graph = args.graph == 1 or (args.graph < 0 and world == 1 and GRAPH_DEFAULT)
     tr = make_trainer(args.arch, args.batch, dtype, device, engine=args.engine,
-                      world=world, rank=rank, bucket_mb=args.bucket_mb, image_size=args.image_size)
+                      world=world, rank=rank, bucket_mb=args.bucket_mb, image_size=args.image_size,
+                      graph=graph)
 
     for i in range(args.warmup):
         tr.step(i)
@@ -107,6 +112,7 @@ def main():
             "config": {"model": args.arch, "global_batch": args.batch * world,
                        "per_gpu_batch": args.batch, "seq_len": None,
                        "parallelism": f"dp{world}", "engine": tr.engine,
+                       "hip_graph": bool(getattr(tr, "graphed", None)),
                        "optimizer": "SGD(lr=0.1, momentum=0.9, wd=1e-4)"},
             "loss": loss,
             "max_mem_gb": round(torch.cuda.max_memory_allocated(device) / 1e9, 2),

@@ -57,12 +57,12 @@ class _TorchTrainer:
 
 def make_trainer(arch: str, batch: int, dtype: torch.dtype, device: torch.device,
                  engine: str = "auto", world: int = 1, rank: int = 0, bucket_mb: float = 32.0,
-                 image_size: int = 224):
+                 image_size: int = 224, graph: bool = False):
     if engine in ("auto", "native"):
         from .models import native
         if native.supports(arch, dtype):
             return native.NativeTrainer(arch, batch, dtype, device, world, rank, bucket_mb,
-                                        image_size)
+                                        image_size, graph=graph)
         if engine == "native":
             raise RuntimeError(f"native engine unavailable for {arch}/{dtype}")
     return _TorchTrainer(arch, batch, dtype, device, world, rank, bucket_mb, image_size)

@@ -842,7 +842,8 @@ class NativeSGD(torch.optim.Optimizer):
 class NativeTrainer:
     engine = "native"
 
-    def __init__(self, arch, batch, dtype, device, world=1, rank=0, bucket_mb=32.0, image_size=224):
+    def __init__(self, arch, batch, dtype, device, world=1, rank=0, bucket_mb=32.0, image_size=224,
+                 graph: bool = False):
         from .resnet import build_model
         from ..data.synthetic import SyntheticImageNet
         torch.manual_seed(0)
@@ -862,8 +863,20 @@ class NativeTrainer:
             from ..amp import LossScaler
             self.scaler = LossScaler()
         self._loss = None
+        self.graphed = None
+        if graph:
+            if world > 1:
+                raise ValueError("graph capture of the distributed step is not enabled (RCCL "
+                                 "collectives stay eager); use graph=False with world > 1")
+            from ..runtime.graphs import GraphedNativeStep
+            self.graphed = GraphedNativeStep(self.model, self.opt, self.gen, batch, self.scaler,
+                                             device)
 
     def step(self, i: int) -> None:
+        if self.graphed is not None:
+            self.graphed.run((i * self.world + self.rank) * self.batch)
+            self._loss = self.graphed.loss
+            return
         ids = torch.arange(self.batch, dtype=torch.int64) + (i * self.world + self.rank) * self.batch
         x, y = self.gen(ids)
         out = self.net(x)

@@ -1,0 +1,107 @@
+"""HIP-graph capture of one full native training step.
+
+The reference's step is ~500 autograd-recorded ATen/cuDNN launches issued from Python every
+iteration. The native engine already collapses the network into one explicit
+schedule of our gfx950 kernels (``models/native.py``); this module goes one step further and
+records that whole schedule -- on-device batch generation, forward, fused loss+gradient,
+backward (main stream + the weight-gradient stream, forked and joined with events), fused SGD,
+AMP loss-scale update -- into ONE HIP graph, replayed with a single launch per step:
+
+* the host cost per step drops from ~600 kernel launches (ctypes + allocator + Python) to one
+  ``hipGraphLaunch`` plus a 1-element fill (the batch's first sample id); this is what keeps a
+  single-process multi-GPU driver (DataParallel) and small per-GPU batches from being
+  launch-bound, and removes inter-launch gaps on the device;
+* every buffer the step touches has a fixed address (workspaces are grown by the eager step
+  that precedes capture; activations come from the graph's private memory pool);
+* values that change between steps are device-resident (sample-id offset, AMP loss scale, found-inf
+  flag) -- the only host-side hyper-parameter baked into the graph, the learning rate, triggers
+  a re-capture when the LR scheduler changes it.
+
+Used by :class:`~pytorch_distributed_amd.models.native.NativeTrainer` (``bench.py --graph``) and the
+entrypoints (``MX_GRAPH=1``).
+"""
+from __future__ import annotations
+
+from typing import Callable, Optional
+
+import torch
+
+from ..ops import native_ops as K
+
+__all__ = ["GraphedNativeStep", "native_train_step"]
+
+
+def native_train_step(model, opt, x: torch.Tensor, y: torch.Tensor, scaler=None) -> torch.Tensor:
+    """forward -> CE loss + d(loss)/d(logits) in one kernel -> native backward -> fused SGD, with no
+    autograd bookkeeping (the same kernel sequence as ``loss.backward(); opt.step()`` through the
+    module's autograd node). Returns the (unscaled) mean loss as a device scalar."""
+    B = x.shape[0]
+    logits = model.native_forward(x, train=True, save=True)
+    loss = torch.empty((), dtype=torch.float32, device=logits.device)
+    rows = torch.empty(B, dtype=torch.float32, device=logits.device)
+    dlog16 = torch.empty(B, model.fc_rows, dtype=model.dtype, device=logits.device)
+    gdev = None
+    if scaler is not None and scaler.enabled:
+        scaler._lazy_init(logits.device)
+        gdev = scaler.scale_tensor          # d(scale * loss) / d(loss), device-resident
+    K.xent(logits, y, rows, loss, dlog=dlog16, gscale=1.0 / B, gdev=gdev)
+    model.native_backward(dlog16)
+    if gdev is not None:
+        opt.step_amp(scaler.scale_tensor, scaler.found_inf)     # unscale + inf check + skip on device
+        torch._amp_update_scale_(scaler.scale_tensor, scaler._growth_tracker, scaler.found_inf,
+                                 scaler.growth_factor, scaler.backoff_factor, scaler.growth_interval)
+    else:
+        opt.step()
+    opt.zero_grad()
+    return loss
+
+
+class GraphedNativeStep:
+    """Capture-once / replay-per-step driver of :func:`native_train_step`.
+
+    ``gen(ids) -> (x, y)`` is the on-device batch generator; the batch's sample ids are
+    ``first_id + arange(batch)`` with ``first_id`` held in a device scalar, so one graph serves
+    every step. The first :meth:`run` executes the step eagerly (on a side stream, which also
+    grows every workspace to its final size) and then captures it; later calls replay.
+    """
+
+    def __init__(self, model, opt, gen: Callable, batch: int, scaler=None,
+                 device: Optional[torch.device] = None) -> None:
+        self.model, self.opt, self.gen, self.batch, self.scaler = model, opt, gen, batch, scaler
+        self.device = torch.device(device) if device is not None else model.device
+        self.ids_base = torch.arange(batch, dtype=torch.int64, device=self.device)
+        self.ids_off = torch.zeros(1, dtype=torch.int64, device=self.device)
+        self.graph: Optional[torch.cuda.CUDAGraph] = None
+        self.loss: Optional[torch.Tensor] = None
+        self._lr = None
+        self.captures = 0
+
+    def _body(self) -> None:
+        x, y = self.gen(self.ids_base + self.ids_off)
+        self.loss = native_train_step(self.model, self.opt, x, y, self.scaler)
+
+    def run(self, first_id: int) -> None:
+        self.ids_off.fill_(int(first_id))
+        lr = self.opt.param_groups[0]["lr"]
+        if self.graph is not None and lr == self._lr:
+            self.graph.replay()
+            self.loss = self._graph_loss
+            return
+        # eager step (the real step for this batch), off the default stream as graph capture
+        # requires, then record the identical schedule
+        cur = torch.cuda.current_stream(self.device)
+        side = torch.cuda.Stream(self.device)
+        side.wait_stream(cur)
+        with torch.cuda.stream(side):
+            self._body()
+        cur.wait_stream(side)
+        eager_loss = self.loss
+        self.graph = None
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            self._body()
+        self.graph = g
+        self._graph_loss = self.loss      # written by each replay
+        self.loss = eager_loss            # this step's value (the capture executed nothing)
+        self._lr = lr
+        self.captures += 1

@@ -113,7 +113,9 @@ def train(dataloader, model, criterion, optimizer, scheduler, epoch: int, ctx: C
             print("epoch: {}, step: {}".format(epoch, step), flush=True)
         samples = samples.to(ctx.device, non_blocking=True)
         labels = labels.to(ctx.device, non_blocking=True)
-        if scaler is not None and scaler.enabled:
+        if getattr(model, "graph_step_ok", None) is not None and model.graph_step_ok(scaler):
+            loss = model.train_step(samples, labels, optimizer)     # DP: HIP-graph replay per GPU
+        elif scaler is not None and scaler.enabled:
             with _autocast(ctx):
                 outputs = model(samples)
                 loss = criterion(outputs, labels)

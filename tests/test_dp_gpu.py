@@ -41,3 +41,47 @@ def test_native_dataparallel_matches_single_model():
     opt_dp.step()
     torch.cuda.synchronize()
     assert torch.equal(dp.module.flat_params, dp.replicas[0].flat_params)
+
+
+def test_native_dataparallel_graph_step_matches_eager():
+    """train_step replayed from per-replica HIP graphs == the same schedule launched eagerly (bit
+    for bit, 4 steps incl. SGD), and its first step == crit(dp(x), y).backward() (autograd DP with
+    ATen's cross-entropy: equal up to the 16-bit rounding of dlogits)."""
+    from pytorch_distributed_amd.data import SyntheticImageNet
+    from pytorch_distributed_amd.models import build_model
+    from pytorch_distributed_amd.models.native import NativeResNet
+    from pytorch_distributed_amd.parallel import DataParallel
+    torch.manual_seed(0)
+    sd = build_model("resnet18").state_dict()
+    dps = []
+    for _ in range(3):
+        r = build_model("resnet18")
+        r.load_state_dict(sd)
+        dps.append(DataParallel(NativeResNet(r, device=DEV, image_size=64), device_ids=[0, 0]))
+    auto, eager, graphed = dps
+    assert graphed.graph_step_ok()
+    gen = eager.module.input_generator(SyntheticImageNet("train", image_size=64))
+    x, y = gen(torch.arange(16))
+    crit = torch.nn.CrossEntropyLoss()
+    oa = auto.make_optimizer(lr=0.05, momentum=0.9, weight_decay=1e-4)
+    oa.zero_grad()
+    la = crit(auto(x), y)
+    la.backward()
+    oe = eager.make_optimizer(lr=0.05, momentum=0.9, weight_decay=1e-4)
+    og = graphed.make_optimizer(lr=0.05, momentum=0.9, weight_decay=1e-4)
+    for step in range(4):
+        x, y = gen(torch.arange(16) + 16 * step)
+        le = eager.train_step(x, y, oe, graph=False)
+        lg = graphed.train_step(x, y, og)
+        torch.cuda.synchronize()
+        if step == 0:
+            assert abs(la.item() - lg.item()) < 1e-4 * abs(la.item())
+            err = ((auto.module.flat_grad - graphed.module.flat_grad).norm()
+                   / auto.module.flat_grad.norm()).item()
+            assert err < 2e-2, err
+        assert le.item() == lg.item(), (step, le.item(), lg.item())
+        assert torch.equal(eager.module.flat_grad, graphed.module.flat_grad), step
+        assert torch.equal(eager.module.flat_params, graphed.module.flat_params), step
+        assert torch.equal(graphed.module.flat_params, graphed.replicas[0].flat_params)
+        assert torch.equal(eager.module.flat_buffers, graphed.module.flat_buffers)
+    assert graphed._graphs[0].graph is not None and eager._graphs[0].graph is None
