@@ -129,6 +129,10 @@ class NativeResNet(nn.Module):
         self._side = (torch.cuda.Stream(device) if os.environ.get("PDA_WGRAD_STREAM", "1") != "0"
                       else None)
         self.ws_w = Workspace(device) if self._side is not None else self.ws
+        # optionally run the dgrad/BN-backward chain (the critical path) on a high-priority stream
+        self._chain = (torch.cuda.Stream(device, priority=-1)
+                       if self._side is not None and os.environ.get("PDA_CHAIN_PRIO", "0") == "1"
+                       else None)
         self._keep: List[torch.Tensor] = []
         self.refresh_shadow()
 
@@ -499,6 +503,16 @@ class NativeResNet(nn.Module):
             red.grads_ready(upto)
 
     def native_backward(self, dlog16: torch.Tensor) -> None:
+        if self._chain is None:
+            return self._native_backward(dlog16)
+        cur = torch.cuda.current_stream(self.device)
+        self._chain.wait_stream(cur)
+        with torch.cuda.stream(self._chain):
+            self._native_backward(dlog16)
+        cur.wait_stream(self._chain)
+        dlog16.record_stream(self._chain)
+
+    def _native_backward(self, dlog16: torch.Tensor) -> None:
         """dlog16: [B, fc_rows] 16-bit d(loss)/d(logits) (zero padded).
 
         Schedule per bottleneck block (last to first): finish the tail BN backward (its reduction

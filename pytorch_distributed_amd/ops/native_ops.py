@@ -81,6 +81,8 @@ _WGRAD_TARGET = int(os.environ.get("PDA_WGRAD_TARGET", 2 * _NUM_CU))
 
 
 _SINGLE_STAGE = os.environ.get("PDA_SINGLE_STAGE", "1") != "0"
+# scale on the split-K block targets (the wgrads run beside the dgrad chain on a second stream)
+_WGRAD_TB_SCALE = float(os.environ.get("PDA_WGRAD_TB_SCALE", "1.0"))
 
 
 def pick_tile(M: int, N: int, K: Optional[int] = None) -> Tuple[int, int]:
@@ -214,6 +216,7 @@ def wgrad_plan(g: ConvGeom, Nb: int, tile: Optional[Tuple[int, int]] = None,
         target_blocks = target_blocks or tb
     if target_blocks is None:
         target_blocks = _WGRAD_TARGET
+    target_blocks = max(1, int(target_blocks * _WGRAD_TB_SCALE))
     if tile:
         bm, bn = tile
     tiles = math.ceil(M / abs(bm)) * math.ceil(N / bn)

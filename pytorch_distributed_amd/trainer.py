@@ -163,10 +163,15 @@ def validate(dataloader, model, criterion, epoch: int, ctx: Context) -> float:
             labels = labels.to(ctx.device, non_blocking=True)
             outputs = model(samples).float()
             stats[0] += criterion(outputs, labels)
-            _, preds = outputs.topk(5, -1, True, True)
-            hit = torch.eq(preds, labels.unsqueeze(1))
-            stats[1] += hit[:, :1].sum()
-            stats[2] += hit.sum()
+            if ctx.engine == "native" and outputs.is_cuda:
+                from .ops import native_ops as K
+                # one HIP kernel: label rank per row -> top-1 / top-5 hit counters (K11)
+                K.topk_hits(outputs.contiguous(), labels, stats[1:3])
+            else:
+                _, preds = outputs.topk(5, -1, True, True)
+                hit = torch.eq(preds, labels.unsqueeze(1))
+                stats[1] += hit[:, :1].sum()
+                stats[2] += hit.sum()
             stats[3] += samples.size(0)
     if ctx.distributed:
         import torch.distributed as dist
