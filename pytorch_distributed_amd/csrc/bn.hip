@@ -1,4 +1,5 @@
-// BatchNorm (+ReLU, +residual, +pool) kernels for gfx950, NHWC 16-bit activations, f32 statistics.
+// BatchNorm (+ReLU, +residual, +pool) kernels for gfx950, NHWC bf16/f16 (or exact-f32) activations,
+// f32 statistics.
 //
 // Replaces cuDNN BatchNorm train fwd/bwd + ATen ReLU/threshold_backward/add/max_pool2d/avg_pool2d
 // of the reference stack. Statistics are computed from the conv
@@ -20,20 +21,6 @@ namespace {
 
 constexpr int NT = 256;
 
-template <int DT>
-__device__ __forceinline__ void unpack8(const i32x4& v, float* f) {
-  const u16* h = reinterpret_cast<const u16*>(&v);
-#pragma unroll
-  for (int e = 0; e < 8; ++e) f[e] = ld16<DT>(h[e]);
-}
-template <int DT>
-__device__ __forceinline__ i32x4 pack8(const float* f) {
-  i32x4 v;
-  u16* h = reinterpret_cast<u16*>(&v);
-#pragma unroll
-  for (int e = 0; e < 8; ++e) h[e] = st16<DT>(f[e]);
-  return v;
-}
 __device__ __forceinline__ void ld8f(const float* p, float* f) {
   const f32x4 a = *reinterpret_cast<const f32x4*>(p);
   const f32x4 b = *reinterpret_cast<const f32x4*>(p + 4);
@@ -140,9 +127,9 @@ __device__ __forceinline__ void ld8p(const float* p, f32x2* f) {
 // so the per-channel coefficients are loaded once, and the math runs on packed pairs.
 template <int DT>
 __global__ __launch_bounds__(NT) void bn_apply_kernel(
-    const u16* __restrict__ y, const float* __restrict__ sc, const float* __restrict__ sh,
-    const u16* __restrict__ r2, const float* __restrict__ sc2, const float* __restrict__ sh2,
-    u16* __restrict__ out, int n8, int C, int mode, int relu) {
+    const void* __restrict__ y, const float* __restrict__ sc, const float* __restrict__ sh,
+    const void* __restrict__ r2, const float* __restrict__ sc2, const float* __restrict__ sh2,
+    void* __restrict__ out, int n8, int C, int mode, int relu) {
   const int C8 = C >> 3;
   const int stride = gridDim.x * NT;
   const bool fixed = (stride % C8) == 0;
@@ -159,6 +146,19 @@ __global__ __launch_bounds__(NT) void bn_apply_kernel(
         ld8p<DT>(sh2 + c0, b2);
       }
       cprev = c0;
+    }
+    if constexpr (DT == DT_F32) {
+      float yv[8], rv[8], o[8];
+      load8<DT>(y, (size_t)i * 8, yv);
+      if (mode) load8<DT>(r2, (size_t)i * 8, rv);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        float v = yv[e] * a[e >> 1][e & 1] + b[e >> 1][e & 1];
+        if (mode) v += mode == 2 ? rv[e] * a2[e >> 1][e & 1] + b2[e >> 1][e & 1] : rv[e];
+        o[e] = relu ? fmaxf(v, 0.f) : v;
+      }
+      store8<DT>(out, (size_t)i * 8, o);
+      continue;
     }
     const i32x4 yv = reinterpret_cast<const i32x4*>(y)[i];
     i32x4 rv = {0, 0, 0, 0};
@@ -182,10 +182,10 @@ __global__ __launch_bounds__(NT) void bn_apply_kernel(
 // ------------------------------------------------------------------ stem: bn + relu + maxpool 3x3/2/1
 // y: [N,H,W,C], out: [N,Ho,Wo,C], arg: [N,Ho,Wo,C] uint8 window index (0..8)
 template <int DT>
-__global__ __launch_bounds__(NT) void stem_pool_kernel(const u16* __restrict__ y,
+__global__ __launch_bounds__(NT) void stem_pool_kernel(const void* __restrict__ y,
                                                        const float* __restrict__ sc,
                                                        const float* __restrict__ sh,
-                                                       u16* __restrict__ out,
+                                                       void* __restrict__ out,
                                                        uint8_t* __restrict__ arg, int N, int H,
                                                        int W, int C, int Ho, int Wo, FastDiv dCK,
                                                        FastDiv dWo, FastDiv dHo) {
@@ -208,7 +208,7 @@ __global__ __launch_bounds__(NT) void stem_pool_kernel(const u16* __restrict__ y
         const int xx = xo * 2 - 1 + dx;
         if ((unsigned)xx >= (unsigned)W) continue;
         float v[8];
-        unpack8<DT>(*reinterpret_cast<const i32x4*>(y + ((n * H + yy) * W + xx) * C + ck * 8), v);
+        load8<DT>(y, ((n * H + yy) * W + xx) * C + ck * 8, v);
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
           const float r = fmaxf(v[e] * a[e] + b[e], 0.f);
@@ -216,7 +216,7 @@ __global__ __launch_bounds__(NT) void stem_pool_kernel(const u16* __restrict__ y
         }
       }
     }
-    reinterpret_cast<i32x4*>(out)[i] = pack8<DT>(best);
+    store8<DT>(out, (size_t)i * 8, best);
     uint64_t packed = 0;
 #pragma unroll
     for (int e = 0; e < 8; ++e) packed |= (uint64_t)bi[e] << (8 * e);
@@ -226,10 +226,10 @@ __global__ __launch_bounds__(NT) void stem_pool_kernel(const u16* __restrict__ y
 
 // gradient of relu(bn(y)) through the max-pool: dA[n,y,x,c] = sum over windows whose argmax is here
 template <int DT>
-__global__ __launch_bounds__(NT) void maxpool_bwd_kernel(const u16* __restrict__ dout,
-                                                         const u16* __restrict__ dout2,
+__global__ __launch_bounds__(NT) void maxpool_bwd_kernel(const void* __restrict__ dout,
+                                                         const void* __restrict__ dout2,
                                                          const uint8_t* __restrict__ arg,
-                                                         u16* __restrict__ din, int N, int H, int W,
+                                                         void* __restrict__ din, int N, int H, int W,
                                                          int C, int Ho, int Wo, FastDiv dCK,
                                                          FastDiv dW, FastDiv dH) {
   const int CK = C / 8;
@@ -251,10 +251,10 @@ __global__ __launch_bounds__(NT) void maxpool_bwd_kernel(const u16* __restrict__
         const uint32_t o = (n * Ho + yo) * Wo + xo;
         const uint64_t a = reinterpret_cast<const uint64_t*>(arg)[o * CK + ck];
         float d[8];
-        unpack8<DT>(*reinterpret_cast<const i32x4*>(dout + o * C + ck * 8), d);
+        load8<DT>(dout, o * C + ck * 8, d);
         if (dout2) {
           float d2[8];
-          unpack8<DT>(*reinterpret_cast<const i32x4*>(dout2 + o * C + ck * 8), d2);
+          load8<DT>(dout2, o * C + ck * 8, d2);
 #pragma unroll
           for (int e = 0; e < 8; ++e) d[e] += d2[e];
         }
@@ -264,20 +264,20 @@ __global__ __launch_bounds__(NT) void maxpool_bwd_kernel(const u16* __restrict__
           if ((int)((a >> (8 * e)) & 0xff) == me) g[e] += d[e];
       }
     }
-    reinterpret_cast<i32x4*>(din)[i] = pack8<DT>(g);
+    store8<DT>(din, (size_t)i * 8, g);
   }
 }
 
 // ------------------------------------------------------------------ head: tail + global avg pool
 // out[n][c] = mean_{hw} relu(bn3(y3) + shortcut) ; shortcut: mode 1 = res tensor, 2 = bn_ds(y_ds)
 template <int DT>
-__global__ __launch_bounds__(NT) void tail_pool_kernel(const u16* __restrict__ y,
+__global__ __launch_bounds__(NT) void tail_pool_kernel(const void* __restrict__ y,
                                                        const float* __restrict__ sc,
                                                        const float* __restrict__ sh,
-                                                       const u16* __restrict__ r2,
+                                                       const void* __restrict__ r2,
                                                        const float* __restrict__ sc2,
                                                        const float* __restrict__ sh2,
-                                                       u16* __restrict__ out, int HW, int C,
+                                                       void* __restrict__ out, int HW, int C,
                                                        int mode) {
   const int n = blockIdx.x;
   const int CK = C / 8;
@@ -294,8 +294,8 @@ __global__ __launch_bounds__(NT) void tail_pool_kernel(const u16* __restrict__ y
     for (int pp = 0; pp < HW; ++pp) {
       const size_t off = ((size_t)n * HW + pp) * C + ck * 8;
       float v[8], w[8];
-      unpack8<DT>(*reinterpret_cast<const i32x4*>(y + off), v);
-      unpack8<DT>(*reinterpret_cast<const i32x4*>(r2 + off), w);
+      load8<DT>(y, off, v);
+      load8<DT>(r2, off, w);
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
         float s = w[e];
@@ -306,7 +306,7 @@ __global__ __launch_bounds__(NT) void tail_pool_kernel(const u16* __restrict__ y
     const float inv = 1.f / (float)HW;
 #pragma unroll
     for (int e = 0; e < 8; ++e) acc[e] *= inv;
-    *reinterpret_cast<i32x4*>(out + (size_t)n * C + ck * 8) = pack8<DT>(acc);
+    store8<DT>(out, (size_t)n * C + ck * 8, acc);
   }
 }
 
@@ -316,11 +316,11 @@ __global__ __launch_bounds__(NT) void tail_pool_kernel(const u16* __restrict__ y
 //            3 = no mask (dz given in g1, e.g. downsample branch re-reading the tail's dz)
 // Outputs partials [G][NQ][C]: q0 = sum dz, q1 = sum dz*y, q2 = sum dz*y2 (mode 2); dz stored if dz_out.
 struct BwdArgs {
-  const u16* g1; const u16* g2; const u16* gp; int HW;
-  const u16* y; const float* sc; const float* sh;
-  const u16* y2; const float* sc2; const float* sh2;
+  const void* g1; const void* g2; const void* gp; int HW;
+  const void* y; const float* sc; const float* sh;
+  const void* y2; const float* sc2; const float* sh2;
   int mode;
-  u16* dz_out;
+  void* dz_out;
   float* part; int nq;
   long long rows; int C;
   long long rows_per_block;
@@ -330,15 +330,15 @@ template <int DT>
 __device__ __forceinline__ void load_grad(const BwdArgs& a, long long row, int c0, float* g) {
   if (a.gp) {
     const long long n = row / a.HW;
-    unpack8<DT>(*reinterpret_cast<const i32x4*>(a.gp + n * a.C + c0), g);
+    load8<DT>(a.gp, n * a.C + c0, g);
     const float inv = 1.f / (float)a.HW;
 #pragma unroll
     for (int e = 0; e < 8; ++e) g[e] *= inv;
   } else {
-    unpack8<DT>(*reinterpret_cast<const i32x4*>(a.g1 + row * a.C + c0), g);
+    load8<DT>(a.g1, row * a.C + c0, g);
     if (a.g2) {
       float h[8];
-      unpack8<DT>(*reinterpret_cast<const i32x4*>(a.g2 + row * a.C + c0), h);
+      load8<DT>(a.g2, row * a.C + c0, h);
 #pragma unroll
       for (int e = 0; e < 8; ++e) g[e] += h[e];
     }
@@ -350,7 +350,7 @@ template <int DT>
 __device__ __forceinline__ void make_dz(const BwdArgs& a, long long row, int c0, float* dz,
                                         float* yv, float* y2v) {
   load_grad<DT>(a, row, c0, dz);
-  unpack8<DT>(*reinterpret_cast<const i32x4*>(a.y + row * a.C + c0), yv);
+  load8<DT>(a.y, row * a.C + c0, yv);
   if (a.mode == 3) return;
   float s[8], h[8];
   ld8f(a.sc + c0, s);
@@ -359,7 +359,7 @@ __device__ __forceinline__ void make_dz(const BwdArgs& a, long long row, int c0,
 #pragma unroll
   for (int e = 0; e < 8; ++e) pre[e] = yv[e] * s[e] + h[e];
   if (a.mode >= 1) {
-    unpack8<DT>(*reinterpret_cast<const i32x4*>(a.y2 + row * a.C + c0), y2v);
+    load8<DT>(a.y2, row * a.C + c0, y2v);
     if (a.mode == 2) {
       ld8f(a.sc2 + c0, s);
       ld8f(a.sh2 + c0, h);
@@ -392,7 +392,7 @@ __global__ __launch_bounds__(NT) void bn_bwd_reduce_kernel(BwdArgs a) {
       for (long long row = r0 + rsub; row < r1; row += rpi) {
         float dz[8], yv[8], y2v[8];
         make_dz<DT>(a, row, c0, dz, yv, y2v);
-        if (a.dz_out) *reinterpret_cast<i32x4*>(a.dz_out + row * a.C + c0) = pack8<DT>(dz);
+        if (a.dz_out) store8<DT>(a.dz_out, row * a.C + c0, dz);
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
           q0[e] += dz[e];
@@ -434,9 +434,9 @@ __global__ __launch_bounds__(NT) void bn_bwd_reduce_kernel(BwdArgs a) {
 // of the network (400x112x112x64) less, and one launch less. Rows = input pixels (N*H*W).
 template <int DT>
 __global__ __launch_bounds__(NT) void stem_bwd_reduce_kernel(
-    const u16* __restrict__ dout, const u16* __restrict__ dout2, const uint8_t* __restrict__ arg,
-    const u16* __restrict__ y, const float* __restrict__ sc, const float* __restrict__ sh,
-    u16* __restrict__ dz_out, float* __restrict__ part, long long rows, long long rows_per_block,
+    const void* __restrict__ dout, const void* __restrict__ dout2, const uint8_t* __restrict__ arg,
+    const void* __restrict__ y, const float* __restrict__ sc, const float* __restrict__ sh,
+    void* __restrict__ dz_out, float* __restrict__ part, long long rows, long long rows_per_block,
     int H, int W, int C, int Ho, int Wo, FastDiv dW, FastDiv dH) {
   __shared__ float red[2][NT][8];
   const int CK = C / 8;
@@ -462,7 +462,7 @@ __global__ __launch_bounds__(NT) void stem_bwd_reduce_kernel(
         const int yo0 = (int)yy >> 1, xo0 = (int)x >> 1;
         const int yo1 = ((yy & 1) && yo0 + 1 < Ho) ? yo0 + 1 : yo0;
         const int xo1 = ((x & 1) && xo0 + 1 < Wo) ? xo0 + 1 : xo0;
-        i32x4 dv[4], dv2[4];
+        Raw8<DT> dv[4], dv2[4];
         uint64_t am[4];
         int me[4];
 #pragma unroll
@@ -471,22 +471,22 @@ __global__ __launch_bounds__(NT) void stem_bwd_reduce_kernel(
           const bool live = ((w & 2) == 0 || yo1 != yo0) && ((w & 1) == 0 || xo1 != xo0);
           const uint32_t o = (n * Ho + yo) * Wo + xo;
           am[w] = reinterpret_cast<const uint64_t*>(arg)[o * CK + cc];
-          dv[w] = *reinterpret_cast<const i32x4*>(dout + (size_t)o * C + c0);
-          if (dout2) dv2[w] = *reinterpret_cast<const i32x4*>(dout2 + (size_t)o * C + c0);
+          dv[w] = ldraw8<DT>(dout, (size_t)o * C + c0);
+          if (dout2) dv2[w] = ldraw8<DT>(dout2, (size_t)o * C + c0);
           me[w] = live ? ((int)yy - (yo * 2 - 1)) * 3 + ((int)x - (xo * 2 - 1)) : 9;
         }
         float yv[8];
-        unpack8<DT>(*reinterpret_cast<const i32x4*>(y + row * C + c0), yv);
+        load8<DT>(y, row * C + c0, yv);
         float g[8];
 #pragma unroll
         for (int e = 0; e < 8; ++e) g[e] = 0.f;
 #pragma unroll
         for (int w = 0; w < 4; ++w) {
           float d[8];
-          unpack8<DT>(dv[w], d);
+          cvt8<DT>(dv[w], d);
           if (dout2) {
             float d2[8];
-            unpack8<DT>(dv2[w], d2);
+            cvt8<DT>(dv2[w], d2);
 #pragma unroll
             for (int e = 0; e < 8; ++e) d[e] += d2[e];
           }
@@ -497,9 +497,9 @@ __global__ __launch_bounds__(NT) void stem_bwd_reduce_kernel(
 #pragma unroll
         for (int e = 0; e < 8; ++e) g[e] = yv[e] * s[e] + h[e] > 0.f ? g[e] : 0.f;
         // statistics of the stored (rounded) dz, as the apply kernel re-reads it
-        const i32x4 pk = pack8<DT>(g);
-        *reinterpret_cast<i32x4*>(dz_out + row * C + c0) = pk;
-        unpack8<DT>(pk, g);
+        const Raw8<DT> pk = pk8<DT>(g);
+        straw8<DT>(dz_out, row * C + c0, pk);
+        cvt8<DT>(pk, g);
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
           q0[e] += g[e];
@@ -561,42 +561,42 @@ __global__ __launch_bounds__(1024) void bn_bwd_finalize_kernel(
 
 // dy = k1*dz + k2*y + k3 ; dz recomputed from (g, mask) exactly as in the reduce, or read (dz_in)
 template <int DT>
-__global__ __launch_bounds__(NT) void bn_bwd_apply_kernel(BwdArgs a, const u16* __restrict__ dz_in,
-                                                          const u16* __restrict__ ysel,
+__global__ __launch_bounds__(NT) void bn_bwd_apply_kernel(BwdArgs a, const void* __restrict__ dz_in,
+                                                          const void* __restrict__ ysel,
                                                           const float* __restrict__ k1,
                                                           const float* __restrict__ k2,
                                                           const float* __restrict__ k3,
-                                                          u16* __restrict__ dy) {
+                                                          void* __restrict__ dy) {
   const long long n8 = a.rows * (a.C / 8);
   for (long long i = blockIdx.x * (long long)NT + threadIdx.x; i < n8; i += (long long)gridDim.x * NT) {
     const long long row = i / (a.C / 8);
     const int c0 = (int)(i - row * (a.C / 8)) * 8;
     float dz[8], yv[8], y2v[8];
     if (dz_in) {
-      unpack8<DT>(reinterpret_cast<const i32x4*>(dz_in)[i], dz);
+      load8<DT>(dz_in, (size_t)i * 8, dz);
     } else {
       make_dz<DT>(a, row, c0, dz, yv, y2v);
     }
-    unpack8<DT>(reinterpret_cast<const i32x4*>(ysel)[i], yv);
+    load8<DT>(ysel, (size_t)i * 8, yv);
     float A[8], B[8], Cc[8], o[8];
     ld8f(k1 + c0, A);
     ld8f(k2 + c0, B);
     ld8f(k3 + c0, Cc);
 #pragma unroll
     for (int e = 0; e < 8; ++e) o[e] = A[e] * dz[e] + B[e] * yv[e] + Cc[e];
-    reinterpret_cast<i32x4*>(dy)[i] = pack8<DT>(o);
+    store8<DT>(dy, (size_t)i * 8, o);
   }
 }
 
 // dz read back (the common case: the consumer conv's dgrad epilogue stored it): pure stream,
 // loop-invariant channel chunk (see bn_apply_kernel), packed math.
 template <int DT>
-__global__ __launch_bounds__(NT) void bn_bwd_apply_dz_kernel(const u16* __restrict__ dz_in,
-                                                             const u16* __restrict__ ysel,
+__global__ __launch_bounds__(NT) void bn_bwd_apply_dz_kernel(const void* __restrict__ dz_in,
+                                                             const void* __restrict__ ysel,
                                                              const float* __restrict__ k1,
                                                              const float* __restrict__ k2,
                                                              const float* __restrict__ k3,
-                                                             u16* __restrict__ dy, int n8, int C) {
+                                                             void* __restrict__ dy, int n8, int C) {
   const int C8 = C >> 3;
   const int stride = gridDim.x * NT;
   const bool fixed = (stride % C8) == 0;
@@ -609,6 +609,16 @@ __global__ __launch_bounds__(NT) void bn_bwd_apply_dz_kernel(const u16* __restri
       ld8p<DT>(k2 + c0, B);
       ld8p<DT>(k3 + c0, K3);
       cprev = c0;
+    }
+    if constexpr (DT == DT_F32) {
+      float dz[8], yv[8], o[8];
+      load8<DT>(dz_in, (size_t)i * 8, dz);
+      load8<DT>(ysel, (size_t)i * 8, yv);
+#pragma unroll
+      for (int e = 0; e < 8; ++e)
+        o[e] = A[e >> 1][e & 1] * dz[e] + B[e >> 1][e & 1] * yv[e] + K3[e >> 1][e & 1];
+      store8<DT>(dy, (size_t)i * 8, o);
+      continue;
     }
     const i32x4 dz = reinterpret_cast<const i32x4*>(dz_in)[i];
     const i32x4 yv = reinterpret_cast<const i32x4*>(ysel)[i];
@@ -689,8 +699,9 @@ int pda_bn_apply(const void* y, const float* sc, const float* sh, const void* r2
   if (numel / 8 >= (1ll << 31)) return -2;
   const int n8 = (int)(numel / 8);
   const int g = grid_for(n8);
-#define ARGS (const u16*)y, sc, sh, (const u16*)r2, sc2, sh2, (u16*)out, n8, C, mode, relu
+#define ARGS (const void*)y, sc, sh, (const void*)r2, sc2, sh2, (void*)out, n8, C, mode, relu
   if (dt == DT_BF16) hipLaunchKernelGGL(bn_apply_kernel<DT_BF16>, dim3(g), dim3(NT), 0, st, ARGS);
+  else if (dt == DT_F32) hipLaunchKernelGGL(bn_apply_kernel<DT_F32>, dim3(g), dim3(NT), 0, st, ARGS);
   else hipLaunchKernelGGL(bn_apply_kernel<DT_F16>, dim3(g), dim3(NT), 0, st, ARGS);
 #undef ARGS
   return (int)hipGetLastError();
@@ -700,9 +711,10 @@ int pda_stem_pool(const void* y, const float* sc, const float* sh, void* out, vo
                   int H, int W, int C, int Ho, int Wo, int dt, hipStream_t st) {
   if ((long long)N * H * W * (C / 8) >= (1ll << 31)) return -2;
   const int g = grid_for((long long)N * Ho * Wo * (C / 8));
-#define ARGS (const u16*)y, sc, sh, (u16*)out, (uint8_t*)arg, N, H, W, C, Ho, Wo, make_div(C / 8), \
+#define ARGS (const void*)y, sc, sh, (void*)out, (uint8_t*)arg, N, H, W, C, Ho, Wo, make_div(C / 8), \
              make_div(Wo), make_div(Ho)
   if (dt == DT_BF16) hipLaunchKernelGGL(stem_pool_kernel<DT_BF16>, dim3(g), dim3(NT), 0, st, ARGS);
+  else if (dt == DT_F32) hipLaunchKernelGGL(stem_pool_kernel<DT_F32>, dim3(g), dim3(NT), 0, st, ARGS);
   else hipLaunchKernelGGL(stem_pool_kernel<DT_F16>, dim3(g), dim3(NT), 0, st, ARGS);
 #undef ARGS
   return (int)hipGetLastError();
@@ -712,9 +724,10 @@ int pda_maxpool_bwd(const void* dout, const void* dout2, const void* arg, void* 
                     int W, int C, int Ho, int Wo, int dt, hipStream_t st) {
   if ((long long)N * H * W * (C / 8) >= (1ll << 31)) return -2;
   const int g = grid_for((long long)N * H * W * (C / 8));
-#define ARGS (const u16*)dout, (const u16*)dout2, (const uint8_t*)arg, (u16*)din, N, H, W, C, Ho, Wo, \
+#define ARGS (const void*)dout, (const void*)dout2, (const uint8_t*)arg, (void*)din, N, H, W, C, Ho, Wo, \
              make_div(C / 8), make_div(W), make_div(H)
   if (dt == DT_BF16) hipLaunchKernelGGL(maxpool_bwd_kernel<DT_BF16>, dim3(g), dim3(NT), 0, st, ARGS);
+  else if (dt == DT_F32) hipLaunchKernelGGL(maxpool_bwd_kernel<DT_F32>, dim3(g), dim3(NT), 0, st, ARGS);
   else hipLaunchKernelGGL(maxpool_bwd_kernel<DT_F16>, dim3(g), dim3(NT), 0, st, ARGS);
 #undef ARGS
   return (int)hipGetLastError();
@@ -723,8 +736,9 @@ int pda_maxpool_bwd(const void* dout, const void* dout2, const void* arg, void* 
 int pda_tail_pool(const void* y, const float* sc, const float* sh, const void* r2, const float* sc2,
                   const float* sh2, void* out, int N, int HW, int C, int mode, int dt,
                   hipStream_t st) {
-#define ARGS (const u16*)y, sc, sh, (const u16*)r2, sc2, sh2, (u16*)out, HW, C, mode
+#define ARGS (const void*)y, sc, sh, (const void*)r2, sc2, sh2, (void*)out, HW, C, mode
   if (dt == DT_BF16) hipLaunchKernelGGL(tail_pool_kernel<DT_BF16>, dim3(N), dim3(NT), 0, st, ARGS);
+  else if (dt == DT_F32) hipLaunchKernelGGL(tail_pool_kernel<DT_F32>, dim3(N), dim3(NT), 0, st, ARGS);
   else hipLaunchKernelGGL(tail_pool_kernel<DT_F16>, dim3(N), dim3(NT), 0, st, ARGS);
 #undef ARGS
   return (int)hipGetLastError();
@@ -740,10 +754,10 @@ struct BwdArgsC {  // mirrors ops/ext.py
 
 static BwdArgs to_args(const BwdArgsC* c) {
   BwdArgs a;
-  a.g1 = (const u16*)c->g1; a.g2 = (const u16*)c->g2; a.gp = (const u16*)c->gp; a.HW = c->HW;
-  a.y = (const u16*)c->y; a.sc = c->sc; a.sh = c->sh;
-  a.y2 = (const u16*)c->y2; a.sc2 = c->sc2; a.sh2 = c->sh2;
-  a.mode = c->mode; a.dz_out = (u16*)c->dz_out;
+  a.g1 = (const void*)c->g1; a.g2 = (const void*)c->g2; a.gp = (const void*)c->gp; a.HW = c->HW;
+  a.y = (const void*)c->y; a.sc = c->sc; a.sh = c->sh;
+  a.y2 = (const void*)c->y2; a.sc2 = c->sc2; a.sh2 = c->sh2;
+  a.mode = c->mode; a.dz_out = (void*)c->dz_out;
   a.part = c->part; a.nq = c->nq; a.rows = c->rows; a.C = c->C; a.rows_per_block = 0;
   return a;
 }
@@ -753,7 +767,7 @@ int pda_bn_bwd_reduce(const BwdArgsC* c, int G, int dt, hipStream_t st) {
   BwdArgs a = to_args(c);
   a.rows_per_block = (a.rows + G - 1) / G;
 #define K(D) hipLaunchKernelGGL(bn_bwd_reduce_kernel<D>, dim3(G), dim3(NT), 0, st, a)
-  if (dt == DT_BF16) K(DT_BF16); else K(DT_F16);
+  if (dt == DT_BF16) K(DT_BF16); else if (dt == DT_F32) K(DT_F32); else K(DT_F16);
 #undef K
   return (int)hipGetLastError();
 }
@@ -765,11 +779,11 @@ int pda_stem_bwd_reduce(const void* dout, const void* dout2, const void* arg, co
   const long long rows = (long long)N * H * W;
   if (rows * C >= (1ll << 31) || C % 8) return -2;
   const long long rpb = (rows + G - 1) / G;
-#define K(D) hipLaunchKernelGGL(stem_bwd_reduce_kernel<D>, dim3(G), dim3(NT), 0, st, (const u16*)dout, \
-                                (const u16*)dout2, (const uint8_t*)arg, (const u16*)y, sc, sh,       \
-                                (u16*)dz_out, part, rows, rpb, H, W, C, Ho, Wo, make_div(W),          \
+#define K(D) hipLaunchKernelGGL(stem_bwd_reduce_kernel<D>, dim3(G), dim3(NT), 0, st, (const void*)dout, \
+                                (const void*)dout2, (const uint8_t*)arg, (const void*)y, sc, sh,       \
+                                (void*)dz_out, part, rows, rpb, H, W, C, Ho, Wo, make_div(W),          \
                                 make_div(H))
-  if (dt == DT_BF16) K(DT_BF16); else K(DT_F16);
+  if (dt == DT_BF16) K(DT_BF16); else if (dt == DT_F32) K(DT_F32); else K(DT_F16);
 #undef K
   return (int)hipGetLastError();
 }
@@ -789,15 +803,15 @@ int pda_bn_bwd_apply(const BwdArgsC* c, const void* dz_in, const void* ysel, con
   const int g = grid_for(a.rows * (a.C / 8));
   if (dz_in && a.rows * (a.C / 8) < (1ll << 31)) {
     const int n8 = (int)(a.rows * (a.C / 8));
-#define K(D) hipLaunchKernelGGL(bn_bwd_apply_dz_kernel<D>, dim3(g), dim3(NT), 0, st, (const u16*)dz_in, \
-                                (const u16*)ysel, k1, k2, k3, (u16*)dy, n8, a.C)
-    if (dt == DT_BF16) K(DT_BF16); else K(DT_F16);
+#define K(D) hipLaunchKernelGGL(bn_bwd_apply_dz_kernel<D>, dim3(g), dim3(NT), 0, st, (const void*)dz_in, \
+                                (const void*)ysel, k1, k2, k3, (void*)dy, n8, a.C)
+    if (dt == DT_BF16) K(DT_BF16); else if (dt == DT_F32) K(DT_F32); else K(DT_F16);
 #undef K
     return (int)hipGetLastError();
   }
-#define K(D) hipLaunchKernelGGL(bn_bwd_apply_kernel<D>, dim3(g), dim3(NT), 0, st, a, (const u16*)dz_in, \
-                                (const u16*)ysel, k1, k2, k3, (u16*)dy)
-  if (dt == DT_BF16) K(DT_BF16); else K(DT_F16);
+#define K(D) hipLaunchKernelGGL(bn_bwd_apply_kernel<D>, dim3(g), dim3(NT), 0, st, a, (const void*)dz_in, \
+                                (const void*)ysel, k1, k2, k3, (void*)dy)
+  if (dt == DT_BF16) K(DT_BF16); else if (dt == DT_F32) K(DT_F32); else K(DT_F16);
 #undef K
   return (int)hipGetLastError();
 }

@@ -64,6 +64,76 @@ template <> __device__ __forceinline__ f32x4 mfma16<DT_F16>(s16x8 a, s16x8 b, f3
                                                 __builtin_bit_cast(f16x8, b), c, 0, 0, 0);
 }
 
+// ---- MFMA 16x16x4 f32 (exact fp32 path, MX_DTYPE=fp32) --------------------------------------
+__device__ __forceinline__ f32x4 mfma16_f32(float a, float b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+
+// ---- 8 consecutive activation elements of any storage dtype <-> f32[8] -------------------------
+// 16-bit: one 16-B chunk; f32: two. Element offsets (not bytes) index the tensor.
+template <int DT> struct Raw8 { i32x4 v; };
+template <> struct Raw8<DT_F32> { f32x4 a, b; };
+
+template <int DT> __device__ __forceinline__ Raw8<DT> ldraw8(const void* base, size_t idx) {
+  Raw8<DT> r;
+  if constexpr (DT == DT_F32) {
+    const f32x4* p = reinterpret_cast<const f32x4*>(reinterpret_cast<const float*>(base) + idx);
+    r.a = p[0];
+    r.b = p[1];
+  } else {
+    r.v = *reinterpret_cast<const i32x4*>(reinterpret_cast<const u16*>(base) + idx);
+  }
+  return r;
+}
+template <int DT> __device__ __forceinline__ void straw8(void* base, size_t idx, const Raw8<DT>& r) {
+  if constexpr (DT == DT_F32) {
+    f32x4* p = reinterpret_cast<f32x4*>(reinterpret_cast<float*>(base) + idx);
+    p[0] = r.a;
+    p[1] = r.b;
+  } else {
+    *reinterpret_cast<i32x4*>(reinterpret_cast<u16*>(base) + idx) = r.v;
+  }
+}
+template <int DT> __device__ __forceinline__ void cvt8(const Raw8<DT>& r, float* f) {
+  if constexpr (DT == DT_F32) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) { f[e] = r.a[e]; f[4 + e] = r.b[e]; }
+  } else {
+    const u16* h = reinterpret_cast<const u16*>(&r.v);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) f[e] = DT == DT_BF16 ? bf16_to_f32(h[e]) : f16_to_f32(h[e]);
+  }
+}
+template <int DT> __device__ __forceinline__ Raw8<DT> pk8(const float* f) {
+  Raw8<DT> r;
+  if constexpr (DT == DT_F32) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) { r.a[e] = f[e]; r.b[e] = f[4 + e]; }
+  } else {
+    u16* h = reinterpret_cast<u16*>(&r.v);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) h[e] = DT == DT_BF16 ? f32_to_bf16(f[e]) : f32_to_f16(f[e]);
+  }
+  return r;
+}
+template <int DT> __device__ __forceinline__ void load8(const void* base, size_t idx, float* f) {
+  cvt8<DT>(ldraw8<DT>(base, idx), f);
+}
+template <int DT> __device__ __forceinline__ void store8(void* base, size_t idx, const float* f) {
+  straw8<DT>(base, idx, pk8<DT>(f));
+}
+
+// runtime-dtype scalar access (small kernels: data generation, head, optimizer shadow)
+__device__ __forceinline__ void st_any(void* base, size_t i, float v, int dt) {
+  if (dt == DT_F32) reinterpret_cast<float*>(base)[i] = v;
+  else reinterpret_cast<u16*>(base)[i] = dt == DT_BF16 ? f32_to_bf16(v) : f32_to_f16(v);
+}
+__device__ __forceinline__ float ld_any(const void* base, size_t i, int dt) {
+  if (dt == DT_F32) return reinterpret_cast<const float*>(base)[i];
+  const u16 h = reinterpret_cast<const u16*>(base)[i];
+  return dt == DT_BF16 ? bf16_to_f32(h) : f16_to_f32(h);
+}
+
 // ---- fast unsigned division by a runtime constant (n < 2^31) --------------------------------
 struct FastDiv {
   uint32_t d, m, s;

@@ -1,5 +1,6 @@
 // Implicit-GEMM convolution for gfx950 (MI355X): forward, data-gradient and weight-gradient,
-// NHWC activations, OHWI ("KRSC") weights, bf16/f16 inputs, MFMA 16x16x32 with f32 accumulation.
+// NHWC activations, OHWI ("KRSC") weights, bf16/f16 inputs on MFMA 16x16x32 with f32 accumulation,
+// or exact f32 inputs (MX_DTYPE=fp32, the reference scripts' precision) on MFMA 16x16x4 f32.
 //
 // Replaces cuDNN conv fwd/dgrad/wgrad of the reference stack: every
 // Conv2d of ResNet (all 23 ResNet-50 shapes + the 7x7 stem) and the fc layer (as a 1x1 conv on a
@@ -25,7 +26,6 @@
 
 namespace {
 
-constexpr int BK = 64;
 constexpr int NT = 256;
 
 enum Pass : int { FWD = 0, DGRAD = 1, WGRAD = 2 };
@@ -61,9 +61,9 @@ struct ConvParams {
   const float* pro_sh;
   // DGRAD fused BatchNorm-backward epilogue (emode < 0: plain dX store)
   int emode, enq;                 // 0 relu(bn(y)), 1 relu(bn(y)+ey2), 2 relu(bn(y)+bn2(ey2))
-  const u16* ey; const float* esc; const float* esh;
-  const u16* ey2; const float* esc2; const float* esh2;
-  const u16* eg2;                  // optional second gradient summed into dA
+  const void* ey; const float* esc; const float* esh;
+  const void* ey2; const float* esc2; const float* esh2;
+  const void* eg2;                 // optional second gradient summed into dA
   float* epart;                    // [ncls*tiles_m][enq][N] partial sums
 };
 
@@ -115,6 +115,25 @@ __device__ __forceinline__ s16x8 frag_col(const char* lds, int cb, int s, int la
   return r;
 }
 
+// COL tile of f32 (exact-fp32 path): 32 k-rows x BC cols of 4 B, 16-B chunks XOR-swizzled by
+// 4 * ((krow >> 2) & 3) so the four k-groups of a fragment read land in disjoint bank quarters.
+template <int BC>
+__device__ __forceinline__ int col_addr_f32(int krow, int chunk) {
+  return krow * (BC * 4) + ((chunk ^ (((krow >> 2) & 3) << 2)) << 4);
+}
+// lane holds col cb+(l&15), k = 16*s + 4*(l>>4) + 0..3 (the k order of frag_row on an f32 ROW tile)
+template <int BC>
+__device__ __forceinline__ f32x4 frag_col_f32(const char* lds, int cb, int s, int lane) {
+  const int g = lane >> 4, col = cb + (lane & 15);
+  f32x4 r;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int krow = s * 16 + 4 * g + j;
+    r[j] = *reinterpret_cast<const float*>(lds + col_addr_f32<BC>(krow, col >> 2) + ((col & 3) << 2));
+  }
+  return r;
+}
+
 // ================================================================= kernel
 // STAGES = 2: double-buffered LDS, one barrier per k-tile (deep-K layers).
 // STAGES = 1: single LDS buffer (half the LDS -> one more resident block per CU) for the many
@@ -125,14 +144,20 @@ template <int PASS, int DT, int BM, int BN, int STAGES>
 // MFMA) need ~250 registers and 64 KiB of LDS: two blocks per CU.
 __global__ __launch_bounds__(NT, (STAGES == 1 && BM * BN <= 128 * 128) ? 3 : 2) void conv_gemm_kernel(ConvParams p) {
   // A tile: FWD/DGRAD ROW [BM][64]; WGRAD COL [64][BM]. B tile: FWD ROW [BN][64]; else COL [64][BN]
-  constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2;
+  // element geometry: 16-bit operands move 8 elements per 16-B chunk and 64 k per 128-B tile row;
+  // the exact-f32 path (DT_F32, MFMA 16x16x4 f32) moves 4 per chunk and 32 k per row
+  constexpr bool F32 = DT == DT_F32;
+  constexpr int ES = F32 ? 4 : 2;        // element bytes
+  constexpr int EPC = 16 / ES;           // elements per 16-B chunk
+  constexpr int BKE = 128 / ES;          // k per tile (one 128-B row)
+  constexpr int A_BYTES = BM * 128, B_BYTES = BN * 128;
   constexpr int STAGE = A_BYTES + B_BYTES;
   constexpr int RED_BYTES = 3 * NT * 8 * 4;
-  constexpr int C_BYTES = BM * BN * 2;   // staged 16-bit C tile of the epilogue
+  constexpr int C_BYTES = BM * BN * ES;  // staged C tile of the epilogue
   constexpr int LDS_0 = STAGES * STAGE > RED_BYTES ? STAGES * STAGE : RED_BYTES;
   constexpr int LDS_BYTES = LDS_0 > C_BYTES ? LDS_0 : C_BYTES;
   static_assert(BN <= NT, "stats reduction: one thread per column");
-  static_assert(BM * BN * 2 <= LDS_BYTES, "C tile must fit in the staging buffers");
+  static_assert(BM * BN * ES <= LDS_BYTES, "C tile must fit in the staging buffers");
   static_assert(3 * NT * 8 * 4 <= LDS_BYTES, "stats reduction must fit");
   __shared__ __attribute__((aligned(16))) char smem[LDS_BYTES];
 
@@ -162,7 +187,7 @@ __global__ __launch_bounds__(NT, (STAGES == 1 && BM * BN <= 128 * 128) ? 3 : 2) 
     ntap = p.ntaps[split];
     kend = ntap * p.Cout;
   }
-  const int nk = (kend - kbeg + BK - 1) / BK;
+  const int nk = (kend - kbeg + BKE - 1) / BKE;
 
   // ---- per-thread loader precompute -------------------------------------------------
   // Operands are read with buffer loads (32-bit byte offsets, hardware range check): a padding
@@ -186,7 +211,7 @@ __global__ __launch_bounds__(NT, (STAGES == 1 && BM * BN <= 128 * 128) ? 3 : 2) 
         const uint32_t img = fdiv(mm, p.dHoWo), rem = mm - img * p.dHoWo.d;
         const uint32_t yo = fdiv(rem, p.dWo), xo = rem - yo * p.dWo.d;
         const int y0 = (int)yo * p.stride - p.pad, x0 = (int)xo * p.stride - p.pad;
-        a_base[i] = (((int)img * p.H + y0) * p.W + x0) * p.Cin * 2;
+        a_base[i] = (((int)img * p.H + y0) * p.W + x0) * p.Cin * ES;
         for (int r = 0, t = 0; r < p.R; ++r) {
           const bool yok = (unsigned)(y0 + r) < (unsigned)p.H;
           for (int q = 0; q < p.S; ++q, ++t)
@@ -195,7 +220,7 @@ __global__ __launch_bounds__(NT, (STAGES == 1 && BM * BN <= 128 * 128) ? 3 : 2) 
       } else {  // DGRAD: class-grid pixel (yi, xi); tap t of the class reads dY[yi + dy_t][xi + dx_t]
         const uint32_t img = fdiv(mm, p.dHcWc), rem = mm - img * p.dHcWc.d;
         const uint32_t yi = fdiv(rem, p.dWc), xi = rem - yi * p.dWc.d;
-        a_base[i] = (((int)img * p.Ho + (int)yi) * p.Wo + (int)xi) * p.Cout * 2;
+        a_base[i] = (((int)img * p.Ho + (int)yi) * p.Wo + (int)xi) * p.Cout * ES;
         for (int t = 0; t < ntap; ++t) {
           if ((unsigned)((int)yi + p.tdy[split][t]) < (unsigned)p.Ho &&
               (unsigned)((int)xi + p.tdx[split][t]) < (unsigned)p.Wo)
@@ -205,12 +230,12 @@ __global__ __launch_bounds__(NT, (STAGES == 1 && BM * BN <= 128 * 128) ? 3 : 2) 
       a_mask[i] = okm ? msk : 0ull;
     }
   } else {
-    constexpr int CPR = BM / 8, RPI = NT / CPR;
-    const int col = m0 + (tid % CPR) * 8;
+    constexpr int CPR = BM / EPC, RPI = NT / CPR;
+    const int col = m0 + (tid % CPR) * EPC;
 #pragma unroll
     for (int i = 0; i < AR; ++i) {
       a_krow[i] = tid / CPR + RPI * i;
-      a_off[i] = col < p.M ? (uint32_t)((kbeg + a_krow[i]) * p.Cout + col) * 2u : OOB;
+      a_off[i] = col < p.M ? (uint32_t)((kbeg + a_krow[i]) * p.Cout + col) * (uint32_t)ES : OOB;
     }
   }
   // B
@@ -219,22 +244,22 @@ __global__ __launch_bounds__(NT, (STAGES == 1 && BM * BN <= 128 * 128) ? 3 : 2) 
 #pragma unroll
     for (int i = 0; i < BR; ++i) {
       const int n = n0 + (tid >> 3) + 32 * i;
-      b_off[i] = n < p.N ? (uint32_t)(n * p.Kpad + (tid & 7) * 8) * 2u : OOB;
+      b_off[i] = n < p.N ? (uint32_t)(n * p.Kpad + (tid & 7) * EPC) * (uint32_t)ES : OOB;
     }
   } else if constexpr (PASS == DGRAD) {
-    constexpr int CPR = BN / 8, RPI = NT / CPR;
-    const int col = n0 + (tid % CPR) * 8;
+    constexpr int CPR = BN / EPC, RPI = NT / CPR;
+    const int col = n0 + (tid % CPR) * EPC;
 #pragma unroll
     for (int i = 0; i < BR; ++i)
-      b_off[i] = col < p.N ? (uint32_t)((tid / CPR + RPI * i) * p.R * p.S * p.Cin + col) * 2u : OOB;
+      b_off[i] = col < p.N ? (uint32_t)((tid / CPR + RPI * i) * p.R * p.S * p.Cin + col) * (uint32_t)ES : OOB;
   }
   // WGRAD B gather: fixed column chunk per thread -> (tap, c)
   int wb_r = 0, wb_s = 0, wb_c = 0;
   bool wb_colok = true;
   const bool wb_direct = PASS == WGRAD && p.R == 1 && p.S == 1 && p.stride == 1 && p.pad == 0;
   if constexpr (PASS == WGRAD) {
-    constexpr int CPR = BN / 8;
-    const int col = n0 + (tid % CPR) * 8;
+    constexpr int CPR = BN / EPC;
+    const int col = n0 + (tid % CPR) * EPC;
     wb_colok = col < p.N;
     const int tap = col >> p.log2Cin;
     wb_c = col & ((1 << p.log2Cin) - 1);
@@ -246,14 +271,14 @@ __global__ __launch_bounds__(NT, (STAGES == 1 && BM * BN <= 128 * 128) ? 3 : 2) 
   // buffer resources (wave-uniform: built from kernel arguments only)
   uint32_t a_bytes, b_bytes;
   if constexpr (PASS == FWD) {
-    a_bytes = (uint32_t)p.Nb * p.H * p.W * p.Cin * 2u;
-    b_bytes = (uint32_t)p.N * p.Kpad * 2u;
+    a_bytes = (uint32_t)p.Nb * p.H * p.W * p.Cin * (uint32_t)ES;
+    b_bytes = (uint32_t)p.N * p.Kpad * (uint32_t)ES;
   } else if constexpr (PASS == DGRAD) {
-    a_bytes = (uint32_t)p.Nb * p.Ho * p.Wo * p.Cout * 2u;
-    b_bytes = (uint32_t)p.Cout * p.R * p.S * p.Cin * 2u;
+    a_bytes = (uint32_t)p.Nb * p.Ho * p.Wo * p.Cout * (uint32_t)ES;
+    b_bytes = (uint32_t)p.Cout * p.R * p.S * p.Cin * (uint32_t)ES;
   } else {
-    a_bytes = (uint32_t)p.K * p.Cout * 2u;
-    b_bytes = (uint32_t)p.Nb * p.H * p.W * p.Cin * 2u;
+    a_bytes = (uint32_t)p.K * p.Cout * (uint32_t)ES;
+    b_bytes = (uint32_t)p.Nb * p.H * p.W * p.Cin * (uint32_t)ES;
   }
   const __amdgpu_buffer_rsrc_t rsa = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p.a), (short)0,
                                                                          (int)a_bytes, 0x00020000);
@@ -270,7 +295,7 @@ __global__ __launch_bounds__(NT, (STAGES == 1 && BM * BN <= 128 * 128) ? 3 : 2) 
   f32x2 psc[4], psh[4];
   auto pro_coeffs = [&](int c) {
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
+    for (int k = 0; k < EPC / 2; ++k) {
       psc[k] = *reinterpret_cast<const f32x2*>(p.pro_sc + c + 2 * k);
       psh[k] = *reinterpret_cast<const f32x2*>(p.pro_sh + c + 2 * k);
     }
@@ -280,6 +305,13 @@ __global__ __launch_bounds__(NT, (STAGES == 1 && BM * BN <= 128 * 128) ? 3 : 2) 
   // zeroes exactly the negative values (and -0) -- one v_pk_max_i16 per pair
   typedef short s16x2 __attribute__((ext_vector_type(2)));
   auto pro_apply = [&](i32x4& v) {
+    if constexpr (F32) {   // one f32 element per dword
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+        v[k] = __float_as_int(fmaxf(__builtin_fmaf(__int_as_float(v[k]), psc[k >> 1][k & 1],
+                                                   psh[k >> 1][k & 1]), 0.f));
+      return;
+    }
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
       const f32x2 u = unpack2<DT>((uint32_t)v[k]);
@@ -290,14 +322,14 @@ __global__ __launch_bounds__(NT, (STAGES == 1 && BM * BN <= 128 * 128) ? 3 : 2) 
   };
 
   auto load_tile = [&](int kt) {
-    const int k0 = kbeg + kt * BK;
+    const int k0 = kbeg + kt * BKE;
     // ---------------- A
     if constexpr (PASS == FWD) {
-      const int k = k0 + (tid & 7) * 8;
+      const int k = k0 + (tid & 7) * EPC;
       const int tap = k >> p.log2Cin;
       const int c = k & ((1 << p.log2Cin) - 1);
       const int r = (int)fdiv(tap, p.dS), q = tap - r * p.S;
-      const int toff = ((r * p.W + q) * p.Cin + c) * 2;
+      const int toff = ((r * p.W + q) * p.Cin + c) * ES;
       const bool tap_ok = tap < p.R * p.S;
 #pragma unroll
       for (int i = 0; i < AR; ++i) {
@@ -308,16 +340,16 @@ __global__ __launch_bounds__(NT, (STAGES == 1 && BM * BN <= 128 * 128) ? 3 : 2) 
       if (pro) pro_coeffs(c);
     } else if constexpr (PASS == DGRAD) {
       const int ti = k0 / p.Cout;  // tile lies in one tap (Cout % 64 == 0)
-      const int c = k0 - ti * p.Cout + (tid & 7) * 8;
+      const int c = k0 - ti * p.Cout + (tid & 7) * EPC;
       const int tsel = ti < 9 ? ti : 0;
-      const int toff = ((p.tdy[split][tsel] * p.Wo + p.tdx[split][tsel]) * p.Cout + c) * 2;
+      const int toff = ((p.tdy[split][tsel] * p.Wo + p.tdx[split][tsel]) * p.Cout + c) * ES;
 #pragma unroll
       for (int i = 0; i < AR; ++i) {
         const bool ok = ((uint32_t)a_mask[i] >> ti) & 1u;
         ra[i] = bld(rsa, ok ? (uint32_t)(a_base[i] + toff) : OOB);
       }
     } else {  // WGRAD A: dY rows m (k), cols n1 (COL tile [64][BM])
-      const uint32_t koff = (uint32_t)(kt * BK * p.Cout) * 2u;
+      const uint32_t koff = (uint32_t)(kt * BKE * p.Cout) * (uint32_t)ES;
 #pragma unroll
       for (int i = 0; i < AR; ++i)
         ra[i] = bld(rsa, (k0 + a_krow[i] < kend) ? a_off[i] + koff : OOB);
@@ -325,24 +357,24 @@ __global__ __launch_bounds__(NT, (STAGES == 1 && BM * BN <= 128 * 128) ? 3 : 2) 
     // ---------------- B
     if constexpr (PASS == FWD) {
 #pragma unroll
-      for (int i = 0; i < BR; ++i) rb[i] = bld(rsb, b_off[i] + (uint32_t)k0 * 2u);
+      for (int i = 0; i < BR; ++i) rb[i] = bld(rsb, b_off[i] + (uint32_t)k0 * (uint32_t)ES);
     } else if constexpr (PASS == DGRAD) {
       const int ti = k0 / p.Cout;
       const int tap = p.taps[split][ti < 9 ? ti : 0];
-      const uint32_t uoff = (uint32_t)(((k0 - ti * p.Cout) * p.R * p.S + tap) * p.Cin) * 2u;
+      const uint32_t uoff = (uint32_t)(((k0 - ti * p.Cout) * p.R * p.S + tap) * p.Cin) * (uint32_t)ES;
 #pragma unroll
       for (int i = 0; i < BR; ++i) rb[i] = bld(rsb, b_off[i] + uoff);
     } else if (wb_direct) {  // WGRAD B, 1x1 stride-1 conv: X rows ARE the GEMM rows
-      constexpr int CPR = BN / 8, RPI = NT / CPR;
+      constexpr int CPR = BN / EPC, RPI = NT / CPR;
 #pragma unroll
       for (int i = 0; i < BR; ++i) {
         const int m = k0 + tid / CPR + RPI * i;
         const bool ok = wb_colok && m < kend;
-        rb[i] = bld(rsb, ok ? (uint32_t)(m * p.Cin + wb_c) * 2u : OOB);
+        rb[i] = bld(rsb, ok ? (uint32_t)(m * p.Cin + wb_c) * (uint32_t)ES : OOB);
         pv[i] = ok;
       }
     } else {  // WGRAD B: gathered X rows m, cols (tap, c)
-      constexpr int CPR = BN / 8, RPI = NT / CPR;
+      constexpr int CPR = BN / EPC, RPI = NT / CPR;
 #pragma unroll
       for (int i = 0; i < BR; ++i) {
         const int krow = tid / CPR + RPI * i;
@@ -353,7 +385,7 @@ __global__ __launch_bounds__(NT, (STAGES == 1 && BM * BN <= 128 * 128) ? 3 : 2) 
         const uint32_t yo = fdiv(rem, p.dWo), xo = rem - yo * p.dWo.d;
         const int y = (int)yo * p.stride - p.pad + wb_r, x = (int)xo * p.stride - p.pad + wb_s;
         ok = ok && (unsigned)y < (unsigned)p.H && (unsigned)x < (unsigned)p.W;
-        const int off = ((((int)img * p.H + y) * p.W + x) * p.Cin + wb_c) * 2;
+        const int off = ((((int)img * p.H + y) * p.W + x) * p.Cin + wb_c) * ES;
         rb[i] = bld(rsb, ok ? (uint32_t)off : OOB);
         if constexpr (PASS == WGRAD) pv[i] = ok;
       }
@@ -372,23 +404,28 @@ __global__ __launch_bounds__(NT, (STAGES == 1 && BM * BN <= 128 * 128) ? 3 : 2) 
         *reinterpret_cast<i32x4*>(sa + row_addr((tid >> 3) + 32 * i, tid & 7)) = ra[i];
       }
     } else {
-      constexpr int CPR = BM / 8, RPI = NT / CPR;
+      constexpr int CPR = BM / EPC, RPI = NT / CPR;
 #pragma unroll
-      for (int i = 0; i < AR; ++i)
-        *reinterpret_cast<i32x4*>(sa + col_addr<BM>(tid / CPR + RPI * i, tid % CPR)) = ra[i];
+      for (int i = 0; i < AR; ++i) {
+        const int ca = F32 ? col_addr_f32<BM>(tid / CPR + RPI * i, tid % CPR)
+                           : col_addr<BM>(tid / CPR + RPI * i, tid % CPR);
+        *reinterpret_cast<i32x4*>(sa + ca) = ra[i];
+      }
     }
     if constexpr (B_ROW) {
 #pragma unroll
       for (int i = 0; i < BR; ++i)
         *reinterpret_cast<i32x4*>(sb + row_addr((tid >> 3) + 32 * i, tid & 7)) = rb[i];
     } else {
-      constexpr int CPR = BN / 8, RPI = NT / CPR;
+      constexpr int CPR = BN / EPC, RPI = NT / CPR;
 #pragma unroll
       for (int i = 0; i < BR; ++i) {
         if constexpr (PASS == WGRAD) {
           if (pro && pv[i]) pro_apply(rb[i]);
         }
-        *reinterpret_cast<i32x4*>(sb + col_addr<BN>(tid / CPR + RPI * i, tid % CPR)) = rb[i];
+        const int cb_ = F32 ? col_addr_f32<BN>(tid / CPR + RPI * i, tid % CPR)
+                            : col_addr<BN>(tid / CPR + RPI * i, tid % CPR);
+        *reinterpret_cast<i32x4*>(sb + cb_) = rb[i];
       }
     }
   };
@@ -423,6 +460,28 @@ __global__ __launch_bounds__(NT, (STAGES == 1 && BM * BN <= 128 * 128) ? 3 : 2) 
     const char* sb = sa + A_BYTES;
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
+      if constexpr (F32) {   // 16 k per step: lane holds 4 k of its row/col; 4 MFMAs 16x16x4 f32
+        f32x4 fa[MI], fb[NI];
+#pragma unroll
+        for (int i = 0; i < MI; ++i) {
+          const int rbase = wr * (BM / 2) + i * 16;
+          if constexpr (A_ROW) fa[i] = __builtin_bit_cast(f32x4, frag_row(sa, rbase, s, lane));
+          else fa[i] = frag_col_f32<BM>(sa, rbase, s, lane);
+        }
+#pragma unroll
+        for (int j = 0; j < NI; ++j) {
+          const int cbase = wc * (BN / 2) + j * 16;
+          if constexpr (B_ROW) fb[j] = __builtin_bit_cast(f32x4, frag_row(sb, cbase, s, lane));
+          else fb[j] = frag_col_f32<BN>(sb, cbase, s, lane);
+        }
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+#pragma unroll
+          for (int i = 0; i < MI; ++i)
+#pragma unroll
+            for (int j = 0; j < NI; ++j) acc[i][j] = mfma16_f32(fb[j][e], fa[i][e], acc[i][j]);
+        continue;
+      } else {
       s16x8 fa[MI], fb[NI];
 #pragma unroll
       for (int i = 0; i < MI; ++i) {
@@ -440,6 +499,7 @@ __global__ __launch_bounds__(NT, (STAGES == 1 && BM * BN <= 128 * 128) ? 3 : 2) 
       for (int i = 0; i < MI; ++i)
 #pragma unroll
         for (int j = 0; j < NI; ++j) acc[i][j] = mfma16<DT>(fb[j], fa[i], acc[i][j]);
+      }
     }
     if constexpr (STAGES == 2) {
       if (kt + 1 < nk) store_tile(cur ^ 1);
@@ -495,9 +555,9 @@ __global__ __launch_bounds__(NT, (STAGES == 1 && BM * BN <= 128 * 128) ? 3 : 2) 
 #pragma unroll
           for (int e = 0; e < 4; ++e) acc[i][j][e] = fmaxf(acc[i][j][e], 0.f);
     }
-    // stage the 16-bit C tile through LDS: [BM][BN], row pitch BN*2 bytes, 16-B chunks swizzled by
-    // row; one packed 8-byte store (4 columns) per MFMA tile per lane.
-    constexpr int CPR = BN / 8;
+    // stage the C tile through LDS: [BM][BN], row pitch BN*ES bytes, 16-B chunks swizzled by
+    // row; one packed 8-byte store (4 columns) per MFMA tile per lane (f32: one 16-B store).
+    constexpr int CPR = BN / EPC;
     auto c_addr = [&](int row, int chunk) { return row * CPR + (chunk ^ (row & (CPR - 1))); };
     {
 #pragma unroll
@@ -506,6 +566,11 @@ __global__ __launch_bounds__(NT, (STAGES == 1 && BM * BN <= 128 * 128) ? 3 : 2) 
 #pragma unroll
         for (int i = 0; i < MI; ++i) {
           const int row = wr * (BM / 2) + i * 16 + lr;
+          if constexpr (F32) {
+            *reinterpret_cast<f32x4*>(smem + row * (BN * 4) + (((col >> 2) ^ (row & (CPR - 1))) << 4)) =
+                acc[i][j];
+            continue;
+          }
           // row & (CPR-1) == lr & (CPR-1) for CPR <= 16 (folded); BN = 256 needs the full row
           const int cbyte = (((col >> 3) ^ (row & (CPR - 1))) << 4) + ((col & 4) << 1);
           uint2 pk;
@@ -515,7 +580,7 @@ __global__ __launch_bounds__(NT, (STAGES == 1 && BM * BN <= 128 * 128) ? 3 : 2) 
         }
       }
     }
-    const u16* ct = reinterpret_cast<const u16*>(smem);
+    const char* ct = smem;
     // coalesced 16-B stores + per-channel partial statistics.
     //  FWD  (stats): q0 = sum y, q1 = sum y^2 of the written tile (BatchNorm forward statistics).
     //  DGRAD (emode >= 0): the tile is dA, the gradient of a = relu(bn(y) [+ res | + bn2(y2)]);
@@ -533,8 +598,8 @@ __global__ __launch_bounds__(NT, (STAGES == 1 && BM * BN <= 128 * 128) ? 3 : 2) 
     // before it is consumed (the first group's before the barrier that publishes the C tile),
     // which bounds the prefetch registers to PD rows.
     constexpr int PD = RPT > 4 ? 4 : RPT;
-    u16* out = reinterpret_cast<u16*>(p.out);
-    const int gcol = n0 + cc * 8;
+    char* outb = reinterpret_cast<char*>(p.out);
+    const int gcol = n0 + cc * EPC;
     auto row_off = [&](int i, bool& ok) -> uint32_t {
       const int grow = m0 + rg + RG * i;
       ok = grow < p.M && gcol < p.N;
@@ -557,7 +622,7 @@ __global__ __launch_bounds__(NT, (STAGES == 1 && BM * BN <= 128 * 128) ? 3 : 2) 
       if constexpr (MODE >= 0) {
         const int cg = gcol < p.N ? gcol : 0;
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
+        for (int k = 0; k < EPC / 2; ++k) {
           esc[k] = f32x2{p.esc[cg + 2 * k], p.esc[cg + 2 * k + 1]};
           esh[k] = f32x2{p.esh[cg + 2 * k], p.esh[cg + 2 * k + 1]};
           if constexpr (MODE == 2) {
@@ -574,9 +639,13 @@ __global__ __launch_bounds__(NT, (STAGES == 1 && BM * BN <= 128 * 128) ? 3 : 2) 
 #pragma unroll
         for (int j = 0; j < PD; ++j) {
           eoff[j] = row_off(g0 + j, eok[j]);
-          if constexpr (MODE >= 0) py[j] = eok[j] ? *reinterpret_cast<const i32x4*>(p.ey + eoff[j]) : z;
-          if constexpr (G2) pg2[j] = eok[j] ? *reinterpret_cast<const i32x4*>(p.eg2 + eoff[j]) : z;
-          if constexpr (MODE >= 1) py2[j] = eok[j] ? *reinterpret_cast<const i32x4*>(p.ey2 + eoff[j]) : z;
+          const size_t bo = (size_t)eoff[j] * ES;
+          if constexpr (MODE >= 0)
+            py[j] = eok[j] ? *reinterpret_cast<const i32x4*>(reinterpret_cast<const char*>(p.ey) + bo) : z;
+          if constexpr (G2)
+            pg2[j] = eok[j] ? *reinterpret_cast<const i32x4*>(reinterpret_cast<const char*>(p.eg2) + bo) : z;
+          if constexpr (MODE >= 1)
+            py2[j] = eok[j] ? *reinterpret_cast<const i32x4*>(reinterpret_cast<const char*>(p.ey2) + bo) : z;
         }
       };
       f32x2 q0[4], q1[4], q2[4];
@@ -590,9 +659,32 @@ __global__ __launch_bounds__(NT, (STAGES == 1 && BM * BN <= 128 * 128) ? 3 : 2) 
 #pragma unroll
         for (int j = 0; j < PD; ++j) {
           const int row = rg + RG * (g0 + j);
-          i32x4 v = *reinterpret_cast<const i32x4*>(ct + c_addr(row, cc) * 8);
+          i32x4 v = *reinterpret_cast<const i32x4*>(ct + c_addr(row, cc) * 16);
           if (!eok[j]) continue;
-          if constexpr (MODE >= 0) {
+          if constexpr (F32) {   // one element per dword
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              const int k = e >> 1, h = e & 1;
+              float f = __int_as_float(v[e]);
+              if constexpr (MODE >= 0) {
+                if constexpr (G2) f += __int_as_float(pg2[j][e]);
+                const float yv = __int_as_float(py[j][e]);
+                float pre = yv * esc[k][h] + esh[k][h];
+                float y2v = 0.f;
+                if constexpr (MODE >= 1) y2v = __int_as_float(py2[j][e]);
+                if constexpr (MODE == 1) pre += y2v;
+                if constexpr (MODE == 2) pre += y2v * esc2[k][h] + esh2[k][h];
+                const float dz = pre > 0.f ? f : 0.f;
+                v[e] = __float_as_int(dz);
+                q0[k][h] += dz;
+                q1[k][h] += dz * yv;
+                if constexpr (MODE == 2) q2[k][h] += dz * y2v;
+              } else if (do_stats) {
+                q0[k][h] += f;
+                q1[k][h] += f * f;
+              }
+            }
+          } else if constexpr (MODE >= 0) {
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
               f32x2 g = unpack2<DT>((uint32_t)v[k]);
@@ -619,17 +711,17 @@ __global__ __launch_bounds__(NT, (STAGES == 1 && BM * BN <= 128 * 128) ? 3 : 2) 
               q1[k] += f * f;
             }
           }
-          *reinterpret_cast<i32x4*>(out + eoff[j]) = v;
+          *reinterpret_cast<i32x4*>(outb + (size_t)eoff[j] * ES) = v;
         }
       }
       if (do_stats) {
         __syncthreads();
         float* red = reinterpret_cast<float*>(smem);  // [NQ][RG][BN]
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          *reinterpret_cast<f32x2*>(red + rg * BN + cc * 8 + 2 * k) = q0[k];
-          *reinterpret_cast<f32x2*>(red + RG * BN + rg * BN + cc * 8 + 2 * k) = q1[k];
-          if constexpr (NQ > 2) *reinterpret_cast<f32x2*>(red + 2 * RG * BN + rg * BN + cc * 8 + 2 * k) = q2[k];
+        for (int k = 0; k < EPC / 2; ++k) {
+          *reinterpret_cast<f32x2*>(red + rg * BN + cc * EPC + 2 * k) = q0[k];
+          *reinterpret_cast<f32x2*>(red + RG * BN + rg * BN + cc * EPC + 2 * k) = q1[k];
+          if constexpr (NQ > 2) *reinterpret_cast<f32x2*>(red + 2 * RG * BN + rg * BN + cc * EPC + 2 * k) = q2[k];
         }
         __syncthreads();
         if (tid < BN) {
@@ -755,6 +847,7 @@ static int dispatch(int dt, int bm, int bn, const ConvParams& p, dim3 grid, hipS
     if constexpr (PASS == WGRAD) { PDA_CASE1(DT_BF16, 256, 128) PDA_CASE1(DT_F16, 256, 128) }
     if constexpr (PASS == DGRAD) { PDA_CASE1(DT_BF16, 128, 256) PDA_CASE1(DT_F16, 128, 256) }
     PDA_CASE1(DT_F16, 128, 128) PDA_CASE1(DT_F16, 128, 64) PDA_CASE1(DT_F16, 64, 128)
+    PDA_CASE1(DT_F32, 128, 128) PDA_CASE1(DT_F32, 128, 64) PDA_CASE1(DT_F32, 64, 128)
 #undef PDA_CASE1
     return -1;
   }
@@ -764,14 +857,16 @@ static int dispatch(int dt, int bm, int bn, const ConvParams& p, dim3 grid, hipS
   PDA_CASE(DT_BF16, 64, 64)
   PDA_CASE(DT_F16, 128, 128) PDA_CASE(DT_F16, 128, 64) PDA_CASE(DT_F16, 64, 128)
   PDA_CASE(DT_F16, 64, 64)
+  PDA_CASE(DT_F32, 128, 128) PDA_CASE(DT_F32, 128, 64) PDA_CASE(DT_F32, 64, 128)
+  PDA_CASE(DT_F32, 64, 64)
 #undef PDA_CASE
   return -1;
 }
 
 // the kernels address operands with 32-bit buffer offsets (range-checked, OOB = 0x80000000)
-static bool fits32(long long a, long long b, long long c) {
-  const long long lim = 0x7fffffffll;
-  return a * 2 < lim && b * 2 < lim && c * 4 < lim;
+static bool fits32(long long a, long long b, long long c, int dt) {
+  const long long lim = 0x7fffffffll, es = dt == DT_F32 ? 4 : 2;
+  return a * es < lim && b * es < lim && c * 4 < lim;
 }
 
 static void fill_geom(ConvParams& p, const ConvDesc& d) {
@@ -792,7 +887,7 @@ int pda_conv_fwd(const ConvDesc* d, const void* x, const void* w, int Kpad, void
                  int out_pitch, const float* bias, float* stats, int relu, const float* pro_sc,
                  const float* pro_sh, int dt, int bm, int bn, hipStream_t st) {
   if (!fits32((long long)d->Nb * d->H * d->W * d->Cin, (long long)d->Cout * Kpad,
-              (long long)d->Nb * d->Ho * d->Wo * d->Cout) || d->R * d->S > 64)
+              (long long)d->Nb * d->Ho * d->Wo * d->Cout, dt) || d->R * d->S > 64)
     return -4;
   ConvParams p{};
   fill_geom(p, *d);
@@ -816,7 +911,7 @@ struct BnEpi {  // mirrors ops/ext.py BnEpi
 int pda_conv_dgrad(const ConvDesc* d, const void* dy, const void* w, void* dx, const BnEpi* epi,
                    int dt, int bm, int bn, hipStream_t st) {
   if (!fits32((long long)d->Nb * d->Ho * d->Wo * d->Cout, (long long)d->Cout * d->R * d->S * d->Cin,
-              (long long)d->Nb * d->H * d->W * d->Cin))
+              (long long)d->Nb * d->H * d->W * d->Cin, dt))
     return -4;
   ConvParams p{};
   fill_geom(p, *d);
@@ -824,9 +919,9 @@ int pda_conv_dgrad(const ConvDesc* d, const void* dy, const void* w, void* dx, c
   p.emode = -1;
   if (epi) {
     p.emode = epi->mode; p.enq = epi->nq;
-    p.ey = (const u16*)epi->y; p.esc = epi->sc; p.esh = epi->sh;
-    p.ey2 = (const u16*)epi->y2; p.esc2 = epi->sc2; p.esh2 = epi->sh2;
-    p.eg2 = (const u16*)epi->g2; p.epart = epi->part;
+    p.ey = epi->y; p.esc = epi->sc; p.esh = epi->sh;
+    p.ey2 = epi->y2; p.esc2 = epi->sc2; p.esh2 = epi->sh2;
+    p.eg2 = epi->g2; p.epart = epi->part;
   }
   p.N = d->Cin; p.out_pitch = d->Cin;
   const int sd = d->stride;
@@ -864,7 +959,7 @@ int pda_conv_wgrad(const ConvDesc* d, const void* dy, const void* x, float* slab
                    int k_chunk, const float* pro_sc, const float* pro_sh, int dt, int bm, int bn,
                    hipStream_t st) {
   if (!fits32((long long)d->Nb * d->Ho * d->Wo * d->Cout, (long long)d->Nb * d->H * d->W * d->Cin,
-              (long long)splits * d->Cout * d->R * d->S * d->Cin))
+              (long long)splits * d->Cout * d->R * d->S * d->Cin, dt))
     return -4;
   ConvParams p{};
   fill_geom(p, *d);

@@ -22,7 +22,7 @@ constexpr int NT = 256;
 // ------------------------------------------------------------------ softmax cross-entropy
 __global__ __launch_bounds__(NT) void xent_kernel(const float* __restrict__ logits, int B, int K,
                                                   int ld_in, const long long* __restrict__ labels,
-                                                  float* __restrict__ loss_rows, u16* __restrict__ dlog,
+                                                  float* __restrict__ loss_rows, void* __restrict__ dlog,
                                                   int ld_out, float gscale, const float* __restrict__ gdev, int dt,
                                                   int want_grad) {
   const int wave = (blockIdx.x * NT + threadIdx.x) >> 6;
@@ -41,11 +41,11 @@ __global__ __launch_bounds__(NT) void xent_kernel(const float* __restrict__ logi
   if (!want_grad) return;
   const float inv = 1.f / s;
   if (gdev) gscale *= gdev[0];
-  u16* d = dlog + (size_t)wave * ld_out;
+  const size_t drow = (size_t)wave * ld_out;
   for (int k = lane; k < ld_out; k += 64) {
     float g = 0.f;
     if (k < K) g = (__expf(x[k] - m) * inv - (k == lab ? 1.f : 0.f)) * gscale;
-    d[k] = dt == DT_BF16 ? f32_to_bf16(g) : f32_to_f16(g);
+    st_any(dlog, drow + k, g, dt);
   }
 }
 
@@ -91,7 +91,7 @@ __global__ __launch_bounds__(NT) void topk_kernel(const float* __restrict__ logi
 // out[c] = scale * sum_r x[r][c]  (x: 16-bit [rows][ld]). Block = 64 columns x 16 row slices
 // (1024 threads): each thread sums every 16th row of its column (independent loads, pipelined),
 // then a fixed-order LDS combine -- deterministic, no serial 400-load chain per column.
-__global__ __launch_bounds__(1024) void col_sum_kernel(const u16* __restrict__ x, int rows, int C,
+__global__ __launch_bounds__(1024) void col_sum_kernel(const void* __restrict__ x, int rows, int C,
                                                        int ld, float scale, float* __restrict__ out,
                                                        int dt, int accumulate) {
   __shared__ float red[16][64];
@@ -101,8 +101,7 @@ __global__ __launch_bounds__(1024) void col_sum_kernel(const u16* __restrict__ x
   if (c < C) {
 #pragma unroll 4
     for (int r = sl; r < rows; r += 16) {
-      const u16 h = x[(size_t)r * ld + c];
-      s += dt == DT_BF16 ? bf16_to_f32(h) : f16_to_f32(h);
+      s += ld_any(x, (size_t)r * ld + c, dt);
     }
   }
   red[sl][cl] = s;
@@ -192,7 +191,7 @@ __global__ void amp_update_kernel(float* scale, int* tracker, const float* found
 }
 
 // stem weight pack: src f32 [Cout][R*S][Cin] (channels-last OHWI) -> dst 16-bit [Cout][Kpad]
-__global__ void pack_stem_kernel(const float* __restrict__ src, u16* __restrict__ dst, int Cout,
+__global__ void pack_stem_kernel(const float* __restrict__ src, void* __restrict__ dst, int Cout,
                                  int RS, int Cin, int Cpad, int Kpad, int dt) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= Cout * Kpad) return;
@@ -200,7 +199,7 @@ __global__ void pack_stem_kernel(const float* __restrict__ src, u16* __restrict_
   const int tap = k / Cpad, c = k - tap * Cpad;
   float v = 0.f;
   if (tap < RS && c < Cin) v = src[((size_t)co * RS + tap) * Cin + c];
-  dst[i] = dt == DT_BF16 ? f32_to_bf16(v) : f32_to_f16(v);
+  st_any(dst, i, v, dt);
 }
 
 // ------------------------------------------------------------------ data
@@ -231,7 +230,7 @@ __global__ void synth_labels_kernel(const long long* __restrict__ ids, int B, ui
 // out: [B][S][S][8] 16-bit; pixel (c,y,x) of sample b: u = hash32(key ^ (pos * 0x27D4EB2F)) >> 8
 __global__ __launch_bounds__(NT) void synth_nhwc8_kernel(const uint32_t* __restrict__ keys,
                                                          const long long* __restrict__ labels,
-                                                         int B, int S, u16* __restrict__ out, int dt) {
+                                                         int B, int S, void* __restrict__ out, int dt) {
   const long long npix = (long long)B * S * S;
   const int hw = S * S;
   for (long long i = blockIdx.x * (long long)NT + threadIdx.x; i < npix; i += (long long)gridDim.x * NT) {
@@ -239,7 +238,7 @@ __global__ __launch_bounds__(NT) void synth_nhwc8_kernel(const uint32_t* __restr
     const int pix = (int)(i - (long long)b * hw);
     const uint32_t key = keys[b];
     const long long lab = labels[b];
-    u16 h[8];
+    float h[8];
 #pragma unroll
     for (int c = 0; c < 3; ++c) {
       const uint32_t pos = (uint32_t)(c * hw + pix);
@@ -247,29 +246,28 @@ __global__ __launch_bounds__(NT) void synth_nhwc8_kernel(const uint32_t* __restr
       const float uf = (float)u * (1.0f / 16777216.0f);
       const float tint = (float)((lab * (2 * c + 3) + c) % 4) / 3.0f;
       const float v = (uf * 0.5f + 0.5f * tint - c_mean[c]) * c_istd[c];
-      h[c] = dt == DT_BF16 ? f32_to_bf16(v) : f32_to_f16(v);
+      h[c] = v;
     }
 #pragma unroll
-    for (int c = 3; c < 8; ++c) h[c] = 0;
-    reinterpret_cast<i32x4*>(out)[i] = *reinterpret_cast<i32x4*>(h);
+    for (int c = 3; c < 8; ++c) h[c] = 0.f;
+#pragma unroll
+    for (int c = 0; c < 8; ++c) st_any(out, (size_t)i * 8 + c, h[c], dt);
   }
 }
 
 __global__ __launch_bounds__(NT) void nchw_to_nhwc8_kernel(const float* __restrict__ x, int B, int C,
-                                                           int H, int W, u16* __restrict__ out,
+                                                           int H, int W, void* __restrict__ out,
                                                            int dt) {
   const long long npix = (long long)B * H * W;
   const int hw = H * W;
   for (long long i = blockIdx.x * (long long)NT + threadIdx.x; i < npix; i += (long long)gridDim.x * NT) {
     const int b = (int)(i / hw);
     const int pix = (int)(i - (long long)b * hw);
-    u16 h[8];
 #pragma unroll
     for (int c = 0; c < 8; ++c) {
       const float v = c < C ? x[((size_t)b * C + c) * hw + pix] : 0.f;
-      h[c] = dt == DT_BF16 ? f32_to_bf16(v) : f32_to_f16(v);
+      st_any(out, (size_t)i * 8 + c, v, dt);
     }
-    reinterpret_cast<i32x4*>(out)[i] = *reinterpret_cast<i32x4*>(h);
   }
 }
 
@@ -280,7 +278,7 @@ __global__ __launch_bounds__(NT) void nchw_to_nhwc8_kernel(const float* __restri
 // K = 16 taps x 16 channels = 256: whole 16-B chunks, MFMA-aligned, no per-chunk tap decode.
 __global__ __launch_bounds__(NT) void synth_s2d_kernel(const uint32_t* __restrict__ keys,
                                                        const long long* __restrict__ labels,
-                                                       int B, int S, u16* __restrict__ out, int dt) {
+                                                       int B, int S, void* __restrict__ out, int dt) {
   const int S2 = S / 2;
   const long long npix = (long long)B * S2 * S2;
   const int hw = S * S;
@@ -290,7 +288,7 @@ __global__ __launch_bounds__(NT) void synth_s2d_kernel(const uint32_t* __restric
     const int oi = rem / S2, oj = rem - oi * S2;
     const uint32_t key = keys[b];
     const long long lab = labels[b];
-    u16 h[16];
+    float h[16];
 #pragma unroll
     for (int pq = 0; pq < 4; ++pq) {
       const int pix = (2 * oi + (pq >> 1)) * S + 2 * oj + (pq & 1);
@@ -301,40 +299,45 @@ __global__ __launch_bounds__(NT) void synth_s2d_kernel(const uint32_t* __restric
         const float uf = (float)u * (1.0f / 16777216.0f);
         const float tint = (float)((lab * (2 * c + 3) + c) % 4) / 3.0f;
         const float v = (uf * 0.5f + 0.5f * tint - c_mean[c]) * c_istd[c];
-        h[pq * 3 + c] = dt == DT_BF16 ? f32_to_bf16(v) : f32_to_f16(v);
+        h[pq * 3 + c] = v;
       }
     }
 #pragma unroll
-    for (int c = 12; c < 16; ++c) h[c] = 0;
-    reinterpret_cast<i32x4*>(out)[2 * i] = reinterpret_cast<i32x4*>(h)[0];
-    reinterpret_cast<i32x4*>(out)[2 * i + 1] = reinterpret_cast<i32x4*>(h)[1];
+    for (int c = 12; c < 16; ++c) h[c] = 0.f;
+    if (dt == DT_F32) {
+      store8<DT_F32>(out, (size_t)i * 16, h);
+      store8<DT_F32>(out, (size_t)i * 16 + 8, h + 8);
+    } else if (dt == DT_BF16) {
+      store8<DT_BF16>(out, (size_t)i * 16, h);
+      store8<DT_BF16>(out, (size_t)i * 16 + 8, h + 8);
+    } else {
+      store8<DT_F16>(out, (size_t)i * 16, h);
+      store8<DT_F16>(out, (size_t)i * 16 + 8, h + 8);
+    }
   }
 }
 
 __global__ __launch_bounds__(NT) void nchw_to_s2d_kernel(const float* __restrict__ x, int B, int C,
-                                                         int S, u16* __restrict__ out, int dt) {
+                                                         int S, void* __restrict__ out, int dt) {
   const int S2 = S / 2;
   const long long npix = (long long)B * S2 * S2;
   for (long long i = blockIdx.x * (long long)NT + threadIdx.x; i < npix; i += (long long)gridDim.x * NT) {
     const int b = (int)(i / (S2 * S2));
     const int rem = (int)(i - (long long)b * S2 * S2);
     const int oi = rem / S2, oj = rem - oi * S2;
-    u16 h[16];
 #pragma unroll
     for (int k = 0; k < 16; ++k) {
       const int pq = k / 3, c = k - pq * 3;
       float v = 0.f;
       if (k < 12 && c < C)
         v = x[(((size_t)b * C + c) * S + 2 * oi + (pq >> 1)) * S + 2 * oj + (pq & 1)];
-      h[k] = dt == DT_BF16 ? f32_to_bf16(v) : f32_to_f16(v);
+      st_any(out, (size_t)i * 16 + k, v, dt);
     }
-    reinterpret_cast<i32x4*>(out)[2 * i] = reinterpret_cast<i32x4*>(h)[0];
-    reinterpret_cast<i32x4*>(out)[2 * i + 1] = reinterpret_cast<i32x4*>(h)[1];
   }
 }
 
 // src f32 OHWI [64][7][7][3] -> dst 16-bit [64][4][4][16]
-__global__ void pack_stem_s2d_kernel(const float* __restrict__ src, u16* __restrict__ dst, int Cout,
+__global__ void pack_stem_s2d_kernel(const float* __restrict__ src, void* __restrict__ dst, int Cout,
                                      int dt) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= Cout * 256) return;
@@ -347,7 +350,7 @@ __global__ void pack_stem_s2d_kernel(const float* __restrict__ src, u16* __restr
     const int r = 2 * ra + (pq >> 1) - 1, s = 2 * sb + (pq & 1) - 1;
     if (r >= 0 && r < 7 && s >= 0 && s < 7) v = src[(((size_t)co * 7 + r) * 7 + s) * 3 + c];
   }
-  dst[i] = dt == DT_BF16 ? f32_to_bf16(v) : f32_to_f16(v);
+  st_any(dst, i, v, dt);
 }
 
 // gradient of the packed weight [64][256] (f32) -> OHWI [64][7][7][3] of the master weight
@@ -376,7 +379,7 @@ int pda_xent(const float* logits, int B, int K, int ld_in, const long long* labe
              float* loss, void* dlog, int ld_out, float gscale, const float* gdev, int dt,
              int want_grad, hipStream_t st) {
   hipLaunchKernelGGL(xent_kernel, dim3((B + 3) / 4), dim3(NT), 0, st, logits, B, K, ld_in, labels,
-                     loss_rows, (u16*)dlog, ld_out, gscale, gdev, dt, want_grad);
+                     loss_rows, dlog, ld_out, gscale, gdev, dt, want_grad);
   if (loss) hipLaunchKernelGGL(mean_kernel, dim3(1), dim3(1024), 0, st, loss_rows, B, loss);
   return (int)hipGetLastError();
 }
@@ -389,7 +392,7 @@ int pda_topk(const float* logits, int B, int K, int ld, const long long* labels,
 
 int pda_col_sum(const void* x, int rows, int C, int ld, float scale, float* out, int dt,
                 int accumulate, hipStream_t st) {
-  hipLaunchKernelGGL(col_sum_kernel, dim3((C + 63) / 64), dim3(1024), 0, st, (const u16*)x, rows, C, ld,
+  hipLaunchKernelGGL(col_sum_kernel, dim3((C + 63) / 64), dim3(1024), 0, st, x, rows, C, ld,
                      scale, out, dt, accumulate);
   return (int)hipGetLastError();
 }
@@ -422,7 +425,7 @@ int pda_amp_update(float* scale, int* tracker, const float* found_inf, float gro
 int pda_pack_stem(const float* src, void* dst, int Cout, int RS, int Cin, int Cpad, int Kpad, int dt,
                   hipStream_t st) {
   const int n = Cout * Kpad;
-  hipLaunchKernelGGL(pack_stem_kernel, dim3((n + 255) / 256), dim3(256), 0, st, src, (u16*)dst, Cout,
+  hipLaunchKernelGGL(pack_stem_kernel, dim3((n + 255) / 256), dim3(256), 0, st, src, dst, Cout,
                      RS, Cin, Cpad, Kpad, dt);
   return (int)hipGetLastError();
 }
@@ -432,7 +435,7 @@ int pda_synth(const long long* ids, int B, unsigned salt, int num_classes, unsig
   hipLaunchKernelGGL(synth_labels_kernel, dim3((B + 255) / 256), dim3(256), 0, st, ids, B, salt,
                      num_classes, keys, labels);
   hipLaunchKernelGGL(synth_nhwc8_kernel, dim3(grid_for((long long)B * S * S, 8192)), dim3(NT), 0, st,
-                     keys, labels, B, S, (u16*)out, dt);
+                     keys, labels, B, S, out, dt);
   return (int)hipGetLastError();
 }
 
@@ -441,19 +444,19 @@ int pda_synth_s2d(const long long* ids, int B, unsigned salt, int num_classes, u
   hipLaunchKernelGGL(synth_labels_kernel, dim3((B + 255) / 256), dim3(256), 0, st, ids, B, salt,
                      num_classes, keys, labels);
   hipLaunchKernelGGL(synth_s2d_kernel, dim3(grid_for((long long)B * (S / 2) * (S / 2), 8192)), dim3(NT),
-                     0, st, keys, labels, B, S, (u16*)out, dt);
+                     0, st, keys, labels, B, S, out, dt);
   return (int)hipGetLastError();
 }
 
 int pda_nchw_to_s2d(const float* x, int B, int C, int S, void* out, int dt, hipStream_t st) {
   hipLaunchKernelGGL(nchw_to_s2d_kernel, dim3(grid_for((long long)B * (S / 2) * (S / 2), 8192)),
-                     dim3(NT), 0, st, x, B, C, S, (u16*)out, dt);
+                     dim3(NT), 0, st, x, B, C, S, out, dt);
   return (int)hipGetLastError();
 }
 
 int pda_pack_stem_s2d(const float* src, void* dst, int Cout, int dt, hipStream_t st) {
   hipLaunchKernelGGL(pack_stem_s2d_kernel, dim3((Cout * 256 + 255) / 256), dim3(256), 0, st, src,
-                     (u16*)dst, Cout, dt);
+                     dst, Cout, dt);
   return (int)hipGetLastError();
 }
 
@@ -465,7 +468,7 @@ int pda_stem_s2d_grad(const float* gp, float* g, int Cout, int accumulate, hipSt
 
 int pda_nchw_to_nhwc8(const float* x, int B, int C, int H, int W, void* out, int dt, hipStream_t st) {
   hipLaunchKernelGGL(nchw_to_nhwc8_kernel, dim3(grid_for((long long)B * H * W, 8192)), dim3(NT), 0, st,
-                     x, B, C, H, W, (u16*)out, dt);
+                     x, B, C, H, W, out, dt);
   return (int)hipGetLastError();
 }
 

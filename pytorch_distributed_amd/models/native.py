@@ -44,7 +44,7 @@ ALIGN = 64  # elements; keeps every segment 16-B aligned in the 16-bit shadow
 
 
 def supports(arch: str, dtype: torch.dtype) -> bool:
-    if dtype not in (torch.bfloat16, torch.float16):
+    if dtype not in (torch.bfloat16, torch.float16, torch.float32):
         return False
     if arch not in ("resnet18", "resnet34", "resnet50", "resnet101", "resnet152"):
         return False
@@ -209,7 +209,11 @@ class NativeResNet(nn.Module):
         self.units = units
         self.flat_params = torch.zeros(off, dtype=torch.float32, device=dev)
         self.flat_grad = torch.zeros(off, dtype=torch.float32, device=dev)
-        self.flat_shadow = torch.zeros(off, dtype=self.dtype, device=dev)
+        # 16-bit engines: the convs read a 16-bit shadow of the f32 master weights (refreshed by the
+        # fused SGD); the exact-fp32 engine reads the master weights themselves
+        self.f32 = self.dtype == torch.float32
+        self.flat_shadow = (self.flat_params if self.f32
+                            else torch.zeros(off, dtype=self.dtype, device=dev))
         # BN buffers
         boff = 0
         for i, u in enumerate(units):
@@ -308,7 +312,8 @@ class NativeResNet(nn.Module):
     @torch.no_grad()
     def refresh_shadow(self) -> None:
         """16-bit shadow of the flat parameters (the SGD kernel keeps it fresh afterwards)."""
-        K.cast_flat(self.flat_params, self.flat_shadow)
+        if not self.f32:
+            K.cast_flat(self.flat_params, self.flat_shadow)
         self._pack_stem()
 
     def _pack_stem(self) -> None:
@@ -811,8 +816,9 @@ class NativeSGD(torch.optim.Optimizer):
     def _launch(self, scale=None, found_inf=None) -> None:
         g = self.param_groups[0]
         m = self.model
-        K.sgd_flat(m.flat_params, m.flat_grad, self.flat_mom, m.flat_shadow, g["lr"], g["momentum"],
-                   g["weight_decay"], self._initialized, scale=scale, found_inf=found_inf)
+        K.sgd_flat(m.flat_params, m.flat_grad, self.flat_mom, None if m.f32 else m.flat_shadow,
+                   g["lr"], g["momentum"], g["weight_decay"], self._initialized, scale=scale,
+                   found_inf=found_inf)
         m._pack_stem()
         if found_inf is None:
             self._initialized = True

@@ -111,7 +111,9 @@ def conv_fwd(x: torch.Tensor, w: torch.Tensor, g: ConvGeom, out: torch.Tensor,
     Kpad = w.shape[-1] if w.dim() == 2 else w[0].numel()
     bm, bn = tile or pick_tile(M, g.Cout, Kpad)
     d = g.desc(Nb)
-    out_f32 = out.dtype == torch.float32
+    # direct (unstaged) f32 store + bias: the fc head (16-bit features -> f32 logits, or any conv
+    # with a bias); f32 activations of the exact-fp32 engine take the staged path with statistics
+    out_f32 = bias is not None or out.dtype != x.dtype
     pitch = out.stride(0) if out.dim() == 2 else g.Cout
     rc = ext.lib().pda_conv_fwd(C.byref(d), ptr(x), ptr(w), Kpad, ptr(out), int(out_f32), pitch,
                                 ptr(bias), ptr(stats), int(relu), ptr(pro[0] if pro else None),
@@ -204,7 +206,8 @@ _WGRAD_TUNED = {
 
 
 def wgrad_plan(g: ConvGeom, Nb: int, tile: Optional[Tuple[int, int]] = None,
-               target_blocks: Optional[int] = None, max_slab_bytes: int = 64 << 20):
+               target_blocks: Optional[int] = None, max_slab_bytes: int = 64 << 20,
+               f32: bool = False):
     M, N, K = g.Cout, g.R * g.S * g.Cin, Nb * g.Ho * g.Wo
     tuned = _WGRAD_TUNED.get((g.Cout, g.R, g.Cin, g.stride, g.Ho)) if _SINGLE_STAGE else None
     bn = 128 if N >= 128 else 64
@@ -214,6 +217,8 @@ def wgrad_plan(g: ConvGeom, Nb: int, tile: Optional[Tuple[int, int]] = None,
     if tuned and not tile:
         (bm, bn), tb = tuned
         target_blocks = target_blocks or tb
+        if f32 and (abs(bm) > 128 or bn > 128):   # 256-wide tiles are 16-bit only
+            bm, bn = -128, 128
     if target_blocks is None:
         target_blocks = _WGRAD_TARGET
     target_blocks = max(1, int(target_blocks * _WGRAD_TB_SCALE))
@@ -235,7 +240,7 @@ def conv_wgrad(dy: torch.Tensor, x: torch.Tensor, g: ConvGeom, grad: torch.Tenso
     """grad (f32, OHWI with cin_real channels, rows of pitch R*S*cin_real) = scale * dW.
     pro = (scale, shift): x is PRE-BatchNorm; the activation relu(x*scale+shift) is recomputed."""
     Nb = dy.shape[0]
-    bm, bn, splits, k_chunk = wgrad_plan(g, Nb, tile, target_blocks)
+    bm, bn, splits, k_chunk = wgrad_plan(g, Nb, tile, target_blocks, f32=dy.dtype == torch.float32)
     M, N = g.Cout, g.R * g.S * g.Cin
     slab = ws.get("wgrad_slab", splits * M * N)
     d = g.desc(Nb)

@@ -380,14 +380,16 @@ def test_synthetic_kernel_matches_torch_generator():
     assert out[..., 3:].abs().max().item() == 0
 
 
+@pytest.mark.parametrize("geo", [(2, 8, 64, 128), (8, 16, 64, 64)])
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
 @pytest.mark.parametrize("mode", ["relu", "res", "ds"])
 @pytest.mark.parametrize("stride", [1, 2])
-def test_dgrad_fused_bn_backward(mode, stride):
+def test_dgrad_fused_bn_backward(mode, stride, dtype, geo):
     """dgrad epilogue (mask + BN-backward partial sums) == plain dgrad followed by the standalone
-    BN-backward reduce/apply."""
+    BN-backward reduce/apply (16-bit and exact-f32 kernels)."""
     K = _k()
-    dtype = torch.bfloat16
-    Nb, H, Cin, Cout = 2, 8, 64, 128
+    tol = 1e-2 if dtype != torch.float32 else 1e-5
+    Nb, H, Cin, Cout = geo
     torch.manual_seed(5)
     g = K.ConvGeom(Nb, H, H, Cin, Cout, 3, 3, stride, 1)
     dy = torch.randn(Nb, g.Ho, g.Wo, Cout, device=DEV).to(dtype)
@@ -435,10 +437,51 @@ def test_dgrad_fused_bn_backward(mode, stride):
     K.bn_bwd_finish(ws, part, G, nq, y, mean, inv, gamma, outs[0], outs[1], dz, dyf, **extra)
     torch.cuda.synchronize()
     if mode != "relu":
-        assert rel_err(dz, dz_ref) < 1e-2
-    assert rel_err(dyf, dy_ref) < 2e-2
+        assert rel_err(dz, dz_ref) < tol
+    assert rel_err(dyf, dy_ref) < 2 * tol
     for a, b in zip(outs, outs_ref):
         if b.abs().sum() > 0:
-            assert rel_err(a, b) < 1e-2
+            assert rel_err(a, b) < tol
     if mode == "ds":
-        assert rel_err(dy2f, dy2_ref) < 2e-2
+        assert rel_err(dy2f, dy2_ref) < 2 * tol
+
+
+@pytest.mark.parametrize("case", CONV_CASES)
+def test_conv_fwd_dgrad_wgrad_exact_f32(case):
+    """Exact-fp32 implicit GEMM (MFMA 16x16x4 f32) vs a float64 CPU reference: errors at fp32
+    rounding level (no 16-bit operand rounding anywhere)."""
+    K = _k()
+    Nb, H, Cin, Cout, k, s = case
+    pad = k // 2
+    torch.manual_seed(0)
+    x = torch.randn(Nb, Cin, H, H) + 0.1
+    w = torch.randn(Cout, Cin, k, k) / math.sqrt(Cin * k * k)
+    xd, wd = x.double(), w.double()
+    y_ref = F.conv2d(xd, wd, stride=s, padding=pad)
+    g = K.ConvGeom(Nb, H, H, Cin, Cout, k, k, s, pad)
+    x_nhwc = x.permute(0, 2, 3, 1).contiguous().to(DEV)
+    w_ohwi = w.permute(0, 2, 3, 1).contiguous().to(DEV)
+    y = torch.empty(Nb, g.Ho, g.Wo, Cout, device=DEV)
+    M = Nb * g.Ho * g.Wo
+    T = K.stats_tiles(M, Cout)
+    stats = torch.zeros(T * 2 * Cout, device=DEV)
+    K.conv_fwd(x_nhwc, w_ohwi.view(Cout, -1), g, y, stats=stats)
+    torch.cuda.synchronize()
+    assert rel_err(y.cpu().double(), y_ref.permute(0, 2, 3, 1)) < 2e-6
+    st = stats.view(T, 2, Cout).sum(0).cpu().double()
+    yb = y_ref.permute(0, 2, 3, 1).reshape(-1, Cout)
+    torch.testing.assert_close(st[0], yb.sum(0), rtol=1e-4, atol=1e-4)
+    torch.testing.assert_close(st[1], (yb * yb).sum(0), rtol=1e-4, atol=1e-4)
+    dy = torch.randn(y_ref.shape)
+    xr = xd.clone().requires_grad_(True)
+    wr = wd.clone().requires_grad_(True)
+    F.conv2d(xr, wr, stride=s, padding=pad).backward(dy.double())
+    dy_nhwc = dy.permute(0, 2, 3, 1).contiguous().to(DEV)
+    dx = torch.full((Nb, H, H, Cin), float("nan"), device=DEV)
+    K.conv_dgrad(dy_nhwc, w_ohwi, g, dx)
+    ws = K.Workspace(DEV)
+    dw = torch.zeros(Cout, k, k, Cin, device=DEV)
+    K.conv_wgrad(dy_nhwc, x_nhwc, g, dw.view(-1), ws)
+    torch.cuda.synchronize()
+    assert rel_err(dx.cpu().double(), xr.grad.permute(0, 2, 3, 1)) < 2e-6
+    assert rel_err(dw.cpu().double(), wr.grad.permute(0, 2, 3, 1)) < 2e-6

@@ -50,3 +50,11 @@ def test_suspend_resume_native(tmp_path):
     r = _run("resnet_ddp_apex.py", tmp_path, MASTER_PORT="29812")
     assert r.returncode == 0, r.stderr[-4000:]
     assert "resume: epoch 0 step 2" in r.stdout
+
+
+def test_entrypoint_native_exact_fp32(tmp_path):
+    """MX_DTYPE=fp32 (the reference scripts' own precision) runs on the native engine too."""
+    r = _run("resnet_single_gpu.py", tmp_path, MX_DTYPE="fp32")
+    assert r.returncode == 0, r.stderr[-4000:]
+    m = (tmp_path / "output" / "resnet_single" / "metrics.jsonl").read_text()
+    assert '"engine": "native"' in m and "float32" in m
