@@ -93,6 +93,12 @@ class DistributedDataParallel(nn.Module):
         self.broadcast_buffers = broadcast_buffers
         dev = next(module.parameters()).device
         self.comm = comm if comm is not None else make_communicator(dev, process_group)
+        # failure detection: poll the RCCL communicator's async error state from a
+        # daemon thread; a dead peer aborts the communicator so collectives return (and the next
+        # bucket wait raises) instead of hanging the job. MX_WATCHDOG=0 disables.
+        import os
+        if hasattr(self.comm, "start_watchdog") and os.environ.get("MX_WATCHDOG", "1") != "0":
+            self.comm.start_watchdog(float(os.environ.get("MX_WATCHDOG_S", "5")))
         self._native = hasattr(module, "flat_params")
         cap = bucket_cap_mb or 32.0
         if self._native:
