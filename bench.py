@@ -51,6 +51,7 @@ def main():
     if args.gpus != world and world > 1:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
     os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    os.environ.setdefault("MX_WATCHDOG", "0")   # timed runs: no polling thread beside the step
     ndev = max(torch.cuda.device_count(), 1)
     device = torch.device("cuda", local_rank % ndev)   # >1 rank per GPU only in CPU-side rehearsals
     torch.cuda.set_device(device)
