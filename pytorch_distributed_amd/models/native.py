@@ -352,6 +352,12 @@ class NativeResNet(nn.Module):
         S = ds.image_size
 
         def gen(ids: torch.Tensor):
+            if ids.device.type == "cpu" and not ids.is_pinned():
+                # a pageable H2D copy blocks the host until the device has drained every earlier
+                # launch (the whole previous step), after which the forward's small kernels run
+                # ahead of the host's launches and leave the GPU idle between them (~0.7 ms/step
+                # measured, tools/gap_analysis.py); from pinned memory the copy is a queued DMA
+                ids = ids.pin_memory()
             ids_d = ids.to(self.device, non_blocking=True)
             B = ids_d.numel()
             x = self._empty(B, S // 2, S // 2, 16)
