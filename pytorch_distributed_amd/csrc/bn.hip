@@ -129,7 +129,7 @@ template <int DT>
 __global__ __launch_bounds__(NT) void bn_apply_kernel(
     const void* __restrict__ y, const float* __restrict__ sc, const float* __restrict__ sh,
     const void* __restrict__ r2, const float* __restrict__ sc2, const float* __restrict__ sh2,
-    void* __restrict__ out, int n8, int C, int mode, int relu) {
+    void* __restrict__ out, int n8, int C, int mode, int relu, uint8_t* __restrict__ mask) {
   const int C8 = C >> 3;
   const int stride = gridDim.x * NT;
   const bool fixed = (stride % C8) == 0;
@@ -158,12 +158,19 @@ __global__ __launch_bounds__(NT) void bn_apply_kernel(
         o[e] = relu ? fmaxf(v, 0.f) : v;
       }
       store8<DT>(out, (size_t)i * 8, o);
+      if (mask) {
+        uint32_t bits = 0;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) bits |= (o[e] > 0.f ? 1u : 0u) << e;
+        mask[i] = (uint8_t)bits;
+      }
       continue;
     }
     const i32x4 yv = reinterpret_cast<const i32x4*>(y)[i];
     i32x4 rv = {0, 0, 0, 0};
     if (mode) rv = reinterpret_cast<const i32x4*>(r2)[i];
     i32x4 o;
+    uint32_t bits = 0;   // ReLU mask of the output (bit e = element e > 0), for the backward
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
       f32x2 v = unpack2<DT>((uint32_t)yv[k]) * a[k] + b[k];
@@ -174,8 +181,11 @@ __global__ __launch_bounds__(NT) void bn_apply_kernel(
       }
       if (relu) v = f32x2{fmaxf(v.x, 0.f), fmaxf(v.y, 0.f)};
       o[k] = (int)pack2<DT>(v);
+      bits |= (v.x > 0.f ? 1u : 0u) << (2 * k);
+      bits |= (v.y > 0.f ? 1u : 0u) << (2 * k + 1);
     }
     reinterpret_cast<i32x4*>(out)[i] = o;
+    if (mask) mask[i] = (uint8_t)bits;
   }
 }
 
@@ -693,13 +703,16 @@ static FastDiv make_div(uint32_t d) {
   return f;
 }
 
+// mask (nullable): one byte per 8 elements, bit e = (output element e > 0) -- lets the backward of an
+// identity-shortcut tail skip re-reading the residual to rebuild its ReLU mask
 int pda_bn_apply(const void* y, const float* sc, const float* sh, const void* r2, const float* sc2,
-                 const float* sh2, void* out, long long numel, int C, int mode, int relu, int dt,
-                 hipStream_t st) {
+                 const float* sh2, void* out, long long numel, int C, int mode, int relu,
+                 void* mask, int dt, hipStream_t st) {
   if (numel / 8 >= (1ll << 31)) return -2;
   const int n8 = (int)(numel / 8);
   const int g = grid_for(n8);
-#define ARGS (const void*)y, sc, sh, (const void*)r2, sc2, sh2, (void*)out, n8, C, mode, relu
+#define ARGS (const void*)y, sc, sh, (const void*)r2, sc2, sh2, (void*)out, n8, C, mode, relu, \
+             (uint8_t*)mask
   if (dt == DT_BF16) hipLaunchKernelGGL(bn_apply_kernel<DT_BF16>, dim3(g), dim3(NT), 0, st, ARGS);
   else if (dt == DT_F32) hipLaunchKernelGGL(bn_apply_kernel<DT_F32>, dim3(g), dim3(NT), 0, st, ARGS);
   else hipLaunchKernelGGL(bn_apply_kernel<DT_F16>, dim3(g), dim3(NT), 0, st, ARGS);

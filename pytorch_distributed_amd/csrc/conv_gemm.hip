@@ -60,10 +60,12 @@ struct ConvParams {
   const float* pro_sc;
   const float* pro_sh;
   // DGRAD fused BatchNorm-backward epilogue (emode < 0: plain dX store)
-  int emode, enq;                 // 0 relu(bn(y)), 1 relu(bn(y)+ey2), 2 relu(bn(y)+bn2(ey2))
+  int emode, enq;                 // 0 relu(bn(y)), 1 relu(bn(y)+ey2), 2 relu(bn(y)+bn2(ey2)),
+                                  // 3 as 1 with the ReLU mask read from emask (no residual read)
   const void* ey; const float* esc; const float* esh;
   const void* ey2; const float* esc2; const float* esh2;
   const void* eg2;                 // optional second gradient summed into dA
+  const uint8_t* emask;            // mode 3: forward ReLU bitmask of a (1 byte per 8 elements)
   float* epart;                    // [ncls*tiles_m][enq][N] partial sums
 };
 
@@ -618,8 +620,9 @@ __global__ __launch_bounds__(NT, (STAGES == 1 && BM * BN <= 128 * 128) ? 3 : 2) 
       constexpr bool G2 = decltype(g2_c)::value != 0;
       constexpr int NQ = MODE == 2 ? 3 : 2;
       const bool do_stats = MODE >= 0 || (PASS == FWD && p.stats != nullptr);
+      constexpr bool Y2 = MODE == 1 || MODE == 2;   // residual / shortcut tensor read
       f32x2 esc[4], esh[4], esc2[4], esh2[4];
-      if constexpr (MODE >= 0) {
+      if constexpr (MODE >= 0 && MODE != 3) {
         const int cg = gcol < p.N ? gcol : 0;
 #pragma unroll
         for (int k = 0; k < EPC / 2; ++k) {
@@ -634,6 +637,7 @@ __global__ __launch_bounds__(NT, (STAGES == 1 && BM * BN <= 128 * 128) ? 3 : 2) 
       uint32_t eoff[PD];
       bool eok[PD];
       i32x4 py[PD], pg2[PD], py2[PD];
+      uint32_t pm[PD];
       auto prefetch = [&](int g0) {
         const i32x4 z = {0, 0, 0, 0};
 #pragma unroll
@@ -644,8 +648,9 @@ __global__ __launch_bounds__(NT, (STAGES == 1 && BM * BN <= 128 * 128) ? 3 : 2) 
             py[j] = eok[j] ? *reinterpret_cast<const i32x4*>(reinterpret_cast<const char*>(p.ey) + bo) : z;
           if constexpr (G2)
             pg2[j] = eok[j] ? *reinterpret_cast<const i32x4*>(reinterpret_cast<const char*>(p.eg2) + bo) : z;
-          if constexpr (MODE >= 1)
+          if constexpr (Y2)
             py2[j] = eok[j] ? *reinterpret_cast<const i32x4*>(reinterpret_cast<const char*>(p.ey2) + bo) : z;
+          if constexpr (MODE == 3) pm[j] = eok[j] ? (uint32_t)p.emask[eoff[j] >> 3] >> (eoff[j] & 7) : 0u;
         }
       };
       f32x2 q0[4], q1[4], q2[4];
@@ -669,12 +674,16 @@ __global__ __launch_bounds__(NT, (STAGES == 1 && BM * BN <= 128 * 128) ? 3 : 2) 
               if constexpr (MODE >= 0) {
                 if constexpr (G2) f += __int_as_float(pg2[j][e]);
                 const float yv = __int_as_float(py[j][e]);
-                float pre = yv * esc[k][h] + esh[k][h];
-                float y2v = 0.f;
-                if constexpr (MODE >= 1) y2v = __int_as_float(py2[j][e]);
-                if constexpr (MODE == 1) pre += y2v;
-                if constexpr (MODE == 2) pre += y2v * esc2[k][h] + esh2[k][h];
-                const float dz = pre > 0.f ? f : 0.f;
+                float y2v = 0.f, dz;
+                if constexpr (MODE == 3) {
+                  dz = ((pm[j] >> e) & 1u) ? f : 0.f;
+                } else {
+                  float pre = yv * esc[k][h] + esh[k][h];
+                  if constexpr (Y2) y2v = __int_as_float(py2[j][e]);
+                  if constexpr (MODE == 1) pre += y2v;
+                  if constexpr (MODE == 2) pre += y2v * esc2[k][h] + esh2[k][h];
+                  dz = pre > 0.f ? f : 0.f;
+                }
                 v[e] = __float_as_int(dz);
                 q0[k][h] += dz;
                 q1[k][h] += dz * yv;
@@ -690,12 +699,17 @@ __global__ __launch_bounds__(NT, (STAGES == 1 && BM * BN <= 128 * 128) ? 3 : 2) 
               f32x2 g = unpack2<DT>((uint32_t)v[k]);
               if constexpr (G2) g += unpack2<DT>((uint32_t)pg2[j][k]);
               const f32x2 yv = unpack2<DT>((uint32_t)py[j][k]);
-              f32x2 pre = yv * esc[k] + esh[k];
-              f32x2 y2v = f32x2{0.f, 0.f};
-              if constexpr (MODE >= 1) y2v = unpack2<DT>((uint32_t)py2[j][k]);
-              if constexpr (MODE == 1) pre += y2v;
-              if constexpr (MODE == 2) pre += y2v * esc2[k] + esh2[k];
-              f32x2 dz = f32x2{pre.x > 0.f ? g.x : 0.f, pre.y > 0.f ? g.y : 0.f};
+              f32x2 y2v = f32x2{0.f, 0.f}, dz;
+              if constexpr (MODE == 3) {
+                const uint32_t mb = pm[j] >> (2 * k);
+                dz = f32x2{(mb & 1u) ? g.x : 0.f, (mb & 2u) ? g.y : 0.f};
+              } else {
+                f32x2 pre = yv * esc[k] + esh[k];
+                if constexpr (Y2) y2v = unpack2<DT>((uint32_t)py2[j][k]);
+                if constexpr (MODE == 1) pre += y2v;
+                if constexpr (MODE == 2) pre += y2v * esc2[k] + esh2[k];
+                dz = f32x2{pre.x > 0.f ? g.x : 0.f, pre.y > 0.f ? g.y : 0.f};
+              }
               const uint32_t o = pack2<DT>(dz);
               if constexpr (G2) dz = unpack2<DT>(o);   // statistics of the stored (rounded) dz
               v[k] = (int)o;
@@ -748,6 +762,7 @@ __global__ __launch_bounds__(NT, (STAGES == 1 && BM * BN <= 128 * 128) ? 3 : 2) 
       if (p.emode < 0) rows(IC<-1>{}, IC<0>{});
       else if (p.emode == 0) { if (g2) rows(IC<0>{}, IC<1>{}); else rows(IC<0>{}, IC<0>{}); }
       else if (p.emode == 1) { if (g2) rows(IC<1>{}, IC<1>{}); else rows(IC<1>{}, IC<0>{}); }
+      else if (p.emode == 3) { if (g2) rows(IC<3>{}, IC<1>{}); else rows(IC<3>{}, IC<0>{}); }
       else { if (g2) rows(IC<2>{}, IC<1>{}); else rows(IC<2>{}, IC<0>{}); }
     } else {
       rows(IC<-1>{}, IC<0>{});
@@ -906,6 +921,7 @@ struct BnEpi {  // mirrors ops/ext.py BnEpi
   const void* y; const float* sc; const float* sh;
   const void* y2; const float* sc2; const float* sh2;
   const void* g2; float* part;
+  const void* mask;
 };
 
 int pda_conv_dgrad(const ConvDesc* d, const void* dy, const void* w, void* dx, const BnEpi* epi,
@@ -922,6 +938,7 @@ int pda_conv_dgrad(const ConvDesc* d, const void* dy, const void* w, void* dx, c
     p.ey = epi->y; p.esc = epi->sc; p.esh = epi->sh;
     p.ey2 = epi->y2; p.esc2 = epi->sc2; p.esh2 = epi->sh2;
     p.eg2 = epi->g2; p.epart = epi->part;
+    p.emask = (const uint8_t*)epi->mask;
   }
   p.N = d->Cin; p.out_pitch = d->Cin;
   const int sd = d->stride;

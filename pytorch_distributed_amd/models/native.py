@@ -123,6 +123,7 @@ class NativeResNet(nn.Module):
         import os
         self.fuse_prologue = os.environ.get("PDA_FUSE_PROLOGUE", "1") != "0"
         self.fused_stem_bwd = os.environ.get("PDA_FUSED_STEM_BWD", "1") != "0"
+        self.tail_mask = os.environ.get("PDA_TAIL_MASK", "1") != "0"
         # weight gradients on a second HIP stream: nothing in the backward chain consumes them, so
         # the (compute-bound) wgrad GEMMs fill the CUs left idle by the (HBM-bound) BN-backward
         # passes and small finalize launches of the dgrad chain on the main stream
@@ -474,7 +475,13 @@ class NativeResNet(nn.Module):
                 if yd is not None:
                     K.bn_apply(ys[-1], sc, sh, out, y2=yd, scale2=b.ds.state[2], shift2=b.ds.state[3])
                 else:
-                    K.bn_apply(ys[-1], sc, sh, out, res=h)
+                    # identity tail: keep its ReLU bitmask (1/16 of the tensor) so the backward
+                    # rebuilds the mask without re-reading the residual
+                    mask = (torch.empty(out.numel() // 8, dtype=torch.uint8, device=self.device)
+                            if save and self.tail_mask else None)
+                    K.bn_apply(ys[-1], sc, sh, out, res=h, mask=mask)
+                    if save:
+                        rec["mask"] = mask
             if save:
                 rec["ys"], rec["acts"], rec["yd"] = ys, acts, yd
                 saved["blocks"].append(rec)
@@ -601,7 +608,7 @@ class NativeResNet(nn.Module):
         self._grads_zero = False
         self._fwd_ctx = None
 
-    def _tail_args(self, b: Block, rec):
+    def _tail_args(self, b: Block, rec, use_mask: bool = False):
         """Tensors describing a = relu(bn3(y3) + shortcut) of block b for the BN-backward."""
         ul = b.units[-1]
         sl = rec[f"s{len(b.units) - 1}"]
@@ -609,6 +616,8 @@ class NativeResNet(nn.Module):
         if b.ds is not None:
             sd = rec["sd"]
             d.update(y2=rec["yd"], scale2=sd[2], shift2=sd[3])
+        elif use_mask and rec.get("mask") is not None:
+            d.update(mask=rec["mask"])
         else:
             d.update(res=rec["x"])
         return d
@@ -688,7 +697,8 @@ class NativeResNet(nn.Module):
             elif prev is not None:
                 pb, prec = prev
                 Gp = K.dgrad_slabs(g, Nb)
-                epi, part_p, nq_p = K.bn_epilogue(ws, Gp, g2=shortcut_g, **self._tail_args(pb, prec))
+                epi, part_p, nq_p = K.bn_epilogue(ws, Gp, g2=shortcut_g,
+                                                  **self._tail_args(pb, prec, use_mask=True))
                 K.conv_dgrad(dy, self.w16_ohwi(u), g, out, epi=epi)      # out = dz of prev tail
                 prev_tail = (out, part_p, Gp, nq_p)
             else:

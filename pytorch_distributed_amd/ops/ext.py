@@ -47,7 +47,7 @@ class BnEpi(C.Structure):
     _fields_ = [("mode", C.c_int), ("nq", C.c_int),
                 ("y", C.c_void_p), ("sc", C.c_void_p), ("sh", C.c_void_p),
                 ("y2", C.c_void_p), ("sc2", C.c_void_p), ("sh2", C.c_void_p),
-                ("g2", C.c_void_p), ("part", C.c_void_p)]
+                ("g2", C.c_void_p), ("part", C.c_void_p), ("mask", C.c_void_p)]
 
 
 _V, _I, _F, _L, _U = C.c_void_p, C.c_int, C.c_float, C.c_longlong, C.c_uint
@@ -59,7 +59,7 @@ _SIGS = {
     "pda_bn_finalize_fwd": [_V, _I, _I, _F, _V, _V, _F, _F, _V, _V, _V, _V, _V, _V, _V, _I, _V],
     "pda_slab_reduce": [_V, _I, _I, _I, _V, _V],
     "pda_bn_eval_coeffs": [_V, _V, _V, _V, _F, _I, _V, _V, _V],
-    "pda_bn_apply": [_V, _V, _V, _V, _V, _V, _V, _L, _I, _I, _I, _I, _V],
+    "pda_bn_apply": [_V, _V, _V, _V, _V, _V, _V, _L, _I, _I, _I, _V, _I, _V],
     "pda_stem_pool": [_V, _V, _V, _V, _V, _I, _I, _I, _I, _I, _I, _I, _V],
     "pda_maxpool_bwd": [_V, _V, _V, _V, _I, _I, _I, _I, _I, _I, _I, _V],
     "pda_tail_pool": [_V, _V, _V, _V, _V, _V, _V, _I, _I, _I, _I, _I, _V],

@@ -164,15 +164,18 @@ def conv_dgrad(dy: torch.Tensor, w: torch.Tensor, g: ConvGeom, dx: torch.Tensor,
 
 
 def bn_epilogue(ws: "Workspace", G: int, y, scale, shift, res=None, y2=None, scale2=None,
-                shift2=None, g2=None):
+                shift2=None, g2=None, mask=None):
     """Describe the BN-backward reduction a dgrad epilogue performs for a = relu(bn(y) [+res | +bn2(y2)]).
+    ``mask`` (the forward's ReLU bitmask of a, see :func:`bn_apply`) replaces ``res``: the epilogue
+    then reads one byte per 8 elements instead of the residual tensor (mode 3).
     Returns (epi, part, nq); ``part`` holds G*nq*C floats after the dgrad."""
     C_ = y.shape[-1]
-    mode = 2 if y2 is not None else (1 if res is not None else 0)
+    mode = 3 if mask is not None else (2 if y2 is not None else (1 if res is not None else 0))
     nq = 3 if mode == 2 else 2
     part = ws.get("bn_part", G * nq * C_)
     epi = ext.BnEpi(mode, nq, ptr(y), ptr(scale), ptr(shift),
-                    ptr(y2 if y2 is not None else res), ptr(scale2), ptr(shift2), ptr(g2), ptr(part))
+                    ptr(y2 if y2 is not None else res), ptr(scale2), ptr(shift2), ptr(g2), ptr(part),
+                    ptr(mask))
     return epi, part, nq
 
 
@@ -292,12 +295,15 @@ def bn_eval_coeffs(gamma, beta, rmean, rvar, eps, scale, shift) -> None:
     check(rc, "bn_eval_coeffs")
 
 
-def bn_apply(y, scale, shift, out, res=None, y2=None, scale2=None, shift2=None, relu=True):
+def bn_apply(y, scale, shift, out, res=None, y2=None, scale2=None, shift2=None, relu=True,
+             mask=None):
+    """out = act(bn(y) [+ res | + bn2(y2)]); mask (uint8, numel/8) optionally receives the output's
+    ReLU bitmask (bit e of byte i: element 8i+e > 0)."""
     mode = 2 if y2 is not None else (1 if res is not None else 0)
     r2 = y2 if y2 is not None else res
     rc = ext.lib().pda_bn_apply(ptr(y), ptr(scale), ptr(shift), ptr(r2), ptr(scale2), ptr(shift2),
-                                ptr(out), y.numel(), y.shape[-1], mode, int(relu), dt_of(y),
-                                stream(y.device))
+                                ptr(out), y.numel(), y.shape[-1], mode, int(relu), ptr(mask),
+                                dt_of(y), stream(y.device))
     check(rc, "bn_apply")
     return out
 

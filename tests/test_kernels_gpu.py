@@ -382,7 +382,7 @@ def test_synthetic_kernel_matches_torch_generator():
 
 @pytest.mark.parametrize("geo", [(2, 8, 64, 128), (8, 16, 64, 64)])
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
-@pytest.mark.parametrize("mode", ["relu", "res", "ds"])
+@pytest.mark.parametrize("mode", ["relu", "res", "ds", "mask"])
 @pytest.mark.parametrize("stride", [1, 2])
 def test_dgrad_fused_bn_backward(mode, stride, dtype, geo):
     """dgrad epilogue (mask + BN-backward partial sums) == plain dgrad followed by the standalone
@@ -404,7 +404,7 @@ def test_dgrad_fused_bn_backward(mode, stride, dtype, geo):
     gamma, gamma2 = torch.rand(Cin, device=DEV) + 0.5, torch.rand(Cin, device=DEV) + 0.5
     ws = K.Workspace(DEV)
     kw = {}
-    if mode == "res":
+    if mode in ("res", "mask"):
         kw = dict(res=y2)
     elif mode == "ds":
         kw = dict(y2=y2, scale2=sc2, shift2=sh2)
@@ -424,6 +424,10 @@ def test_dgrad_fused_bn_backward(mode, stride, dtype, geo):
              g2=g2 if use_g2 else None, dz_buf=dz_ref, **kw, **extra)
     # fused
     G = K.dgrad_slabs(g, Nb)
+    if mode == "mask":   # the forward tail's ReLU bitmask replaces the residual read
+        mask = torch.empty(y.numel() // 8, dtype=torch.uint8, device=DEV)
+        K.bn_apply(y, sc, sh, torch.empty_like(y), res=y2, mask=mask)
+        kw = dict(mask=mask)
     epi, part, nq = K.bn_epilogue(ws, G, y, sc, sh, g2=g2 if use_g2 else None, **kw)
     dz = torch.empty_like(y)
     K.conv_dgrad(dy, w, g, dz, epi=epi)
