@@ -22,8 +22,9 @@ import time
 
 import torch
 
-BASELINE = {1: 717.0, 8: 5546.7}
-GRAPH_DEFAULT = os.environ.get("PDA_GRAPH", "0") == "1"   # BASELINE.md derived images/sec (other hardware)
+BASELINE = {1: 717.0, 8: 5546.7}      # BASELINE.md derived images/sec (other hardware)
+BASELINE_DP = {1: 717.0, 8: 1301.2}   # the nn.DataParallel bar of result.png
+GRAPH_DEFAULT = os.environ.get("PDA_GRAPH", "0") == "1"
 
 
 def parse():
@@ -38,6 +39,8 @@ def parse():
     ap.add_argument("--bucket-mb", type=float, default=32.0)
     ap.add_argument("--image-size", type=int, default=224)
     ap.add_argument("--profile-steps", type=int, default=0)
+    ap.add_argument("--dp", action="store_true",
+                    help="single-process DataParallel over --gpus devices (resnet_dp.py config)")
     ap.add_argument("--graph", type=int, default=-1,
                     help="capture the step in a HIP graph (1/0; default: on for 1 GPU, native engine)")
     return ap.parse_args()
@@ -67,19 +70,29 @@ def main():
     from pytorch_distributed_amd.bench_step import make_trainer
     dtype = {"bf16": torch.bfloat16, "fp16": torch.float16, "fp32": torch.float32}[args.dtype]
     graph = args.graph == 1 or (args.graph < 0 and world == 1 and GRAPH_DEFAULT)
-    tr = make_trainer(args.arch, args.batch, dtype, device, engine=args.engine,
-                      world=world, rank=rank, bucket_mb=args.bucket_mb, image_size=args.image_size,
-                      graph=graph)
+    if args.dp:
+        if world > 1:
+            raise SystemExit("--dp is one process driving --gpus devices; do not launch it with torchrun")
+        from pytorch_distributed_amd.bench_step import make_dp_trainer
+        tr = make_dp_trainer(args.arch, args.batch, dtype, args.gpus, args.image_size)
+        world = args.gpus            # images/sec over all devices of the process
+        sync_all = lambda: [torch.cuda.synchronize(d) for d in range(args.gpus)]  # noqa: E731
+    else:
+        tr = make_trainer(args.arch, args.batch, dtype, device, engine=args.engine,
+                          world=world, rank=rank, bucket_mb=args.bucket_mb, image_size=args.image_size,
+                          graph=graph)
+        sync_all = torch.cuda.synchronize
 
     for i in range(args.warmup):
         tr.step(i)
-    torch.cuda.synchronize()
+    sync_all()
+    multi_proc = world > 1 and not args.dp
 
     def barrier():
-        if world > 1:
+        if multi_proc:
             import torch.distributed as dist
             dist.barrier()
-        torch.cuda.synchronize()
+        sync_all()
 
     barrier()
     t0 = time.perf_counter()
@@ -87,7 +100,7 @@ def main():
         tr.step(args.warmup + i)
     barrier()
     elapsed = time.perf_counter() - t0
-    if world > 1:
+    if multi_proc:
         import torch.distributed as dist
         t = torch.tensor([elapsed], device=device, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -95,7 +108,7 @@ def main():
     loss = tr.last_loss()
     ms = 1000.0 * elapsed / max(args.steps, 1)
     value = args.batch * world * args.steps / elapsed
-    base = BASELINE.get(world)
+    base = (BASELINE_DP if args.dp else BASELINE).get(world)
     if rank == 0:
         rec = {
             "metric": "images/sec (whole node) ResNet-50 bs=400",
@@ -112,14 +125,15 @@ def main():
             "data": "synthetic (on-device generated 3x224x224, random-init weights)",
             "config": {"model": args.arch, "global_batch": args.batch * world,
                        "per_gpu_batch": args.batch, "seq_len": None,
-                       "parallelism": f"dp{world}", "engine": tr.engine,
+                       "parallelism": (f"dataparallel{world}" if args.dp else f"dp{world}"),
+                       "engine": tr.engine,
                        "hip_graph": bool(getattr(tr, "graphed", None)),
                        "optimizer": "SGD(lr=0.1, momentum=0.9, wd=1e-4)"},
             "loss": loss,
             "max_mem_gb": round(torch.cuda.max_memory_allocated(device) / 1e9, 2),
         }
         print(json.dumps(rec), flush=True)
-    if world > 1:
+    if multi_proc:
         import torch.distributed as dist
         dist.destroy_process_group()
 

@@ -55,6 +55,46 @@ class _TorchTrainer:
         return None if self._loss is None else float(self._loss.item())
 
 
+class _DPTrainer:
+    """Single-process multi-GPU DataParallel step (the reference's ``resnet_dp.py`` configuration):
+    one native replica per GPU, each replica's forward+loss+backward replayed from a HIP graph,
+    one grouped in-process RCCL all-reduce, replicated fused SGD. Each GPU generates its own chunk
+    of the global batch (no scatter from GPU 0)."""
+
+    engine = "native-dp"
+
+    def __init__(self, arch, batch, dtype, devices, image_size):
+        from .models.native import NativeResNet
+        from .models.resnet import build_model
+        from .parallel.dp import DataParallel
+        torch.manual_seed(0)
+        dev0 = torch.device("cuda", devices[0])
+        self.dp = DataParallel(NativeResNet(build_model(arch), device=dev0, dtype=dtype,
+                                            image_size=image_size), device_ids=list(devices))
+        self.opt = self.dp.make_optimizer(lr=0.1, momentum=0.9, weight_decay=1e-4)
+        ds = SyntheticImageNet("train", seed=0, image_size=image_size)
+        self.gens = [m.input_generator(ds) for m in self.dp.all_modules]
+        self.batch, self.n = batch, len(devices)
+        self.graphed = True
+        self._loss = None
+
+    def step(self, i: int) -> None:
+        base = i * self.batch * self.n
+        xs, ys = [], []
+        for r, g in enumerate(self.gens):
+            x, y = g(torch.arange(self.batch, dtype=torch.int64) + base + r * self.batch)
+            xs.append(x)
+            ys.append(y)
+        self._loss = self.dp.train_step_chunks(xs, ys, self.opt)
+
+    def last_loss(self) -> Optional[float]:
+        return None if self._loss is None else float(self._loss.item())
+
+
+def make_dp_trainer(arch: str, batch: int, dtype: torch.dtype, ngpus: int, image_size: int = 224):
+    return _DPTrainer(arch, batch, dtype, list(range(ngpus)), image_size)
+
+
 def make_trainer(arch: str, batch: int, dtype: torch.dtype, device: torch.device,
                  engine: str = "auto", world: int = 1, rank: int = 0, bucket_mb: float = 32.0,
                  image_size: int = 224, graph: bool = False):

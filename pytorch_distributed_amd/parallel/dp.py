@@ -254,11 +254,15 @@ class DataParallel(nn.Module):
         optimizer.step()``: the loss is the mean over the GLOBAL batch (each replica's gradient
         is scaled by 1/B_global), BN statistics are per replica, BN buffers follow replica 0,
         gradients are SUM-all-reduced by one grouped RCCL call, then the replicated fused SGD."""
-        from ..ops import native_ops as K
-        self._broadcast_state()
-        B = samples.shape[0]
         xs = torch.chunk(samples, len(self.device_ids), 0)
         ys = torch.chunk(labels, len(self.device_ids), 0)
+        return self.train_step_chunks(xs, ys, optimizer, graph)
+
+    def train_step_chunks(self, xs, ys, optimizer, graph: bool = True) -> torch.Tensor:
+        """:meth:`train_step` on per-replica input chunks (e.g. generated on each GPU directly,
+        skipping the scatter from ``device_ids[0]``)."""
+        self._broadcast_state()
+        B = sum(x.shape[0] for x in xs)
         if getattr(self, "_graphs", None) is None or [x.shape for x in xs] != self._graph_shapes:
             self._graphs = [_ReplicaGraph(m, x.shape, B) for m, x in zip(self.all_modules, xs)]
             self._graph_shapes = [x.shape for x in xs]
