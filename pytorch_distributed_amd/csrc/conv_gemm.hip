@@ -155,11 +155,14 @@ __global__ __launch_bounds__(NT, (STAGES == 1 && BM * BN <= 128 * 128) ? 3 : 2) 
   constexpr int A_BYTES = BM * 128, B_BYTES = BN * 128;
   constexpr int STAGE = A_BYTES + B_BYTES;
   constexpr int RED_BYTES = 3 * NT * 8 * 4;
-  constexpr int C_BYTES = BM * BN * ES;  // staged C tile of the epilogue
+  // staged C tile of the epilogue; f32 stages it in two row halves (one per wave row), so the
+  // epilogue needs no more LDS than the main loop and f32 tiles keep 3 resident blocks per CU
+  constexpr int NH = F32 ? 2 : 1;
+  constexpr int C_BYTES = BM / NH * BN * ES;
   constexpr int LDS_0 = STAGES * STAGE > RED_BYTES ? STAGES * STAGE : RED_BYTES;
   constexpr int LDS_BYTES = LDS_0 > C_BYTES ? LDS_0 : C_BYTES;
   static_assert(BN <= NT, "stats reduction: one thread per column");
-  static_assert(BM * BN * ES <= LDS_BYTES, "C tile must fit in the staging buffers");
+  static_assert(C_BYTES <= LDS_BYTES, "C tile must fit in the staging buffers");
   static_assert(3 * NT * 8 * 4 <= LDS_BYTES, "stats reduction must fit");
   __shared__ __attribute__((aligned(16))) char smem[LDS_BYTES];
 
@@ -561,18 +564,27 @@ __global__ __launch_bounds__(NT, (STAGES == 1 && BM * BN <= 128 * 128) ? 3 : 2) 
     // row; one packed 8-byte store (4 columns) per MFMA tile per lane (f32: one 16-B store).
     constexpr int CPR = BN / EPC;
     auto c_addr = [&](int row, int chunk) { return row * CPR + (chunk ^ (row & (CPR - 1))); };
-    {
+    // f32: the waves of wave-row h write their tiles to local rows [0, BM/2) of the LDS image
+    auto stage_f32 = [&](int h) {
+      if (wr != h) return;
+#pragma unroll
+      for (int j = 0; j < NI; ++j) {
+        const int col = wc * (BN / 2) + j * 16 + 4 * lg;
+#pragma unroll
+        for (int i = 0; i < MI; ++i) {
+          const int row = i * 16 + lr;
+          *reinterpret_cast<f32x4*>(smem + row * (BN * 4) + (((col >> 2) ^ (row & (CPR - 1))) << 4)) =
+              acc[i][j];
+        }
+      }
+    };
+    if constexpr (!F32) {
 #pragma unroll
       for (int j = 0; j < NI; ++j) {
         const int col = wc * (BN / 2) + j * 16 + 4 * lg;
 #pragma unroll
         for (int i = 0; i < MI; ++i) {
           const int row = wr * (BM / 2) + i * 16 + lr;
-          if constexpr (F32) {
-            *reinterpret_cast<f32x4*>(smem + row * (BN * 4) + (((col >> 2) ^ (row & (CPR - 1))) << 4)) =
-                acc[i][j];
-            continue;
-          }
           // row & (CPR-1) == lr & (CPR-1) for CPR <= 16 (folded); BN = 256 needs the full row
           const int cbyte = (((col >> 3) ^ (row & (CPR - 1))) << 4) + ((col & 4) << 1);
           uint2 pk;
@@ -596,10 +608,11 @@ __global__ __launch_bounds__(NT, (STAGES == 1 && BM * BN <= 128 * 128) ? 3 : 2) 
     const int rg = tid / CPR;          // row group
     constexpr int RG = NT / CPR;       // row groups
     constexpr int RPT = BM / RG;       // rows per thread
+    constexpr int RPTH = RPT / NH;     // ... per staged half
     // rows are processed in groups of PD; the fused-epilogue operands of a group are loaded
     // before it is consumed (the first group's before the barrier that publishes the C tile),
     // which bounds the prefetch registers to PD rows.
-    constexpr int PD = RPT > 4 ? 4 : RPT;
+    constexpr int PD = RPTH > 4 ? 4 : RPTH;
     char* outb = reinterpret_cast<char*>(p.out);
     const int gcol = n0 + cc * EPC;
     auto row_off = [&](int i, bool& ok) -> uint32_t {
@@ -656,14 +669,20 @@ __global__ __launch_bounds__(NT, (STAGES == 1 && BM * BN <= 128 * 128) ? 3 : 2) 
       f32x2 q0[4], q1[4], q2[4];
 #pragma unroll
       for (int k = 0; k < 4; ++k) { q0[k] = f32x2{0.f, 0.f}; q1[k] = q0[k]; q2[k] = q0[k]; }
-      prefetch(0);
+#pragma unroll
+      for (int h = 0; h < NH; ++h) {
+      if constexpr (F32) {
+        if (h > 0) __syncthreads();   // every thread is done reading the previous half
+        stage_f32(h);
+      }
+      prefetch(h * RPTH);
       __syncthreads();
 #pragma unroll
-      for (int g0 = 0; g0 < RPT; g0 += PD) {
-        if (g0 > 0) prefetch(g0);
+      for (int g0 = 0; g0 < RPTH; g0 += PD) {
+        if (g0 > 0) prefetch(h * RPTH + g0);
 #pragma unroll
         for (int j = 0; j < PD; ++j) {
-          const int row = rg + RG * (g0 + j);
+          const int row = rg + RG * (g0 + j);   // local row of the staged half
           i32x4 v = *reinterpret_cast<const i32x4*>(ct + c_addr(row, cc) * 16);
           if (!eok[j]) continue;
           if constexpr (F32) {   // one element per dword
@@ -727,6 +746,7 @@ __global__ __launch_bounds__(NT, (STAGES == 1 && BM * BN <= 128 * 128) ? 3 : 2) 
           }
           *reinterpret_cast<i32x4*>(outb + (size_t)eoff[j] * ES) = v;
         }
+      }
       }
       if (do_stats) {
         __syncthreads();
