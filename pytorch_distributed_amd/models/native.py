@@ -124,6 +124,7 @@ class NativeResNet(nn.Module):
         self.fuse_prologue = os.environ.get("PDA_FUSE_PROLOGUE", "1") != "0"
         self.fused_stem_bwd = os.environ.get("PDA_FUSED_STEM_BWD", "1") != "0"
         self.tail_mask = os.environ.get("PDA_TAIL_MASK", "1") != "0"
+        self.ds_stream = os.environ.get("PDA_DS_STREAM", "1") != "0"
         # weight gradients on a second HIP stream: nothing in the backward chain consumes them, so
         # the (compute-bound) wgrad GEMMs fill the CUs left idle by the (HBM-bound) BN-backward
         # passes and small finalize launches of the dgrad chain on the main stream
@@ -388,9 +389,10 @@ class NativeResNet(nn.Module):
         return out
 
     # ------------------------------------------------------------------ forward
-    def _conv_bn(self, u: ConvBN, x: torch.Tensor, train: bool, pro=None) -> torch.Tensor:
+    def _conv_bn(self, u: ConvBN, x: torch.Tensor, train: bool, pro=None, ws=None) -> torch.Tensor:
         """y = conv(x) and BN coefficients (batch stats in training, running stats in eval).
         ``pro=(scale, shift)``: x is the previous PRE-BN tensor; the conv applies BN+ReLU on load."""
+        ws = self.ws if ws is None else ws
         Nb = x.shape[0]
         g = u.geom(Nb)
         M = Nb * g.Ho * g.Wo
@@ -398,13 +400,13 @@ class NativeResNet(nn.Module):
         st = u.state
         if train:
             T = K.stats_tiles(M, u.cout)
-            part = self.ws.get("fwd_stats", T * 2 * u.cout)
+            part = ws.get("fwd_stats", T * 2 * u.cout)
             K.conv_fwd(x, self.w16(u), g, y, stats=part, pro=pro)
             K.bn_finalize_fwd(part, T, u.cout, M, self.gamma(u), self.beta(u), u.bn.eps,
                               u.bn.momentum if u.bn.momentum is not None else 0.1,
                               st[0], st[1], st[2], st[3], self.rmean(u), self.rvar(u),
                               self.flat_nbt[u.nbt_idx:u.nbt_idx + 1], update_running=True,
-                              ws=self.ws)
+                              ws=ws)
         else:
             K.conv_fwd(x, self.w16(u), g, y, pro=pro)
             K.bn_eval_coeffs(self.gamma(u), self.beta(u), self.rmean(u), self.rvar(u), u.bn.eps,
@@ -442,6 +444,13 @@ class NativeResNet(nn.Module):
             a = h
             ys, acts = [], [h]
             pro = None
+            yd = None
+            ds_side = b.ds is not None and self._side is not None and self.ds_stream
+            if ds_side:   # the shortcut conv (+BN stats) runs beside conv1..conv3 on the 2nd stream
+                cur = torch.cuda.current_stream(self.device)
+                self._side.wait_stream(cur)
+                with torch.cuda.stream(self._side):
+                    yd = self._conv_bn(b.ds, h, train, ws=self.ws_w)
             for j, u in enumerate(b.units):
                 y = self._conv_bn(u, a, train, pro)
                 ys.append(y)
@@ -456,9 +465,11 @@ class NativeResNet(nn.Module):
                         a, pro = self._empty(*y.shape), None
                         K.bn_apply(y, sc, sh, a, relu=True)
                         acts.append(a)
-            yd = None
             if b.ds is not None:
-                yd = self._conv_bn(b.ds, h, train)
+                if ds_side:
+                    cur.wait_stream(self._side)
+                else:
+                    yd = self._conv_bn(b.ds, h, train)
                 if save:
                     rec["sd"] = b.ds.state
             ul = b.units[-1]
