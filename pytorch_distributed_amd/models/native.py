@@ -662,6 +662,7 @@ class NativeResNet(nn.Module):
         sl = rec[f"s{n - 1}"]
         dz, part, G, nq = tail
         dy = self._empty(*ys[-1].shape)
+        sc_ev = None
         if b.ds is not None:
             sd = rec["sd"]
             dyd = self._empty(*yd.shape)
@@ -669,18 +670,29 @@ class NativeResNet(nn.Module):
                             self.dbeta(ul), dz, dy, y2=yd, mean2=sd[0], invstd2=sd[1],
                             gamma2=self.gamma(b.ds), dgamma2=self.dgamma(b.ds), dbeta2=self.dbeta(b.ds),
                             dy2_out=dyd, accumulate=acc)
-            # shortcut branch first: its dX is the second gradient source of the previous tail
+            # shortcut branch first: its dX is the second gradient source of the previous tail.
+            # On the second stream its dgrad overlaps the conv3/conv2 chain; an event marks it for
+            # the conv1 dgrad epilogue (or the stem) that consumes it
             g = b.ds.geom(Nb)
+            shortcut_g = self._empty(*x.shape)
+            if self._side is not None and self.ds_stream:
+                self._side.wait_stream(torch.cuda.current_stream(self.device))
+                with torch.cuda.stream(self._side):
+                    K.conv_dgrad(dyd, self.w16_ohwi(b.ds), g, shortcut_g)
+                sc_ev = torch.cuda.Event()
+                sc_ev.record(self._side)
+                self._keep.extend([dyd, shortcut_g])
+            else:
+                K.conv_dgrad(dyd, self.w16_ohwi(b.ds), g, shortcut_g)
             self._wgrad(lambda w, u=b.ds, g=g, dyd=dyd: K.conv_wgrad(dyd, x, g, self.wgrad_view(u), w,
                                                                     accumulate=acc), dyd, x)
-            shortcut_g = self._empty(*x.shape)
-            K.conv_dgrad(dyd, self.w16_ohwi(b.ds), g, shortcut_g)
         else:
             K.bn_bwd_finish(ws, part, G, nq, ys[-1], sl[0], sl[1], self.gamma(ul), self.dgamma(ul),
                             self.dbeta(ul), dz, dy, accumulate=acc)
             shortcut_g = dz
         dx_main = None
         prev_tail = None
+        cur = torch.cuda.current_stream(self.device)
         for j in range(n - 1, -1, -1):
             u = b.units[j]
             a_in = acts[j]
@@ -707,6 +719,8 @@ class NativeResNet(nn.Module):
                 dy = dyp
             elif prev is not None:
                 pb, prec = prev
+                if sc_ev is not None:
+                    cur.wait_event(sc_ev)
                 Gp = K.dgrad_slabs(g, Nb)
                 epi, part_p, nq_p = K.bn_epilogue(ws, Gp, g2=shortcut_g,
                                                   **self._tail_args(pb, prec, use_mask=True))
@@ -715,6 +729,8 @@ class NativeResNet(nn.Module):
             else:
                 K.conv_dgrad(dy, self.w16_ohwi(u), g, out)
                 dx_main = out
+        if sc_ev is not None:   # the caller (next tail / stem backward) reads shortcut_g on main
+            cur.wait_event(sc_ev)
         return dx_main, shortcut_g, prev_tail
 
     # ------------------------------------------------------------------ nn.Module API
