@@ -156,3 +156,31 @@ def test_suspend_resume_cli(tmp_path):
     assert r.returncode == 0, r.stderr[-3000:]
     assert "resume: epoch 0 step 3" in r.stdout
     assert "epoch: 0, step: 3" in r.stdout and "epoch: 0, step: 2" not in r.stdout
+
+
+def test_resume_from_reference_format_checkpoint(tmp_path):
+    """Interop: a latest.pt written the way the reference writes it -- plain torch model / SGD /
+    StepLR state_dicts of a torchvision-layout model (reference restnet_ddp.py:37-44) -- resumes in
+    this framework's trainer; the final weights load back into the plain torch model."""
+    from pytorch_distributed_amd.models import build_model
+    torch.manual_seed(0)
+    model = build_model("resnet18", 10)          # the CLI env below uses MX_NUM_CLASSES=10
+    opt = torch.optim.SGD(model.parameters(), lr=0.1, momentum=0.9, weight_decay=1e-4)
+    sched = torch.optim.lr_scheduler.StepLR(opt, step_size=30, gamma=0.1)
+    x, y = torch.randn(4, 3, 32, 32), torch.randint(0, 10, (4,))
+    nn.functional.cross_entropy(model(x), y).backward()
+    opt.step()                                  # populates momentum buffers
+    out = tmp_path / "output" / "resnet_single"
+    out.mkdir(parents=True)
+    torch.save({"model": model.state_dict(), "optimizer": opt.state_dict(),
+                "scheduler": sched.state_dict(), "acc": 0.25, "epoch": 0, "step": 2},
+               out / "latest.pt")
+    env = _env(tmp_path, MX_EPOCHS="1", MX_STEPS_PER_EPOCH="4", MX_LOG_EVERY="1")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "resnet_single_gpu.py")], cwd=tmp_path,
+                       env=env, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert "resume: epoch 0 step 2 (best acc 0.25)" in r.stdout
+    assert "epoch: 0, step: 2" in r.stdout and "epoch: 0, step: 1" not in r.stdout
+    best = out / "best.pt"
+    if best.exists():                           # written only if accuracy beat 0.25
+        build_model("resnet18", 10).load_state_dict(torch.load(best, weights_only=True))

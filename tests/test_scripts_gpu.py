@@ -58,3 +58,25 @@ def test_entrypoint_native_exact_fp32(tmp_path):
     assert r.returncode == 0, r.stderr[-4000:]
     m = (tmp_path / "output" / "resnet_single" / "metrics.jsonl").read_text()
     assert '"engine": "native"' in m and "float32" in m
+
+
+def test_native_resume_from_reference_format_checkpoint(tmp_path):
+    """A latest.pt in the reference's format (plain torch ResNet-50 / SGD / StepLR state_dicts,
+    OIHW weights, per-parameter momentum buffers) resumes on the native engine."""
+    from pytorch_distributed_amd.models import build_model
+    torch.manual_seed(0)
+    model = build_model("resnet50")
+    opt = torch.optim.SGD(model.parameters(), lr=0.01, momentum=0.9, weight_decay=1e-4)
+    sched = torch.optim.lr_scheduler.StepLR(opt, step_size=30, gamma=0.1)
+    torch.nn.functional.cross_entropy(model(torch.randn(2, 3, 64, 64)),
+                                      torch.tensor([1, 2])).backward()
+    opt.step()
+    out = tmp_path / "output" / "resnet_single"
+    out.mkdir(parents=True)
+    torch.save({"model": model.state_dict(), "optimizer": opt.state_dict(),
+                "scheduler": sched.state_dict(), "acc": 0.5, "epoch": 1, "step": 1},
+               out / "latest.pt")
+    r = _run("resnet_single_gpu.py", tmp_path, MX_LOG_EVERY="1")
+    assert r.returncode == 0, r.stderr[-4000:]
+    assert "resume: epoch 1 step 1 (best acc 0.5)" in r.stdout
+    assert "epoch: 1, step: 1" in r.stdout and "epoch: 1, step: 0" not in r.stdout
