@@ -11,7 +11,7 @@ from __future__ import annotations
 
 import dataclasses
 import os
-from dataclasses import dataclass, field
+from dataclasses import dataclass
 from typing import Optional, Sequence
 
 __all__ = ["RunConfig", "SCRIPT_DEFAULTS", "config_for", "parse_cli"]

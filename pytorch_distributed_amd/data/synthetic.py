@@ -19,11 +19,11 @@ bit-compatible in the label and the uniform ``u`` (tested).
 from __future__ import annotations
 
 import math
-from typing import Iterator, Optional, Sequence, Tuple
+from typing import Iterator, Optional, Tuple
 
 import torch
 
-from .sampler import DistributedSampler, SequentialIndices
+from .sampler import SequentialIndices
 
 __all__ = [
     "MEAN", "STD", "hash32", "labels_for", "synthetic_images", "SyntheticImageNet",

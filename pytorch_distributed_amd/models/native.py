@@ -27,7 +27,7 @@ re-points their parameters/buffers into the flat storage.
 from __future__ import annotations
 
 import math
-from dataclasses import dataclass, field
+from dataclasses import dataclass
 from typing import Callable, Dict, List, Optional, Tuple
 
 import torch
@@ -36,7 +36,7 @@ from torch import nn
 from ..ops import ext
 from ..ops import native_ops as K
 from ..ops.native_ops import ConvGeom, Workspace
-from .resnet import BasicBlock, Bottleneck, ResNet
+from .resnet import Bottleneck, ResNet
 
 __all__ = ["NativeResNet", "NativeSGD", "NativeCrossEntropy", "NativeTrainer", "supports"]
 

@@ -23,7 +23,7 @@ Design (MI355X-first):
 """
 from __future__ import annotations
 
-from typing import Callable, List, Optional, Sequence
+from typing import List, Optional, Sequence
 
 import torch
 
