@@ -122,12 +122,18 @@ def spawn(fn: Callable, args: tuple = (), nprocs: Optional[int] = None, bind_num
     return mp.spawn(_child, args=(fn, args, bind_numa), nprocs=nprocs, join=join)
 
 
-def init_distributed(env: DistEnv, backend: str, timeout_s: float = 1800.0) -> None:
+def init_distributed(env: DistEnv, backend: str, timeout_s: float = 1800.0,
+                     device: Optional[torch.device] = None) -> None:
+    """TCP rendezvous (reference ``restnet_ddp.py:94``). With ``device`` the RCCL communicator is
+    created eagerly here (``device_id``), not lazily inside the first collective of the timed
+    epoch loop."""
     import datetime
     import torch.distributed as dist
     if dist.is_initialized():
         return
+    kw = {"device_id": device} if (backend == "nccl" and device is not None
+                                   and device.type == "cuda") else {}
     dist.init_process_group(backend=backend,
                             init_method=f"tcp://{env.master_addr}:{env.master_port}",
                             world_size=env.world_size, rank=env.rank,
-                            timeout=datetime.timedelta(seconds=timeout_s))
+                            timeout=datetime.timedelta(seconds=timeout_s), **kw)

@@ -267,7 +267,7 @@ def run(cfg: RunConfig, mode: str, local_rank: int = 0, nprocs: Optional[int] = 
     if distributed:
         env = dist_env(local_rank, nprocs)
         backend = "nccl" if device.type == "cuda" else "gloo"
-        init_distributed(env, backend)
+        init_distributed(env, backend, device=device)
         ctx.rank, ctx.world, ctx.distributed = env.rank, env.world_size, env.world_size > 1 or True
     save_path = Path(cfg.save_path)
     save_path.mkdir(exist_ok=True, parents=True)

@@ -64,9 +64,15 @@ class SuspendMonitor:
         return False
 
     def requested(self, group=None) -> bool:
-        """Collective decision: True on every rank iff any rank was asked to suspend."""
+        """Collective decision: True on every rank iff any rank was asked to suspend.
+
+        The collective runs every ``MX_SUSPEND_POLL`` steps (default 1, the reference polls every
+        step); all ranks tick in lockstep, so they agree on which steps poll."""
         local = self.local_requested()
         import torch.distributed as dist
+        every = max(1, int(os.environ.get("MX_SUSPEND_POLL", "1")))
+        if self.global_step % every:
+            return False
         if dist.is_available() and dist.is_initialized():
             import torch
             backend = dist.get_backend(group)
