@@ -27,6 +27,18 @@ BASELINE_DP = {1: 717.0, 8: 1301.2}   # the nn.DataParallel bar of result.png
 GRAPH_DEFAULT = os.environ.get("PDA_GRAPH", "0") == "1"
 
 
+def _metric_name() -> str:
+    """The headline metric exactly as BASELINE.json names it."""
+    try:
+        with open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "BASELINE.json")) as f:
+            return json.load(f)["metric"]
+    except (OSError, ValueError, KeyError):
+        return "images/sec (whole node) ResNet-50 bs=400 at 1/2/4/8 MI355X; scaling efficiency"
+
+
+METRIC = _metric_name()
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -111,7 +123,7 @@ def main():
     base = (BASELINE_DP if args.dp else BASELINE).get(world)
     if rank == 0:
         rec = {
-            "metric": "images/sec (whole node) ResNet-50 bs=400",
+            "metric": METRIC,
             "value": round(value, 2),
             "unit": "images/sec",
             "n_gpus": world,
