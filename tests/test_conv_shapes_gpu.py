@@ -85,3 +85,43 @@ def test_resnet50_conv_shape_all_tiles(shape):
             if not e < 1e-2:
                 bad.append((t, f"wgrad/{tb}", e))
     assert not bad, bad
+
+
+@pytest.mark.parametrize("shape", SHAPES, ids=[s[0] for s in SHAPES])
+def test_resnet50_conv_shape_all_tiles_exact_f32(shape):
+    """The exact-fp32 path (MFMA 16x16x4 f32) on every ResNet-50 shape and every f32 tile, against
+    a float64 CPU reference: errors at fp32 rounding level."""
+    from pytorch_distributed_amd.ops import ext
+    ext.load(required=True)
+    from pytorch_distributed_amd.ops import native_ops as K
+    _, H, Cin, Cout, k, s = shape
+    Nb, pad = 2, k // 2
+    torch.manual_seed(1)
+    x = torch.randn(Nb, Cin, H, H, dtype=torch.float64) + 0.1
+    w = torch.randn(Cout, Cin, k, k, dtype=torch.float64) / math.sqrt(Cin * k * k)
+    xr, wr = x.clone().requires_grad_(True), w.clone().requires_grad_(True)
+    y_ref = F.conv2d(xr, wr, stride=s, padding=pad)
+    dy = torch.randn_like(y_ref)
+    y_ref.backward(dy)
+    g = K.ConvGeom(Nb, H, H, Cin, Cout, k, k, s, pad)
+    x_nhwc = x.permute(0, 2, 3, 1).contiguous().float().to(DEV)
+    w_ohwi = w.permute(0, 2, 3, 1).contiguous().float().to(DEV)
+    dy_nhwc = dy.permute(0, 2, 3, 1).contiguous().float().to(DEV)
+    yr = y_ref.detach().permute(0, 2, 3, 1)
+    dxr = xr.grad.permute(0, 2, 3, 1)
+    dwr = wr.grad.permute(0, 2, 3, 1)
+    ws = K.Workspace(DEV)
+    bad = []
+    for t in TILES:
+        y = torch.full((Nb, g.Ho, g.Wo, Cout), float("nan"), device=DEV)
+        K.conv_fwd(x_nhwc, w_ohwi.view(Cout, -1), g, y, tile=t)
+        dx = torch.full((Nb, H, H, Cin), float("nan"), device=DEV)
+        K.conv_dgrad(dy_nhwc, w_ohwi, g, dx, tile=t)
+        dw = torch.full((Cout, k, k, Cin), float("nan"), device=DEV)
+        K.conv_wgrad(dy_nhwc, x_nhwc, g, dw.view(-1), ws, tile=t, target_blocks=512)
+        torch.cuda.synchronize()
+        for name, a, b in (("fwd", y, yr), ("dgrad", dx, dxr), ("wgrad", dw, dwr)):
+            e = rel_err(a.cpu().double(), b)
+            if not e < 1e-5:
+                bad.append((t, name, e))
+    assert not bad, bad
