@@ -441,20 +441,24 @@ __global__ __launch_bounds__(NT) void bn_bwd_reduce_kernel(BwdArgs a) {
 // Stem backward, one pass: maxpool gradient gather (as maxpool_bwd_kernel) -> ReLU mask of
 // relu(bn(y0)) -> dz stored -> per-block partials q0 = sum dz, q1 = sum dz*y0. Replaces
 // maxpool_bwd (write dA0) + bn_bwd_reduce (re-read dA0): one full read of the largest activation
-// of the network (400x112x112x64) less, and one launch less. Rows = input pixels (N*H*W).
+// of the network (400x112x112x64) less, and one launch less.
+// Work item = one 2x2 quad of input pixels (2yo..2yo+1, 2xo..2xo+1) x 8 channels: the pooling
+// windows covering it are exactly (yo..yo+1) x (xo..xo+1) (3x3/2, pad 1), so each window's argmax
+// bytes and gradient(s) are gathered ONCE per quad instead of once per pixel (4x less gather
+// traffic; the per-pixel form was request-bound at ~190 B of loads per 16 B stored).
 template <int DT>
 __global__ __launch_bounds__(NT) void stem_bwd_reduce_kernel(
     const void* __restrict__ dout, const void* __restrict__ dout2, const uint8_t* __restrict__ arg,
     const void* __restrict__ y, const float* __restrict__ sc, const float* __restrict__ sh,
-    void* __restrict__ dz_out, float* __restrict__ part, long long rows, long long rows_per_block,
-    int H, int W, int C, int Ho, int Wo, FastDiv dW, FastDiv dH) {
+    void* __restrict__ dz_out, float* __restrict__ part, long long quads, long long quads_per_block,
+    int H, int W, int C, int Ho, int Wo, FastDiv dWo, FastDiv dHo) {
   __shared__ float red[2][NT][8];
   const int CK = C / 8;
   const int tpr = CK < NT ? CK : NT;
   const int rpi = NT / tpr;
   const int ck = threadIdx.x % tpr, rsub = threadIdx.x / tpr;
-  const long long r0 = blockIdx.x * rows_per_block;
-  const long long r1 = min(rows, r0 + rows_per_block);
+  const long long r0 = blockIdx.x * quads_per_block;
+  const long long r1 = min(quads, r0 + quads_per_block);
   for (int cbase = 0; cbase < CK; cbase += tpr) {
     const int cc = cbase + ck, c0 = cc * 8;
     float q0[8], q1[8], s[8], h[8];
@@ -463,57 +467,77 @@ __global__ __launch_bounds__(NT) void stem_bwd_reduce_kernel(
     ld8f(sc + c0, s);
     ld8f(sh + c0, h);
     if (threadIdx.x < tpr * rpi) {
-      for (long long row = r0 + rsub; row < r1; row += rpi) {
-        const uint32_t p2 = fdiv((uint32_t)row, dW), x = (uint32_t)row - p2 * W;
-        const uint32_t n = fdiv(p2, dH), yy = p2 - n * H;
-        // the (up to) 2x2 pooling windows covering (yy, x): yo in {yy/2, yy/2 + (yy odd)}, same for
-        // x. All four loads are issued unconditionally from clamped (valid) addresses so they
-        // overlap; a window that does not exist gets the impossible argmax id 9 (no match).
-        const int yo0 = (int)yy >> 1, xo0 = (int)x >> 1;
-        const int yo1 = ((yy & 1) && yo0 + 1 < Ho) ? yo0 + 1 : yo0;
-        const int xo1 = ((x & 1) && xo0 + 1 < Wo) ? xo0 + 1 : xo0;
+      for (long long qd = r0 + rsub; qd < r1; qd += rpi) {
+        const uint32_t p2 = fdiv((uint32_t)qd, dWo), xo = (uint32_t)qd - p2 * Wo;
+        const uint32_t n = fdiv(p2, dHo), yo = p2 - n * Ho;
+        const bool y1 = (int)yo + 1 < Ho, x1 = (int)xo + 1 < Wo;
+        // gather the 4 windows (w bit 1: yo+1, bit 0: xo+1); a window past the edge re-reads a
+        // valid one and gets argmax bytes 0xff, which match no tap
         Raw8<DT> dv[4], dv2[4];
         uint64_t am[4];
-        int me[4];
 #pragma unroll
         for (int w = 0; w < 4; ++w) {
-          const int yo = (w & 2) ? yo1 : yo0, xo = (w & 1) ? xo1 : xo0;
-          const bool live = ((w & 2) == 0 || yo1 != yo0) && ((w & 1) == 0 || xo1 != xo0);
-          const uint32_t o = (n * Ho + yo) * Wo + xo;
-          am[w] = reinterpret_cast<const uint64_t*>(arg)[o * CK + cc];
+          const bool live = ((w & 2) == 0 || y1) && ((w & 1) == 0 || x1);
+          const uint32_t o = (n * Ho + yo + ((w & 2) && y1 ? 1 : 0)) * Wo + xo + ((w & 1) && x1 ? 1 : 0);
+          const uint64_t a8 = reinterpret_cast<const uint64_t*>(arg)[o * CK + cc];
+          am[w] = live ? a8 : ~0ull;
           dv[w] = ldraw8<DT>(dout, (size_t)o * C + c0);
           if (dout2) dv2[w] = ldraw8<DT>(dout2, (size_t)o * C + c0);
-          me[w] = live ? ((int)yy - (yo * 2 - 1)) * 3 + ((int)x - (xo * 2 - 1)) : 9;
         }
-        float yv[8];
-        load8<DT>(y, row * C + c0, yv);
-        float g[8];
+        // the quad's 4 pixels (pixel bit 1: row 2yo+1, bit 0: col 2xo+1); a pixel past an odd
+        // edge loads the quad's first pixel and is neither stored nor counted
+        Raw8<DT> yr[4];
+        bool pin[4];
+        size_t prow[4];
 #pragma unroll
-        for (int e = 0; e < 8; ++e) g[e] = 0.f;
+        for (int px = 0; px < 4; ++px) {
+          const int yy = 2 * (int)yo + (px >> 1), x = 2 * (int)xo + (px & 1);
+          pin[px] = yy < H && x < W;
+          prow[px] = ((size_t)n * H + (pin[px] ? yy : 2 * (int)yo)) * W + (pin[px] ? x : 2 * (int)xo);
+          yr[px] = ldraw8<DT>(y, prow[px] * C + c0);
+        }
+        float d[4][8];
 #pragma unroll
         for (int w = 0; w < 4; ++w) {
-          float d[8];
-          cvt8<DT>(dv[w], d);
+          cvt8<DT>(dv[w], d[w]);
           if (dout2) {
             float d2[8];
             cvt8<DT>(dv2[w], d2);
 #pragma unroll
-            for (int e = 0; e < 8; ++e) d[e] += d2[e];
+            for (int e = 0; e < 8; ++e) d[w][e] += d2[e];
           }
-#pragma unroll
-          for (int e = 0; e < 8; ++e)
-            if ((int)((am[w] >> (8 * e)) & 0xff) == me[w]) g[e] += d[e];
         }
 #pragma unroll
-        for (int e = 0; e < 8; ++e) g[e] = yv[e] * s[e] + h[e] > 0.f ? g[e] : 0.f;
-        // statistics of the stored (rounded) dz, as the apply kernel re-reads it
-        const Raw8<DT> pk = pk8<DT>(g);
-        straw8<DT>(dz_out, row * C + c0, pk);
-        cvt8<DT>(pk, g);
+        for (int px = 0; px < 4; ++px) {
+          const int py = px >> 1, pxx = px & 1;
+          float g[8];
 #pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          q0[e] += g[e];
-          q1[e] += g[e] * yv[e];
+          for (int e = 0; e < 8; ++e) g[e] = 0.f;
+#pragma unroll
+          for (int w = 0; w < 4; ++w) {
+            const int wy = w >> 1, wx = w & 1;
+            // window (yo+wy) covers rows 2(yo+wy)-1 .. 2(yo+wy)+1: pixel row 2yo+py is inside iff
+            // py - 2wy >= -1, i.e. not (py = 0, wy = 1); same for columns (compile-time)
+            if ((wy && !py) || (wx && !pxx)) continue;
+            const int me = (py + 1 - 2 * wy) * 3 + (pxx + 1 - 2 * wx);
+#pragma unroll
+            for (int e = 0; e < 8; ++e)
+              if ((int)((am[w] >> (8 * e)) & 0xff) == me) g[e] += d[w][e];
+          }
+          float yv[8];
+          cvt8<DT>(yr[px], yv);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) g[e] = yv[e] * s[e] + h[e] > 0.f ? g[e] : 0.f;
+          if (!pin[px]) continue;
+          // statistics of the stored (rounded) dz, as the apply kernel re-reads it
+          const Raw8<DT> pk = pk8<DT>(g);
+          straw8<DT>(dz_out, prow[px] * C + c0, pk);
+          cvt8<DT>(pk, g);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            q0[e] += g[e];
+            q1[e] += g[e] * yv[e];
+          }
         }
       }
     }
@@ -790,12 +814,14 @@ int pda_stem_bwd_reduce(const void* dout, const void* dout2, const void* arg, co
                         const float* sc, const float* sh, void* dz_out, float* part, int G, int N,
                         int H, int W, int C, int Ho, int Wo, int dt, hipStream_t st) {
   const long long rows = (long long)N * H * W;
-  if (rows * C >= (1ll << 31) || C % 8) return -2;
-  const long long rpb = (rows + G - 1) / G;
+  // the quad decomposition assumes the 3x3/2 pad-1 pooling geometry
+  if (rows * C >= (1ll << 31) || C % 8 || Ho != (H + 1) / 2 || Wo != (W + 1) / 2) return -2;
+  const long long quads = (long long)N * Ho * Wo;
+  const long long qpb = (quads + G - 1) / G;
 #define K(D) hipLaunchKernelGGL(stem_bwd_reduce_kernel<D>, dim3(G), dim3(NT), 0, st, (const void*)dout, \
                                 (const void*)dout2, (const uint8_t*)arg, (const void*)y, sc, sh,       \
-                                (void*)dz_out, part, rows, rpb, H, W, C, Ho, Wo, make_div(W),          \
-                                make_div(H))
+                                (void*)dz_out, part, quads, qpb, H, W, C, Ho, Wo, make_div(Wo),        \
+                                make_div(Ho))
   if (dt == DT_BF16) K(DT_BF16); else if (dt == DT_F32) K(DT_F32); else K(DT_F16);
 #undef K
   return (int)hipGetLastError();
