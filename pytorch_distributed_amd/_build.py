@@ -1,7 +1,8 @@
 """In-tree build of the native libraries for gfx950 (no JIT cache, no torch headers).
 
 * ``libpda_kernels.so`` -- every HIP kernel (``csrc/*.hip``), C ABI launchers.
-* ``libpda_comm.so``    -- the C++ RCCL communicator (``csrc/comm/*.cpp``), links ``librccl``.
+* ``libpda_comm.so``    -- the C++ RCCL communicator and gradient-bucket reducer
+  (``csrc/comm/*.cpp``), links ``librccl``.
 
 Both are loaded with ``ctypes`` by :mod:`pytorch_distributed_amd.ops.ext` /
 :mod:`pytorch_distributed_amd.parallel.rccl`, so they travel with the repo
@@ -25,7 +26,7 @@ HIPCC = os.path.join(ROCM, "bin", "hipcc")
 ARCH = os.environ.get("PDA_ARCH", "gfx950")
 
 KERNEL_SRCS = ["conv_gemm.hip", "bn.hip", "misc.hip"]
-COMM_SRCS = ["comm/rccl_comm.cpp"]
+COMM_SRCS = ["comm/rccl_comm.cpp", "comm/reducer.cpp"]
 CFLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wno-unused-result"]
 
 

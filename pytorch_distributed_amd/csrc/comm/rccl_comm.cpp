@@ -15,24 +15,12 @@
 #include <cstring>
 #include <vector>
 
+#include "comm.h"
+
+using pda::Comm;
+using pda::to_nccl;
+
 namespace {
-
-struct Comm {
-  std::vector<ncclComm_t> comms;  // 1 for multi-process, ndev for in-process
-  std::vector<int> devices;
-};
-
-ncclDataType_t to_nccl(int dt) {
-  switch (dt) {
-    case 0: return ncclFloat32;
-    case 1: return ncclBfloat16;
-    case 2: return ncclFloat16;
-    case 3: return ncclInt64;
-    case 4: return ncclFloat64;
-    case 5: return ncclInt32;
-    default: return ncclFloat32;
-  }
-}
 
 ncclRedOp_t to_op(int op) {
   switch (op) {

@@ -17,6 +17,7 @@ the native backward schedule (see :class:`NativeReducer`).
 """
 from __future__ import annotations
 
+import os
 from typing import List, Optional, Sequence
 
 import torch
@@ -58,12 +59,23 @@ class NativeReducer:
         self._next = 0
         self._works: List = []
         self.prescale = True
+        # RCCL communicator: the bucket state machine runs in C++ (csrc/comm/reducer.cpp);
+        # PDA_CPP_REDUCER=0 keeps the Python loop below (A/B, and the gloo/CPU communicators)
+        self.native = None
+        if (hasattr(comm, "make_bucket_reducer") and flat_grad.is_cuda
+                and os.environ.get("PDA_CPP_REDUCER", "1") != "0"):
+            self.native = comm.make_bucket_reducer(flat_grad, self.buckets)
 
     def reset(self) -> None:
         self._next = 0
         self._works = []
+        if self.native is not None:
+            self.native.reset()
 
     def grads_ready(self, upto: int) -> None:
+        if self.native is not None:
+            self.native.ready(upto)
+            return
         while self._next < len(self.buckets) and self.buckets[self._next][1] <= upto:
             s, e = self.buckets[self._next]
             view = self.flat[s:e]
@@ -77,6 +89,9 @@ class NativeReducer:
             self._next += 1
 
     def finish(self) -> None:
+        if self.native is not None:
+            self.native.finish()
+            return
         self.grads_ready(self.flat.numel())
         for w in self._works:
             self.comm.wait(w)
@@ -96,7 +111,6 @@ class DistributedDataParallel(nn.Module):
         # failure detection: poll the RCCL communicator's async error state from a
         # daemon thread; a dead peer aborts the communicator so collectives return (and the next
         # bucket wait raises) instead of hanging the job. MX_WATCHDOG=0 disables.
-        import os
         if hasattr(self.comm, "start_watchdog") and os.environ.get("MX_WATCHDOG", "1") != "0":
             self.comm.start_watchdog(float(os.environ.get("MX_WATCHDOG_S", "5")))
         self._native = hasattr(module, "flat_params")

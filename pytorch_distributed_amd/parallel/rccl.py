@@ -24,7 +24,7 @@ import torch.distributed as dist
 
 from .comm import Communicator
 
-__all__ = ["RcclCommunicator", "RcclGroup", "load"]
+__all__ = ["RcclBucketReducer", "RcclCommunicator", "RcclGroup", "load"]
 
 LIBPATH = Path(__file__).resolve().parent.parent / "_lib" / "libpda_comm.so"
 _LIB: Optional[C.CDLL] = None
@@ -56,11 +56,18 @@ def load() -> C.CDLL:
             "pda_group_allreduce": [V, C.POINTER(V), Z, I, I, C.POINTER(V)],
             "pda_group_broadcast": [V, C.POINTER(V), Z, I, I, C.POINTER(V)],
             "pda_group_reduce": [V, C.POINTER(V), Z, I, I, I, C.POINTER(V)],
+            "pda_reducer_create": [V, V, I, I, C.POINTER(C.c_longlong), I, V, C.POINTER(V)],
+            "pda_reducer_ready": [V, C.c_longlong, V],
+            "pda_reducer_finish": [V, V, V],
+            "pda_reducer_reset": [V],
+            "pda_reducer_destroy": [V],
         }
         for n, a in sigs.items():
             f = getattr(lib, n)
             f.argtypes = a
             f.restype = I
+        lib.pda_reducer_launched.argtypes = [V]
+        lib.pda_reducer_launched.restype = C.c_longlong
         lib.pda_comm_error_string.argtypes = [I]
         lib.pda_comm_error_string.restype = C.c_char_p
         _LIB = lib
@@ -110,6 +117,10 @@ class RcclCommunicator(Communicator):
         done.record(self.stream)
         t.record_stream(self.stream)
         return done
+
+    def make_bucket_reducer(self, flat: torch.Tensor, buckets) -> "RcclBucketReducer":
+        """Native bucket reducer over contiguous ``(begin, end)`` element ranges of ``flat``."""
+        return RcclBucketReducer(self, flat, buckets)
 
     def wait(self, handle) -> None:
         if getattr(self, "_watchdog_error", None) is not None:
@@ -179,6 +190,61 @@ class RcclCommunicator(Communicator):
         if self._h:
             load().pda_comm_destroy(self._h, int(abort))
             self._h = C.c_void_p()
+
+
+class RcclBucketReducer:
+    """Python handle of the C++ gradient-bucket reducer (``csrc/comm/reducer.cpp``).
+
+    ``ready(upto)`` launches, on the communicator's stream, an ncclAvg all-reduce of every bucket
+    whose gradients are final (ordered after the current stream by a pre-created HIP event);
+    ``finish()`` launches the rest and makes the current stream wait for the last bucket. The
+    host never blocks and no Python object is created per bucket."""
+
+    def __init__(self, comm: RcclCommunicator, flat: torch.Tensor, buckets) -> None:
+        if not flat.is_contiguous() or flat.dtype not in _DT:
+            raise ValueError("flat gradient must be a contiguous tensor of a supported dtype")
+        self.comm = comm
+        self.flat = flat
+        self.buckets = [(int(s), int(e)) for s, e in buckets]
+        arr = (C.c_longlong * (2 * len(self.buckets)))(*[v for b in self.buckets for v in b])
+        self._h = C.c_void_p()
+        _check(load().pda_reducer_create(comm._h, flat.data_ptr(), _DT[flat.dtype], _OPS["avg"], arr,
+                                         len(self.buckets), comm.stream.cuda_stream, C.byref(self._h)),
+               "reducer_create")
+
+    def _live(self) -> None:
+        if not self.comm._h or getattr(self.comm, "_watchdog_error", None) is not None:
+            self.comm.check()
+            raise RuntimeError("RCCL communicator closed")
+
+    def ready(self, upto: int) -> None:
+        self._live()
+        st = torch.cuda.current_stream(self.comm.device).cuda_stream
+        _check(load().pda_reducer_ready(self._h, int(upto), st), "reducer_ready")
+
+    def finish(self) -> None:
+        self._live()
+        st = torch.cuda.current_stream(self.comm.device).cuda_stream
+        _check(load().pda_reducer_finish(self._h, st, st), "reducer_finish")
+
+    def reset(self) -> None:
+        load().pda_reducer_reset(self._h)
+
+    @property
+    def launched(self) -> int:
+        """Total bucket all-reduces launched since construction."""
+        return int(load().pda_reducer_launched(self._h))
+
+    def close(self) -> None:
+        if self._h:
+            load().pda_reducer_destroy(self._h)
+            self._h = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 class RcclGroup:

@@ -103,3 +103,47 @@ def test_rccl_communicator_world1():
         c.close()
     finally:
         dist.destroy_process_group()
+
+
+def test_native_ddp_cpp_reducer_world1():
+    """DDP over the native RCCL communicator: the C++ bucket reducer (csrc/comm/reducer.cpp)
+    launches every bucket once per step, ordered after both backward streams, and the averaged
+    gradient at world size 1 equals the local gradient bit for bit."""
+    if dist.is_initialized():
+        pytest.skip("process group already initialised")
+    port = _port()
+    dev = torch.device("cuda", 0)
+    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", world_size=1, rank=0,
+                            device_id=dev)
+    try:
+        from pytorch_distributed_amd.data import SyntheticImageNet
+        from pytorch_distributed_amd.models import build_model
+        from pytorch_distributed_amd.models.native import NativeResNet
+        from pytorch_distributed_amd.parallel import DistributedDataParallel
+        from pytorch_distributed_amd.parallel.rccl import RcclCommunicator
+        torch.manual_seed(0)
+        ref = build_model("resnet50")
+        local = NativeResNet(build_model("resnet50"), device=dev, image_size=64)
+        local.load_state_dict(ref.state_dict())
+        model = NativeResNet(ref, device=dev, image_size=64)
+        comm = RcclCommunicator(dev)
+        ddp = DistributedDataParallel(model, bucket_cap_mb=8.0, comm=comm)
+        red = ddp.reducer
+        assert red.native is not None, "C++ reducer not in use"
+        nb = len(red.buckets)
+        assert nb >= 3
+        gen = model.input_generator(SyntheticImageNet("train", image_size=64))
+        crit, lcrit = model.make_criterion(), local.make_criterion()
+        for step in range(2):
+            x, y = gen(torch.arange(8) + 8 * step)
+            model.zero_grad_flat()
+            crit(ddp(x), y).backward()
+            local.zero_grad_flat()
+            lcrit(local(x), y).backward()
+            torch.cuda.synchronize()
+            assert red.native.launched == nb * (step + 1)
+            assert torch.equal(model.flat_grad, local.flat_grad)
+        red.native.close()
+        comm.close()
+    finally:
+        dist.destroy_process_group()
