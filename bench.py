@@ -70,6 +70,12 @@ def main():
     ndev = max(torch.cuda.device_count(), 1)
     device = torch.device("cuda", local_rank % ndev)   # >1 rank per GPU only in CPU-side rehearsals
     torch.cuda.set_device(device)
+    if world > 1 and os.environ.get("PDA_BIND_NUMA", "1") != "0":
+        # one rank per GPU, pinned to that GPU's NUMA node as the reference's
+        # hfai.multiprocessing.spawn(bind_numa=True)
+        sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+        from pytorch_distributed_amd.launch import bind_numa
+        bind_numa(local_rank % ndev)
     if world > 1:
         import torch.distributed as dist
         backend = os.environ.get("PDA_DIST_BACKEND", "nccl")

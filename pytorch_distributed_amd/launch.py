@@ -91,10 +91,16 @@ def _gpu_numa_cpus(local_rank: int) -> Optional[Sequence[int]]:
 
 
 def bind_numa(local_rank: int) -> bool:
+    """Pin this process to the CPUs of GPU ``local_rank``'s NUMA node (intersected with the CPUs
+    it may already use, so a cgroup cpuset is respected); False when nothing was changed."""
     cpus = _gpu_numa_cpus(local_rank)
     if not cpus:
         return False
     try:
+        allowed = os.sched_getaffinity(0)
+        cpus = sorted(set(cpus) & allowed)
+        if not cpus or set(cpus) == allowed:
+            return False
         os.sched_setaffinity(0, cpus)
         return True
     except OSError:

@@ -64,3 +64,17 @@ def test_reference_style_script_on_platform_api(tmp_path, monkeypatch):
     same, total = (tmp_path / "result.txt").read_text().split()
     assert same == "True"          # DDP kept the replicas identical
     assert int(total) == 16        # validation counters reduced across both ranks
+
+
+def test_bind_numa_respects_allowed_cpus():
+    """bind_numa never widens the CPU set and is a no-op without KFD topology (CPU boxes)."""
+    import os
+    from pytorch_distributed_amd.launch import bind_numa
+    before = os.sched_getaffinity(0)
+    changed = bind_numa(0)
+    after = os.sched_getaffinity(0)
+    assert isinstance(changed, bool)
+    assert after <= before and after
+    if not changed:
+        assert after == before
+    os.sched_setaffinity(0, before)
