@@ -46,6 +46,7 @@ class RunConfig:
     log_every: int = 100
     metrics: bool = False            # write output/<run>/metrics.jsonl
     bucket_mb: float = 0.0           # DDP bucket cap (0 = framework default)
+    sync_bn: bool = False            # SyncBatchNorm in DDP (reference: per-GPU statistics)
     grad_sync: bool = True
 
     def replace(self, **kw) -> "RunConfig":
@@ -81,6 +82,7 @@ _ENV = {
     "MX_LOG_EVERY": ("log_every", int),
     "MX_METRICS": ("metrics", lambda s: s not in ("", "0", "false", "False")),
     "MX_BUCKET_MB": ("bucket_mb", float),
+    "MX_SYNC_BN": ("sync_bn", lambda s: s not in ("", "0", "false", "False")),
 }
 
 

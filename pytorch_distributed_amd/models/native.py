@@ -333,6 +333,13 @@ class NativeResNet(nn.Module):
         self._reducer = reducer
 
     @torch.no_grad()
+    def set_sync_bn(self, comm) -> None:
+        """SyncBatchNorm over ``comm`` (None: per-rank statistics, the reference's behaviour):
+        every BN finalize of every workspace all-reduces its per-channel sums first."""
+        for v in list(vars(self).values()):
+            if isinstance(v, Workspace):
+                v.sync_comm = comm
+
     def sync_from_rank0(self, comm) -> None:
         comm.broadcast(self.flat_params, 0)
         self.broadcast_buffers_from_rank0(comm)

@@ -62,11 +62,16 @@ class ConvGeom:
 
 
 class Workspace:
-    """Grow-only scratch buffers (split-K slabs, BN partials) reused by every layer on a stream."""
+    """Grow-only scratch buffers (split-K slabs, BN partials) reused by every layer on a stream.
+
+    ``sync_comm``: when set (SyncBatchNorm, :func:`~pytorch_distributed_amd.parallel.ddp.
+    convert_sync_batchnorm`), every BatchNorm finalize of this workspace first all-reduces its
+    per-channel sums over the communicator, so statistics and their gradients are global."""
 
     def __init__(self, device) -> None:
         self.device = device
         self._bufs = {}
+        self.sync_comm = None
 
     def get(self, name: str, numel: int, dtype=torch.float32) -> torch.Tensor:
         b = self._bufs.get(name)
@@ -278,10 +283,25 @@ def prereduce(part: torch.Tensor, G: int, QC: int, ws: Optional["Workspace"] = N
     return out, s
 
 
+def _sync_sums(part: torch.Tensor, G: int, QC: int, ws: Optional["Workspace"]):
+    """SyncBatchNorm: [G][QC] partials -> one [QC] row (own slab kernel, fixed order), summed over
+    the ranks of ``ws.sync_comm`` (ordered on the current stream). Returns (part, G, world)."""
+    comm = getattr(ws, "sync_comm", None)
+    if comm is None or comm.world_size == 1:
+        return part, G, 1
+    tot = ws.get("bn_sync", QC)
+    if ext.lib().pda_slab_reduce(ptr(part), G, QC, 1, ptr(tot), stream(part.device)) < 0:
+        raise RuntimeError("slab_reduce launch failed")
+    comm.all_reduce(tot)
+    return tot, 1, comm.world_size
+
+
 def bn_finalize_fwd(part: torch.Tensor, T: int, C_: int, count: int, gamma, beta, eps, momentum,
                     mean, invstd, scale, shift, rmean=None, rvar=None, nbt=None,
                     update_running: bool = True, ws: Optional["Workspace"] = None) -> None:
     part, T = prereduce(part, T, 2 * C_, ws)
+    part, T, world = _sync_sums(part, T, 2 * C_, ws)
+    count = count * world
     rc = ext.lib().pda_bn_finalize_fwd(ptr(part), T, C_, float(count), ptr(gamma), ptr(beta),
                                        float(eps), float(momentum), ptr(mean), ptr(invstd), ptr(scale),
                                        ptr(shift), ptr(rmean), ptr(rvar), ptr(nbt),
@@ -407,13 +427,17 @@ def _bn_bwd_tail(ws, part, G, nq, mode, a, y, mean, invstd, gamma, dgamma, dbeta
     L = ext.lib()
     dt = dt_of(y)
     part, G = prereduce(part, G, nq * C_, ws)
+    part, G, world = _sync_sums(part, G, nq * C_, ws)
+    # SyncBN: the input-gradient coefficients need the GLOBAL sums, while gamma/beta keep the
+    # per-rank gradient (torch SyncBatchNorm) that the DDP bucket average then combines
+    gscale = gscale / world
     k = ws.get("bn_k", 6 * C_)
-    check(L.pda_bn_bwd_finalize(ptr(part), G, nq, 1, C_, float(rows), ptr(gamma), ptr(mean),
+    check(L.pda_bn_bwd_finalize(ptr(part), G, nq, 1, C_, float(rows * world), ptr(gamma), ptr(mean),
                                 ptr(invstd), ptr(dgamma), ptr(dbeta), ptr(k[0:C_]),
                                 ptr(k[C_:2 * C_]), ptr(k[2 * C_:3 * C_]), float(gscale),
                                 int(accumulate), st), "bn_bwd_finalize")
     if mode == 2:
-        check(L.pda_bn_bwd_finalize(ptr(part), G, nq, 2, C_, float(rows), ptr(gamma2), ptr(mean2),
+        check(L.pda_bn_bwd_finalize(ptr(part), G, nq, 2, C_, float(rows * world), ptr(gamma2), ptr(mean2),
                                     ptr(invstd2), ptr(dgamma2), ptr(dbeta2), ptr(k[3 * C_:4 * C_]),
                                     ptr(k[4 * C_:5 * C_]), ptr(k[5 * C_:6 * C_]), float(gscale),
                                     int(accumulate), st), "bn_bwd_finalize2")

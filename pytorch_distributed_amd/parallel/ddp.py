@@ -26,7 +26,7 @@ from torch import nn
 from .comm import Communicator, make_communicator
 from .reducer import MiB, Reducer, plan_buckets
 
-__all__ = ["DistributedDataParallel", "NativeReducer"]
+__all__ = ["DistributedDataParallel", "NativeReducer", "convert_sync_batchnorm"]
 
 
 class NativeReducer:
@@ -98,11 +98,23 @@ class NativeReducer:
         self.reset()
 
 
+def convert_sync_batchnorm(module: nn.Module, process_group=None) -> nn.Module:
+    """``torch.nn.SyncBatchNorm.convert_sync_batchnorm`` counterpart (optional, off by
+    default -- the reference keeps per-GPU statistics). A native model is flagged and, once
+    wrapped in :class:`DistributedDataParallel`, all-reduces its BatchNorm sums (forward
+    Σx/Σx², backward Σdz/Σdz·y) over a dedicated communicator before every finalize; a plain
+    torch model gets ``nn.SyncBatchNorm`` layers."""
+    if hasattr(module, "set_sync_bn"):
+        module.sync_bn = True
+        return module
+    return nn.SyncBatchNorm.convert_sync_batchnorm(module, process_group)
+
+
 class DistributedDataParallel(nn.Module):
     def __init__(self, module: nn.Module, device_ids: Optional[List[int]] = None,
                  output_device=None, broadcast_buffers: bool = True,
                  bucket_cap_mb: Optional[float] = None, process_group=None,
-                 comm: Optional[Communicator] = None) -> None:
+                 comm: Optional[Communicator] = None, sync_bn: Optional[bool] = None) -> None:
         super().__init__()
         self.module = module
         self.broadcast_buffers = broadcast_buffers
@@ -119,6 +131,14 @@ class DistributedDataParallel(nn.Module):
             module.sync_from_rank0(self.comm)                    # M2: one flat broadcast
             self.reducer = NativeReducer(module.flat_grad, module.grad_boundaries(), self.comm, cap)
             module.attach_reducer(self.reducer)
+            self.bn_comm = None
+            if (sync_bn if sync_bn is not None else getattr(module, "sync_bn", False)) \
+                    and self.comm.world_size > 1:
+                # SyncBN collectives run on the compute stream while bucket all-reduces run on
+                # the comm stream: a second RCCL communicator keeps the two sequences independent
+                self.bn_comm = (make_communicator(dev, process_group)
+                                if hasattr(self.comm, "make_bucket_reducer") else self.comm)
+                module.set_sync_bn(self.bn_comm)
         else:
             with torch.no_grad():
                 for t in list(module.parameters()) + list(module.buffers()):   # M2

@@ -279,7 +279,9 @@ def run(cfg: RunConfig, mode: str, local_rank: int = 0, nprocs: Optional[int] = 
         from .parallel.dp import DataParallel
         model = DataParallel(model)
     elif distributed:
-        from .parallel.ddp import DistributedDataParallel
+        from .parallel.ddp import DistributedDataParallel, convert_sync_batchnorm
+        if cfg.sync_bn:
+            model = convert_sync_batchnorm(model)
         model = DistributedDataParallel(model, device_ids=[local_rank] if device.type == "cuda" else None,
                                         bucket_cap_mb=cfg.bucket_mb or None)
     per_rank_batch = cfg.batch_size
