@@ -184,3 +184,19 @@ def test_resume_from_reference_format_checkpoint(tmp_path):
     best = out / "best.pt"
     if best.exists():                           # written only if accuracy beat 0.25
         build_model("resnet18", 10).load_state_dict(torch.load(best, weights_only=True))
+
+
+def test_convert_sync_batchnorm_keeps_state_dict_and_env_flag():
+    """MX_SYNC_BN / convert_sync_batchnorm: a plain torch model gets nn.SyncBatchNorm layers with the
+    torchvision state_dict keys unchanged (the native engine path is tested on the GPU:
+    tests/test_ddp_gpu.py::test_native_ddp_sync_batchnorm_two_ranks); off by default."""
+    from pytorch_distributed_amd.config import config_for
+    from pytorch_distributed_amd.models import build_model
+    from pytorch_distributed_amd.parallel import convert_sync_batchnorm
+    m = build_model("resnet18", 10)
+    keys = list(m.state_dict())
+    s = convert_sync_batchnorm(m)
+    assert list(s.state_dict()) == keys
+    assert sum(isinstance(x, nn.SyncBatchNorm) for x in s.modules()) == 20
+    assert not config_for("ddp", env={}).sync_bn
+    assert config_for("ddp", env={"MX_SYNC_BN": "1"}).sync_bn
