@@ -1,0 +1,43 @@
+"""The driver's multi-GPU bench contract, rehearsed on one GPU: ``bench.py`` launched by
+``torch.distributed.run`` with 2 ranks (gloo stands in for RCCL, which refuses two ranks on one
+device). Covers env-rank parsing, the DDP-wrapped native step, the barrier/synchronize timing
+bracket, the MAX-over-ranks elapsed time and the single JSON line from rank 0."""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def test_bench_torchrun_two_ranks(tmp_path):
+    env = dict(os.environ)
+    env.update({"PDA_DIST_BACKEND": "gloo", "PDA_BIND_NUMA": "0", "OMP_NUM_THREADS": "4",
+                "HSA_ENABLE_IPC_MODE_LEGACY": "0"})
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(_port()),
+           os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "2", "--warmup", "1",
+           "--batch", "16", "--image-size", "64"]
+    r = subprocess.run(cmd, cwd=tmp_path, env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-4000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout          # rank 0 only
+    rec = json.loads(lines[0])
+    assert rec["n_gpus"] == 2 and rec["steps"] == 2 and rec["warmup"] == 1
+    assert rec["config"]["global_batch"] == 32 and rec["config"]["parallelism"] == "dp2"
+    assert rec["config"]["engine"] == "native" and rec["config"]["hip_graph"] is False
+    assert rec["value"] > 0 and rec["ms_per_step"] > 0
+    assert abs(rec["value"] - 32 * 1000.0 / rec["ms_per_step"]) / rec["value"] < 1e-2
+    assert rec["loss"] == rec["loss"]         # finite, not NaN
