@@ -9,16 +9,38 @@ weights. W untimed warm-up steps, then EXACTLY K timed steps bracketed by a
 barrier + device synchronize on both sides; the MAX elapsed over ranks is used.
 Rank 0 prints ONE JSON line.
 
+Self-validation for N > 1 (everything below runs AFTER the timed region):
+
+* ``rccl_world``: the rank count RCCL itself reports for the gradient communicator
+  (``ncclCommCount``), next to ``n_gpus`` from the launcher;
+* ``buckets`` / ``bucket_bytes``: the gradient-bucket plan (identical on every rank:
+  DistributedDataParallel verifies it across ranks at construction);
+* ``exposed_comm_ms`` / ``bucket_allreduce_ms``: ``--diag-steps`` extra steps with HIP
+  timing events around every bucket all-reduce and at the end of backward; exposed =
+  backward end -> last bucket done (the part of communication NOT hidden by backward);
+* ``weights_consistent``: a bit-exact checksum of the parameters and momentum buffers,
+  all-reduced MIN and MAX over ranks; a mismatch (ranks that silently diverged) makes
+  the run exit non-zero. ``PDA_BENCH_PERTURB_RANK=r`` perturbs rank r (test hook);
+* finite rendezvous / RCCL-init timeouts (``PDA_DIST_TIMEOUT_S``), so a missing rank is
+  an error, not a hang.
+
+``fp32_images_per_sec``: a short pass of the same step in exact fp32 (the reference
+scripts' precision) so the like-for-like number is measured in the same run. For N > 1
+each rank runs it without gradient all-reduce (per-GPU fp32 compute, aggregated).
+
 Reference metric: images/sec whole node at bs 400/GPU; published
-(derived) 717.0 img/s on 1 GPU and 5,546.7 img/s on 8 GPUs (AMP-DDP "Apex").
+(derived) 717.0 img/s on 1 GPU (fp32/TF32) and 5,546.7 img/s on 8 GPUs (AMP-DDP "Apex").
 """
 from __future__ import annotations
 
 import argparse
+import datetime
 import json
 import os
+import statistics
 import sys
 import time
+import traceback
 
 import torch
 
@@ -50,84 +72,197 @@ def parse():
     ap.add_argument("--engine", default="auto", choices=["auto", "native", "torch"])
     ap.add_argument("--bucket-mb", type=float, default=32.0)
     ap.add_argument("--image-size", type=int, default=224)
-    ap.add_argument("--profile-steps", type=int, default=0)
+    ap.add_argument("--device", default="cuda", choices=["cuda", "cpu"],
+                    help="cpu: rehearsal of the launch/validation contract without a GPU")
     ap.add_argument("--dp", action="store_true",
                     help="single-process DataParallel over --gpus devices (resnet_dp.py config)")
     ap.add_argument("--graph", type=int, default=-1,
-                    help="capture the step in a HIP graph (1/0; default: on for 1 GPU, native engine)")
+                    help="capture the step in a HIP graph (1/0; default off, PDA_GRAPH=1 turns it "
+                         "on for 1 GPU)")
+    ap.add_argument("--diag-steps", type=int, default=3,
+                    help="N>1: extra untimed steps with bucket timing events")
+    ap.add_argument("--fp32-steps", type=int, default=5,
+                    help="timed steps of the exact-fp32 pass (0: skip)")
     return ap.parse_args()
+
+
+class Ctx:
+    def __init__(self, args):
+        self.args = args
+        self.world = int(os.environ.get("WORLD_SIZE", "1"))
+        self.rank = int(os.environ.get("RANK", "0"))
+        self.local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+        self.cuda = args.device == "cuda"
+        if self.cuda:
+            ndev = max(torch.cuda.device_count(), 1)
+            self.device = torch.device("cuda", self.local_rank % ndev)  # >1 rank/GPU: rehearsals only
+            torch.cuda.set_device(self.device)
+        else:
+            ndev = 1
+            self.device = torch.device("cpu")
+        self.ndev = ndev
+        self.multi = self.world > 1 and not args.dp
+
+    def sync(self):
+        if self.cuda:
+            if self.args.dp:
+                for d in range(self.args.gpus):
+                    torch.cuda.synchronize(d)
+            else:
+                torch.cuda.synchronize(self.device)
+
+    def barrier(self):
+        if self.multi:
+            import torch.distributed as dist
+            dist.barrier()
+        self.sync()
+
+    def allreduce_max(self, x: float) -> float:
+        if not self.multi:
+            return x
+        import torch.distributed as dist
+        dev = self.device if dist.get_backend() == "nccl" else torch.device("cpu")
+        t = torch.tensor([x], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t.item())
+
+
+def _timed(ctx: Ctx, tr, first: int, steps: int) -> float:
+    ctx.barrier()
+    t0 = time.perf_counter()
+    for i in range(steps):
+        tr.step(first + i)
+    ctx.barrier()
+    return ctx.allreduce_max(time.perf_counter() - t0)
+
+
+def _diagnostics(ctx: Ctx, tr, first: int) -> dict:
+    """N>1, after the timed region: bucket plan, RCCL world, exposed communication."""
+    out = {"comm": None, "rccl_world": None, "buckets": None, "bucket_bytes": None,
+           "exposed_comm_ms": None, "bucket_allreduce_ms": None}
+    net = getattr(tr, "net", None)
+    red = getattr(net, "reducer", None)
+    if net is None or red is None:
+        return out
+    out["comm"] = type(net.comm).__name__
+    out["rccl_world"] = getattr(net, "rccl_world", None)
+    if getattr(red, "buckets", None):
+        out["buckets"] = len(red.buckets)
+        out["bucket_bytes"] = red.bucket_bytes
+    nat = getattr(red, "native", None)
+    if nat is not None and ctx.args.diag_steps > 0:
+        exp, per = [], []
+        nat.set_timing(True)
+        for i in range(ctx.args.diag_steps):
+            tr.step(first + i)
+            ctx.sync()
+            e, b = nat.timing()
+            exp.append(e)
+            per.append(b)
+        nat.set_timing(False)
+        out["exposed_comm_ms"] = round(statistics.median(exp), 4)
+        out["bucket_allreduce_ms"] = [round(statistics.median(c), 4) for c in zip(*per)]
+    return out
+
+
+def _verify_consistent(ctx: Ctx, tr) -> dict:
+    """Bit-exact parameter + momentum checksum, MIN/MAX over ranks (N>1)."""
+    cs = tr.state_checksum()
+    perturb = os.environ.get("PDA_BENCH_PERTURB_RANK")
+    if perturb is not None and int(perturb) == ctx.rank:
+        cs = cs + 1
+    if not ctx.multi:
+        return {"weights_consistent": None, "checksum": [int(v) for v in cs.tolist()]}
+    import torch.distributed as dist
+    dev = ctx.device if dist.get_backend() == "nccl" else torch.device("cpu")
+    lo, hi = cs.to(dev).clone(), cs.to(dev).clone()
+    dist.all_reduce(lo, op=dist.ReduceOp.MIN)
+    dist.all_reduce(hi, op=dist.ReduceOp.MAX)
+    ok = bool(torch.equal(lo, hi))
+    return {"weights_consistent": ok, "checksum": [int(v) for v in cs.tolist()]}
+
+
+def _fp32_pass(ctx: Ctx, args) -> dict:
+    """Short exact-fp32 pass (reference precision), each rank locally (no all-reduce)."""
+    from pytorch_distributed_amd.bench_step import make_trainer
+    tr = make_trainer(args.arch, args.batch, torch.float32, ctx.device, engine=args.engine,
+                      world=1, rank=0, bucket_mb=args.bucket_mb, image_size=args.image_size)
+    for i in range(2):
+        tr.step(i)
+    el = _timed(ctx, tr, 2, args.fp32_steps)
+    world = ctx.world if ctx.multi else 1
+    res = {"fp32_images_per_sec": round(args.batch * world * args.fp32_steps / el, 2),
+           "fp32_ms_per_step": round(1000.0 * el / args.fp32_steps, 3),
+           "fp32_engine": tr.engine,
+           "fp32_mode": "single" if world == 1 else "per-rank local steps, no all-reduce"}
+    del tr
+    return res
 
 
 def main():
     args = parse()
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    if args.gpus != world and world > 1:
-        print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
+    ctx = Ctx(args)
+    if args.gpus != ctx.world and ctx.world > 1:
+        print(f"warning: --gpus {args.gpus} but WORLD_SIZE {ctx.world}", file=sys.stderr)
     os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
     os.environ.setdefault("MX_WATCHDOG", "0")   # timed runs: no polling thread beside the step
-    ndev = max(torch.cuda.device_count(), 1)
-    device = torch.device("cuda", local_rank % ndev)   # >1 rank per GPU only in CPU-side rehearsals
-    torch.cuda.set_device(device)
-    if world > 1 and os.environ.get("PDA_BIND_NUMA", "1") != "0":
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    if ctx.world > 1 and ctx.cuda and os.environ.get("PDA_BIND_NUMA", "1") != "0":
         # one rank per GPU, pinned to that GPU's NUMA node as the reference's
         # hfai.multiprocessing.spawn(bind_numa=True) (SURVEY R18)
-        sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
         from pytorch_distributed_amd.launch import bind_numa
-        bind_numa(local_rank % ndev)
-    if world > 1:
+        bind_numa(ctx.local_rank % ctx.ndev)
+    if ctx.world > 1:
         import torch.distributed as dist
-        backend = os.environ.get("PDA_DIST_BACKEND", "nccl")
+        timeout = datetime.timedelta(seconds=float(os.environ.get("PDA_DIST_TIMEOUT_S", "600")))
+        backend = os.environ.get("PDA_DIST_BACKEND", "nccl" if ctx.cuda else "gloo")
+        os.environ.setdefault("PDA_RCCL_INIT_TIMEOUT_S", str(timeout.total_seconds()))
         if backend == "nccl":
-            dist.init_process_group("nccl", device_id=device)
+            dist.init_process_group("nccl", device_id=ctx.device, timeout=timeout)
         else:
-            dist.init_process_group(backend)
+            dist.init_process_group(backend, timeout=timeout)
 
-    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
     from pytorch_distributed_amd.bench_step import make_trainer
     dtype = {"bf16": torch.bfloat16, "fp16": torch.float16, "fp32": torch.float32}[args.dtype]
-    graph = args.graph == 1 or (args.graph < 0 and world == 1 and GRAPH_DEFAULT)
+    graph = args.graph == 1 or (args.graph < 0 and ctx.world == 1 and GRAPH_DEFAULT)
+    world = ctx.world
     if args.dp:
-        if world > 1:
+        if ctx.world > 1:
             raise SystemExit("--dp is one process driving --gpus devices; do not launch it with torchrun")
         from pytorch_distributed_amd.bench_step import make_dp_trainer
         tr = make_dp_trainer(args.arch, args.batch, dtype, args.gpus, args.image_size)
         world = args.gpus            # images/sec over all devices of the process
-        sync_all = lambda: [torch.cuda.synchronize(d) for d in range(args.gpus)]  # noqa: E731
     else:
-        tr = make_trainer(args.arch, args.batch, dtype, device, engine=args.engine,
-                          world=world, rank=rank, bucket_mb=args.bucket_mb, image_size=args.image_size,
-                          graph=graph)
-        sync_all = torch.cuda.synchronize
+        tr = make_trainer(args.arch, args.batch, dtype, ctx.device, engine=args.engine,
+                          world=ctx.world, rank=ctx.rank, bucket_mb=args.bucket_mb,
+                          image_size=args.image_size, graph=graph)
 
     for i in range(args.warmup):
         tr.step(i)
-    sync_all()
-    multi_proc = world > 1 and not args.dp
-
-    def barrier():
-        if multi_proc:
-            import torch.distributed as dist
-            dist.barrier()
-        sync_all()
-
-    barrier()
-    t0 = time.perf_counter()
-    for i in range(args.steps):
-        tr.step(args.warmup + i)
-    barrier()
-    elapsed = time.perf_counter() - t0
-    if multi_proc:
-        import torch.distributed as dist
-        t = torch.tensor([elapsed], device=device, dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    ctx.sync()
+    elapsed = _timed(ctx, tr, args.warmup, args.steps)   # barrier + sync on both sides, MAX
     loss = tr.last_loss()
+    nxt = args.warmup + args.steps
+    diag = _diagnostics(ctx, tr, nxt) if ctx.multi else {}
+    consistency = _verify_consistent(ctx, tr) if hasattr(tr, "state_checksum") else {}
     ms = 1000.0 * elapsed / max(args.steps, 1)
     value = args.batch * world * args.steps / elapsed
     base = (BASELINE_DP if args.dp else BASELINE).get(world)
-    if rank == 0:
+    cfg = {"model": args.arch, "global_batch": args.batch * world,
+           "per_gpu_batch": args.batch, "seq_len": None,
+           "parallelism": (f"dataparallel{world}" if args.dp else f"dp{world}"),
+           "engine": tr.engine,
+           "hip_graph": bool(getattr(tr, "graphed", None)),
+           "optimizer": "SGD(lr=0.1, momentum=0.9, wd=1e-4)",
+           "bucket_cap_mb": args.bucket_mb if ctx.multi else None}
+    max_mem = round(torch.cuda.max_memory_allocated(ctx.device) / 1e9, 2) if ctx.cuda else None
+    fp32 = {}
+    if args.fp32_steps > 0 and args.dtype != "fp32" and not args.dp:
+        del tr
+        if ctx.cuda:
+            torch.cuda.empty_cache()
+        fp32 = _fp32_pass(ctx, args)
+    if ctx.rank == 0:
         rec = {
             "metric": METRIC,
             "value": round(value, 2),
@@ -139,22 +274,36 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": round(value / base, 3) if base else None,
+            "vs_baseline_precision": (f"{args.dtype} (this run) vs the reference's fp32/TF32 bar"
+                                      if args.dtype != "fp32" else "fp32 vs fp32/TF32"),
             "dtype": args.dtype,
             "data": "synthetic (on-device generated 3x224x224, random-init weights)",
-            "config": {"model": args.arch, "global_batch": args.batch * world,
-                       "per_gpu_batch": args.batch, "seq_len": None,
-                       "parallelism": (f"dataparallel{world}" if args.dp else f"dp{world}"),
-                       "engine": tr.engine,
-                       "hip_graph": bool(getattr(tr, "graphed", None)),
-                       "optimizer": "SGD(lr=0.1, momentum=0.9, wd=1e-4)"},
+            "config": cfg,
             "loss": loss,
-            "max_mem_gb": round(torch.cuda.max_memory_allocated(device) / 1e9, 2),
+            "max_mem_gb": max_mem,
+            **diag, **consistency, **fp32,
         }
+        if fp32 and base:
+            rec["vs_baseline_fp32"] = round(fp32["fp32_images_per_sec"] / base, 3)
         print(json.dumps(rec), flush=True)
-    if multi_proc:
+    if consistency.get("weights_consistent") is False:
+        print(f"bench: rank {ctx.rank}: parameters differ across ranks after training "
+              f"(checksum {consistency['checksum']})", file=sys.stderr, flush=True)
+        sys.stderr.flush()
+        os._exit(3)
+    if ctx.multi:
         import torch.distributed as dist
         dist.destroy_process_group()
 
 
 if __name__ == "__main__":
-    main()
+    try:
+        main()
+    except SystemExit:
+        raise
+    except BaseException:
+        # a failed rank must not hang in teardown (stuck collective threads): report and leave
+        traceback.print_exc()
+        sys.stderr.flush()
+        sys.stdout.flush()
+        os._exit(1)

@@ -12,7 +12,24 @@ from torch import nn
 
 from .data.synthetic import SyntheticImageNet
 
-__all__ = ["make_trainer"]
+__all__ = ["make_trainer", "tensor_checksum"]
+
+
+def tensor_checksum(tensors) -> torch.Tensor:
+    """Bit-exact, order-independent checksum of float tensors: int64[2] = (sum of the raw bit
+    patterns, sum of bit pattern x (index mod 65521 + 1)), with wrapping int64 arithmetic. Equal
+    on two ranks iff (with overwhelming probability) every element is bitwise equal."""
+    tensors = [t for t in tensors if t is not None and t.numel()]
+    dev = tensors[0].device
+    c = torch.zeros(2, dtype=torch.int64, device=dev)
+    ints = {4: torch.int32, 2: torch.int16, 8: torch.int64}
+    for t in tensors:
+        x = t.detach().contiguous().view(-1)
+        b = x.view(ints[x.element_size()]).to(torch.int64)
+        w = torch.arange(b.numel(), dtype=torch.int64, device=dev) % 65521 + 1
+        c[0] += b.sum()
+        c[1] += (b * w).sum()
+    return c
 
 
 class _TorchTrainer:
@@ -43,7 +60,7 @@ class _TorchTrainer:
         ids = torch.arange(self.batch, device=self.device) + (i * self.world + self.rank) * self.batch
         x, y = self.ds.batch(ids, device=self.device)
         x = x.contiguous(memory_format=torch.channels_last)
-        with torch.autocast("cuda", dtype=self.dtype, enabled=self.dtype != torch.float32):
+        with torch.autocast(self.device.type, dtype=self.dtype, enabled=self.dtype != torch.float32):
             out = self.net(x)
         loss = self.crit(out.float(), y)
         self.opt.zero_grad(set_to_none=False)
@@ -53,6 +70,11 @@ class _TorchTrainer:
 
     def last_loss(self) -> Optional[float]:
         return None if self._loss is None else float(self._loss.item())
+
+    def state_checksum(self) -> torch.Tensor:
+        ps = list(self.model.parameters())
+        moms = [self.opt.state.get(p, {}).get("momentum_buffer") for p in ps]
+        return tensor_checksum(ps + moms)
 
 
 class _DPTrainer:
@@ -89,6 +111,14 @@ class _DPTrainer:
 
     def last_loss(self) -> Optional[float]:
         return None if self._loss is None else float(self._loss.item())
+
+    def state_checksum(self) -> torch.Tensor:
+        """Replica 0's checksum; raises if any replica's weights differ from it (the replicated
+        SGD must keep every GPU's copy bit-identical)."""
+        sums = [tensor_checksum([m.flat_params]).cpu() for m in self.dp.all_modules]
+        if any(not torch.equal(sums[0], c) for c in sums[1:]):
+            raise RuntimeError(f"DataParallel replicas diverged: {[c.tolist() for c in sums]}")
+        return sums[0]
 
 
 def make_dp_trainer(arch: str, batch: int, dtype: torch.dtype, ngpus: int, image_size: int = 224):

@@ -32,7 +32,7 @@ class RunConfig:
     arch: str = "resnet50"
     num_classes: int = 1000
     # --- framework extensions (MX_* env) ---
-    dtype: str = "auto"              # auto | fp32 | bf16 | fp16 (auto: bf16 on GPU, fp32 on CPU; fp16 for ddp_amp)
+    dtype: str = "auto"              # auto | fp32 | bf16 | fp16 (auto: fp32 = the reference's precision; ddp_amp: fp16)
     device: str = "auto"             # auto | cuda | cpu
     data: str = "synthetic"          # synthetic | folder:<path>
     image_size: int = 224
@@ -47,7 +47,6 @@ class RunConfig:
     metrics: bool = False            # write output/<run>/metrics.jsonl
     bucket_mb: float = 0.0           # DDP bucket cap (0 = framework default)
     sync_bn: bool = False            # SyncBatchNorm in DDP (reference: per-GPU statistics)
-    grad_sync: bool = True
 
     def replace(self, **kw) -> "RunConfig":
         return dataclasses.replace(self, **kw)

@@ -41,6 +41,10 @@ from .resnet import Bottleneck, ResNet
 __all__ = ["NativeResNet", "NativeSGD", "NativeCrossEntropy", "NativeTrainer", "supports"]
 
 ALIGN = 64  # elements; keeps every segment 16-B aligned in the 16-bit shadow
+# DDP bucket boundaries (block boundaries of the flat gradient) are padded to multiples of
+# 8 ranks x 7 xGMI links x 256 B: every bucket then splits into equal 256-B-aligned per-rank /
+# per-link slices for any world size dividing 8 (parallel/reducer.py cost model)
+BUCKET_QUANTUM = 8 * 7 * 256 // 4   # f32 elements (3584)
 
 
 def supports(arch: str, dtype: torch.dtype) -> bool:
@@ -53,6 +57,10 @@ def supports(arch: str, dtype: torch.dtype) -> bool:
 
 def _align(n: int) -> int:
     return (n + ALIGN - 1) // ALIGN * ALIGN
+
+
+def _align_q(n: int) -> int:
+    return (n + BUCKET_QUANTUM - 1) // BUCKET_QUANTUM * BUCKET_QUANTUM
 
 
 # ====================================================================== plan objects
@@ -174,8 +182,7 @@ class NativeResNet(nn.Module):
         self.feat_dim = self.fc.in_features
         if self.num_classes > 1024 or self.feat_dim % 64:
             raise ValueError("unsupported head shape")
-        self.fc_rows = _align(self.num_classes) if self.num_classes % 64 else self.num_classes
-        self.fc_rows = int(math.ceil(self.num_classes / 64) * 64)
+        self.fc_rows = int(math.ceil(self.num_classes / 64) * 64)   # fc rows padded to the tile
 
     def _units_in_grad_order(self):
         """(block-or-None, [ConvBN...]) groups in backward completion order."""
@@ -192,6 +199,7 @@ class NativeResNet(nn.Module):
         off += _align(self.num_classes)
         self.fc_w_off = off
         off += self.fc_rows * self.feat_dim
+        off = _align_q(off)
         self.fc_seg_end = off
         self.block_bounds: List[int] = [off]
         units: List[ConvBN] = []
@@ -204,6 +212,7 @@ class NativeResNet(nn.Module):
                 u.bn_off = off
                 off += 2 * _align(u.cout)   # gamma, beta
                 units.append(u)
+            off = _align_q(off)
             if isinstance(b, Block):
                 b.seg = (start, off)
             self.block_bounds.append(off)
@@ -222,8 +231,11 @@ class NativeResNet(nn.Module):
             u.buf_off = boff
             boff += 2 * _align(u.cout)
             u.nbt_idx = i
-        self.flat_buffers = torch.zeros(boff, dtype=torch.float32, device=dev)
-        self.flat_nbt = torch.zeros(len(units), dtype=torch.int64, device=dev)
+        # running mean/var (f32) and num_batches_tracked (int64) share ONE byte store, so DDP's
+        # per-forward buffer sync (M4) is a single broadcast
+        self.flat_bufstore = torch.zeros(boff * 4 + len(units) * 8, dtype=torch.uint8, device=dev)
+        self.flat_buffers = self.flat_bufstore[:boff * 4].view(torch.float32)
+        self.flat_nbt = self.flat_bufstore[boff * 4:].view(torch.int64)
         self.stem_packed = torch.zeros(64, 256, dtype=self.dtype, device=dev)   # [64][4][4][16]
         self.stem_wgrad = torch.zeros(64 * 256, dtype=torch.float32, device=dev)
         self.bn_state = torch.zeros(sum(4 * _align(u.cout) for u in units), dtype=torch.float32,
@@ -347,8 +359,18 @@ class NativeResNet(nn.Module):
 
     @torch.no_grad()
     def broadcast_buffers_from_rank0(self, comm) -> None:
-        comm.broadcast(self.flat_buffers, 0)
-        comm.broadcast(self.flat_nbt, 0)
+        comm.broadcast(self.flat_bufstore, 0)     # running stats + counters: one collective
+
+    def layout_signature(self) -> List[int]:
+        """Integers every DDP rank must agree on before any collective (torch DDP's
+        ``_verify_param_shape_across_processes``): flat sizes, geometry,
+        precision and a digest of every parameter's shape and offset."""
+        import zlib
+        desc = ";".join(f"{n}:{tuple(p.shape)}:{(p.data_ptr() - self.flat_params.data_ptr()) // 4}"
+                        for n, p in self.named_parameters())
+        dt = {torch.float32: 0, torch.bfloat16: 1, torch.float16: 2}[self.dtype]
+        return [self.numel, self.flat_bufstore.numel(), self.image_size, dt, self.num_classes,
+                len(self.block_bounds), zlib.crc32(desc.encode())]
 
     def zero_grad_flat(self) -> None:
         self.flat_grad.zero_()
@@ -421,7 +443,8 @@ class NativeResNet(nn.Module):
         return y
 
     def _coeffs(self, u: ConvBN, train: bool):
-        """(scale, shift) tensors -- eval needs private copies (state is shared)."""
+        """(scale, shift) of unit ``u`` written by its finalize (train) / eval-coefficient kernel:
+        views of the shared per-unit state, valid until the next forward of the same unit."""
         return u.state[2], u.state[3]
 
     def native_forward(self, x: torch.Tensor, train: bool, save: bool) -> torch.Tensor:
@@ -963,3 +986,8 @@ class NativeTrainer:
 
     def last_loss(self):
         return None if self._loss is None else float(self._loss.item())
+
+    def state_checksum(self) -> torch.Tensor:
+        """Bit-exact checksum of master weights + momentum (bench cross-rank consistency)."""
+        from ..bench_step import tensor_checksum
+        return tensor_checksum([self.model.flat_params, self.opt.flat_mom])

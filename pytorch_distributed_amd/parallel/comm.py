@@ -32,7 +32,9 @@ class Communicator:
     def wait(self, handle: Any) -> None:
         raise NotImplementedError
 
-    def all_reduce(self, t: torch.Tensor) -> None:
+    def all_reduce(self, t: torch.Tensor, op: str = "sum") -> None:
+        if op != "sum":
+            raise NotImplementedError(op)
         self.wait(self.all_reduce_async(t))
 
     def broadcast(self, t: torch.Tensor, src: int = 0) -> None:
@@ -54,6 +56,11 @@ class ProcessGroupCommunicator(Communicator):
     def wait(self, handle) -> None:
         if handle is not None:
             handle.wait()
+
+    _OPS = {"sum": dist.ReduceOp.SUM, "max": dist.ReduceOp.MAX, "min": dist.ReduceOp.MIN}
+
+    def all_reduce(self, t: torch.Tensor, op: str = "sum") -> None:
+        dist.all_reduce(t, op=self._OPS[op], group=self.group)
 
     def broadcast(self, t: torch.Tensor, src: int = 0) -> None:
         dist.broadcast(t, src=src, group=self.group)

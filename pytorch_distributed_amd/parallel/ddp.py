@@ -18,7 +18,7 @@ the native backward schedule (see :class:`NativeReducer`).
 from __future__ import annotations
 
 import os
-from typing import List, Optional, Sequence
+from typing import List, Optional, Sequence, Tuple
 
 import torch
 from torch import nn
@@ -26,7 +26,26 @@ from torch import nn
 from .comm import Communicator, make_communicator
 from .reducer import MiB, Reducer, plan_buckets
 
-__all__ = ["DistributedDataParallel", "NativeReducer", "convert_sync_batchnorm"]
+__all__ = ["DistributedDataParallel", "NativeReducer", "convert_sync_batchnorm",
+           "plan_native_buckets", "verify_across_ranks"]
+
+
+def plan_native_buckets(boundaries: Sequence[int], elem_bytes: int, bucket_cap_mb: float = 32.0,
+                        first_bucket_mb: float = 1.0,
+                        last_bucket_mb: Optional[float] = 2.0) -> List[Tuple[int, int]]:
+    """Contiguous ``(begin, end)`` element ranges of a flat gradient whose segments complete at
+    ``boundaries`` (gradient-production order). Pure function of its arguments, so every rank
+    computes the same plan (and it is checked across ranks at construction)."""
+    segs = []
+    prev = 0
+    for b in boundaries:
+        if b > prev:
+            segs.append((prev, b))
+            prev = b
+    groups = plan_buckets([(e - s) * elem_bytes for s, e in segs], int(bucket_cap_mb * MiB),
+                          int(first_bucket_mb * MiB),
+                          int(last_bucket_mb * MiB) if last_bucket_mb else None)
+    return [(segs[g[0]][0], segs[g[-1]][1]) for g in groups]
 
 
 class NativeReducer:
@@ -36,26 +55,19 @@ class NativeReducer:
     elements of the flat gradient that are final (the flat buffer is laid out in
     gradient-production order). Each bucket whose end is covered is launched on
     the communicator stream immediately; :meth:`finish` makes the compute stream
-    wait for all of them.
+    wait for all of them. ``defer=True`` launches every bucket at :meth:`finish`
+    instead (no overlap; used with SyncBatchNorm so two communicators never have
+    collectives in flight at the same time).
     """
 
     def __init__(self, flat_grad: torch.Tensor, boundaries: Sequence[int], comm: Communicator,
                  bucket_cap_mb: float = 32.0, first_bucket_mb: float = 1.0,
-                 last_bucket_mb: Optional[float] = 2.0) -> None:
+                 last_bucket_mb: Optional[float] = 2.0, buckets=None, defer: bool = False) -> None:
         self.flat = flat_grad
         self.comm = comm
-        # boundaries: cumulative element offsets at which gradient segments complete
-        segs = []
-        prev = 0
-        for b in boundaries:
-            if b > prev:
-                segs.append((prev, b))
-                prev = b
-        es = flat_grad.element_size()
-        groups = plan_buckets([(e - s) * es for s, e in segs], int(bucket_cap_mb * MiB),
-                              int(first_bucket_mb * MiB),
-                              int(last_bucket_mb * MiB) if last_bucket_mb else None)
-        self.buckets = [(segs[g[0]][0], segs[g[-1]][1]) for g in groups]
+        self.buckets = list(buckets) if buckets is not None else plan_native_buckets(
+            boundaries, flat_grad.element_size(), bucket_cap_mb, first_bucket_mb, last_bucket_mb)
+        self.defer = defer
         self._next = 0
         self._works: List = []
         self.prescale = True
@@ -66,6 +78,11 @@ class NativeReducer:
                 and os.environ.get("PDA_CPP_REDUCER", "1") != "0"):
             self.native = comm.make_bucket_reducer(flat_grad, self.buckets)
 
+    @property
+    def bucket_bytes(self) -> List[int]:
+        es = self.flat.element_size()
+        return [(e - s) * es for s, e in self.buckets]
+
     def reset(self) -> None:
         self._next = 0
         self._works = []
@@ -73,6 +90,11 @@ class NativeReducer:
             self.native.reset()
 
     def grads_ready(self, upto: int) -> None:
+        if self.defer:
+            return
+        self._launch_upto(upto)
+
+    def _launch_upto(self, upto: int) -> None:
         if self.native is not None:
             self.native.ready(upto)
             return
@@ -92,10 +114,32 @@ class NativeReducer:
         if self.native is not None:
             self.native.finish()
             return
-        self.grads_ready(self.flat.numel())
+        self._launch_upto(self.flat.numel())
         for w in self._works:
             self.comm.wait(w)
         self.reset()
+
+    def close(self) -> None:
+        if self.native is not None:
+            self.native.close()
+            self.native = None
+
+
+def verify_across_ranks(comm: Communicator, values: Sequence[int], names: Sequence[str],
+                        device: torch.device) -> None:
+    """Raise on every rank if the ranks disagree on ``values`` (one MIN and one MAX all-reduce of
+    a small int64 vector) -- torch DDP's ``_verify_param_shape_across_processes`` (SURVEY §2.8
+    M3): a rank with a different architecture, image size, precision or bucket plan would
+    otherwise issue collectives of different sizes and hang or corrupt its peers."""
+    v = torch.tensor([int(x) for x in values], dtype=torch.int64, device=device)
+    lo, hi = v.clone(), v.clone()
+    comm.all_reduce(lo, "min")
+    comm.all_reduce(hi, "max")
+    lo, hi = lo.tolist(), hi.tolist()
+    bad = [f"{n}: min {a} max {b}" for n, a, b in zip(names, lo, hi) if a != b]
+    if bad:
+        raise RuntimeError(f"DistributedDataParallel: ranks disagree on the model/bucket layout "
+                           f"(rank {comm.rank}): " + "; ".join(bad))
 
 
 def convert_sync_batchnorm(module: nn.Module, process_group=None) -> nn.Module:
@@ -127,23 +171,46 @@ class DistributedDataParallel(nn.Module):
             self.comm.start_watchdog(float(os.environ.get("MX_WATCHDOG_S", "5")))
         self._native = hasattr(module, "flat_params")
         cap = bucket_cap_mb or 32.0
+        self.bn_comm = None
         if self._native:
+            use_sync_bn = bool(sync_bn if sync_bn is not None else getattr(module, "sync_bn", False)) \
+                and self.comm.world_size > 1
+            buckets = plan_native_buckets(module.grad_boundaries(), module.flat_grad.element_size(), cap)
+            import zlib
+            digest = zlib.crc32(repr(buckets).encode())
+            sig = module.layout_signature()
+            verify_across_ranks(self.comm, sig + [len(buckets), digest, int(use_sync_bn)],
+                                [f"layout[{i}]" for i in range(len(sig))]
+                                + ["num_buckets", "bucket_plan_crc", "sync_bn"], dev)   # M3
             module.sync_from_rank0(self.comm)                    # M2: one flat broadcast
-            self.reducer = NativeReducer(module.flat_grad, module.grad_boundaries(), self.comm, cap)
+            self.reducer = NativeReducer(module.flat_grad, module.grad_boundaries(), self.comm, cap,
+                                         buckets=buckets, defer=use_sync_bn)
             module.attach_reducer(self.reducer)
-            self.bn_comm = None
-            if (sync_bn if sync_bn is not None else getattr(module, "sync_bn", False)) \
-                    and self.comm.world_size > 1:
-                # SyncBN collectives run on the compute stream while bucket all-reduces run on
-                # the comm stream: a second RCCL communicator keeps the two sequences independent
+            if use_sync_bn:
+                # SyncBN collectives run on the compute stream, bucket all-reduces on the comm
+                # stream of a second RCCL communicator. Two communicators with collectives in
+                # flight at once can deadlock when ranks order them differently, so with SyncBN
+                # the buckets are deferred to the end of backward (no overlap): the two
+                # communicators' collectives never run concurrently.
                 self.bn_comm = (make_communicator(dev, process_group)
                                 if hasattr(self.comm, "make_bucket_reducer") else self.comm)
                 module.set_sync_bn(self.bn_comm)
         else:
+            params = [p for p in module.parameters()]
+            import zlib
+            shapes = zlib.crc32(repr([tuple(p.shape) for p in params]).encode())
+            verify_across_ranks(self.comm, [len(params), sum(p.numel() for p in params), shapes,
+                                            len(list(module.buffers()))],
+                                ["num_params", "numel", "shapes_crc", "num_buffers"], dev)   # M3
             with torch.no_grad():
                 for t in list(module.parameters()) + list(module.buffers()):   # M2
                     self.comm.broadcast(t.data, 0)
             self.reducer = Reducer(module.parameters(), self.comm, cap)
+
+    @property
+    def rccl_world(self) -> Optional[int]:
+        """Ranks as counted by RCCL itself (None when the communicator is not native RCCL)."""
+        return self.comm.rccl_count if hasattr(self.comm, "rccl_count") else None
 
     def _sync_buffers(self) -> None:
         if self._native:

@@ -134,8 +134,7 @@ class DataParallel(nn.Module):
             r = NativeResNet(ref, device=dev, dtype=m.dtype, image_size=m.image_size)
             with torch.no_grad():
                 r.flat_params.copy_(m.flat_params)
-                r.flat_buffers.copy_(m.flat_buffers)
-                r.flat_nbt.copy_(m.flat_nbt)
+                r.flat_bufstore.copy_(m.flat_bufstore)
             r.refresh_shadow()
         return r
 
@@ -164,13 +163,12 @@ class DataParallel(nn.Module):
         if not self.replicas:
             return
         if self._native:
-            for name in ("flat_buffers", "flat_nbt"):
-                ts = [getattr(m, name) for m in self.all_modules]
-                if self.group is not None:
-                    self.group.broadcast(ts, 0)
-                else:
-                    for t in ts[1:]:
-                        t.copy_(ts[0], non_blocking=True)
+            ts = [m.flat_bufstore for m in self.all_modules]   # running stats + counters
+            if self.group is not None:
+                self.group.broadcast(ts, 0)
+            else:
+                for t in ts[1:]:
+                    t.copy_(ts[0], non_blocking=True)
             return
         src = list(self.module.parameters()) + list(self.module.buffers())
         for r in self.replicas:

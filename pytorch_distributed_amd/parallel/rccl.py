@@ -24,12 +24,13 @@ import torch.distributed as dist
 
 from .comm import Communicator
 
-__all__ = ["RcclBucketReducer", "RcclCommunicator", "RcclGroup", "load"]
+__all__ = ["CommAbortedError", "RcclBucketReducer", "RcclCommunicator", "RcclGroup", "load"]
 
 LIBPATH = Path(__file__).resolve().parent.parent / "_lib" / "libpda_comm.so"
 _LIB: Optional[C.CDLL] = None
 _DT = {torch.float32: 0, torch.bfloat16: 1, torch.float16: 2, torch.int64: 3, torch.float64: 4,
-       torch.int32: 5}
+       torch.int32: 5, torch.uint8: 6}
+ERR_ABORTED = 1001   # csrc/comm/comm.h kErrAborted
 _OPS = {"sum": 0, "avg": 1, "max": 2, "min": 3}
 _gen = itertools.count()
 
@@ -47,7 +48,10 @@ def load() -> C.CDLL:
             "pda_comm_init_rank": [C.c_char_p, I, I, I, C.POINTER(V)],
             "pda_comm_init_all": [C.POINTER(I), I, C.POINTER(V)],
             "pda_comm_destroy": [V, I],
+            "pda_comm_abort": [V, I],
+            "pda_comm_is_aborted": [V],
             "pda_comm_check": [V],
+            "pda_comm_count": [V, C.POINTER(I)],
             "pda_allreduce": [V, V, V, Z, I, I, V],
             "pda_broadcast": [V, V, V, Z, I, I, V],
             "pda_reduce": [V, V, V, Z, I, I, I, V],
@@ -61,6 +65,9 @@ def load() -> C.CDLL:
             "pda_reducer_finish": [V, V, V],
             "pda_reducer_reset": [V],
             "pda_reducer_destroy": [V],
+            "pda_reducer_num_buckets": [V],
+            "pda_reducer_set_timing": [V, I],
+            "pda_reducer_timing": [V, C.POINTER(C.c_float)],
         }
         for n, a in sigs.items():
             f = getattr(lib, n)
@@ -74,10 +81,15 @@ def load() -> C.CDLL:
     return _LIB
 
 
+class CommAbortedError(RuntimeError):
+    """The communicator was aborted (watchdog saw an asynchronous error, or it was closed)."""
+
+
 def _check(rc: int, what: str) -> None:
     if rc != 0:
-        msg = load().pda_comm_error_string(rc).decode() if rc > 0 else "hip error"
-        raise RuntimeError(f"RCCL {what} failed: {msg} ({rc})")
+        msg = load().pda_comm_error_string(rc).decode()
+        cls = CommAbortedError if rc == ERR_ABORTED else RuntimeError
+        raise cls(f"RCCL {what} failed: {msg} ({rc})")
 
 
 class RcclCommunicator(Communicator):
@@ -101,9 +113,43 @@ class RcclCommunicator(Communicator):
         else:
             uid = store.get(key)
         self._h = C.c_void_p()
-        _check(lib.pda_comm_init_rank(uid, self.world_size, self.rank, self.device.index,
-                                      C.byref(self._h)), "init_rank")
+        self._init_rank(lib, uid)
         self.stream = torch.cuda.Stream(self.device, priority=-1)
+        self._watchdog_error = None
+        self._watchdog = None
+        self._watchdog_stop = None
+
+    def _init_rank(self, lib, uid: bytes) -> None:
+        """``ncclCommInitRank`` blocks until every rank has joined; run it with a deadline
+        (``PDA_RCCL_INIT_TIMEOUT_S``, default 600 s) so a missing or mismatched rank becomes a
+        clear error instead of a silent hang (ctypes releases the GIL during the call)."""
+        import threading
+        timeout = float(os.environ.get("PDA_RCCL_INIT_TIMEOUT_S", "600"))
+        res = {}
+
+        def run():
+            res["rc"] = lib.pda_comm_init_rank(uid, self.world_size, self.rank, self.device.index,
+                                               C.byref(self._h))
+        t = threading.Thread(target=run, name="rccl-init", daemon=True)
+        t.start()
+        t.join(timeout)
+        if t.is_alive():
+            raise TimeoutError(f"ncclCommInitRank did not complete within {timeout:.0f} s on rank "
+                               f"{self.rank}/{self.world_size} (a rank missing or stuck?)")
+        _check(res["rc"], "init_rank")
+
+    def _live(self) -> C.c_void_p:
+        """The native handle, or raise if the communicator was closed / aborted by the watchdog."""
+        if not self._h or self._watchdog_error is not None:
+            self.check()
+        return self._h
+
+    @property
+    def rccl_count(self) -> int:
+        """Number of ranks RCCL itself reports for this communicator (``ncclCommCount``)."""
+        n = C.c_int(0)
+        _check(load().pda_comm_count(self._live(), C.byref(n)), "comm_count")
+        return int(n.value)
 
     # async on the comm stream ----------------------------------------------------------
     def all_reduce_async(self, t: torch.Tensor, op: str = "sum"):
@@ -111,7 +157,7 @@ class RcclCommunicator(Communicator):
         ready = torch.cuda.Event()
         ready.record(cur)
         self.stream.wait_event(ready)
-        _check(load().pda_allreduce(self._h, t.data_ptr(), t.data_ptr(), t.numel(), _DT[t.dtype],
+        _check(load().pda_allreduce(self._live(), t.data_ptr(), t.data_ptr(), t.numel(), _DT[t.dtype],
                                     _OPS[op], self.stream.cuda_stream), "allreduce")
         done = torch.cuda.Event()
         done.record(self.stream)
@@ -123,7 +169,7 @@ class RcclCommunicator(Communicator):
         return RcclBucketReducer(self, flat, buckets)
 
     def wait(self, handle) -> None:
-        if getattr(self, "_watchdog_error", None) is not None:
+        if self._watchdog_error is not None:
             self.check()
         if handle is not None:
             torch.cuda.current_stream(self.device).wait_event(handle)
@@ -131,22 +177,22 @@ class RcclCommunicator(Communicator):
     # ordered on the current stream ----------------------------------------------------
     def broadcast(self, t: torch.Tensor, src: int = 0) -> None:
         st = torch.cuda.current_stream(self.device).cuda_stream
-        _check(load().pda_broadcast(self._h, t.data_ptr(), t.data_ptr(), t.numel(), _DT[t.dtype], src,
+        _check(load().pda_broadcast(self._live(), t.data_ptr(), t.data_ptr(), t.numel(), _DT[t.dtype], src,
                                     st), "broadcast")
 
     def all_reduce(self, t: torch.Tensor, op: str = "sum") -> None:
         st = torch.cuda.current_stream(self.device).cuda_stream
-        _check(load().pda_allreduce(self._h, t.data_ptr(), t.data_ptr(), t.numel(), _DT[t.dtype],
+        _check(load().pda_allreduce(self._live(), t.data_ptr(), t.data_ptr(), t.numel(), _DT[t.dtype],
                                     _OPS[op], st), "allreduce")
 
     def reduce(self, t: torch.Tensor, dst: int = 0, op: str = "sum") -> None:
         st = torch.cuda.current_stream(self.device).cuda_stream
-        _check(load().pda_reduce(self._h, t.data_ptr(), t.data_ptr(), t.numel(), _DT[t.dtype], _OPS[op],
+        _check(load().pda_reduce(self._live(), t.data_ptr(), t.data_ptr(), t.numel(), _DT[t.dtype], _OPS[op],
                                  dst, st), "reduce")
 
     def all_gather(self, out: torch.Tensor, t: torch.Tensor) -> None:
         st = torch.cuda.current_stream(self.device).cuda_stream
-        _check(load().pda_allgather(self._h, t.data_ptr(), out.data_ptr(), t.numel(), _DT[t.dtype], st),
+        _check(load().pda_allgather(self._live(), t.data_ptr(), out.data_ptr(), t.numel(), _DT[t.dtype], st),
                "allgather")
 
     def barrier(self) -> None:
@@ -155,41 +201,63 @@ class RcclCommunicator(Communicator):
         torch.cuda.current_stream(self.device).synchronize()
 
     def check(self) -> None:
-        """Raise if the communicator saw an asynchronous error (dead peer, network)."""
-        err = getattr(self, "_watchdog_error", None)
+        """Raise if the communicator saw an asynchronous error (dead peer, network) or was aborted."""
+        err = self._watchdog_error
         if err is not None:
-            raise RuntimeError(f"RCCL communicator aborted by watchdog: {err}")
+            raise CommAbortedError(f"RCCL communicator aborted by watchdog: {err}")
+        if not self._h:
+            raise CommAbortedError("RCCL communicator closed")
         _check(load().pda_comm_check(self._h), "async")
 
+    @property
+    def aborted(self) -> bool:
+        return not self._h or bool(load().pda_comm_is_aborted(self._h))
+
+    def abort(self) -> None:
+        """Abort in-flight and future collectives WITHOUT freeing the communicator (that happens in
+        :meth:`close` on the owning thread): blocked collectives return, later enqueues -- including
+        every bucket launch of a reducer built on it -- fail with :class:`CommAbortedError`."""
+        if self._h:
+            load().pda_comm_abort(self._h, 2000)
+
     def start_watchdog(self, interval_s: float = 5.0) -> None:
-        """Poll ``ncclCommGetAsyncError`` from a daemon thread; on an error (e.g. a dead peer)
-        abort the communicator so collectives blocked on it return instead of hanging, and make
-        the next :meth:`check` / :meth:`wait` raise (SURVEY §5.3 failure detection)."""
+        """Poll ``ncclCommGetAsyncError`` from a daemon thread; on an error (e.g. a dead peer) abort
+        the communicator so collectives blocked on it return instead of hanging, and make the next
+        :meth:`check` / :meth:`wait` / bucket launch raise (SURVEY §5.3 failure detection). The
+        thread never frees anything (csrc/comm/comm.h lifetime model)."""
         import threading
+        stop = threading.Event()
+        lib, h = load(), self._h
 
         def run():
-            while self._h and getattr(self, "_watchdog_on", False):
-                rc = load().pda_comm_check(self._h)
-                if rc != 0:
-                    self._watchdog_error = load().pda_comm_error_string(rc).decode() if rc > 0 else rc
-                    load().pda_comm_destroy(self._h, 1)
-                    self._h = C.c_void_p()
+            while not stop.wait(interval_s):
+                rc = lib.pda_comm_check(h)
+                if rc == ERR_ABORTED:
                     return
-                threading.Event().wait(interval_s)
+                if rc != 0:
+                    self._watchdog_error = lib.pda_comm_error_string(rc).decode()
+                    lib.pda_comm_abort(h, 2000)
+                    return
 
-        self._watchdog_on = True
+        self._watchdog_stop = stop
         t = threading.Thread(target=run, name="rccl-watchdog", daemon=True)
         t.start()
         self._watchdog = t
 
     def stop_watchdog(self) -> None:
-        self._watchdog_on = False
+        if self._watchdog_stop is not None:
+            self._watchdog_stop.set()
+        if self._watchdog is not None:
+            self._watchdog.join()
+        self._watchdog = self._watchdog_stop = None
 
     def close(self, abort: bool = False) -> None:
+        """Stop the watchdog, then drop this handle's reference (reducers built on the
+        communicator keep the native struct alive, aborted, until they are closed too)."""
         self.stop_watchdog()
         if self._h:
-            load().pda_comm_destroy(self._h, int(abort))
-            self._h = C.c_void_p()
+            h, self._h = self._h, C.c_void_p()
+            load().pda_comm_destroy(h, int(abort))
 
 
 class RcclBucketReducer:
@@ -208,37 +276,54 @@ class RcclBucketReducer:
         self.buckets = [(int(s), int(e)) for s, e in buckets]
         arr = (C.c_longlong * (2 * len(self.buckets)))(*[v for b in self.buckets for v in b])
         self._h = C.c_void_p()
-        _check(load().pda_reducer_create(comm._h, flat.data_ptr(), _DT[flat.dtype], _OPS["avg"], arr,
+        _check(load().pda_reducer_create(comm._live(), flat.data_ptr(), _DT[flat.dtype], _OPS["avg"], arr,
                                          len(self.buckets), comm.stream.cuda_stream, C.byref(self._h)),
                "reducer_create")
 
-    def _live(self) -> None:
-        if not self.comm._h or getattr(self.comm, "_watchdog_error", None) is not None:
-            self.comm.check()
-            raise RuntimeError("RCCL communicator closed")
+    def _hh(self) -> C.c_void_p:
+        if not self._h:
+            raise CommAbortedError("bucket reducer closed")
+        return self._h
 
     def ready(self, upto: int) -> None:
-        self._live()
         st = torch.cuda.current_stream(self.comm.device).cuda_stream
-        _check(load().pda_reducer_ready(self._h, int(upto), st), "reducer_ready")
+        self._rc(load().pda_reducer_ready(self._hh(), int(upto), st), "reducer_ready")
 
     def finish(self) -> None:
-        self._live()
         st = torch.cuda.current_stream(self.comm.device).cuda_stream
-        _check(load().pda_reducer_finish(self._h, st, st), "reducer_finish")
+        self._rc(load().pda_reducer_finish(self._hh(), st, st), "reducer_finish")
+
+    def _rc(self, rc: int, what: str) -> None:
+        if rc == ERR_ABORTED and self.comm._watchdog_error is not None:
+            raise CommAbortedError(f"RCCL {what}: communicator aborted by watchdog: "
+                                   f"{self.comm._watchdog_error}")
+        _check(rc, what)
 
     def reset(self) -> None:
-        load().pda_reducer_reset(self._h)
+        load().pda_reducer_reset(self._hh())
 
     @property
     def launched(self) -> int:
         """Total bucket all-reduces launched since construction."""
         return int(load().pda_reducer_launched(self._h))
 
+    def set_timing(self, on: bool) -> None:
+        """Record per-bucket / exposed-communication timing events from the next step on (the
+        events cost a few us per bucket: diagnostics only, never in a timed run)."""
+        _check(load().pda_reducer_set_timing(self._h, int(bool(on))), "reducer_set_timing")
+
+    def timing(self):
+        """After a timed step has completed (synchronise first): ``(exposed_ms, [bucket_ms...])``
+        -- exposed = backward end -> last bucket all-reduce done on the comm stream."""
+        nb = len(self.buckets)
+        out = (C.c_float * (nb + 1))()
+        _check(load().pda_reducer_timing(self._h, out), "reducer_timing")
+        return float(out[0]), [float(v) for v in out[1:]]
+
     def close(self) -> None:
         if self._h:
-            load().pda_reducer_destroy(self._h)
-            self._h = C.c_void_p()
+            h, self._h = self._h, C.c_void_p()
+            load().pda_reducer_destroy(h)
 
     def __del__(self):
         try:
@@ -276,3 +361,8 @@ class RcclGroup:
     def reduce(self, ts: List[torch.Tensor], root: int = 0, op: str = "sum") -> None:
         _check(load().pda_group_reduce(self._h, self._bufs(ts), ts[0].numel(), _DT[ts[0].dtype],
                                        _OPS[op], root, self._streams()), "group_reduce")
+
+    def close(self) -> None:
+        if self._h:
+            h, self._h = self._h, C.c_void_p()
+            load().pda_comm_destroy(h, 0)

@@ -10,10 +10,28 @@ Design (MI355X-first):
   *view* into it (``gradient_as_bucket_view``) -- no bucket copy-in/copy-out;
   with the native engine the whole model's gradients already live in ONE flat
   buffer laid out in gradient-production order, so buckets are just slices;
-* bucket sizes are chosen for xGMI: a ring all-reduce of S bytes over n ranks
-  moves 2(n-1)/n*S per link, so per-bucket latency, not bandwidth, dominates for
-  small buckets; middle buckets default to 32 MiB and the *last* bucket (the one
+* bucket sizes are chosen for xGMI: middle buckets default to 32 MiB, the first
+  (fc) bucket fires as soon as its gradient exists, and the *last* bucket (the one
   exposed after backward ends) is kept small (2 MiB) so the tail is short;
+* xGMI cost model behind the defaults. An MI355X node is 8 GPUs, each with 7
+  point-to-point xGMI links of ~153 GB/s. RCCL runs an 8-rank all-reduce over several channels
+  so all 7 links carry traffic; each rank moves 2(n-1)/n * S bytes:
+
+      T(S) ~= alpha + 2 * (7/8) * S / (7 * 153 GB/s * eta),  alpha ~ 15-30 us, eta ~ 0.6-0.8
+
+  ResNet-50 has S_total = 102 MB of f32 gradients per step: ~0.25 ms of link time against
+  ~20 ms of backward at bs 400, so bandwidth never binds. What the plan optimises instead:
+    1. the number of collectives -- each costs alpha on the comm stream plus a kernel launch whose
+       workgroups compete with backward for CUs. 32 MiB middle buckets give 5-6 collectives per
+       step, and at 32 MiB alpha is < 10 % of T(S);
+    2. the exposed tail -- the bucket completing when backward ends (stem + layer1) runs after the
+       last backward kernel. Capping it at 2 MiB bounds the tail at ~alpha + 4 us (~30 us);
+    3. alignment -- the native engine pads every bucket boundary to a multiple of
+       8 ranks x 7 links x 256 B (``models/native.py`` BUCKET_QUANTUM), so RCCL's per-rank /
+       per-channel chunks are equal and 256-B aligned for any world size dividing 8.
+  ``bench.py`` reports the measured per-bucket all-reduce time and the exposed tail
+  (``bucket_allreduce_ms``, ``exposed_comm_ms``) for N > 1, so the model can be checked on a
+  real node;
 * readiness: ``Tensor.register_post_accumulate_grad_hook`` (generic modules) or
   the native engine's ``on_grads_ready(offset)`` callback; a ready bucket is
   pre-scaled by 1/world and all-reduced (SUM) asynchronously through a
@@ -79,6 +97,7 @@ class Bucket:
         self.params = params
         self.offsets = offsets
         self.pending = len(params)
+        self.got = set()      # indices of params whose gradient arrived this step
         self.work = None
 
     def view_for(self, j: int) -> torch.Tensor:
@@ -119,6 +138,10 @@ class Reducer:
         self._armed = False
         self.enabled = True
 
+    @property
+    def bucket_bytes(self) -> List[int]:
+        return [b.buffer.numel() * b.buffer.element_size() for b in self.buckets]
+
     # -- backward-time machinery ---------------------------------------------------------
     def _arm(self) -> None:
         if self._armed:
@@ -126,6 +149,7 @@ class Reducer:
         self._armed = True
         for b in self.buckets:
             b.pending = len(b.params)
+            b.got = set()
             b.work = None
         torch.autograd.Variable._execution_engine.queue_callback(self._finalize)
 
@@ -140,6 +164,7 @@ class Reducer:
         elif p.grad.data_ptr() != view.data_ptr():
             view.copy_(p.grad)
         p.grad = view
+        b.got.add(j)
         b.pending -= 1
         if b.pending == 0:
             self._launch(b)
@@ -150,8 +175,12 @@ class Reducer:
 
     def _finalize(self) -> None:
         for b in self.buckets:
-            if b.work is None:  # params that received no grad this step: reduce zeros
+            if b.work is None:
+                # params that received no gradient this step contribute ZEROS (their bucket view
+                # still holds last step's values: never reduce those)
                 for j, p in enumerate(b.params):
+                    if j not in b.got:
+                        b.view_for(j).zero_()
                     if p.grad is None or p.grad.data_ptr() != b.view_for(j).data_ptr():
                         p.grad = b.view_for(j)
                 self._launch(b)

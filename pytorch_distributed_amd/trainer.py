@@ -33,7 +33,8 @@ from .utils.checkpoint import load_latest, save_best, save_latest
 from .utils.metrics import MetricsLog, gpu_mem_gb
 from .utils.suspend import SuspendMonitor, go_suspend
 
-__all__ = ["Context", "train", "validate", "run", "resolve_device", "resolve_dtype"]
+__all__ = ["Context", "train", "validate", "run", "resolve_device", "resolve_dtype",
+           "load_model_state"]
 
 
 @dataclass
@@ -66,9 +67,13 @@ def resolve_device(cfg: RunConfig, local_rank: int = 0) -> torch.device:
 
 
 def resolve_dtype(cfg: RunConfig, device: torch.device) -> torch.dtype:
+    """``auto`` = the reference script's precision: fp32 for the single / DP / DDP scripts
+    (``resnet_single_gpu.py:27-31``, ``resnet_dp.py:21-25``, ``restnet_ddp.py:26-30`` run
+    without autocast), fp16 for the AMP script (its SCRIPT_DEFAULTS). bf16 is opt-in
+    (``MX_DTYPE=bf16``)."""
     d = cfg.dtype
     if d == "auto":
-        d = "bf16" if device.type == "cuda" else "fp32"
+        d = "fp32"
     return {"fp32": torch.float32, "bf16": torch.bfloat16, "fp16": torch.float16}[d]
 
 
@@ -89,6 +94,13 @@ def _autocast(ctx: Context):
 
 def _unwrap(model: nn.Module) -> nn.Module:
     return getattr(model, "module", model)
+
+
+def load_model_state(model: nn.Module, state_dict) -> None:
+    """Resume-time model load (reference ``restnet_ddp.py:127-132`` loads into the unwrapped
+    module). DataParallel must load through the wrapper, which re-copies the weights into every
+    replica -- loading only ``.module`` would leave replicas 1..N-1 on their old weights."""
+    (model if hasattr(model, "replicas") else _unwrap(model)).load_state_dict(state_dict)
 
 
 def _sync_step(ctx: Context) -> None:
@@ -268,7 +280,9 @@ def run(cfg: RunConfig, mode: str, local_rank: int = 0, nprocs: Optional[int] = 
         env = dist_env(local_rank, nprocs)
         backend = "nccl" if device.type == "cuda" else "gloo"
         init_distributed(env, backend, device=device)
-        ctx.rank, ctx.world, ctx.distributed = env.rank, env.world_size, env.world_size > 1 or True
+        # the DDP scripts take the distributed code path (sampler, all-reduced validation) even
+        # with a single process, as the reference does
+        ctx.rank, ctx.world, ctx.distributed = env.rank, env.world_size, True
     save_path = Path(cfg.save_path)
     save_path.mkdir(exist_ok=True, parents=True)
     ctx.metrics = MetricsLog(save_path / "metrics.jsonl", enabled=cfg.metrics and ctx.is_main)
@@ -296,7 +310,7 @@ def run(cfg: RunConfig, mode: str, local_rank: int = 0, nprocs: Optional[int] = 
     best_acc, start_epoch, start_step = 0.0, 0, 0
     ckpt = load_latest(save_path)
     if ckpt is not None:
-        _unwrap(model).load_state_dict(ckpt["model"])
+        load_model_state(model, ckpt["model"])
         optimizer.load_state_dict(ckpt["optimizer"])
         scheduler.load_state_dict(ckpt["scheduler"])
         if ctx.scaler is not None and "scaler" in ckpt:

@@ -1,0 +1,69 @@
+"""The driver's ``bench.py`` contract rehearsed on the CPU (gloo, no GPU): one JSON line from rank
+0 with the headline keys, MAX-over-ranks timing, the N>1 self-validation keys (bucket plan,
+cross-rank bit-exact weight checksum) -- and a rank whose weights diverge makes the run exit
+non-zero (``PDA_BENCH_PERTURB_RANK`` test hook)."""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ARGS = ["--device", "cpu", "--arch", "resnet18", "--batch", "2", "--image-size", "32",
+        "--steps", "2", "--warmup", "1", "--dtype", "fp32", "--fp32-steps", "0"]
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _run(nproc, extra_env=None, tmp=None):
+    env = dict(os.environ)
+    env.update({"OMP_NUM_THREADS": "2", "PDA_BIND_NUMA": "0"})
+    env.update(extra_env or {})
+    if nproc == 1:
+        cmd = [sys.executable, os.path.join(ROOT, "bench.py"), *ARGS]
+    else:
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node",
+               str(nproc), "--master-addr", "127.0.0.1", "--master-port", str(_port()),
+               os.path.join(ROOT, "bench.py"), "--gpus", str(nproc), *ARGS]
+    return subprocess.run(cmd, cwd=tmp, env=env, capture_output=True, text=True, timeout=600)
+
+
+def _record(r):
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout + r.stderr[-3000:]
+    return json.loads(lines[0])
+
+
+def test_bench_cpu_single(tmp_path):
+    r = _run(1, tmp=tmp_path)
+    assert r.returncode == 0, r.stderr[-3000:]
+    rec = _record(r)
+    for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step",
+              "higher_is_better", "scaling", "vs_baseline", "dtype", "data", "config"):
+        assert k in rec, k
+    assert rec["n_gpus"] == 1 and rec["steps"] == 2 and rec["warmup"] == 1
+    assert abs(rec["value"] - 2 * 1000.0 / rec["ms_per_step"]) / rec["value"] < 1e-2
+
+
+def test_bench_cpu_two_ranks_self_validation(tmp_path):
+    r = _run(2, tmp=tmp_path)
+    assert r.returncode == 0, r.stderr[-4000:]
+    rec = _record(r)
+    assert rec["n_gpus"] == 2 and rec["config"]["global_batch"] == 4
+    assert rec["config"]["parallelism"] == "dp2"
+    assert rec["weights_consistent"] is True
+    assert rec["buckets"] >= 1 and len(rec["bucket_bytes"]) == rec["buckets"]
+    assert sum(rec["bucket_bytes"]) >= 11_000_000 * 4     # every ResNet-18 gradient is bucketed
+    assert rec["comm"] == "ProcessGroupCommunicator"
+
+
+def test_bench_cpu_diverged_rank_fails(tmp_path):
+    r = _run(2, {"PDA_BENCH_PERTURB_RANK": "1"}, tmp=tmp_path)
+    assert r.returncode != 0
+    assert "parameters differ across ranks" in r.stderr

@@ -41,3 +41,10 @@ def test_bench_torchrun_two_ranks(tmp_path):
     assert rec["value"] > 0 and rec["ms_per_step"] > 0
     assert abs(rec["value"] - 32 * 1000.0 / rec["ms_per_step"]) / rec["value"] < 1e-2
     assert rec["loss"] == rec["loss"]         # finite, not NaN
+    # N>1 self-validation (driver's first multi-GPU run must prove itself)
+    assert rec["weights_consistent"] is True
+    assert rec["buckets"] >= 3 and len(rec["bucket_bytes"]) == rec["buckets"]
+    assert all(b % (8 * 7 * 256) == 0 for b in rec["bucket_bytes"])
+    assert rec["comm"] == "ProcessGroupCommunicator" and rec["rccl_world"] is None   # gloo here
+    # the like-for-like exact-fp32 pass
+    assert rec["fp32_images_per_sec"] > 0 and rec["fp32_engine"] == "native"

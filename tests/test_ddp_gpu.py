@@ -143,8 +143,66 @@ def test_native_ddp_cpp_reducer_world1():
             torch.cuda.synchronize()
             assert red.native.launched == nb * (step + 1)
             assert torch.equal(model.flat_grad, local.flat_grad)
+        # bucket boundaries sit on the xGMI quantum (8 ranks x 7 links x 256 B)
+        from pytorch_distributed_amd.models.native import BUCKET_QUANTUM
+        assert all(s % BUCKET_QUANTUM == 0 and e % BUCKET_QUANTUM == 0 for s, e in red.buckets)
+        assert ddp.rccl_world == 1
+        # timing diagnostics (bench.py exposed_comm_ms / bucket_allreduce_ms)
+        red.native.set_timing(True)
+        x, y = gen(torch.arange(8) + 64)
+        model.zero_grad_flat()
+        crit(ddp(x), y).backward()
+        torch.cuda.synchronize()
+        exposed, per = red.native.timing()
+        red.native.set_timing(False)
+        assert exposed >= 0.0 and len(per) == nb and all(v >= 0.0 for v in per), (exposed, per)
         red.native.close()
         comm.close()
+    finally:
+        dist.destroy_process_group()
+
+
+def test_rccl_abort_world1_reducer_raises_cleanly():
+    """Failure handling: after an abort (what the watchdog does on an async error)
+    the bucket reducer's launches raise CommAbortedError instead of touching a freed
+    communicator, and the communicator / reducer can then be closed in either order."""
+    if dist.is_initialized():
+        pytest.skip("process group already initialised")
+    port = _port()
+    dev = torch.device("cuda", 0)
+    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", world_size=1, rank=0,
+                            device_id=dev)
+    try:
+        from pytorch_distributed_amd.parallel.rccl import CommAbortedError, RcclCommunicator
+        for close_comm_first in (True, False):
+            comm = RcclCommunicator(dev)
+            assert comm.rccl_count == 1 and not comm.aborted
+            flat = torch.ones(4 * 3584, device=dev)
+            red = comm.make_bucket_reducer(flat, [(0, 3584), (3584, 4 * 3584)])
+            red.ready(3584)
+            red.finish()
+            torch.cuda.synchronize()
+            assert torch.equal(flat, torch.ones_like(flat))      # avg over 1 rank
+            comm.abort()
+            assert comm.aborted
+            with pytest.raises(CommAbortedError):
+                red.ready(3584)
+            with pytest.raises(CommAbortedError):
+                red.finish()
+            with pytest.raises(CommAbortedError):
+                comm.all_reduce(flat)
+            with pytest.raises(CommAbortedError):
+                comm.check()
+            if close_comm_first:
+                comm.close()
+                red.close()
+            else:
+                red.close()
+                comm.close()
+            with pytest.raises(CommAbortedError):
+                red.ready(1)
+            with pytest.raises(CommAbortedError):
+                comm.broadcast(flat)
     finally:
         dist.destroy_process_group()
 

@@ -85,3 +85,23 @@ def test_native_dataparallel_graph_step_matches_eager():
         assert torch.equal(graphed.module.flat_params, graphed.replicas[0].flat_params)
         assert torch.equal(eager.module.flat_buffers, graphed.module.flat_buffers)
     assert graphed._graphs[0].graph is not None and eager._graphs[0].graph is None
+
+
+def test_native_dataparallel_resume_reloads_every_replica():
+    """Resuming a DataParallel run (trainer.load_model_state, used by run()) must put the
+    checkpoint weights into EVERY replica, not only replica 0."""
+    from pytorch_distributed_amd.models import build_model
+    from pytorch_distributed_amd.models.native import NativeResNet
+    from pytorch_distributed_amd.parallel import DataParallel
+    from pytorch_distributed_amd.trainer import load_model_state
+    torch.manual_seed(0)
+    dp = DataParallel(NativeResNet(build_model("resnet18"), device=DEV, image_size=64),
+                      device_ids=[0, 0])
+    torch.manual_seed(123)                      # a different "checkpoint"
+    ck = NativeResNet(build_model("resnet18"), device=DEV, image_size=64)
+    assert not torch.equal(dp.module.flat_params, ck.flat_params)
+    load_model_state(dp, ck.state_dict())
+    torch.cuda.synchronize()
+    assert torch.equal(dp.module.flat_params, ck.flat_params)
+    assert torch.equal(dp.replicas[0].flat_params, ck.flat_params)
+    assert torch.equal(dp.replicas[0].flat_shadow, ck.flat_shadow)
