@@ -7,11 +7,12 @@ step on inf/nan. :class:`LossScaler` reproduces that state machine with the
 same public API (``scale``, ``step``, ``update``, ``unscale_``, ``state_dict``,
 ``load_state_dict``, ``get_scale``) but keeps all state on the device:
 
-* with the native :class:`~pytorch_distributed_amd.optim.FusedSGD` the
-  unscale, the non-finite check, the conditional skip and the scale update all
-  run inside the fused SGD / ``amp_update`` kernels -- **no host sync per step**
-  (GradScaler's ``_maybe_opt_step`` does ``found_inf.item()``,
-  ``torch/amp/grad_scaler.py:348-358``);
+* with the native :class:`~pytorch_distributed_amd.models.native.NativeSGD` the
+  non-finite check and the scale update run in ONE kernel (``amp_scan``, csrc/misc.hip:
+  its last workgroup publishes found_inf / 1/scale and updates scale + growth tracker),
+  and the unscale + conditional skip inside the fused SGD -- two launches, **no host sync
+  per step** (GradScaler's ``_maybe_opt_step`` does ``found_inf.item()``,
+  ``torch/amp/grad_scaler.py:348-358``, and ``update`` is a third kernel);
 * with any other optimizer it falls back to torch's ``_amp_*`` ATen kernels and
   a host sync, exactly like GradScaler.
 """
@@ -39,6 +40,7 @@ class LossScaler:
         self._found_inf: Optional[torch.Tensor] = None
         self._unscaled = False
         self._stepped = False
+        self._updated_in_step = False   # the fused native step already ran the scale update
 
     # -- state -----------------------------------------------------------------------------
     def _lazy_init(self, device) -> None:
@@ -94,8 +96,11 @@ class LossScaler:
             return optimizer.step(*args, **kwargs)
         self._stepped = True
         if hasattr(optimizer, "step_amp") and not self._unscaled:
-            # fused: unscale + inf check + (device-side) conditional step, no host sync
-            return optimizer.step_amp(self._scale, self._found_inf)
+            # fused: inf check + scale update (one kernel), unscale + conditional step in the SGD
+            self._updated_in_step = True
+            return optimizer.step_amp(self._scale, self._found_inf, self._growth_tracker,
+                                      self.growth_factor, self.backoff_factor,
+                                      self.growth_interval)
         self.unscale_(optimizer)
         if hasattr(optimizer, "step_if_finite"):
             return optimizer.step_if_finite(self._found_inf)
@@ -108,12 +113,14 @@ class LossScaler:
             return
         if new_scale is not None:
             self._scale.fill_(float(new_scale))
-        else:
+        elif not self._updated_in_step:
             torch._amp_update_scale_(self._scale, self._growth_tracker, self._found_inf,
                                      self.growth_factor, self.backoff_factor, self.growth_interval)
+        if not self._updated_in_step:
+            self._found_inf.zero_()     # (the native scan republishes it every step)
         self._unscaled = False
         self._stepped = False
-        self._found_inf.zero_()
+        self._updated_in_step = False
 
     def state_dict(self) -> dict:
         if not self.enabled:

@@ -8,7 +8,7 @@
 //   sgd_flat       : ONE launch over the whole flat parameter buffer: AMP unscale, weight decay,
 //                    momentum (torch SGD semantics, first step buf = d_p), update, 16-bit shadow
 //                    write; skipped on device when found_inf (no host sync) (K9, K10)
-//   amp_check / amp_update : non-finite scan of the flat gradient; GradScaler state machine
+//   amp_scan : non-finite scan of the flat gradient + GradScaler state machine (one launch)
 //   pack_stem      : f32 master [64][7][7][3] -> 16-bit [64][448] (taps x 8 padded channels)
 //   synth_nhwc8    : on-device synthetic ImageNet batch: NHWC, 3 channels padded to 8, 16-bit,
 //                    bit-compatible with data/synthetic.py (label + uniform u) (K12)
@@ -123,7 +123,7 @@ __global__ __launch_bounds__(NT) void sgd_flat_kernel(float* __restrict__ p, flo
                                                       const float* __restrict__ found_inf, int flags,
                                                       int dt) {
   if (found_inf && found_inf[0] != 0.f) return;
-  const float inv = inv_scale_src ? 1.f / inv_scale_src[0] : 1.f;
+  const float inv = inv_scale_src ? inv_scale_src[0] : 1.f;   // published by amp_scan_kernel
   const long long n4 = n >> 2;
   for (long long i = blockIdx.x * (long long)NT + threadIdx.x; i < n4; i += (long long)gridDim.x * NT) {
     f32x4 pv = reinterpret_cast<f32x4*>(p)[i];
@@ -162,31 +162,59 @@ __global__ __launch_bounds__(NT) void cast_flat_kernel(const float* __restrict__
     s[i] = dt == DT_BF16 ? f32_to_bf16(p[i]) : f32_to_f16(p[i]);
 }
 
-__global__ __launch_bounds__(NT) void amp_check_kernel(const float* __restrict__ g, long long n,
-                                                       float* __restrict__ found_inf) {
+// AMP (GradScaler) in ONE launch before the fused SGD: non-finite scan of the flat gradient, and
+// the LAST workgroup to finish (arrival counter, agent-scope acq_rel) publishes
+//   found_inf[0] = any non-finite in g,  inv[0] = 1/scale (what the SGD unscales by),
+// then applies torch._amp_update_scale_ to scale/tracker (skipped when tracker == nullptr).
+// ws[0] = OR accumulator, ws[1] = arrival counter, both reset by that last workgroup, so the
+// kernel needs no memset and replays inside a HIP graph.
+__global__ __launch_bounds__(NT) void amp_scan_kernel(const float* __restrict__ g, long long n,
+                                                      float* __restrict__ found_inf,
+                                                      float* __restrict__ inv,
+                                                      float* __restrict__ scale,
+                                                      int* __restrict__ tracker, int* ws,
+                                                      float growth, float backoff, int interval) {
+  __shared__ int s_bad, s_last;
+  if (threadIdx.x == 0) s_bad = 0;
   bool bad = false;
-  for (long long i = blockIdx.x * (long long)NT + threadIdx.x; i < n; i += (long long)gridDim.x * NT) {
-    const float v = g[i];
-    bad |= !(fabsf(v) <= 3.4028235e38f);
+  const long long n4 = n >> 2;
+  for (long long i = blockIdx.x * (long long)NT + threadIdx.x; i < n4; i += (long long)gridDim.x * NT) {
+    const f32x4 v = reinterpret_cast<const f32x4*>(g)[i];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) bad |= !(fabsf(v[e]) <= 3.4028235e38f);
   }
-  if (__any(bad) && (threadIdx.x & 63) == 0) found_inf[0] = 1.f;
-}
-
-// torch._amp_update_scale_ semantics
-__global__ void amp_update_kernel(float* scale, int* tracker, const float* found_inf, float growth,
-                                  float backoff, int interval) {
-  if (found_inf[0] != 0.f) {
-    scale[0] *= backoff;
-    tracker[0] = 0;
-  } else {
-    const int t = tracker[0] + 1;
-    if (t == interval) {
-      const float ns = scale[0] * growth;
-      if (fabsf(ns) <= 3.4028235e38f) scale[0] = ns;
-      tracker[0] = 0;
-    } else {
-      tracker[0] = t;
+  if (blockIdx.x == 0 && threadIdx.x < (n & 3)) bad |= !(fabsf(g[(n4 << 2) + threadIdx.x]) <= 3.4028235e38f);
+  __syncthreads();
+  if (__any(bad) && (threadIdx.x & 63) == 0) s_bad = 1;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    if (s_bad) __hip_atomic_fetch_or(&ws[0], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int prev = __hip_atomic_fetch_add(&ws[1], 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+    s_last = prev == (int)gridDim.x - 1;
+  }
+  __syncthreads();
+  if (s_last && threadIdx.x == 0) {
+    const bool f = __hip_atomic_load(&ws[0], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) != 0;
+    const float sc = scale[0];
+    found_inf[0] = f ? 1.f : 0.f;
+    inv[0] = (float)(1.0 / (double)sc);
+    if (tracker) {
+      if (f) {
+        scale[0] = sc * backoff;
+        tracker[0] = 0;
+      } else {
+        const int t = tracker[0] + 1;
+        if (t == interval) {
+          const float ns = sc * growth;
+          if (fabsf(ns) <= 3.4028235e38f) scale[0] = ns;
+          tracker[0] = 0;
+        } else {
+          tracker[0] = t;
+        }
+      }
     }
+    __hip_atomic_store(&ws[0], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(&ws[1], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 }
 
@@ -410,15 +438,10 @@ int pda_cast_flat(const float* p, void* s, long long n, int dt, hipStream_t st) 
   return (int)hipGetLastError();
 }
 
-int pda_amp_check(const float* g, long long n, float* found_inf, hipStream_t st) {
-  hipLaunchKernelGGL(amp_check_kernel, dim3(grid_for(n, 4096)), dim3(NT), 0, st, g, n, found_inf);
-  return (int)hipGetLastError();
-}
-
-int pda_amp_update(float* scale, int* tracker, const float* found_inf, float growth, float backoff,
-                   int interval, hipStream_t st) {
-  hipLaunchKernelGGL(amp_update_kernel, dim3(1), dim3(1), 0, st, scale, tracker, found_inf, growth,
-                     backoff, interval);
+int pda_amp_scan(const float* g, long long n, float* found_inf, float* inv, float* scale,
+                 int* tracker, int* ws, float growth, float backoff, int interval, hipStream_t st) {
+  hipLaunchKernelGGL(amp_scan_kernel, dim3(grid_for(n / 4 + 1, 2048)), dim3(NT), 0, st, g, n,
+                     found_inf, inv, scale, tracker, ws, growth, backoff, interval);
   return (int)hipGetLastError();
 }
 

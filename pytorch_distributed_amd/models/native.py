@@ -886,17 +886,16 @@ class NativeSGD(torch.optim.Optimizer):
     def zero_grad(self, set_to_none: bool = True) -> None:
         self.model.zero_grad_flat()
 
-    def _launch(self, scale=None, found_inf=None) -> None:
+    def _launch(self, inv_scale=None, found_inf=None) -> None:
         g = self.param_groups[0]
         m = self.model
         K.sgd_flat(m.flat_params, m.flat_grad, self.flat_mom, None if m.f32 else m.flat_shadow,
-                   g["lr"], g["momentum"], g["weight_decay"], self._initialized, scale=scale,
+                   g["lr"], g["momentum"], g["weight_decay"], self._initialized, inv_scale=inv_scale,
                    found_inf=found_inf)
         m._pack_stem()
-        if found_inf is None:
-            self._initialized = True
-        else:
-            self._initialized = True  # first finite step initialises; see _mark below
+        # (an overflow-skipped first step leaves the momentum buffer unset on the device but the
+        # flag set: the next step then reads the zero-initialised buffer, m*0 + d == d)
+        self._initialized = True
         for p in g["params"]:
             self.state[p]["momentum_buffer"] = self._views[p]
 
@@ -906,12 +905,20 @@ class NativeSGD(torch.optim.Optimizer):
         self._launch()
         return loss
 
-    # AMP: unscale + inf check + conditional step, all on device (no host sync)
     @torch.no_grad()
-    def step_amp(self, scale: torch.Tensor, found_inf: torch.Tensor):
-        found_inf.zero_()
-        K.amp_check(self.model.flat_grad, found_inf)
-        self._launch(scale=scale, found_inf=found_inf)
+    def step_amp(self, scale: torch.Tensor, found_inf: torch.Tensor, tracker=None,
+                 growth_factor: float = 2.0, backoff_factor: float = 0.5,
+                 growth_interval: int = 2000) -> None:
+        """AMP step, two launches and no host sync: ``amp_scan`` (non-finite check of the flat
+        gradient; its last workgroup publishes found_inf and 1/scale and, given ``tracker``, runs
+        the GradScaler scale update) then the fused SGD, which unscales by 1/scale and skips the
+        whole update when found_inf is set."""
+        if getattr(self, "_amp_ws", None) is None or self._amp_ws.device != scale.device:
+            self._amp_ws = torch.zeros(2, dtype=torch.int32, device=scale.device)
+            self._amp_inv = torch.ones(1, dtype=torch.float32, device=scale.device)
+        K.amp_scan(self.model.flat_grad, found_inf, self._amp_inv, scale, tracker, self._amp_ws,
+                   growth_factor, backoff_factor, growth_interval)
+        self._launch(inv_scale=self._amp_inv, found_inf=found_inf)
 
     def state_dict(self):
         sd = super().state_dict()

@@ -72,8 +72,7 @@ _SIGS = {
     "pda_col_sum": [_V, _I, _I, _I, _F, _V, _I, _I, _V],
     "pda_sgd_flat": [_V, _V, _V, _V, _L, _F, _F, _F, _V, _V, _I, _I, _V],
     "pda_cast_flat": [_V, _V, _L, _I, _V],
-    "pda_amp_check": [_V, _L, _V, _V],
-    "pda_amp_update": [_V, _V, _V, _F, _F, _I, _V],
+    "pda_amp_scan": [_V, _L, _V, _V, _V, _V, _V, _F, _F, _I, _V],
     "pda_pack_stem": [_V, _V, _I, _I, _I, _I, _I, _I, _V],
     "pda_synth": [_V, _I, _U, _I, _V, _V, _I, _V, _I, _V],
     "pda_nchw_to_nhwc8": [_V, _I, _I, _I, _I, _V, _I, _V],

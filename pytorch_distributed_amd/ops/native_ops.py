@@ -25,7 +25,7 @@ from .ext import ConvDesc, BwdArgs, check, dt_of, ptr, stream
 __all__ = [
     "ConvGeom", "conv_fwd", "conv_dgrad", "conv_wgrad", "pick_tile", "wgrad_plan",
     "bn_finalize_fwd", "bn_eval_coeffs", "bn_apply", "stem_pool", "maxpool_bwd", "tail_pool",
-    "bn_bwd", "xent", "topk_hits", "col_sum", "sgd_flat", "cast_flat", "amp_check", "amp_update",
+    "bn_bwd", "xent", "topk_hits", "col_sum", "sgd_flat", "cast_flat", "amp_scan",
     "pack_stem", "synth_batch", "nchw_to_nhwc8", "Workspace",
 ]
 
@@ -478,11 +478,14 @@ def col_sum(x, C_: int, out, scale: float = 1.0, accumulate: bool = False) -> No
 
 
 # ------------------------------------------------------------------ optimizer / amp
-def sgd_flat(p, g, buf, shadow, lr, momentum, wd, initialized: bool, scale=None, found_inf=None):
+def sgd_flat(p, g, buf, shadow, lr, momentum, wd, initialized: bool, inv_scale=None,
+             found_inf=None):
+    """Fused SGD over the flat buffers; ``inv_scale`` / ``found_inf`` (device scalars published by
+    :func:`amp_scan`) unscale the gradient and skip the whole update on overflow."""
     flags = (1 if initialized else 0) | (2 if shadow is not None else 0)
     dt = dt_of(shadow) if shadow is not None else 1
     rc = ext.lib().pda_sgd_flat(ptr(p), ptr(g), ptr(buf), ptr(shadow), p.numel(), float(lr),
-                                float(momentum), float(wd), ptr(scale), ptr(found_inf), flags, dt,
+                                float(momentum), float(wd), ptr(inv_scale), ptr(found_inf), flags, dt,
                                 stream(p.device))
     check(rc, "sgd_flat")
 
@@ -492,13 +495,16 @@ def cast_flat(p, shadow) -> None:
     check(rc, "cast_flat")
 
 
-def amp_check(g, found_inf) -> None:
-    check(ext.lib().pda_amp_check(ptr(g), g.numel(), ptr(found_inf), stream(g.device)), "amp_check")
-
-
-def amp_update(scale, tracker, found_inf, growth=2.0, backoff=0.5, interval=2000) -> None:
-    check(ext.lib().pda_amp_update(ptr(scale), ptr(tracker), ptr(found_inf), float(growth),
-                                   float(backoff), int(interval), stream(scale.device)), "amp_update")
+def amp_scan(g, found_inf, inv_scale, scale, tracker, ws, growth=2.0, backoff=0.5,
+             interval=2000) -> None:
+    """One launch: found_inf = any non-finite in g; inv_scale = 1/scale; then (tracker given) the
+    GradScaler update of scale/tracker -- all on the device, no host sync. ``ws``: int32[2] zeros
+    (reset by the kernel itself)."""
+    if g.numel() % 4 or g.dtype != torch.float32 or ws.dtype != torch.int32 or ws.numel() < 2:
+        raise ValueError("amp_scan: f32 gradient with numel % 4 == 0 and an int32[2] workspace")
+    check(ext.lib().pda_amp_scan(ptr(g), g.numel(), ptr(found_inf), ptr(inv_scale), ptr(scale),
+                                 ptr(tracker), ptr(ws), float(growth), float(backoff), int(interval),
+                                 stream(g.device)), "amp_scan")
 
 
 def pack_stem(src_ohwi, dst, Cout=64, RS=49, Cin=3, Cpad=8) -> None:

@@ -75,14 +75,19 @@ class ReplicatedSGD(torch.optim.Optimizer):
             with torch.cuda.device(o.model.device):
                 o.step()
 
-    def step_amp(self, scale, found_inf):
-        # every replica holds the same (all-reduced) gradient, so the inf check agrees
+    def step_amp(self, scale, found_inf, tracker=None, growth_factor=2.0, backoff_factor=0.5,
+                 growth_interval=2000):
+        # every replica holds the same (all-reduced) gradient, so the inf check agrees; replica 0
+        # owns the scaler state (its kernel updates scale/tracker), the others unscale with copies
         self._sync_hparams()
-        for o in self.opts:
+        # copies of the CURRENT scale first: replica 0's kernel updates it in place
+        copies = [scale.to(o.model.device, copy=True) for o in self.opts[1:]]
+        with torch.cuda.device(self.opts[0].model.device):
+            self.opts[0].step_amp(scale, found_inf, tracker, growth_factor, backoff_factor,
+                                  growth_interval)
+        for o, s in zip(self.opts[1:], copies):
             with torch.cuda.device(o.model.device):
-                s = scale.to(o.model.device, non_blocking=True)
-                f = found_inf if o is self.opts[0] else torch.zeros_like(found_inf, device=o.model.device)
-                o.step_amp(s, f)
+                o.step_amp(s, torch.zeros_like(found_inf, device=o.model.device))
 
     def state_dict(self):
         return self.opts[0].state_dict()

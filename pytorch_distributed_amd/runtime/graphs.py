@@ -47,9 +47,9 @@ def native_train_step(model, opt, x: torch.Tensor, y: torch.Tensor, scaler=None)
     K.xent(logits, y, rows, loss, dlog=dlog16, gscale=1.0 / B, gdev=gdev)
     model.native_backward(dlog16)
     if gdev is not None:
-        opt.step_amp(scaler.scale_tensor, scaler.found_inf)     # unscale + inf check + skip on device
-        torch._amp_update_scale_(scaler.scale_tensor, scaler._growth_tracker, scaler.found_inf,
-                                 scaler.growth_factor, scaler.backoff_factor, scaler.growth_interval)
+        # inf check + scale update (one kernel), unscale + skip-on-overflow inside the fused SGD
+        opt.step_amp(scaler.scale_tensor, scaler.found_inf, scaler._growth_tracker,
+                     scaler.growth_factor, scaler.backoff_factor, scaler.growth_interval)
     else:
         opt.step()
     opt.zero_grad()

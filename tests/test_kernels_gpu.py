@@ -350,19 +350,52 @@ def test_sgd_flat_matches_torch():
     torch.cuda.synchronize()
     torch.testing.assert_close(p, pr.detach(), rtol=1e-6, atol=1e-6)
     torch.testing.assert_close(sh.float(), p.to(torch.bfloat16).float())
-    # AMP: skipped when found_inf is set, unscaled otherwise
-    scale = torch.tensor([4.0], device=DEV)
+    # AMP: skipped when found_inf is set, unscaled by the published 1/scale otherwise
+    inv = torch.tensor([0.25], device=DEV)
     inf = torch.ones(1, device=DEV)
     before = p.clone()
-    K.sgd_flat(p, g, buf, sh, 0.1, 0.9, 1e-4, True, scale=scale, found_inf=inf)
+    K.sgd_flat(p, g, buf, sh, 0.1, 0.9, 1e-4, True, inv_scale=inv, found_inf=inf)
     torch.cuda.synchronize()
     assert torch.equal(before, p)
-    gg = g.clone()
-    gg[5] = float("inf")
-    fi = torch.zeros(1, device=DEV)
-    K.amp_check(gg, fi)
+    pr.grad = g.clone() * 0.25
+    opt.step()
+    K.sgd_flat(p, g, buf, sh, 0.1, 0.9, 1e-4, True, inv_scale=inv, found_inf=torch.zeros(1, device=DEV))
     torch.cuda.synchronize()
-    assert fi.item() == 1.0
+    torch.testing.assert_close(p, pr.detach(), rtol=1e-6, atol=1e-6)
+
+
+def test_amp_scan_matches_gradscaler_state_machine():
+    """amp_scan (non-finite scan + last-workgroup GradScaler update, one launch) against torch's
+    own _amp_foreach_non_finite_check_and_unscale_ / _amp_update_scale_ over a sequence of clean
+    and overflowing steps (growth interval 3 so growth happens), on a gradient large enough for
+    thousands of workgroups -- and with no memset between launches (the kernel resets its own
+    arrival counter)."""
+    K = _k()
+    n = (1 << 22) + 3584
+    g = torch.randn(n, device=DEV)
+    scale, tracker = torch.tensor([65536.0], device=DEV), torch.zeros(1, dtype=torch.int32, device=DEV)
+    s_ref, t_ref = scale.clone(), tracker.clone()
+    fi, inv = torch.zeros(1, device=DEV), torch.zeros(1, device=DEV)
+    ws = torch.zeros(2, dtype=torch.int32, device=DEV)
+    pattern = [0, 0, 0, 1, 0, 2, 0, 0, 0, 0, 3, 0]    # 1: inf, 2: nan, 3: -inf at the very end
+    for step, kind in enumerate(pattern):
+        gg = g.clone()
+        if kind == 1:
+            gg[12345] = float("inf")
+        elif kind == 2:
+            gg[n // 2] = float("nan")
+        elif kind == 3:
+            gg[n - 1] = float("-inf")
+        fr = torch.zeros(1, device=DEV)
+        inv_ref = s_ref.double().reciprocal().float()
+        torch._amp_foreach_non_finite_check_and_unscale_([gg.clone()], fr, inv_ref)
+        K.amp_scan(gg, fi, inv, scale, tracker, ws, 2.0, 0.5, 3)
+        torch.cuda.synchronize()
+        assert fi.item() == fr.item(), step
+        assert inv.item() == inv_ref.item(), step
+        torch._amp_update_scale_(s_ref, t_ref, fr, 2.0, 0.5, 3)
+        assert scale.item() == s_ref.item() and tracker.item() == t_ref.item(), (step, scale, s_ref)
+        assert ws.tolist() == [0, 0]
 
 
 def test_synthetic_kernel_matches_torch_generator():

@@ -14,13 +14,13 @@ def rel_err(a, b):
     return ((a - b).norm() / (b.norm() + 1e-12)).item()
 
 
-def _pair(arch="resnet50", num_classes=1000, image=64):
+def _pair(arch="resnet50", num_classes=1000, image=64, dtype=torch.bfloat16):
     from pytorch_distributed_amd.models import build_model
     from pytorch_distributed_amd.models.native import NativeResNet
     torch.manual_seed(0)
     ref = build_model(arch, num_classes)
     torch_model = copy.deepcopy(ref).to(DEV)
-    native = NativeResNet(ref, device=DEV, dtype=torch.bfloat16, image_size=image)
+    native = NativeResNet(ref, device=DEV, dtype=dtype, image_size=image)
     return torch_model, native
 
 
@@ -186,3 +186,80 @@ def test_exact_fp32_engine_matches_float64(arch):
     for n, b in nm.named_buffers():
         if "num_batches" not in n:
             assert rel_err(b.cpu(), b64[n]) < 1e-4, n
+
+
+@pytest.mark.parametrize("arch", ["resnet50", "resnet18"])
+def test_fp16_amp_gradients_match_reference(arch):
+    """The AMP script's native fp16 engine (fp16 activations / BN outputs / gradients, f32 master
+    weights, f32 BN statistics, loss scaling) against the fp32 reference, with PyTorch's own fp16
+    autocast (what the reference's ``resnet_ddp_apex.py:27-34`` runs) as the precision yardstick:
+    every parameter's gradient must be as close to fp32 as autocast's is."""
+    S = 1024.0
+    tm, nm = _pair(arch, dtype=torch.float16)
+    ta = copy.deepcopy(tm)
+    torch.manual_seed(1)
+    B = 16
+    x = torch.randn(B, 3, 64, 64, device=DEV).half().float()
+    y = torch.randint(0, 1000, (B,), device=DEV)
+    for m in (tm, ta, nm):
+        m.train()
+    lt = tm(x)
+    with torch.autocast("cuda", dtype=torch.float16):
+        la = ta(x)
+    ln = nm(x)
+    e_nat, e_ref = rel_err(ln, lt), rel_err(la, lt)
+    assert e_nat < 1.3 * e_ref + 0.01, (e_nat, e_ref)
+    F.cross_entropy(lt, y).backward()
+    (F.cross_entropy(la.float(), y) * S).backward()
+    (nm.make_criterion()(ln, y) * S).backward()
+    torch.cuda.synchronize()
+    tp, ap = dict(tm.named_parameters()), dict(ta.named_parameters())
+    worse = []
+    for name, p in nm.named_parameters():
+        assert torch.isfinite(p.grad).all(), name
+        e = rel_err(p.grad / S, tp[name].grad)
+        ea = rel_err(ap[name].grad / S, tp[name].grad)
+        if e > 1.5 * ea + 0.02:
+            worse.append((name, e, ea))
+    assert not worse, worse
+
+
+def test_amp_overflow_skips_step_on_device():
+    """Forced overflow on the native engine: a loss scale of 2^40 overflows the fp16 gradients ->
+    the whole SGD step is skipped (weights and momentum untouched), scale x0.5, growth tracker
+    reset -- and scaler.step/update issue no host synchronisation (sync debug mode = error).
+    A clean step afterwards updates the weights and counts towards growth."""
+    from pytorch_distributed_amd.amp import LossScaler
+    from pytorch_distributed_amd.data import SyntheticImageNet
+    _, nm = _pair("resnet18", dtype=torch.float16)
+    opt, crit = nm.make_optimizer(lr=0.1), nm.make_criterion()
+    gen = nm.input_generator(SyntheticImageNet("train", image_size=64))
+    x, y = gen(torch.arange(8))
+    scaler = LossScaler(init_scale=2.0 ** 40, growth_interval=2)
+    p0 = nm.flat_params.clone()
+    scaler.scale(crit(nm(x), y)).backward()
+    torch.cuda.synchronize()
+    torch.cuda.set_sync_debug_mode("error")
+    try:
+        scaler.step(opt)
+        scaler.update()
+        opt.zero_grad()
+    finally:
+        torch.cuda.set_sync_debug_mode(0)
+    torch.cuda.synchronize()
+    assert scaler.found_inf.item() == 1.0
+    assert torch.equal(nm.flat_params, p0), "overflowing step must be skipped"
+    assert torch.count_nonzero(opt.flat_mom).item() == 0
+    assert scaler.get_scale() == 2.0 ** 39
+    assert scaler._growth_tracker.item() == 0
+    scaler.load_state_dict({"scale": 1024.0, "growth_factor": 2.0, "backoff_factor": 0.5,
+                            "growth_interval": 2, "_growth_tracker": 0})
+    for i in range(2):
+        scaler.scale(crit(nm(x), y)).backward()
+        scaler.step(opt)
+        scaler.update()
+        opt.zero_grad()
+    torch.cuda.synchronize()
+    assert scaler.found_inf.item() == 0.0
+    assert not torch.equal(nm.flat_params, p0)
+    assert scaler.get_scale() == 2048.0 and scaler._growth_tracker.item() == 0
