@@ -6,7 +6,7 @@
 // epilogue's per-tile partial sums (conv_gemm.hip) or by the column-reduce kernel below; every
 // cross-workgroup sum is a deterministic slab reduction (no float atomics).
 //
-//   bn_finalize_fwd : partial [T][2][C] -> mean, invstd, scale = g*invstd, shift = b - mean*scale,
+//   bn_finalize_tot : f64 totals [2][C] -> mean, invstd, scale = g*invstd, shift = b - mean*scale,
 //                     running-stat update (momentum, unbiased var), num_batches_tracked += 1
 //   bn_apply        : a = act(y*scale + shift [+ res | + y2*scale2 + shift2]), 16 B / lane
 //   stem_pool       : a = relu(bn(y)) then 3x3/s2/p1 max-pool with a uint8 argmax per output
@@ -65,25 +65,19 @@ __device__ __forceinline__ void tree_reduce2(double (&red)[2][64][17], int g, in
 }
 
 // ------------------------------------------------------------------ forward finalize
-// part: [T][2][C] (sum, sumsq) partials. One block = 16 channels x 64 partial-lanes.
-__global__ __launch_bounds__(1024) void bn_finalize_fwd_kernel(
-    const float* __restrict__ part, int T, int C, float count, const float* __restrict__ gamma,
+// From f64 totals tot[2][C] = (sum y, sum y^2) -- the in-launch statistics of the conv forward
+// (conv_gemm.hip bn_stats_finalize, fin_mode 1), after the SyncBatchNorm all-reduce. The
+// single-process path finalizes inside the conv launch itself.
+__global__ __launch_bounds__(256) void bn_finalize_tot_kernel(
+    const double* __restrict__ tot, int C, double count, const float* __restrict__ gamma,
     const float* __restrict__ beta, float eps, float momentum, float* __restrict__ mean_out,
     float* __restrict__ invstd_out, float* __restrict__ scale, float* __restrict__ shift,
     float* __restrict__ run_mean, float* __restrict__ run_var, long long* __restrict__ nbt,
     int update_running) {
-  __shared__ double red[2][64][17];
-  const int cl = threadIdx.x & 15, g = threadIdx.x >> 4;
-  const int c = blockIdx.x * 16 + cl;
-  double s1 = 0.0, s2 = 0.0;
-  if (c < C) slab_sum2(part, T, 2 * C, c, C + c, g, s1, s2);
-  red[0][g][cl] = s1;
-  red[1][g][cl] = s2;
-  tree_reduce2(red, g, cl);
-  if (g == 0 && c < C) {
-    const double a = red[0][0][cl], b = red[1][0][cl];
-    const double mean = a / count;
-    double var = b / count - mean * mean;
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c < C) {
+    const double mean = tot[c] / count;
+    double var = tot[C + c] / count - mean * mean;
     if (var < 0.0) var = 0.0;
     const float inv = (float)(1.0 / sqrt(var + (double)eps));
     const float sc = gamma[c] * inv;
@@ -700,11 +694,11 @@ int pda_slab_reduce(const float* in, int G, int QC, int S, float* out, hipStream
   return (int)hipGetLastError() ? -1 : s;
 }
 
-int pda_bn_finalize_fwd(const float* part, int T, int C, float count, const float* gamma,
+int pda_bn_finalize_tot(const double* tot, int C, double count, const float* gamma,
                         const float* beta, float eps, float momentum, float* mean, float* invstd,
                         float* scale, float* shift, float* rmean, float* rvar, long long* nbt,
                         int update_running, hipStream_t st) {
-  hipLaunchKernelGGL(bn_finalize_fwd_kernel, dim3((C + 15) / 16), dim3(1024), 0, st, part, T, C, count,
+  hipLaunchKernelGGL(bn_finalize_tot_kernel, dim3((C + 255) / 256), dim3(256), 0, st, tot, C, count,
                      gamma, beta, eps, momentum, mean, invstd, scale, shift, rmean, rvar, nbt,
                      update_running);
   return (int)hipGetLastError();

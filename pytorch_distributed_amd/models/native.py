@@ -9,8 +9,9 @@ are explicit schedules of our gfx950 kernels (``ops/native_ops.py``):
   generated/converted straight into the 2x2 space-to-depth layout (12 of 16 channels used),
   so the 7x7/2 stem becomes a 4x4/1 MFMA implicit GEMM with K = 256 (whole 16-B chunks);
 * every conv is the implicit-GEMM MFMA kernel (fwd / dgrad / split-K wgrad); the
-  forward epilogue emits BatchNorm partial statistics, so BN costs one finalize
-  launch plus one fused apply(+ReLU, +residual, +pool) pass;
+  forward epilogue emits BatchNorm partial statistics and its last-arriving
+  workgroups finalize them inside the same launch, so BN costs one fused
+  apply(+ReLU, +residual, +pool) pass (or nothing: the next conv's prologue);
 * parameters live in ONE flat f32 buffer laid out in *gradient-production order*
   (fc, layer4.2 ... layer1.0, stem) so DDP buckets are contiguous slices that
   complete in order during backward; ``.grad`` of every parameter is a view into
@@ -424,18 +425,14 @@ class NativeResNet(nn.Module):
         ws = self.ws if ws is None else ws
         Nb = x.shape[0]
         g = u.geom(Nb)
-        M = Nb * g.Ho * g.Wo
         y = self._empty(Nb, g.Ho, g.Wo, u.cout)
         st = u.state
-        if train:
-            T = K.stats_tiles(M, u.cout)
-            part = ws.get("fwd_stats", T * 2 * u.cout)
-            K.conv_fwd(x, self.w16(u), g, y, stats=part, pro=pro)
-            K.bn_finalize_fwd(part, T, u.cout, M, self.gamma(u), self.beta(u), u.bn.eps,
-                              u.bn.momentum if u.bn.momentum is not None else 0.1,
-                              st[0], st[1], st[2], st[3], self.rmean(u), self.rvar(u),
-                              self.flat_nbt[u.nbt_idx:u.nbt_idx + 1], update_running=True,
-                              ws=ws)
+        if train:   # batch statistics + BN finalize inside the conv launch
+            bn = K.BnStats(ws, self.gamma(u), self.beta(u), u.bn.eps,
+                           u.bn.momentum if u.bn.momentum is not None else 0.1,
+                           st[0], st[1], st[2], st[3], self.rmean(u), self.rvar(u),
+                           self.flat_nbt[u.nbt_idx:u.nbt_idx + 1], update_running=True)
+            K.conv_fwd(x, self.w16(u), g, y, pro=pro, bn=bn)
         else:
             K.conv_fwd(x, self.w16(u), g, y, pro=pro)
             K.bn_eval_coeffs(self.gamma(u), self.beta(u), self.rmean(u), self.rvar(u), u.bn.eps,
@@ -678,7 +675,7 @@ class NativeResNet(nn.Module):
                         N * H * W, C_)
         K.check(ext.lib().pda_bn_bwd_reduce(ext.C.byref(a), G, ext.dt_of(dz), ext.stream(dz.device)),
                 "bn_bwd_reduce")
-        return dz, part, G, nq
+        return dz, part, G, nq, None
 
     def _block_backward(self, b: Block, rec, tail, prev, acc):
         """Returns (dx_main, shortcut_grad, prev_tail) -- the last is the fused reduction of the
@@ -690,7 +687,7 @@ class NativeResNet(nn.Module):
         n = len(b.units)
         ul = b.units[-1]
         sl = rec[f"s{n - 1}"]
-        dz, part, G, nq = tail
+        dz, part, G, nq, ktail = tail   # ktail: coefficients if the producing dgrad finalized
         dy = self._empty(*ys[-1].shape)
         sc_ev = None
         if b.ds is not None:
@@ -699,7 +696,7 @@ class NativeResNet(nn.Module):
             K.bn_bwd_finish(ws, part, G, nq, ys[-1], sl[0], sl[1], self.gamma(ul), self.dgamma(ul),
                             self.dbeta(ul), dz, dy, y2=yd, mean2=sd[0], invstd2=sd[1],
                             gamma2=self.gamma(b.ds), dgamma2=self.dgamma(b.ds), dbeta2=self.dbeta(b.ds),
-                            dy2_out=dyd, accumulate=acc)
+                            dy2_out=dyd, accumulate=acc, k=ktail)
             # shortcut branch first: its dX is the second gradient source of the previous tail.
             # On the second stream its dgrad overlaps the conv3/conv2 chain; an event marks it for
             # the conv1 dgrad epilogue (or the stem) that consumes it
@@ -718,7 +715,7 @@ class NativeResNet(nn.Module):
                                                                     accumulate=acc), dyd, x)
         else:
             K.bn_bwd_finish(ws, part, G, nq, ys[-1], sl[0], sl[1], self.gamma(ul), self.dgamma(ul),
-                            self.dbeta(ul), dz, dy, accumulate=acc)
+                            self.dbeta(ul), dz, dy, accumulate=acc, k=ktail)
             shortcut_g = dz
         dx_main = None
         prev_tail = None
@@ -741,21 +738,36 @@ class NativeResNet(nn.Module):
                 up = b.units[j - 1]
                 sp = rec[f"s{j - 1}"]
                 Gp = K.dgrad_slabs(g, Nb)
-                epi, part_p, nq_p = K.bn_epilogue(ws, Gp, ys[j - 1], sp[2], sp[3])
+                # the dgrad's epilogue reduces AND (last-arriving workgroups) finalizes bn_{j-1}
+                fin = K.BnBwd(self.gamma(up), sp[0], sp[1], self.dgamma(up), self.dbeta(up),
+                              accumulate=acc)
+                epi, part_p, nq_p, kp = K.bn_epilogue(ws, Gp, ys[j - 1], sp[2], sp[3], fin=fin,
+                                                      tiles_n=K.dgrad_tiles_n(g, Nb))
                 K.conv_dgrad(dy, self.w16_ohwi(u), g, out, epi=epi)      # out = dz of bn_{j-1}
                 dyp = self._empty(*ys[j - 1].shape)
                 K.bn_bwd_finish(ws, part_p, Gp, nq_p, ys[j - 1], sp[0], sp[1], self.gamma(up),
-                                self.dgamma(up), self.dbeta(up), out, dyp, accumulate=acc)
+                                self.dgamma(up), self.dbeta(up), out, dyp, accumulate=acc, k=kp)
                 dy = dyp
             elif prev is not None:
                 pb, prec = prev
                 if sc_ev is not None:
                     cur.wait_event(sc_ev)
                 Gp = K.dgrad_slabs(g, Nb)
-                epi, part_p, nq_p = K.bn_epilogue(ws, Gp, g2=shortcut_g,
-                                                  **self._tail_args(pb, prec, use_mask=True))
+                ulp = pb.units[-1]
+                slp = prec[f"s{len(pb.units) - 1}"]
+                if pb.ds is not None:
+                    sdp = prec["sd"]
+                    fin = K.BnBwd(self.gamma(ulp), slp[0], slp[1], self.dgamma(ulp), self.dbeta(ulp),
+                                  self.gamma(pb.ds), sdp[0], sdp[1], self.dgamma(pb.ds),
+                                  self.dbeta(pb.ds), accumulate=acc, k_name="bn_kt")
+                else:
+                    fin = K.BnBwd(self.gamma(ulp), slp[0], slp[1], self.dgamma(ulp), self.dbeta(ulp),
+                                  accumulate=acc, k_name="bn_kt")
+                epi, part_p, nq_p, kp = K.bn_epilogue(ws, Gp, g2=shortcut_g, fin=fin,
+                                                      tiles_n=K.dgrad_tiles_n(g, Nb),
+                                                      **self._tail_args(pb, prec, use_mask=True))
                 K.conv_dgrad(dy, self.w16_ohwi(u), g, out, epi=epi)      # out = dz of prev tail
-                prev_tail = (out, part_p, Gp, nq_p)
+                prev_tail = (out, part_p, Gp, nq_p, kp)
             else:
                 K.conv_dgrad(dy, self.w16_ohwi(u), g, out)
                 dx_main = out

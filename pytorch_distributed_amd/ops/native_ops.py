@@ -24,7 +24,7 @@ from .ext import ConvDesc, BwdArgs, check, dt_of, ptr, stream
 
 __all__ = [
     "ConvGeom", "conv_fwd", "conv_dgrad", "conv_wgrad", "pick_tile", "wgrad_plan",
-    "bn_finalize_fwd", "bn_eval_coeffs", "bn_apply", "stem_pool", "maxpool_bwd", "tail_pool",
+    "BnStats", "BnBwd", "stats_totals", "dgrad_tiles_n", "bn_finalize_tot", "bn_eval_coeffs", "bn_apply", "stem_pool", "maxpool_bwd", "tail_pool",
     "bn_bwd", "xent", "topk_hits", "col_sum", "sgd_flat", "cast_flat", "amp_scan",
     "pack_stem", "synth_batch", "nchw_to_nhwc8", "Workspace",
 ]
@@ -80,6 +80,15 @@ class Workspace:
             self._bufs[name] = b
         return b[:numel]
 
+    def counters(self, numel: int) -> torch.Tensor:
+        """int32 arrival counters of in-launch reductions: zero when allocated, and every kernel
+        that uses them leaves them zero again (its last arrivers reset them)."""
+        b = self._bufs.get("_counters")
+        if b is None or b.numel() < numel:
+            b = torch.zeros(max(numel, 64), dtype=torch.int32, device=self.device)
+            self._bufs["_counters"] = b
+        return b[:numel]
+
 
 _NUM_CU = 256
 _WGRAD_TARGET = int(os.environ.get("PDA_WGRAD_TARGET", 2 * _NUM_CU))
@@ -104,27 +113,87 @@ def pick_tile(M: int, N: int, K: Optional[int] = None) -> Tuple[int, int]:
 
 
 # ------------------------------------------------------------------ conv
+class BnStats:
+    """BatchNorm (training) statistics computed inside a conv forward launch: the conv epilogue
+    writes per-M-tile shifted partial sums and the last-arriving workgroups combine them in f64
+    and finalize mean / invstd / scale / shift and the running statistics -- no separate
+    reduction or finalize launch (csrc/conv_gemm.hip bn_stats_finalize). With SyncBatchNorm
+    (``ws.sync_comm``) the launch stops at f64 totals, which are all-reduced before a small
+    finalize kernel."""
+
+    def __init__(self, ws: "Workspace", gamma, beta, eps: float, momentum: float, mean, invstd,
+                 scale, shift, rmean=None, rvar=None, nbt=None, update_running: bool = True):
+        self.ws, self.gamma, self.beta = ws, gamma, beta
+        self.eps, self.momentum = float(eps), float(momentum)
+        self.mean, self.invstd, self.scale, self.shift = mean, invstd, scale, shift
+        self.rmean, self.rvar, self.nbt, self.update = rmean, rvar, nbt, update_running
+
+
 def conv_fwd(x: torch.Tensor, w: torch.Tensor, g: ConvGeom, out: torch.Tensor,
              stats: Optional[torch.Tensor] = None, bias: Optional[torch.Tensor] = None,
              relu: bool = False, tile: Optional[Tuple[int, int]] = None,
-             pro: Optional[Tuple[torch.Tensor, torch.Tensor]] = None) -> torch.Tensor:
+             pro: Optional[Tuple[torch.Tensor, torch.Tensor]] = None,
+             bn: Optional[BnStats] = None) -> torch.Tensor:
     """out[M, Cout] (16-bit or f32) = conv(x, w). w: [Cout, Kpad] 16-bit, Kpad = w.shape[1].
-    stats (f32, >= ceil(M/bm)*2*Cout) receives per-M-tile (sum, sumsq) partials.
-    pro = (scale, shift): x is a PRE-BatchNorm tensor and the conv consumes relu(x*scale+shift)."""
+    stats (f32, >= ceil(M/bm)*3*Cout) receives per-M-tile shifted partials (sum(y-s),
+    sum((y-s)^2), s) -- see :func:`stats_totals`; ``bn`` (:class:`BnStats`) instead finalizes
+    BatchNorm inside the launch. pro = (scale, shift): x is a PRE-BatchNorm tensor and the conv
+    consumes relu(x*scale+shift)."""
     Nb = x.shape[0]
     M = Nb * g.Ho * g.Wo
     Kpad = w.shape[-1] if w.dim() == 2 else w[0].numel()
-    bm, bn = tile or pick_tile(M, g.Cout, Kpad)
+    bm, bn_ = tile or pick_tile(M, g.Cout, Kpad)
     d = g.desc(Nb)
     # direct (unstaged) f32 store + bias: the fc head (16-bit features -> f32 logits, or any conv
     # with a bias); f32 activations of the exact-fp32 engine take the staged path with statistics
     out_f32 = bias is not None or out.dtype != x.dtype
     pitch = out.stride(0) if out.dim() == 2 else g.Cout
+    fin = None
+    sync = None
+    if bn is not None:
+        ws = bn.ws
+        T = math.ceil(M / abs(bm))
+        tn = math.ceil(g.Cout / bn_)
+        ch = max(1, math.ceil(math.sqrt(T)))
+        G1 = math.ceil(T / ch)
+        stats = ws.get("fwd_stats", T * 3 * g.Cout)
+        chunk = ws.get("bn_chunk", G1 * 2 * g.Cout, torch.float64)
+        cnt = ws.counters(G1 * tn + tn)
+        sync = getattr(ws, "sync_comm", None)
+        if sync is not None and sync.world_size == 1:
+            sync = None
+        tot = ws.get("bn_tot", 2 * g.Cout, torch.float64) if sync is not None else None
+        fin = ext.BnFin(1 if sync is not None else 2, ch, ptr(chunk), ptr(tot), ptr(cnt),
+                        ptr(bn.gamma), ptr(bn.beta), bn.eps, bn.momentum, ptr(bn.mean),
+                        ptr(bn.invstd), ptr(bn.scale), ptr(bn.shift), ptr(bn.rmean), ptr(bn.rvar),
+                        ptr(bn.nbt), int(bn.update))
     rc = ext.lib().pda_conv_fwd(C.byref(d), ptr(x), ptr(w), Kpad, ptr(out), int(out_f32), pitch,
                                 ptr(bias), ptr(stats), int(relu), ptr(pro[0] if pro else None),
-                                ptr(pro[1] if pro else None), dt_of(x), bm, bn, stream(x.device))
+                                ptr(pro[1] if pro else None), C.byref(fin) if fin is not None else None,
+                                dt_of(x), bm, bn_, stream(x.device))
     check(rc, "conv_fwd")
+    if sync is not None:   # SyncBatchNorm: global f64 totals, then finalize
+        sync.all_reduce(tot)
+        bn_finalize_tot(tot, g.Cout, M * sync.world_size, bn)
     return out
+
+
+def stats_totals(stats: torch.Tensor, M: int, C_: int, bm: int) -> torch.Tensor:
+    """f64 [2][C] (sum y, sum y^2) from conv_fwd's shifted per-tile partials (tests, tools)."""
+    T = math.ceil(M / abs(bm))
+    p = stats[:T * 3 * C_].view(T, 3, C_).double()
+    rows = torch.full((T, 1), float(abs(bm)), dtype=torch.float64, device=stats.device)
+    rows[-1, 0] = M - (T - 1) * abs(bm)
+    d0, d1, sh = p[:, 0], p[:, 1], p[:, 2]
+    return torch.stack([(rows * sh + d0).sum(0), (d1 + sh * (2 * d0 + rows * sh)).sum(0)])
+
+
+def bn_finalize_tot(tot: torch.Tensor, C_: int, count: int, bn: BnStats) -> None:
+    rc = ext.lib().pda_bn_finalize_tot(ptr(tot), C_, float(count), ptr(bn.gamma), ptr(bn.beta),
+                                       bn.eps, bn.momentum, ptr(bn.mean), ptr(bn.invstd),
+                                       ptr(bn.scale), ptr(bn.shift), ptr(bn.rmean), ptr(bn.rvar),
+                                       ptr(bn.nbt), int(bn.update), stream(tot.device))
+    check(rc, "bn_finalize_tot")
 
 
 def stats_tiles(M: int, Cout: int, tile: Optional[Tuple[int, int]] = None) -> int:
@@ -168,12 +237,25 @@ def conv_dgrad(dy: torch.Tensor, w: torch.Tensor, g: ConvGeom, dx: torch.Tensor,
     return dx
 
 
+class BnBwd:
+    """Parameters of the BatchNorm(s) whose backward a dgrad epilogue finalizes in-launch:
+    branch 0 = the BN of y, branch 1 (shortcut tails) = the BN of y2."""
+
+    def __init__(self, gamma, mean, invstd, dgamma, dbeta, gamma2=None, mean2=None, invstd2=None,
+                 dgamma2=None, dbeta2=None, accumulate: bool = False, k_name: str = "bn_k"):
+        self.b = [(gamma, mean, invstd, dgamma, dbeta), (gamma2, mean2, invstd2, dgamma2, dbeta2)]
+        self.accumulate, self.k_name = accumulate, k_name
+
+
 def bn_epilogue(ws: "Workspace", G: int, y, scale, shift, res=None, y2=None, scale2=None,
-                shift2=None, g2=None, mask=None):
+                shift2=None, g2=None, mask=None, fin: Optional[BnBwd] = None, tiles_n: int = 0):
     """Describe the BN-backward reduction a dgrad epilogue performs for a = relu(bn(y) [+res | +bn2(y2)]).
     ``mask`` (the forward's ReLU bitmask of a, see :func:`bn_apply`) replaces ``res``: the epilogue
     then reads one byte per 8 elements instead of the residual tensor (mode 3).
-    Returns (epi, part, nq); ``part`` holds G*nq*C floats after the dgrad."""
+    ``fin`` (:class:`BnBwd`; not with SyncBatchNorm): the dgrad's last-arriving workgroups also
+    finalize the BN backward (gamma/beta gradients + apply coefficients) inside the launch;
+    ``tiles_n`` = the dgrad's column tiles. Returns (epi, part, nq, k): ``part`` holds G*nq*C
+    partials after the dgrad, ``k`` [nq-1][3][C] the apply coefficients (None without fin)."""
     C_ = y.shape[-1]
     mode = 3 if mask is not None else (2 if y2 is not None else (1 if res is not None else 0))
     nq = 3 if mode == 2 else 2
@@ -181,7 +263,29 @@ def bn_epilogue(ws: "Workspace", G: int, y, scale, shift, res=None, y2=None, sca
     epi = ext.BnEpi(mode, nq, ptr(y), ptr(scale), ptr(shift),
                     ptr(y2 if y2 is not None else res), ptr(scale2), ptr(shift2), ptr(g2), ptr(part),
                     ptr(mask))
-    return epi, part, nq
+    k = None
+    sync = getattr(ws, "sync_comm", None)
+    if fin is not None and (sync is None or sync.world_size == 1) and tiles_n > 0:
+        ch = max(1, math.ceil(math.sqrt(G)))
+        G1 = math.ceil(G / ch)
+        chunk = ws.get("bn_chunk", G1 * nq * C_, torch.float64)
+        cnt = ws.counters(G1 * tiles_n + tiles_n)
+        k = ws.get(fin.k_name, (nq - 1) * 3 * C_)
+        epi.fin_mode, epi.fin_ch, epi.accumulate = 1, ch, int(fin.accumulate)
+        epi.chunk, epi.cnt = ptr(chunk), ptr(cnt)
+        epi.count, epi.gscale = float(y.numel() // C_), 1.0
+        for b in range(nq - 1):
+            ga, mu, inv, dg, db = fin.b[b]
+            epi.gamma[b], epi.mean[b], epi.invstd[b] = ptr(ga), ptr(mu), ptr(inv)
+            epi.dgamma[b], epi.dbeta[b] = ptr(dg), ptr(db)
+        epi.k = ptr(k)
+    return epi, part, nq, k
+
+
+def dgrad_tiles_n(g: "ConvGeom", Nb: int, tile: Optional[Tuple[int, int]] = None) -> int:
+    """Column tiles of a dgrad launch (its output channels = the conv's Cin)."""
+    _, bn = tile or dgrad_tile(g, Nb)
+    return math.ceil(g.Cin / bn)
 
 
 # Weight-gradient tile / split-K block target per ResNet conv geometry (Cout, R, Cin, stride, Ho),
@@ -296,19 +400,6 @@ def _sync_sums(part: torch.Tensor, G: int, QC: int, ws: Optional["Workspace"]):
     return tot, 1, comm.world_size
 
 
-def bn_finalize_fwd(part: torch.Tensor, T: int, C_: int, count: int, gamma, beta, eps, momentum,
-                    mean, invstd, scale, shift, rmean=None, rvar=None, nbt=None,
-                    update_running: bool = True, ws: Optional["Workspace"] = None) -> None:
-    part, T = prereduce(part, T, 2 * C_, ws)
-    part, T, world = _sync_sums(part, T, 2 * C_, ws)
-    count = count * world
-    rc = ext.lib().pda_bn_finalize_fwd(ptr(part), T, C_, float(count), ptr(gamma), ptr(beta),
-                                       float(eps), float(momentum), ptr(mean), ptr(invstd), ptr(scale),
-                                       ptr(shift), ptr(rmean), ptr(rvar), ptr(nbt),
-                                       int(update_running), stream(part.device))
-    check(rc, "bn_finalize_fwd")
-
-
 def bn_eval_coeffs(gamma, beta, rmean, rvar, eps, scale, shift) -> None:
     rc = ext.lib().pda_bn_eval_coeffs(ptr(gamma), ptr(beta), ptr(rmean), ptr(rvar), float(eps),
                                       gamma.numel(), ptr(scale), ptr(shift), stream(gamma.device))
@@ -408,13 +499,24 @@ def bn_bwd(ws: Workspace, y, mean, invstd, gamma, scale, shift, dgamma, dbeta, d
 
 def bn_bwd_finish(ws: "Workspace", part, G: int, nq: int, y, mean, invstd, gamma, dgamma, dbeta,
                   dz, dy_out, y2=None, mean2=None, invstd2=None, gamma2=None, dgamma2=None,
-                  dbeta2=None, dy2_out=None, gscale: float = 1.0, accumulate: bool = False) -> None:
+                  dbeta2=None, dy2_out=None, gscale: float = 1.0, accumulate: bool = False,
+                  k=None) -> None:
     """Finalize + apply of a BN backward whose reduction a dgrad epilogue already produced
-    (partials ``part`` [G][nq][C], masked gradient ``dz``)."""
+    (partials ``part`` [G][nq][C], masked gradient ``dz``). ``k`` (from :func:`bn_epilogue` with
+    ``fin``): the dgrad launch already finalized -- only the apply pass(es) run."""
     N, H, W, C_ = y.shape
     mode = 2 if nq == 3 else 1   # dz is materialised in both cases
     a = BwdArgs(None, None, None, 0, ptr(y), None, None, ptr(y2), None, None, mode, None, ptr(part),
                 nq, N * H * W, C_)
+    if k is not None:
+        L, st, dt = ext.lib(), stream(y.device), dt_of(y)
+        check(L.pda_bn_bwd_apply(C.byref(a), ptr(dz), ptr(y), ptr(k[0:C_]), ptr(k[C_:2 * C_]),
+                                 ptr(k[2 * C_:3 * C_]), ptr(dy_out), dt, st), "bn_bwd_apply")
+        if mode == 2:
+            check(L.pda_bn_bwd_apply(C.byref(a), ptr(dz), ptr(y2), ptr(k[3 * C_:4 * C_]),
+                                     ptr(k[4 * C_:5 * C_]), ptr(k[5 * C_:6 * C_]), ptr(dy2_out), dt,
+                                     st), "bn_bwd_apply2")
+        return
     _bn_bwd_tail(ws, part, G, nq, mode, a, y, mean, invstd, gamma, dgamma, dbeta, dy_out,
                  y2, mean2, invstd2, gamma2, dgamma2, dbeta2, dy2_out, dz, gscale, accumulate)
 

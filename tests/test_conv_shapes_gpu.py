@@ -66,13 +66,12 @@ def test_resnet50_conv_shape_all_tiles(shape):
                     bad.append((t, f"wgrad/{tb}", e))
             continue
         y = torch.full((Nb, g.Ho, g.Wo, Cout), float("nan"), device=DEV, dtype=dt)
-        stats = torch.zeros(math.ceil(M / 64) * 2 * Cout, device=DEV)
+        stats = torch.zeros(math.ceil(M / 64) * 3 * Cout, device=DEV)
         K.conv_fwd(x_nhwc, w_ohwi.view(Cout, -1), g, y, stats=stats, tile=t)
         dx = torch.full((Nb, H, H, Cin), float("nan"), device=DEV, dtype=dt)
         K.conv_dgrad(dy_nhwc, w_ohwi, g, dx, tile=t)
         torch.cuda.synchronize()
-        T = math.ceil(M / abs(t[0]))
-        st = stats[:T * 2 * Cout].view(T, 2, Cout).sum(0)
+        st = K.stats_totals(stats, M, Cout, t[0]).float()
         for name, e in (("fwd", rel_err(y, yr)), ("dgrad", rel_err(dx, dxr)),
                         ("stats", rel_err(st[0], y.float().reshape(-1, Cout).sum(0)))):
             if not e < 1e-2:

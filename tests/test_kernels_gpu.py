@@ -56,12 +56,12 @@ def test_conv_fwd_dgrad_wgrad(case, dtype):
     y = torch.empty(Nb, g.Ho, g.Wo, Cout, device=DEV, dtype=dtype)
     M = Nb * g.Ho * g.Wo
     T = K.stats_tiles(M, Cout)
-    stats = torch.zeros(T * 2 * Cout, device=DEV)
+    stats = torch.zeros(T * 3 * Cout, device=DEV)
     K.conv_fwd(x_nhwc, w_ohwi.view(Cout, -1), g, y, stats=stats)
     torch.cuda.synchronize()
     yr = y_ref.permute(0, 2, 3, 1)
     assert rel_err(y, yr) < 1e-2
-    st = stats.view(T, 2, Cout).sum(0)
+    st = K.stats_totals(stats, M, Cout, K.pick_tile(M, Cout)[0]).float()
     yb = y.float().reshape(-1, Cout)
     torch.testing.assert_close(st[0], yb.sum(0), rtol=1e-3, atol=1e-2)
     torch.testing.assert_close(st[1], (yb * yb).sum(0), rtol=1e-3, atol=1e-2)
@@ -130,22 +130,23 @@ def _bn_ref(y, gamma, beta, eps=1e-5):
 
 
 def test_bn_forward_finalize_apply():
+    """bn_finalize_tot (the SyncBatchNorm path: f64 totals -> coefficients + running stats) and
+    bn_apply against the plain PyTorch fp32 BatchNorm."""
     K = _k()
     dtype = torch.bfloat16
     N, H, C = 4, 6, 128
     y = (torch.randn(N, H, H, C, device=DEV) * 2 + 0.5).to(dtype)
     gamma = torch.rand(C, device=DEV) + 0.5
     beta = torch.randn(C, device=DEV)
-    part = y.float().reshape(-1, C)
-    T = 3
-    rows = part.shape[0]
-    chunks = torch.tensor_split(part, T, 0)
-    stats = torch.stack([torch.stack([c.sum(0), (c * c).sum(0)]) for c in chunks]).contiguous()
+    yd = y.double().reshape(-1, C)
+    rows = yd.shape[0]
+    tot = torch.stack([yd.sum(0), (yd * yd).sum(0)]).contiguous()
     st = torch.zeros(4, C, device=DEV)
     rm = torch.zeros(C, device=DEV)
     rv = torch.ones(C, device=DEV)
     nbt = torch.zeros(1, dtype=torch.int64, device=DEV)
-    K.bn_finalize_fwd(stats, T, C, rows, gamma, beta, 1e-5, 0.1, st[0], st[1], st[2], st[3], rm, rv, nbt)
+    bn = K.BnStats(None, gamma, beta, 1e-5, 0.1, st[0], st[1], st[2], st[3], rm, rv, nbt)
+    K.bn_finalize_tot(tot, C, rows, bn)
     out = torch.empty_like(y)
     K.bn_apply(y, st[2], st[3], out, relu=True)
     torch.cuda.synchronize()
@@ -156,6 +157,75 @@ def test_bn_forward_finalize_apply():
     torch.testing.assert_close(rm, 0.1 * mean, rtol=1e-4, atol=1e-5)
     torch.testing.assert_close(rv, 0.9 + 0.1 * var * rows / (rows - 1), rtol=1e-4, atol=1e-5)
     assert int(nbt.item()) == 1
+
+
+def _conv_bn_inlaunch(K, x_nhwc, w2d, g, dtype, gamma, beta, tile=None, ws=None):
+    ws = ws or K.Workspace(DEV)
+    C = g.Cout
+    y = torch.empty(x_nhwc.shape[0], g.Ho, g.Wo, C, device=DEV, dtype=dtype)
+    st = torch.zeros(4, C, device=DEV)
+    rm, rv = torch.zeros(C, device=DEV), torch.ones(C, device=DEV)
+    nbt = torch.zeros(1, dtype=torch.int64, device=DEV)
+    bn = K.BnStats(ws, gamma, beta, 1e-5, 0.1, st[0], st[1], st[2], st[3], rm, rv, nbt)
+    K.conv_fwd(x_nhwc, w2d, g, y, bn=bn, tile=tile)
+    return y, st, rm, rv, nbt, ws
+
+
+@pytest.mark.parametrize("tile", [None, (-128, 128), (128, 64), (64, 128), (-128, 64)])
+def test_conv_fwd_inlaunch_bn_finalize(tile):
+    """BatchNorm statistics finalized INSIDE the conv forward launch (last-arriving workgroups,
+    f64, shifted partials): mean / invstd / scale / shift / running stats / counter against float64
+    statistics of the stored output, on a ragged shape with several column tiles and chunks;
+    bit-identical on a second launch (fixed summation order), counters left at zero."""
+    K = _k()
+    dtype = torch.bfloat16
+    torch.manual_seed(5)
+    Nb, H, Cin, Cout = 7, 29, 64, 192
+    g = K.ConvGeom(Nb, H, H, Cin, Cout, 3, 3, 1, 1)
+    x = (torch.randn(Nb, H, H, Cin, device=DEV) + 0.2).to(dtype)
+    w = (torch.randn(Cout, 3, 3, Cin, device=DEV) / 24).to(dtype)
+    gamma, beta = torch.rand(Cout, device=DEV) + 0.5, torch.randn(Cout, device=DEV)
+    y, st, rm, rv, nbt, ws = _conv_bn_inlaunch(K, x, w.view(Cout, -1), g, dtype, gamma, beta, tile)
+    y2, st2, _, _, _, _ = _conv_bn_inlaunch(K, x, w.view(Cout, -1), g, dtype, gamma, beta, tile, ws)
+    torch.cuda.synchronize()
+    yd = y.double().reshape(-1, Cout)
+    n = yd.shape[0]
+    mean, var = yd.mean(0), yd.var(0, unbiased=False)
+    torch.testing.assert_close(st[0].double(), mean, rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(st[1].double(), 1 / torch.sqrt(var + 1e-5), rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(st[2], gamma * st[1])
+    torch.testing.assert_close(st[3], beta - st[0] * st[2])
+    torch.testing.assert_close(rm.double(), 0.1 * mean, rtol=1e-5, atol=1e-7)
+    torch.testing.assert_close(rv.double(), 0.9 + 0.1 * var * n / (n - 1), rtol=1e-5, atol=1e-7)
+    assert int(nbt.item()) == 1
+    assert torch.equal(y, y2) and torch.equal(st, st2)
+    assert int(ws.counters(64).abs().sum().item()) == 0
+
+
+@pytest.mark.parametrize("dtype,std", [(torch.float32, 0.01), (torch.bfloat16, 0.08)])
+def test_bn_statistics_large_offset_layer1_scale(dtype, std):
+    """Layer-1 scale (1.25 M rows x 64 channels, batch 400 at 56x56) with mean ~10 and std ~0.01
+    (bf16: 0.08, so the stored values -- 1/16 apart at 10 -- still vary): E[y^2] - E[y]^2 from
+    f32 partial sums would cancel catastrophically; the shifted per-tile sums + f64 combination
+    must match float64 statistics of the stored output."""
+    K = _k()
+    torch.manual_seed(11)
+    Nb, H, Cin, Cout = 400, 56, 64, 64
+    g = K.ConvGeom(Nb, H, H, Cin, Cout, 1, 1, 1, 0)
+    x = torch.randn(Nb, H, H, Cin, device=DEV)
+    x[..., 0] = 1.0                                  # constant channel carries the offset
+    w = torch.randn(Cout, Cin, device=DEV) * std / 8
+    w[:, 0] = 10.0 + torch.rand(Cout, device=DEV)    # y_c ~ 10..11 + N(0, std^2)
+    gamma, beta = torch.ones(Cout, device=DEV), torch.zeros(Cout, device=DEV)
+    y, st, rm, rv, nbt, _ = _conv_bn_inlaunch(K, x.to(dtype), w.to(dtype), g, dtype, gamma, beta)
+    torch.cuda.synchronize()
+    yd = y.double().reshape(-1, Cout)
+    mean, var = yd.mean(0), yd.var(0, unbiased=False)
+    assert float(var.min()) > 0
+    got_var = 1.0 / st[1].double() ** 2 - 1e-5
+    torch.testing.assert_close(st[0].double(), mean, rtol=1e-6, atol=1e-6)
+    rel = ((got_var - var).abs() / var).max().item()
+    assert rel < 2e-3, rel
 
 
 @pytest.mark.parametrize("mode", ["relu", "res", "ds"])
@@ -419,9 +489,11 @@ def test_synthetic_kernel_matches_torch_generator():
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
 @pytest.mark.parametrize("mode", ["relu", "res", "ds", "mask"])
 @pytest.mark.parametrize("stride", [1, 2])
-def test_dgrad_fused_bn_backward(mode, stride, dtype, geo):
+@pytest.mark.parametrize("inlaunch", [False, True])
+def test_dgrad_fused_bn_backward(mode, stride, dtype, geo, inlaunch):
     """dgrad epilogue (mask + BN-backward partial sums) == plain dgrad followed by the standalone
-    BN-backward reduce/apply (16-bit and exact-f32 kernels)."""
+    BN-backward reduce/apply (16-bit and exact-f32 kernels). ``inlaunch``: the dgrad's
+    last-arriving workgroups also finalize the BN backward (gamma/beta grads, coefficients)."""
     K = _k()
     tol = 1e-2 if dtype != torch.float32 else 1e-5
     Nb, H, Cin, Cout = geo
@@ -463,18 +535,25 @@ def test_dgrad_fused_bn_backward(mode, stride, dtype, geo):
         mask = torch.empty(y.numel() // 8, dtype=torch.uint8, device=DEV)
         K.bn_apply(y, sc, sh, torch.empty_like(y), res=y2, mask=mask)
         kw = dict(mask=mask)
-    epi, part, nq = K.bn_epilogue(ws, G, y, sc, sh, g2=g2 if use_g2 else None, **kw)
+    outs = [torch.zeros(Cin, device=DEV) for _ in range(4)]
+    fin = None
+    if inlaunch:
+        fin = K.BnBwd(gamma, mean, inv, outs[0], outs[1], *((gamma2, mean2, inv2, outs[2], outs[3])
+                                                            if mode == "ds" else ()))
+    epi, part, nq, kc = K.bn_epilogue(ws, G, y, sc, sh, g2=g2 if use_g2 else None, fin=fin,
+                                      tiles_n=K.dgrad_tiles_n(g, Nb), **kw)
+    assert (kc is not None) == inlaunch
     dz = torch.empty_like(y)
     K.conv_dgrad(dy, w, g, dz, epi=epi)
-    outs = [torch.zeros(Cin, device=DEV) for _ in range(4)]
     dyf = torch.empty_like(y)
     dy2f = torch.empty_like(y)
     extra = {}
     if mode == "ds":
         extra = dict(y2=y2, mean2=mean2, invstd2=inv2, gamma2=gamma2, dgamma2=outs[2], dbeta2=outs[3],
                      dy2_out=dy2f)
-    K.bn_bwd_finish(ws, part, G, nq, y, mean, inv, gamma, outs[0], outs[1], dz, dyf, **extra)
+    K.bn_bwd_finish(ws, part, G, nq, y, mean, inv, gamma, outs[0], outs[1], dz, dyf, k=kc, **extra)
     torch.cuda.synchronize()
+    assert int(ws.counters(64).abs().sum().item()) == 0
     if mode != "relu":
         assert rel_err(dz, dz_ref) < tol
     assert rel_err(dyf, dy_ref) < 2 * tol
@@ -503,11 +582,11 @@ def test_conv_fwd_dgrad_wgrad_exact_f32(case):
     y = torch.empty(Nb, g.Ho, g.Wo, Cout, device=DEV)
     M = Nb * g.Ho * g.Wo
     T = K.stats_tiles(M, Cout)
-    stats = torch.zeros(T * 2 * Cout, device=DEV)
+    stats = torch.zeros(T * 3 * Cout, device=DEV)
     K.conv_fwd(x_nhwc, w_ohwi.view(Cout, -1), g, y, stats=stats)
     torch.cuda.synchronize()
     assert rel_err(y.cpu().double(), y_ref.permute(0, 2, 3, 1)) < 2e-6
-    st = stats.view(T, 2, Cout).sum(0).cpu().double()
+    st = K.stats_totals(stats, M, Cout, K.pick_tile(M, Cout)[0]).cpu()
     yb = y_ref.permute(0, 2, 3, 1).reshape(-1, Cout)
     torch.testing.assert_close(st[0], yb.sum(0), rtol=1e-4, atol=1e-4)
     torch.testing.assert_close(st[1], (yb * yb).sum(0), rtol=1e-4, atol=1e-4)

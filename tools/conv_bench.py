@@ -60,7 +60,7 @@ def main():
         gw = torch.empty(Cout * k * k * Cin, device=dev)
         M = B * g.Ho * g.Wo
         flop = 2.0 * M * Cout * Cin * k * k
-        stats = torch.empty(math.ceil(M / 64) * 2 * Cout, device=dev)
+        stats = torch.empty(math.ceil(M / 64) * 3 * Cout, device=dev)
         for ps in ("fwd", "dgrad", "wgrad"):
             ts = []
             for t in TILES:

@@ -29,7 +29,7 @@ def main():
     dx = torch.empty_like(x)
     gw = torch.empty(Cout * k * k * Cin, device=dev)
     ws = K.Workspace(dev)
-    stats = torch.empty(math.ceil(B * g.Ho * g.Wo / 64) * 2 * Cout, device=dev)
+    stats = torch.empty(math.ceil(B * g.Ho * g.Wo / 64) * 3 * Cout, device=dev)
     for _ in range(reps):
         if ps == "fwd":
             K.conv_fwd(x, w.view(Cout, -1), g, y, stats=stats, tile=tile)
