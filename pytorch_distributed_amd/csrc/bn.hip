@@ -94,6 +94,51 @@ __global__ __launch_bounds__(256) void bn_finalize_tot_kernel(
   if (blockIdx.x == 0 && threadIdx.x == 0 && update_running && nbt) *nbt += 1;
 }
 
+// From the conv epilogue's shifted per-tile partials part[T][3][C] = (sum(y-s), sum((y-s)^2), s)
+// (tiles of `bm` rows, the last one ragged): the separate-launch finalize (PDA_INLAUNCH_BN=0 A/B
+// path). One block = 16 channels x 64 partial lanes; per-lane f64 sums, fixed-shape tree.
+__global__ __launch_bounds__(1024) void bn_finalize_shifted_kernel(
+    const float* __restrict__ part, int T, int C, int bm, int M, const float* __restrict__ gamma,
+    const float* __restrict__ beta, float eps, float momentum, float* __restrict__ mean_out,
+    float* __restrict__ invstd_out, float* __restrict__ scale, float* __restrict__ shift,
+    float* __restrict__ run_mean, float* __restrict__ run_var, long long* __restrict__ nbt,
+    int update_running) {
+  __shared__ double red[2][64][17];
+  const int cl = threadIdx.x & 15, g = threadIdx.x >> 4;
+  const int c = blockIdx.x * 16 + cl;
+  double s1 = 0.0, s2 = 0.0;
+  if (c < C) {
+    for (int t = g; t < T; t += 64) {
+      const float* pt = part + (size_t)t * 3 * C + c;
+      const double d0 = pt[0], d1 = pt[C], sh = pt[2 * C];
+      const double rows = (double)min(bm, M - t * bm);
+      s1 += rows * sh + d0;
+      s2 += d1 + sh * (2.0 * d0 + rows * sh);
+    }
+  }
+  red[0][g][cl] = s1;
+  red[1][g][cl] = s2;
+  tree_reduce2(red, g, cl);
+  if (g == 0 && c < C) {
+    const double count = (double)M;
+    const double mean = red[0][0][cl] / count;
+    double var = red[1][0][cl] / count - mean * mean;
+    if (var < 0.0) var = 0.0;
+    const float inv = (float)(1.0 / sqrt(var + (double)eps));
+    const float sc = gamma[c] * inv;
+    mean_out[c] = (float)mean;
+    invstd_out[c] = inv;
+    scale[c] = sc;
+    shift[c] = beta[c] - (float)mean * sc;
+    if (update_running) {
+      const double unb = count > 1.0 ? var * count / (count - 1.0) : var;
+      run_mean[c] = (1.f - momentum) * run_mean[c] + momentum * (float)mean;
+      run_var[c] = (1.f - momentum) * run_var[c] + momentum * (float)unb;
+    }
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0 && update_running && nbt) *nbt += 1;
+}
+
 // eval-mode scale/shift from running statistics
 __global__ void bn_eval_coeffs_kernel(const float* __restrict__ gamma, const float* __restrict__ beta,
                                       const float* __restrict__ rm, const float* __restrict__ rv,
@@ -700,6 +745,16 @@ int pda_bn_finalize_tot(const double* tot, int C, double count, const float* gam
                         int update_running, hipStream_t st) {
   hipLaunchKernelGGL(bn_finalize_tot_kernel, dim3((C + 255) / 256), dim3(256), 0, st, tot, C, count,
                      gamma, beta, eps, momentum, mean, invstd, scale, shift, rmean, rvar, nbt,
+                     update_running);
+  return (int)hipGetLastError();
+}
+
+int pda_bn_finalize_shifted(const float* part, int T, int C, int bm, int M, const float* gamma,
+                            const float* beta, float eps, float momentum, float* mean,
+                            float* invstd, float* scale, float* shift, float* rmean, float* rvar,
+                            long long* nbt, int update_running, hipStream_t st) {
+  hipLaunchKernelGGL(bn_finalize_shifted_kernel, dim3((C + 15) / 16), dim3(1024), 0, st, part, T, C,
+                     bm, M, gamma, beta, eps, momentum, mean, invstd, scale, shift, rmean, rvar, nbt,
                      update_running);
   return (int)hipGetLastError();
 }

@@ -10,6 +10,7 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef double f64x2 __attribute__((ext_vector_type(2)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef int i32x4 __attribute__((ext_vector_type(4)));
 typedef unsigned short u16;
 
@@ -62,6 +63,18 @@ template <> __device__ __forceinline__ f32x4 mfma16<DT_BF16>(s16x8 a, s16x8 b, f
 }
 template <> __device__ __forceinline__ f32x4 mfma16<DT_F16>(s16x8 a, s16x8 b, f32x4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, a),
+                                                __builtin_bit_cast(f16x8, b), c, 0, 0, 0);
+}
+
+// ---- MFMA 32x32x16 (bf16 / f16): lane l holds A[row l&31][k 8(l>>5)+j] / B[k 8(l>>5)+j][col l&31];
+// D: col = lane&31, row = (reg&3) + 8(reg>>2) + 4(lane>>5)
+template <int DT> __device__ __forceinline__ f32x16 mfma32(s16x8 a, s16x8 b, f32x16 c);
+template <> __device__ __forceinline__ f32x16 mfma32<DT_BF16>(s16x8 a, s16x8 b, f32x16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, a),
+                                                 __builtin_bit_cast(bf16x8, b), c, 0, 0, 0);
+}
+template <> __device__ __forceinline__ f32x16 mfma32<DT_F16>(s16x8 a, s16x8 b, f32x16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8, a),
                                                 __builtin_bit_cast(f16x8, b), c, 0, 0, 0);
 }
 

@@ -115,7 +115,7 @@ __device__ __forceinline__ void st_sc1(T* q, T v) {
 // -- and combine the slab lanes in a fixed order: sums depend only on slab / chunk indices.
 // Counters are reset by their last arrivers (zero between launches).
 template <int BN, int NQ, class LoadAdd>
-__device__ bool inlaunch_combine(char* smem, int slab, int nslab, int ch, int N, int n0, int tn,
+__device__ __forceinline__ bool inlaunch_combine(char* smem, int slab, int nslab, int ch, int N, int n0, int tn,
                                  int tiles_n, int* cnt, double* chunkbuf, LoadAdd load_add) {
   constexpr int Q4 = BN / 4, SL = NT / Q4;
   const int tid = threadIdx.x, quad = tid % Q4, sl = tid / Q4;
@@ -141,7 +141,7 @@ __device__ bool inlaunch_combine(char* smem, int slab, int nslab, int ch, int N,
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
   __syncthreads();
-  auto combine_lanes = [&](double (&acc)[NQ][4]) {   // red[0][q][c] = fixed-order lane sum
+  auto combine_lanes = [&](double (&acc)[NQ][4]) __attribute__((always_inline)) {   // red[0][q][c] = fixed-order lane sum
 #pragma unroll
     for (int q = 0; q < NQ; ++q)
 #pragma unroll
@@ -205,15 +205,17 @@ __device__ bool inlaunch_combine(char* smem, int slab, int nslab, int ch, int N,
 }
 
 // Forward BatchNorm statistics from the conv epilogue's shifted partials (ConvParams fin_*).
-template <int BM, int BN>
-__device__ void bn_stats_finalize(const ConvParams& p, char* smem, int tm, int tn, int tiles_m,
+template <int BM, int BN, class PP>
+__device__ __forceinline__ void bn_stats_finalize(PP& p, char* smem, int tm, int tn, int tiles_m,
                                   int tiles_n, int n0) {
-  auto load_add = [&](int t, int n, double (&acc)[2][4]) {
-    const float* pt = p.stats + (size_t)t * 3 * p.N + n;
+  const float* stats = p.stats;   // (lambdas capture plain values, never the kernel argument)
+  const int N = p.N, M = p.M;
+  auto load_add = [stats, N, M](int t, int n, double (&acc)[2][4]) {
+    const float* pt = stats + (size_t)t * 3 * N + n;
     const f32x4 d0 = *reinterpret_cast<const f32x4*>(pt);
-    const f32x4 d1 = *reinterpret_cast<const f32x4*>(pt + p.N);
-    const f32x4 sh = *reinterpret_cast<const f32x4*>(pt + 2 * p.N);
-    const double rows = (double)min(BM, p.M - t * BM);
+    const f32x4 d1 = *reinterpret_cast<const f32x4*>(pt + N);
+    const f32x4 sh = *reinterpret_cast<const f32x4*>(pt + 2 * N);
+    const double rows = (double)min(BM, M - t * BM);
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
       const double s_ = sh[e], a = d0[e];
@@ -257,13 +259,15 @@ __device__ void bn_stats_finalize(const ConvParams& p, char* smem, int tm, int t
 // Backward BatchNorm finalize from the dgrad epilogue's partials [slab][NQ][N] (q0 = sum dz,
 // q1 = sum dz*y, q2 = sum dz*y2): gamma/beta gradients into the flat gradient buffer and the
 // apply coefficients dy = k1*dz + k2*y + k3 (branch 2, the shortcut BN: k4..k6 for y2).
-template <int BN, int NQ>
-__device__ void bn_bwd_finalize_inlaunch(const ConvParams& p, char* smem, int slab, int nslab,
+template <int BN, int NQ, class PP>
+__device__ __forceinline__ void bn_bwd_finalize_inlaunch(PP& p, char* smem, int slab, int nslab,
                                          int tn, int tiles_n, int n0) {
-  auto load_add = [&](int t, int n, double (&acc)[NQ][4]) {
+  const float* epart = p.epart;   // (lambdas capture plain values, never the kernel argument)
+  const int N = p.N;
+  auto load_add = [epart, N](int t, int n, double (&acc)[NQ][4]) {
 #pragma unroll
     for (int q = 0; q < NQ; ++q) {
-      const f32x4 v = *reinterpret_cast<const f32x4*>(p.epart + ((size_t)t * NQ + q) * p.N + n);
+      const f32x4 v = *reinterpret_cast<const f32x4*>(epart + ((size_t)t * NQ + q) * N + n);
 #pragma unroll
       for (int e = 0; e < 4; ++e) acc[q][e] += (double)v[e];
     }
@@ -274,25 +278,28 @@ __device__ void bn_bwd_finalize_inlaunch(const ConvParams& p, char* smem, int sl
   const double* tot = reinterpret_cast<const double*>(smem + 64);
   const int tid = threadIdx.x;
   if (tid < BN && n0 + tid < p.N) {
-    const int c = n0 + tid;
-    const double count = p.bf_count, gs = p.bf_gscale;
-    const double sdz = tot[tid];
-#pragma unroll
-    for (int b = 0; b < NQ - 1; ++b) {
-      const double sdzy = tot[(1 + b) * BN + tid];
-      const double mu = p.bf_mean[b][c], is = p.bf_invstd[b][c], ga = p.bf_gamma[b][c];
+    // (constant member indices only: a dynamically indexed member array of the kernel argument
+    // makes the compiler copy the whole argument block to scratch)
+    const int c = n0 + tid, N = p.N;
+    const double count = p.bf_count, gs = p.bf_gscale, sdz = tot[tid];
+    const bool accum = p.bf_accumulate != 0;
+    auto branch = [=](double sdzy, const float* gam, const float* mean, const float* inv, float* dg,
+                      float* db, float* k) {
+      const double mu = mean[c], is = inv[c], ga = gam[c];
       const double sdzx = (sdzy - mu * sdz) * is;   // sum dz * xhat
-      float* dg = p.bf_dgamma[b];
-      float* db = p.bf_dbeta[b];
-      dg[c] = (float)(sdzx * gs) + (p.bf_accumulate ? dg[c] : 0.f);
-      db[c] = (float)(sdz * gs) + (p.bf_accumulate ? db[c] : 0.f);
+      dg[c] = (float)(sdzx * gs) + (accum ? dg[c] : 0.f);
+      db[c] = (float)(sdz * gs) + (accum ? db[c] : 0.f);
       const double a = ga * is;
       const double kk2 = -a * is * sdzx / count;
-      float* k = p.bf_k + (size_t)b * 3 * p.N;
       k[c] = (float)a;
-      k[p.N + c] = (float)kk2;
-      k[2 * p.N + c] = (float)(-a * sdz / count - kk2 * mu);
-    }
+      k[N + c] = (float)kk2;
+      k[2 * N + c] = (float)(-a * sdz / count - kk2 * mu);
+    };
+    branch(tot[BN + tid], p.bf_gamma[0], p.bf_mean[0], p.bf_invstd[0], p.bf_dgamma[0],
+           p.bf_dbeta[0], p.bf_k);
+    if constexpr (NQ == 3)
+      branch(tot[2 * BN + tid], p.bf_gamma[1], p.bf_mean[1], p.bf_invstd[1], p.bf_dgamma[1],
+             p.bf_dbeta[1], p.bf_k + 3 * (size_t)N);
   }
 }
 
@@ -344,6 +351,30 @@ __device__ __forceinline__ s16x8 frag_col(const char* lds, int cb, int s, int la
   return r;
 }
 
+// 32x32x16 fragments, k-step s (16 k) of the 64-k tile: lane holds row/col base+(l&31),
+// k 16s + 8(l>>5) .. +7
+__device__ __forceinline__ s16x8 frag_row32(const char* lds, int rb, int s, int lane) {
+  const int row = rb + (lane & 31);
+  const int chunk = s * 2 + (lane >> 5);
+  return *reinterpret_cast<const s16x8*>(lds + row_addr(row, chunk));
+}
+// COL tile: 16-lane group g reads column block cb + 16(g&1), k rows 16s + 8(g>>1) + 0..7 with two
+// transposed reads (ds_read_b64_tr_b16: lane 4q+p addresses row q, columns 4p..4p+3)
+template <int BC>
+__device__ __forceinline__ s16x8 frag_col32(const char* lds, int cb, int s, int lane) {
+  const int g = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3;
+  const int chunk = ((cb + 16 * (g & 1)) >> 3) + (p >> 1);
+  const int k0 = s * 16 + 8 * (g >> 1) + q;
+  const int a0 = col_addr<BC>(k0, chunk) + ((p & 1) << 3);
+  const int a1 = col_addr<BC>(k0 + 4, chunk) + ((p & 1) << 3);
+  s16x4 v0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(s16x4, lds + a0));
+  s16x4 v1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(s16x4, lds + a1));
+  s16x8 r;
+  r[0] = v0[0]; r[1] = v0[1]; r[2] = v0[2]; r[3] = v0[3];
+  r[4] = v1[0]; r[5] = v1[1]; r[6] = v1[2]; r[7] = v1[3];
+  return r;
+}
+
 // COL tile of f32 (exact-fp32 path): 32 k-rows x BC cols of 4 B, 16-B chunks XOR-swizzled by
 // 4 * ((krow >> 2) & 3) so the four k-groups of a fragment read land in disjoint bank quarters.
 template <int BC>
@@ -368,10 +399,24 @@ __device__ __forceinline__ f32x4 frag_col_f32(const char* lds, int cb, int s, in
 // STAGES = 1: single LDS buffer (half the LDS -> one more resident block per CU) for the many
 //             shallow-K layers of ResNet (K = 64..128: nk <= 2), where the per-block
 //             load -> MFMA -> store chain is latency-bound and concurrency matters more.
-template <int PASS, int DT, int BM, int BN, int STAGES>
+// MF = 32: the 16-bit paths issue MFMA 32x32x16 instead of 16x16x32 -- the same FLOP per cycle
+// with half the MFMA instructions and fragment reads, so three times the VALU issue slots per
+// MFMA for the operand gather / BN prologue (the 16x16 main loops are VALU-issue-bound: PMC r1).
+template <int PASS, int DT, int BM, int BN, int STAGES, int MF = 16>
 // 256-wide tiles (single-stage only; wave tile 128x64 / 64x128: a quarter less LDS traffic per
 // MFMA) need ~250 registers and 64 KiB of LDS: two blocks per CU.
-__global__ __launch_bounds__(NT, (STAGES == 1 && BM * BN <= 128 * 128) ? 3 : 2) void conv_gemm_kernel(ConvParams p) {
+__global__ __launch_bounds__(NT, (STAGES == 1 && BM * BN <= 128 * 128) ? 3 : 2) void conv_gemm_kernel(ConvParams p_arg) {
+  static_assert(MF == 16 || (MF == 32 && DT != DT_F32 && BM >= 64 && BN >= 64), "MFMA shape");
+  // Read the parameters in place in the kernarg segment (constant address space). Binding a
+  // reference to the by-value argument instead makes the compiler copy the whole ~1 KB block to
+  // scratch whenever a member array is indexed dynamically (DGRAD tap tables).
+#if defined(__HIP_DEVICE_COMPILE__)
+  (void)p_arg;
+  typedef const __attribute__((address_space(4))) ConvParams KParams;
+  KParams& p = *(KParams*)__builtin_amdgcn_kernarg_segment_ptr();
+#else   // host pass of the template (never executed): the plain argument
+  const ConvParams& p = p_arg;
+#endif
   // A tile: FWD/DGRAD ROW [BM][64]; WGRAD COL [64][BM]. B tile: FWD ROW [BN][64]; else COL [64][BN]
   // element geometry: 16-bit operands move 8 elements per 16-B chunk and 64 k per 128-B tile row;
   // the exact-f32 path (DT_F32, MFMA 16x16x4 f32) moves 4 per chunk and 32 k per row
@@ -518,7 +563,7 @@ __global__ __launch_bounds__(NT, (STAGES == 1 && BM * BN <= 128 * 128) ? 3 : 2) 
                                                                          (int)a_bytes, 0x00020000);
   const __amdgpu_buffer_rsrc_t rsb = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p.b), (short)0,
                                                                          (int)b_bytes, 0x00020000);
-  auto bld = [&](const __amdgpu_buffer_rsrc_t& r, uint32_t off) -> i32x4 {
+  auto bld = [&](const __amdgpu_buffer_rsrc_t& r, uint32_t off) __attribute__((always_inline)) -> i32x4 {
     return __builtin_bit_cast(i32x4, __builtin_amdgcn_raw_buffer_load_b128(r, (int)off, 0, 0));
   };
 
@@ -527,7 +572,7 @@ __global__ __launch_bounds__(NT, (STAGES == 1 && BM * BN <= 128 * 128) ? 3 : 2) 
   const bool pro = (PASS == FWD || PASS == WGRAD) && p.pro_sc != nullptr;
   bool pv[PASS == FWD ? AR : BR];
   f32x2 psc[4], psh[4];
-  auto pro_coeffs = [&](int c) {
+  auto pro_coeffs = [&](int c) __attribute__((always_inline)) {
 #pragma unroll
     for (int k = 0; k < EPC / 2; ++k) {
       psc[k] = *reinterpret_cast<const f32x2*>(p.pro_sc + c + 2 * k);
@@ -538,7 +583,7 @@ __global__ __launch_bounds__(NT, (STAGES == 1 && BM * BN <= 128 * 128) ? 3 : 2) 
   // relu on the packed 16-bit result: bf16/f16 are sign-magnitude, so a signed 16-bit max with 0
   // zeroes exactly the negative values (and -0) -- one v_pk_max_i16 per pair
   typedef short s16x2 __attribute__((ext_vector_type(2)));
-  auto pro_apply = [&](i32x4& v) {
+  auto pro_apply = [&](i32x4& v) __attribute__((always_inline)) {
     if constexpr (F32) {   // one f32 element per dword
 #pragma unroll
       for (int k = 0; k < 4; ++k)
@@ -555,7 +600,7 @@ __global__ __launch_bounds__(NT, (STAGES == 1 && BM * BN <= 128 * 128) ? 3 : 2) 
     }
   };
 
-  auto load_tile = [&](int kt) {
+  auto load_tile = [&](int kt) __attribute__((always_inline)) {
     const int k0 = kbeg + kt * BKE;
     // ---------------- A
     if constexpr (PASS == FWD) {
@@ -626,7 +671,7 @@ __global__ __launch_bounds__(NT, (STAGES == 1 && BM * BN <= 128 * 128) ? 3 : 2) 
     }
   };
 
-  auto store_tile = [&](int buf) {
+  auto store_tile = [&](int buf) __attribute__((always_inline)) {
     char* sa = smem + buf * STAGE;
     char* sb = sa + A_BYTES;
     if constexpr (A_ROW) {
@@ -669,12 +714,20 @@ __global__ __launch_bounds__(NT, (STAGES == 1 && BM * BN <= 128 * 128) ? 3 : 2) 
   // lane ends up holding 4 consecutive COLUMNS of one row: the epilogue writes the C tile with one
   // 8-byte packed LDS store per MFMA tile (and the f32 paths with 16-byte stores) instead of
   // per-element 2-byte stores.
-  constexpr int MI = BM / 32, NI = BN / 32;
-  f32x4 acc[MI][NI];
+  constexpr int MI = BM / 32, NI = BN / 32;      // 16x16 tiles per wave
+  constexpr int MI2 = BM / 64, NI2 = BN / 64;    // 32x32 tiles per wave
+  f32x4 acc[MF == 16 ? MI : 1][MF == 16 ? NI : 1];
+  f32x16 acc2[MF == 32 ? MI2 : 1][MF == 32 ? NI2 : 1];
 #pragma unroll
-  for (int i = 0; i < MI; ++i)
+  for (int i = 0; i < (MF == 16 ? MI : 1); ++i)
 #pragma unroll
-    for (int j = 0; j < NI; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < (MF == 16 ? NI : 1); ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int i = 0; i < (MF == 32 ? MI2 : 1); ++i)
+#pragma unroll
+    for (int j = 0; j < (MF == 32 ? NI2 : 1); ++j)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc2[i][j][e] = 0.f;
 
   if (nk > 0) {
     load_tile(0);
@@ -692,6 +745,28 @@ __global__ __launch_bounds__(NT, (STAGES == 1 && BM * BN <= 128 * 128) ? 3 : 2) 
     if (kt + 1 < nk) load_tile(kt + 1);
     const char* sa = smem + cur * STAGE;
     const char* sb = sa + A_BYTES;
+    if constexpr (MF == 32) {
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {   // k-steps of 16
+        s16x8 fa[MI2], fb[NI2];
+#pragma unroll
+        for (int i = 0; i < MI2; ++i) {
+          const int rbase = wr * (BM / 2) + i * 32;
+          if constexpr (A_ROW) fa[i] = frag_row32(sa, rbase, s, lane);
+          else fa[i] = frag_col32<BM>(sa, rbase, s, lane);
+        }
+#pragma unroll
+        for (int j = 0; j < NI2; ++j) {
+          const int cbase = wc * (BN / 2) + j * 32;
+          if constexpr (B_ROW) fb[j] = frag_row32(sb, cbase, s, lane);
+          else fb[j] = frag_col32<BN>(sb, cbase, s, lane);
+        }
+#pragma unroll
+        for (int i = 0; i < MI2; ++i)
+#pragma unroll
+          for (int j = 0; j < NI2; ++j) acc2[i][j] = mfma32<DT>(fb[j], fa[i], acc2[i][j]);
+      }
+    } else {
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
       if constexpr (F32) {   // 16 k per step: lane holds 4 k of its row/col; 4 MFMAs 16x16x4 f32
@@ -735,6 +810,7 @@ __global__ __launch_bounds__(NT, (STAGES == 1 && BM * BN <= 128 * 128) ? 3 : 2) 
         for (int j = 0; j < NI; ++j) acc[i][j] = mfma16<DT>(fb[j], fa[i], acc[i][j]);
       }
     }
+    }   // MF == 16
     if constexpr (STAGES == 2) {
       if (kt + 1 < nk) store_tile(cur ^ 1);
     }
@@ -743,85 +819,86 @@ __global__ __launch_bounds__(NT, (STAGES == 1 && BM * BN <= 128 * 128) ? 3 : 2) 
 
   // ================================================================ epilogue
   const int lr = lane & 15, lg = lane >> 4;
+  // every accumulator value as (row, 4 consecutive columns) within the wave tile: both MFMA
+  // shapes run with swapped operands (D = C^T), so a lane holds 4 consecutive C columns per
+  // 16x16 tile (MF 16) or per group of 4 accumulator registers (MF 32)
+  auto for_items = [&](auto&& fn) __attribute__((always_inline)) {
+    if constexpr (MF == 32) {
+#pragma unroll
+      for (int i = 0; i < MI2; ++i)
+#pragma unroll
+        for (int j = 0; j < NI2; ++j)
+#pragma unroll
+          for (int r4 = 0; r4 < 4; ++r4) {
+            const f32x4 v = {acc2[i][j][4 * r4], acc2[i][j][4 * r4 + 1], acc2[i][j][4 * r4 + 2],
+                             acc2[i][j][4 * r4 + 3]};
+            fn(i * 32 + (lane & 31), j * 32 + 8 * r4 + 4 * (lane >> 5), v);
+          }
+    } else {
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int j = 0; j < NI; ++j) fn(i * 16 + lr, j * 16 + 4 * lg, acc[i][j]);
+    }
+  };
   if constexpr (PASS == WGRAD) {
     float* slab = reinterpret_cast<float*>(p.out) + (size_t)split * p.M * p.N;
     const bool vec = (p.N & 3) == 0;
+    for_items([&](int rl, int cl, const f32x4& v) {
+      const int row = m0 + wr * (BM / 2) + rl;
+      const int col = n0 + wc * (BN / 2) + cl;
+      if (row >= p.M) return;
+      float* d = slab + (size_t)row * p.N + col;
+      if (vec) {
+        if (col < p.N) *reinterpret_cast<f32x4*>(d) = v;
+      } else {
 #pragma unroll
-    for (int i = 0; i < MI; ++i)
-#pragma unroll
-      for (int j = 0; j < NI; ++j) {
-        const int row = m0 + wr * (BM / 2) + i * 16 + lr;
-        const int col = n0 + wc * (BN / 2) + j * 16 + 4 * lg;
-        if (row >= p.M) continue;
-        float* d = slab + (size_t)row * p.N + col;
-        if (vec) {
-          if (col < p.N) *reinterpret_cast<f32x4*>(d) = acc[i][j];
-        } else {
-#pragma unroll
-          for (int e = 0; e < 4; ++e)
-            if (col + e < p.N) d[e] = acc[i][j][e];
-        }
+        for (int e = 0; e < 4; ++e)
+          if (col + e < p.N) d[e] = v[e];
       }
+    });
     return;
   } else {
     if (p.out_f32) {  // fc logits: f32 + bias, direct stores
       float* out = reinterpret_cast<float*>(p.out);
+      for_items([&](int rl, int cl, const f32x4& v) {
+        const int row = m0 + wr * (BM / 2) + rl;
+        const int col = n0 + wc * (BN / 2) + cl;
+        if (row >= p.M) return;
 #pragma unroll
-      for (int i = 0; i < MI; ++i)
-#pragma unroll
-        for (int j = 0; j < NI; ++j) {
-          const int row = m0 + wr * (BM / 2) + i * 16 + lr;
-          const int col = n0 + wc * (BN / 2) + j * 16 + 4 * lg;
-          if (row >= p.M) continue;
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            const int c = col + e;
-            if (c < p.N) out[(size_t)row * p.out_pitch + c] = acc[i][j][e] + (p.bias ? p.bias[c] : 0.f);
-          }
+        for (int e = 0; e < 4; ++e) {
+          const int c = col + e;
+          if (c < p.N) out[(size_t)row * p.out_pitch + c] = v[e] + (p.bias ? p.bias[c] : 0.f);
         }
+      });
       return;
     }
-    if (p.relu) {
-#pragma unroll
-      for (int i = 0; i < MI; ++i)
-#pragma unroll
-        for (int j = 0; j < NI; ++j)
-#pragma unroll
-          for (int e = 0; e < 4; ++e) acc[i][j][e] = fmaxf(acc[i][j][e], 0.f);
-    }
+    const bool relu = p.relu != 0;
     // stage the C tile through LDS: [BM][BN], row pitch BN*ES bytes, 16-B chunks swizzled by
-    // row; one packed 8-byte store (4 columns) per MFMA tile per lane (f32: one 16-B store).
+    // row; one packed 8-byte store (4 columns) per item per lane (f32: one 16-B store).
     constexpr int CPR = BN / EPC;
     auto c_addr = [&](int row, int chunk) { return row * CPR + (chunk ^ (row & (CPR - 1))); };
     // f32: the waves of wave-row h write their tiles to local rows [0, BM/2) of the LDS image
-    auto stage_f32 = [&](int h) {
+    auto stage_f32 = [&](int h) __attribute__((always_inline)) {
       if (wr != h) return;
-#pragma unroll
-      for (int j = 0; j < NI; ++j) {
-        const int col = wc * (BN / 2) + j * 16 + 4 * lg;
-#pragma unroll
-        for (int i = 0; i < MI; ++i) {
-          const int row = i * 16 + lr;
-          *reinterpret_cast<f32x4*>(smem + row * (BN * 4) + (((col >> 2) ^ (row & (CPR - 1))) << 4)) =
-              acc[i][j];
-        }
-      }
+      for_items([&](int rl, int cl, f32x4 v) {
+        const int col = wc * (BN / 2) + cl;
+        if (relu) v = __builtin_elementwise_max(v, (f32x4){0.f, 0.f, 0.f, 0.f});
+        *reinterpret_cast<f32x4*>(smem + rl * (BN * 4) + (((col >> 2) ^ (rl & (CPR - 1))) << 4)) = v;
+      });
     };
     if constexpr (!F32) {
-#pragma unroll
-      for (int j = 0; j < NI; ++j) {
-        const int col = wc * (BN / 2) + j * 16 + 4 * lg;
-#pragma unroll
-        for (int i = 0; i < MI; ++i) {
-          const int row = wr * (BM / 2) + i * 16 + lr;
-          // row & (CPR-1) == lr & (CPR-1) for CPR <= 16 (folded); BN = 256 needs the full row
-          const int cbyte = (((col >> 3) ^ (row & (CPR - 1))) << 4) + ((col & 4) << 1);
-          uint2 pk;
-          pk.x = pack2<DT>(f32x2{acc[i][j][0], acc[i][j][1]});
-          pk.y = pack2<DT>(f32x2{acc[i][j][2], acc[i][j][3]});
-          *reinterpret_cast<uint2*>(smem + row * (BN * 2) + cbyte) = pk;
-        }
-      }
+      for_items([&](int rl, int cl, f32x4 v) {
+        const int col = wc * (BN / 2) + cl;
+        const int row = wr * (BM / 2) + rl;
+        if (relu) v = __builtin_elementwise_max(v, (f32x4){0.f, 0.f, 0.f, 0.f});
+        // row & (CPR-1) == lr & (CPR-1) for CPR <= 16 (folded); BN = 256 needs the full row
+        const int cbyte = (((col >> 3) ^ (row & (CPR - 1))) << 4) + ((col & 4) << 1);
+        uint2 pk;
+        pk.x = pack2<DT>(f32x2{v[0], v[1]});
+        pk.y = pack2<DT>(f32x2{v[2], v[3]});
+        *reinterpret_cast<uint2*>(smem + row * (BN * 2) + cbyte) = pk;
+      });
     }
     const char* ct = smem;
     // coalesced 16-B stores + per-channel partial statistics.
@@ -844,7 +921,7 @@ __global__ __launch_bounds__(NT, (STAGES == 1 && BM * BN <= 128 * 128) ? 3 : 2) 
     constexpr int PD = RPTH > 4 ? 4 : RPTH;
     char* outb = reinterpret_cast<char*>(p.out);
     const int gcol = n0 + cc * EPC;
-    auto row_off = [&](int i, bool& ok) -> uint32_t {
+    auto row_off = [&](int i, bool& ok) __attribute__((always_inline)) -> uint32_t {
       const int grow = m0 + rg + RG * i;
       ok = grow < p.M && gcol < p.N;
       uint32_t orow = ok ? grow : 0;
@@ -857,7 +934,7 @@ __global__ __launch_bounds__(NT, (STAGES == 1 && BM * BN <= 128 * 128) ? 3 : 2) 
       return orow * (uint32_t)p.out_pitch + gcol;
     };
 
-    auto rows = [&](auto mode_c, auto g2_c) {
+    auto rows = [&](auto mode_c, auto g2_c) __attribute__((always_inline)) {
       constexpr int MODE = decltype(mode_c)::value;   // -1 plain / FWD stats; 0,1,2 BN-backward
       constexpr bool G2 = decltype(g2_c)::value != 0;
       constexpr int NQ = MODE == 2 ? 3 : 2;
@@ -880,7 +957,7 @@ __global__ __launch_bounds__(NT, (STAGES == 1 && BM * BN <= 128 * 128) ? 3 : 2) 
       bool eok[PD];
       i32x4 py[PD], pg2[PD], py2[PD];
       uint32_t pm[PD];
-      auto prefetch = [&](int g0) {
+      auto prefetch = [&](int g0) __attribute__((always_inline)) {
         const i32x4 z = {0, 0, 0, 0};
 #pragma unroll
         for (int j = 0; j < PD; ++j) {
@@ -1124,9 +1201,18 @@ struct ConvDesc {  // mirrors pytorch_distributed_amd/ops/ext.py ConvDesc
   int Nb, H, W, Cin, Cout, R, S, stride, pad, Ho, Wo;
 };
 
+// MFMA shape of the 16-bit kernels (pda_conv_set_mfma): 16 = 16x16x32, 32 = 32x32x16
+static int g_mfma = 16;
+
 template <int PASS, int DT, int BM, int BN, int ST>
 static int launch(const ConvParams& p, dim3 grid, hipStream_t st) {
-  hipLaunchKernelGGL((conv_gemm_kernel<PASS, DT, BM, BN, ST>), grid, dim3(NT), 0, st, p);
+  if constexpr (DT != DT_F32) {
+    if (g_mfma == 32) {
+      hipLaunchKernelGGL((conv_gemm_kernel<PASS, DT, BM, BN, ST, 32>), grid, dim3(NT), 0, st, p);
+      return (int)hipGetLastError();
+    }
+  }
+  hipLaunchKernelGGL((conv_gemm_kernel<PASS, DT, BM, BN, ST, 16>), grid, dim3(NT), 0, st, p);
   return (int)hipGetLastError();
 }
 
@@ -1137,10 +1223,9 @@ static int dispatch(int dt, int bm, int bn, const ConvParams& p, dim3 grid, hipS
 #define PDA_CASE1(D, M_, N_)                                                   \
   if (dt == D && -bm == M_ && bn == N_) return launch<PASS, D, M_, N_, 1>(p, grid, st);
     PDA_CASE1(DT_BF16, 128, 128) PDA_CASE1(DT_BF16, 128, 64) PDA_CASE1(DT_BF16, 64, 128)
-    // 256-wide tiles only where they measured faster (profiles/convbench_r1_v6.txt):
-    // wgrad 256x128 (3x3 layers 3-4), dgrad 128x256 (1x1 with wide Cin)
+    // 256-wide tiles only where they measured faster (profiles/convbench_r1_v6.txt): wgrad 256x128
+    // (3x3 layers 3-4; the dgrad 128x256 tile never beat 128x128 in the step and is not built)
     if constexpr (PASS == WGRAD) { PDA_CASE1(DT_BF16, 256, 128) PDA_CASE1(DT_F16, 256, 128) }
-    if constexpr (PASS == DGRAD) { PDA_CASE1(DT_BF16, 128, 256) PDA_CASE1(DT_F16, 128, 256) }
     PDA_CASE1(DT_F16, 128, 128) PDA_CASE1(DT_F16, 128, 64) PDA_CASE1(DT_F16, 64, 128)
     PDA_CASE1(DT_F32, 128, 128) PDA_CASE1(DT_F32, 128, 64) PDA_CASE1(DT_F32, 64, 128)
 #undef PDA_CASE1
@@ -1186,6 +1271,12 @@ struct BnFin {  // mirrors ops/ext.py BnFin
 };
 
 extern "C" {
+
+int pda_conv_set_mfma(int mf) {
+  if (mf != 16 && mf != 32) return -1;
+  g_mfma = mf;
+  return 0;
+}
 
 // Y[M=Nb*Ho*Wo][Cout] = conv(X, W). W: [Cout][Kpad] 16-bit. stats: [ceil(M/bm)][3][Cout] shifted
 // partials or null; fin (with stats): BatchNorm statistics combined/finalized inside the launch.

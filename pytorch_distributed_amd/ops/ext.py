@@ -74,8 +74,11 @@ _SIGS = {
     "pda_conv_fwd": [C.POINTER(ConvDesc), _V, _V, _I, _V, _I, _I, _V, _V, _I, _V, _V, C.POINTER(BnFin),
                      _I, _I, _I, _V],
     "pda_conv_dgrad": [C.POINTER(ConvDesc), _V, _V, _V, C.POINTER(BnEpi), _I, _I, _I, _V],
+    "pda_conv_set_mfma": [_I],
     "pda_conv_wgrad": [C.POINTER(ConvDesc), _V, _V, _V, _I, _I, _V, _V, _I, _I, _I, _V],
     "pda_wgrad_reduce": [_V, _V, _I, _I, _I, _I, _I, _I, _F, _I, _V],
+    "pda_bn_finalize_shifted": [_V, _I, _I, _I, _I, _V, _V, _F, _F, _V, _V, _V, _V, _V, _V, _V, _I,
+                                _V],
     "pda_bn_finalize_tot": [_V, _I, _D, _V, _V, _F, _F, _V, _V, _V, _V, _V, _V, _V, _I, _V],
     "pda_slab_reduce": [_V, _I, _I, _I, _V, _V],
     "pda_bn_eval_coeffs": [_V, _V, _V, _V, _F, _I, _V, _V, _V],
@@ -121,6 +124,9 @@ def load(required: bool = False) -> Optional[C.CDLL]:
                 continue
             fn.argtypes = argt
             fn.restype = C.c_int
+        if getattr(lib, "pda_conv_set_mfma", None) is not None:
+            # MFMA shape of the 16-bit conv kernels: 16 = 16x16x32, 32 = 32x32x16
+            lib.pda_conv_set_mfma(int(os.environ.get("PDA_MFMA", "16")))
         _LIB = lib
     except OSError as e:
         _ERR = str(e)

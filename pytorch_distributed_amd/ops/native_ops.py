@@ -95,6 +95,10 @@ _WGRAD_TARGET = int(os.environ.get("PDA_WGRAD_TARGET", 2 * _NUM_CU))
 
 
 _SINGLE_STAGE = os.environ.get("PDA_SINGLE_STAGE", "1") != "0"
+# BatchNorm reductions inside the producing conv launch (forward statistics / dgrad epilogue
+# backward finalize); 0 = separate finalize launches (A/B)
+_INLAUNCH_BN_FWD = os.environ.get("PDA_INLAUNCH_BN", "1") not in ("0", "bwd")
+_INLAUNCH_BN_BWD = os.environ.get("PDA_INLAUNCH_BN", "1") not in ("0", "fwd")
 # scale on the split-K block targets (the wgrads run beside the dgrad chain on a second stream)
 _WGRAD_TB_SCALE = float(os.environ.get("PDA_WGRAD_TB_SCALE", "1.0"))
 
@@ -150,6 +154,23 @@ def conv_fwd(x: torch.Tensor, w: torch.Tensor, g: ConvGeom, out: torch.Tensor,
     pitch = out.stride(0) if out.dim() == 2 else g.Cout
     fin = None
     sync = None
+    if bn is not None and not _INLAUNCH_BN_FWD:   # A/B: partials here, finalize in a 2nd launch
+        T = math.ceil(M / abs(bm))
+        stats = bn.ws.get("fwd_stats", T * 3 * g.Cout)
+        rc = ext.lib().pda_conv_fwd(C.byref(d), ptr(x), ptr(w), Kpad, ptr(out), int(out_f32), pitch,
+                                    ptr(bias), ptr(stats), int(relu), ptr(pro[0] if pro else None),
+                                    ptr(pro[1] if pro else None), None, dt_of(x), bm, bn_,
+                                    stream(x.device))
+        check(rc, "conv_fwd")
+        if getattr(bn.ws, "sync_comm", None) is not None and bn.ws.sync_comm.world_size > 1:
+            raise RuntimeError("PDA_INLAUNCH_BN=0 does not support SyncBatchNorm")
+        rc = ext.lib().pda_bn_finalize_shifted(ptr(stats), T, g.Cout, abs(bm), M, ptr(bn.gamma),
+                                               ptr(bn.beta), bn.eps, bn.momentum, ptr(bn.mean),
+                                               ptr(bn.invstd), ptr(bn.scale), ptr(bn.shift),
+                                               ptr(bn.rmean), ptr(bn.rvar), ptr(bn.nbt),
+                                               int(bn.update), stream(x.device))
+        check(rc, "bn_finalize_shifted")
+        return out
     if bn is not None:
         ws = bn.ws
         T = math.ceil(M / abs(bm))
@@ -265,7 +286,8 @@ def bn_epilogue(ws: "Workspace", G: int, y, scale, shift, res=None, y2=None, sca
                     ptr(mask))
     k = None
     sync = getattr(ws, "sync_comm", None)
-    if fin is not None and (sync is None or sync.world_size == 1) and tiles_n > 0:
+    if (fin is not None and (sync is None or sync.world_size == 1) and tiles_n > 0
+            and _INLAUNCH_BN_BWD):
         ch = max(1, math.ceil(math.sqrt(G)))
         G1 = math.ceil(G / ch)
         chunk = ws.get("bn_chunk", G1 * nq * C_, torch.float64)

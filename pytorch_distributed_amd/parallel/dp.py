@@ -269,8 +269,17 @@ class DataParallel(nn.Module):
         if getattr(self, "_graphs", None) is None or [x.shape for x in xs] != self._graph_shapes:
             self._graphs = [_ReplicaGraph(m, x.shape, B) for m, x in zip(self.all_modules, xs)]
             self._graph_shapes = [x.shape for x in xs]
-        for rg, x, y in zip(self._graphs, xs, ys):
-            rg.run(x, y, graph)
+        jobs = list(zip(self._graphs, xs, ys))
+        import os
+        if (graph and len(jobs) > 1 and all(rg.graph is not None for rg in self._graphs)
+                and os.environ.get("PDA_DP_THREADS", "1") != "0"):
+            # one host thread per device: hipGraphLaunch of a ~500-node step costs ~2 ms of host
+            # time, and CUDAGraph.replay releases the GIL, so N replicas enqueue concurrently
+            # instead of staggering device i's start by i x 2 ms (captures stay on this thread)
+            list(self._pool().map(lambda j: j[0].run(j[1], j[2], True), jobs))
+        else:
+            for rg, x, y in jobs:
+                rg.run(x, y, graph)
         if self.replicas:
             self._reduce_grads()
         else:
@@ -281,6 +290,13 @@ class DataParallel(nn.Module):
         for rg, x in zip(self._graphs, xs):
             loss += rg.loss.to(dev0, non_blocking=True) * (x.shape[0] / B)
         return loss
+
+    def _pool(self):
+        if getattr(self, "_executor", None) is None:
+            from concurrent.futures import ThreadPoolExecutor
+            self._executor = ThreadPoolExecutor(max_workers=len(self.device_ids),
+                                                thread_name_prefix="dp-replay")
+        return self._executor
 
     def _arm_callback(self, g):
         if not self._armed:

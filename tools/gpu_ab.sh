@@ -1,6 +1,6 @@
 #!/bin/bash
 # GPU-box script: targeted GPU tests + A/B bench of env toggles (one process per variant).
-# usage: TESTS="tests/x.py" VARIANTS="PDA_FUSE_BWD=0 PDA_FUSE_BWD=1" bash tools/gpu_ab.sh
+# usage: TESTS="tests/x.py" VARIANTS="A=0,B=1 A=1,B=1" bash tools/gpu_ab.sh  (comma = several vars)
 set -o pipefail
 mkdir -p gpurun_out
 export PYTHONUNBUFFERED=1
@@ -11,6 +11,6 @@ fi
 i=0
 for v in ${VARIANTS:-BASE=1}; do
   i=$((i+1)); f=gpurun_out/ab_$i
-  env $v timeout -k 10 300 python bench.py --engine native --steps ${STEPS:-20} --warmup 5 ${BENCH_ARGS} > $f.json 2> $f.err || { echo "FAIL $v"; tail -20 $f.err; exit 1; }
+  env ${v//,/ } timeout -k 10 300 python bench.py --engine native --steps ${STEPS:-20} --warmup 5 ${BENCH_ARGS} > $f.json 2> $f.err || { echo "FAIL $v"; tail -20 $f.err; exit 1; }
   echo "$v $(python -c "import json,sys; r=json.load(open('$f.json')); print(r['value'], r['ms_per_step'], r['loss'])")"
 done

@@ -15,7 +15,7 @@ def family(name: str) -> str:
     if m:
         p = {"0": "fwd", "1": "dgrad", "2": "wgrad"}[m.group(1)]
         st = f" st{m.group(5)}" if m.group(5) else ""
-        pro = f" pro{m.group(6)}" if m.group(6) else ""
+        pro = " mf32" if m.group(6) == "32" else ""
         return f"conv_{p} {m.group(3)}x{m.group(4)}{st}{pro}"
     n = re.sub(r"^void ", "", n)
     n = n.replace("(anonymous namespace)::", "")
