@@ -94,11 +94,64 @@ __global__ __launch_bounds__(256) void bn_finalize_tot_kernel(
   if (blockIdx.x == 0 && threadIdx.x == 0 && update_running && nbt) *nbt += 1;
 }
 
-// From the conv epilogue's shifted per-tile partials part[T][3][C] = (sum(y-s), sum((y-s)^2), s)
-// (tiles of `bm` rows, the last one ragged): the separate-launch finalize (PDA_INLAUNCH_BN=0 A/B
-// path). One block = 16 channels x 64 partial lanes; per-lane f64 sums, fixed-shape tree.
-__global__ __launch_bounds__(1024) void bn_finalize_shifted_kernel(
-    const float* __restrict__ part, int T, int C, int bm, int M, const float* __restrict__ gamma,
+// Forward BatchNorm statistics from the conv epilogue's shifted per-tile partials
+// part[T][3][C] = (sum(y-s), sum((y-s)^2), s) over tiles of `bm` rows (the last one ragged), in
+// two launches: bn_fwd_prereduce (S blocks, each converting a contiguous range of tiles to f64
+// (sum y, sum y^2) for every channel: 16-B loads, (channel quad x slab lane) threads, fixed-order
+// lane combine) -> bn_finalize_slabs (f64 [S][2][C] -> coefficients + running statistics).
+__global__ __launch_bounds__(256) void bn_fwd_prereduce_kernel(const float* __restrict__ part,
+                                                               int T, int C, int bm, int M, int S,
+                                                               double* __restrict__ out) {
+  __shared__ double red[2][1024];   // [q][lane * Q4 + quad] (Q4 * SL <= 256 -> <= 1024 doubles)
+  const int Q4 = C >> 2;
+  const int SL = Q4 >= 256 ? 1 : 256 / Q4;
+  const int t0 = (int)((long long)blockIdx.x * T / S), t1 = (int)((long long)(blockIdx.x + 1) * T / S);
+  for (int qb = 0; qb < Q4; qb += 256 / SL) {
+    const int quad = qb + (int)threadIdx.x % (256 / SL), lane = (int)threadIdx.x / (256 / SL);
+    double a[4] = {0.0, 0.0, 0.0, 0.0}, b[4] = {0.0, 0.0, 0.0, 0.0};
+    if (quad < Q4) {
+      for (int t = t0 + lane; t < t1; t += SL) {
+        const float* pt = part + (size_t)t * 3 * C + quad * 4;
+        const f32x4 d0 = *reinterpret_cast<const f32x4*>(pt);
+        const f32x4 d1 = *reinterpret_cast<const f32x4*>(pt + C);
+        const f32x4 sh = *reinterpret_cast<const f32x4*>(pt + 2 * C);
+        const double rows = (double)min(bm, M - t * bm);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const double s_ = sh[e], x = d0[e];
+          a[e] += rows * s_ + x;
+          b[e] += (double)d1[e] + s_ * (2.0 * x + rows * s_);
+        }
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      red[0][threadIdx.x * 4 + e] = a[e];
+      red[1][threadIdx.x * 4 + e] = b[e];
+    }
+    __syncthreads();
+    // v < 4 * (256 / SL): column (qb * 4 + v) -- sum the SL lanes in order
+    const int W = 256 / SL;
+    for (int v = threadIdx.x; v < 4 * W; v += 256) {
+      const int qi = v >> 2, e = v & 3, col = (qb + qi) * 4 + e;
+      if (qb + qi < Q4) {
+        double sa = 0.0, sb = 0.0;
+        for (int l = 0; l < SL; ++l) {
+          sa += red[0][(l * W + qi) * 4 + e];
+          sb += red[1][(l * W + qi) * 4 + e];
+        }
+        out[((size_t)blockIdx.x * 2) * C + col] = sa;
+        out[((size_t)blockIdx.x * 2 + 1) * C + col] = sb;
+      }
+    }
+  }
+}
+
+// f64 slabs [S][2][C] (sum y, sum y^2) -> mean, invstd, scale, shift, running stats. One block =
+// 16 channels x 64 slab lanes, fixed-shape tree: deterministic.
+__global__ __launch_bounds__(1024) void bn_finalize_slabs_kernel(
+    const double* __restrict__ slabs, int S, int C, double count, const float* __restrict__ gamma,
     const float* __restrict__ beta, float eps, float momentum, float* __restrict__ mean_out,
     float* __restrict__ invstd_out, float* __restrict__ scale, float* __restrict__ shift,
     float* __restrict__ run_mean, float* __restrict__ run_var, long long* __restrict__ nbt,
@@ -107,20 +160,15 @@ __global__ __launch_bounds__(1024) void bn_finalize_shifted_kernel(
   const int cl = threadIdx.x & 15, g = threadIdx.x >> 4;
   const int c = blockIdx.x * 16 + cl;
   double s1 = 0.0, s2 = 0.0;
-  if (c < C) {
-    for (int t = g; t < T; t += 64) {
-      const float* pt = part + (size_t)t * 3 * C + c;
-      const double d0 = pt[0], d1 = pt[C], sh = pt[2 * C];
-      const double rows = (double)min(bm, M - t * bm);
-      s1 += rows * sh + d0;
-      s2 += d1 + sh * (2.0 * d0 + rows * sh);
+  if (c < C)
+    for (int t = g; t < S; t += 64) {
+      s1 += slabs[((size_t)t * 2) * C + c];
+      s2 += slabs[((size_t)t * 2 + 1) * C + c];
     }
-  }
   red[0][g][cl] = s1;
   red[1][g][cl] = s2;
   tree_reduce2(red, g, cl);
   if (g == 0 && c < C) {
-    const double count = (double)M;
     const double mean = red[0][0][cl] / count;
     double var = red[1][0][cl] / count - mean * mean;
     if (var < 0.0) var = 0.0;
@@ -749,12 +797,19 @@ int pda_bn_finalize_tot(const double* tot, int C, double count, const float* gam
   return (int)hipGetLastError();
 }
 
-int pda_bn_finalize_shifted(const float* part, int T, int C, int bm, int M, const float* gamma,
-                            const float* beta, float eps, float momentum, float* mean,
-                            float* invstd, float* scale, float* shift, float* rmean, float* rvar,
-                            long long* nbt, int update_running, hipStream_t st) {
-  hipLaunchKernelGGL(bn_finalize_shifted_kernel, dim3((C + 15) / 16), dim3(1024), 0, st, part, T, C,
-                     bm, M, gamma, beta, eps, momentum, mean, invstd, scale, shift, rmean, rvar, nbt,
+int pda_bn_fwd_prereduce(const float* part, int T, int C, int bm, int M, int S, double* out,
+                         hipStream_t st) {
+  if ((C & 3) || S <= 0 || S > T) return -2;
+  hipLaunchKernelGGL(bn_fwd_prereduce_kernel, dim3(S), dim3(256), 0, st, part, T, C, bm, M, S, out);
+  return (int)hipGetLastError();
+}
+
+int pda_bn_finalize_slabs(const double* slabs, int S, int C, double count, const float* gamma,
+                          const float* beta, float eps, float momentum, float* mean, float* invstd,
+                          float* scale, float* shift, float* rmean, float* rvar, long long* nbt,
+                          int update_running, hipStream_t st) {
+  hipLaunchKernelGGL(bn_finalize_slabs_kernel, dim3((C + 15) / 16), dim3(1024), 0, st, slabs, S, C,
+                     count, gamma, beta, eps, momentum, mean, invstd, scale, shift, rmean, rvar, nbt,
                      update_running);
   return (int)hipGetLastError();
 }

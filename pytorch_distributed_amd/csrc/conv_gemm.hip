@@ -114,33 +114,48 @@ __device__ __forceinline__ void st_sc1(T* q, T v) {
 // spread the work as (slab lane, column quad) with 16-B loads -- many loads in flight per thread
 // -- and combine the slab lanes in a fixed order: sums depend only on slab / chunk indices.
 // Counters are reset by their last arrivers (zero between launches).
+// Level-1 arrival of a workgroup whose partial sums are stored (write-through) by the waves of
+// threads < BN: returns true (block-uniform) in the last arriver of the chunk, after its agent
+// acquire. `flag` is a word of LDS the caller does not need meanwhile.
+template <int BN>
+__device__ __forceinline__ bool inlaunch_arrive(int* flag, int slab, int nslab, int ch, int tn,
+                                                int tiles_n, int* cnt) {
+  const int tid = threadIdx.x;
+  if (tid < BN) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's stores landed
+  __syncthreads();                                                   // ... and every wave's
+  const int chunk = slab / ch, c0 = chunk * ch;
+  const int nin = min(ch, nslab - c0);
+  if (tid == 0) {
+    const int old = __hip_atomic_fetch_add(cnt + chunk * tiles_n + tn, 1, __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_AGENT);
+    flag[0] = old == nin - 1;
+  }
+  __syncthreads();
+  const bool last = flag[0] != 0;
+  if (last && tid == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __syncthreads();
+  return last;
+}
+
+// Level-1 combine (by the chunk's last arriver), level-2 arrival and combine: returns true in the
+// column tile's final reducer with the totals at red[q * BN + c] (f64, smem + 64).
 template <int BN, int NQ, class LoadAdd>
-__device__ __forceinline__ bool inlaunch_combine(char* smem, int slab, int nslab, int ch, int N, int n0, int tn,
-                                 int tiles_n, int* cnt, double* chunkbuf, LoadAdd load_add) {
+__device__ __forceinline__ bool inlaunch_finish(char* smem, int slab, int nslab, int ch, int N,
+                                                int n0, int tn, int tiles_n, int* cnt,
+                                                double* chunkbuf, LoadAdd load_add) {
   constexpr int Q4 = BN / 4, SL = NT / Q4;
   const int tid = threadIdx.x, quad = tid % Q4, sl = tid / Q4;
   const int nq4 = n0 + quad * 4;
   int* flag = reinterpret_cast<int*>(smem);
   double* red = reinterpret_cast<double*>(smem + 64);   // [SL][NQ][BN]
-  // the partial sums of this workgroup were stored by the waves of threads < BN
-  if (tid < BN) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
   const int chunk = slab / ch, c0 = chunk * ch;
   const int nin = min(ch, nslab - c0);
   const int G1 = (nslab + ch - 1) / ch;
   int* cnt1 = cnt + chunk * tiles_n + tn;
   int* cnt2 = cnt + G1 * tiles_n + tn;
-  if (tid == 0) {
-    const int old = __hip_atomic_fetch_add(cnt1, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    flag[0] = old == nin - 1;
-  }
-  __syncthreads();
-  if (!flag[0]) return false;
-  if (tid == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  }
-  __syncthreads();
   auto combine_lanes = [&](double (&acc)[NQ][4]) __attribute__((always_inline)) {   // red[0][q][c] = fixed-order lane sum
 #pragma unroll
     for (int q = 0; q < NQ; ++q)
@@ -204,10 +219,20 @@ __device__ __forceinline__ bool inlaunch_combine(char* smem, int slab, int nslab
   return true;
 }
 
+template <int BN, int NQ, class LoadAdd>
+__device__ __forceinline__ bool inlaunch_combine(char* smem, int slab, int nslab, int ch, int N,
+                                                 int n0, int tn, int tiles_n, int* cnt,
+                                                 double* chunkbuf, LoadAdd load_add) {
+  if (!inlaunch_arrive<BN>(reinterpret_cast<int*>(smem), slab, nslab, ch, tn, tiles_n, cnt))
+    return false;
+  return inlaunch_finish<BN, NQ>(smem, slab, nslab, ch, N, n0, tn, tiles_n, cnt, chunkbuf,
+                                 load_add);
+}
+
 // Forward BatchNorm statistics from the conv epilogue's shifted partials (ConvParams fin_*).
 template <int BM, int BN, class PP>
 __device__ __forceinline__ void bn_stats_finalize(PP& p, char* smem, int tm, int tn, int tiles_m,
-                                  int tiles_n, int n0) {
+                                  int tiles_n, int n0, bool arrived = false) {
   const float* stats = p.stats;   // (lambdas capture plain values, never the kernel argument)
   const int N = p.N, M = p.M;
   auto load_add = [stats, N, M](int t, int n, double (&acc)[2][4]) {
@@ -223,8 +248,10 @@ __device__ __forceinline__ void bn_stats_finalize(PP& p, char* smem, int tm, int
       acc[1][e] += (double)d1[e] + s_ * (2.0 * a + rows * s_);
     }
   };
-  if (!inlaunch_combine<BN, 2>(smem, tm, tiles_m, p.fin_ch, p.N, n0, tn, tiles_n, p.fin_cnt,
-                               p.fin_chunk, load_add))
+  if (arrived ? !inlaunch_finish<BN, 2>(smem, tm, tiles_m, p.fin_ch, p.N, n0, tn, tiles_n,
+                                        p.fin_cnt, p.fin_chunk, load_add)
+              : !inlaunch_combine<BN, 2>(smem, tm, tiles_m, p.fin_ch, p.N, n0, tn, tiles_n,
+                                         p.fin_cnt, p.fin_chunk, load_add))
     return;
   const double* tot = reinterpret_cast<const double*>(smem + 64);
   const int tid = threadIdx.x;
@@ -402,18 +429,35 @@ __device__ __forceinline__ f32x4 frag_col_f32(const char* lds, int cb, int s, in
 // MF = 32: the 16-bit paths issue MFMA 32x32x16 instead of 16x16x32 -- the same FLOP per cycle
 // with half the MFMA instructions and fragment reads, so three times the VALU issue slots per
 // MFMA for the operand gather / BN prologue (the 16x16 main loops are VALU-issue-bound: PMC r1).
-template <int PASS, int DT, int BM, int BN, int STAGES, int MF = 16>
+// Resident blocks per CU the register allocation must allow (one wave per SIMD per block): the
+// 16-bit 64x64 and single-stage 128x64 / 64x128 tiles are held to 5 / 4 (<= 96 / 128 VGPRs) --
+// their fused epilogues would otherwise push them a few registers over and cost a wave per SIMD.
 // 256-wide tiles (single-stage only; wave tile 128x64 / 64x128: a quarter less LDS traffic per
 // MFMA) need ~250 registers and 64 KiB of LDS: two blocks per CU.
-__global__ __launch_bounds__(NT, (STAGES == 1 && BM * BN <= 128 * 128) ? 3 : 2) void conv_gemm_kernel(ConvParams p_arg) {
+template <int DT, int BM, int BN, int STAGES>
+constexpr int conv_min_blocks() {
+#ifdef PDA_CONV_MINB_LEGACY   // A/B: the pre-r2 bounds (tools/build_variant.py)
+  return (STAGES == 1 && BM * BN <= 128 * 128) ? 3 : 2;
+#endif
+  if (DT != DT_F32 && BM * BN <= 64 * 64) return 5;
+  if (DT != DT_F32 && STAGES == 1 && BM * BN <= 128 * 64) return 4;
+  return (STAGES == 1 && BM * BN <= 128 * 128) ? 3 : 2;
+}
+
+template <int PASS, int DT, int BM, int BN, int STAGES, int MF = 16>
+__global__ __launch_bounds__(NT, (conv_min_blocks<DT, BM, BN, STAGES>())) void conv_gemm_kernel(ConvParams p_arg) {
   static_assert(MF == 16 || (MF == 32 && DT != DT_F32 && BM >= 64 && BN >= 64), "MFMA shape");
-  // Read the parameters in place in the kernarg segment (constant address space). Binding a
-  // reference to the by-value argument instead makes the compiler copy the whole ~1 KB block to
-  // scratch whenever a member array is indexed dynamically (DGRAD tap tables).
+  // DGRAD / WGRAD read the parameters in place in the kernarg segment (constant address space):
+  // binding a reference to the by-value argument makes the compiler copy the whole ~1 KB block to
+  // scratch once a member array is indexed dynamically (DGRAD tap tables), and costs WGRAD spills.
+  // FWD keeps the plain argument -- read in place, the compiler re-issues scalar kernarg loads
+  // (with their waits) per epilogue row instead of holding the fields in SGPRs.
 #if defined(__HIP_DEVICE_COMPILE__)
-  (void)p_arg;
   typedef const __attribute__((address_space(4))) ConvParams KParams;
-  KParams& p = *(KParams*)__builtin_amdgcn_kernarg_segment_ptr();
+  auto&& p = [&]() -> decltype(auto) {
+    if constexpr (PASS != FWD) return *(KParams*)__builtin_amdgcn_kernarg_segment_ptr();
+    else return (p_arg);
+  }();
 #else   // host pass of the template (never executed): the plain argument
   const ConvParams& p = p_arg;
 #endif

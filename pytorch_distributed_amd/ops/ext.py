@@ -77,8 +77,8 @@ _SIGS = {
     "pda_conv_set_mfma": [_I],
     "pda_conv_wgrad": [C.POINTER(ConvDesc), _V, _V, _V, _I, _I, _V, _V, _I, _I, _I, _V],
     "pda_wgrad_reduce": [_V, _V, _I, _I, _I, _I, _I, _I, _F, _I, _V],
-    "pda_bn_finalize_shifted": [_V, _I, _I, _I, _I, _V, _V, _F, _F, _V, _V, _V, _V, _V, _V, _V, _I,
-                                _V],
+    "pda_bn_fwd_prereduce": [_V, _I, _I, _I, _I, _I, _V, _V],
+    "pda_bn_finalize_slabs": [_V, _I, _I, _D, _V, _V, _F, _F, _V, _V, _V, _V, _V, _V, _V, _I, _V],
     "pda_bn_finalize_tot": [_V, _I, _D, _V, _V, _F, _F, _V, _V, _V, _V, _V, _V, _V, _I, _V],
     "pda_slab_reduce": [_V, _I, _I, _I, _V, _V],
     "pda_bn_eval_coeffs": [_V, _V, _V, _V, _F, _I, _V, _V, _V],

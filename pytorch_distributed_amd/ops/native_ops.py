@@ -24,7 +24,7 @@ from .ext import ConvDesc, BwdArgs, check, dt_of, ptr, stream
 
 __all__ = [
     "ConvGeom", "conv_fwd", "conv_dgrad", "conv_wgrad", "pick_tile", "wgrad_plan",
-    "BnStats", "BnBwd", "stats_totals", "dgrad_tiles_n", "bn_finalize_tot", "bn_eval_coeffs", "bn_apply", "stem_pool", "maxpool_bwd", "tail_pool",
+    "BnStats", "BnBwd", "stats_totals", "dgrad_tiles_n", "bn_finalize_tot", "bn_finalize_partials", "bn_eval_coeffs", "bn_apply", "stem_pool", "maxpool_bwd", "tail_pool",
     "bn_bwd", "xent", "topk_hits", "col_sum", "sgd_flat", "cast_flat", "amp_scan",
     "pack_stem", "synth_batch", "nchw_to_nhwc8", "Workspace",
 ]
@@ -97,8 +97,9 @@ _WGRAD_TARGET = int(os.environ.get("PDA_WGRAD_TARGET", 2 * _NUM_CU))
 _SINGLE_STAGE = os.environ.get("PDA_SINGLE_STAGE", "1") != "0"
 # BatchNorm reductions inside the producing conv launch (forward statistics / dgrad epilogue
 # backward finalize); 0 = separate finalize launches (A/B)
-_INLAUNCH_BN_FWD = os.environ.get("PDA_INLAUNCH_BN", "1") not in ("0", "bwd")
-_INLAUNCH_BN_BWD = os.environ.get("PDA_INLAUNCH_BN", "1") not in ("0", "fwd")
+_INLAUNCH_BN = os.environ.get("PDA_INLAUNCH_BN", "bwd")     # 1 | 0 | fwd | bwd
+_INLAUNCH_BN_FWD = _INLAUNCH_BN in ("1", "fwd")
+_INLAUNCH_BN_BWD = _INLAUNCH_BN in ("1", "bwd")
 # scale on the split-K block targets (the wgrads run beside the dgrad chain on a second stream)
 _WGRAD_TB_SCALE = float(os.environ.get("PDA_WGRAD_TB_SCALE", "1.0"))
 
@@ -118,12 +119,12 @@ def pick_tile(M: int, N: int, K: Optional[int] = None) -> Tuple[int, int]:
 
 # ------------------------------------------------------------------ conv
 class BnStats:
-    """BatchNorm (training) statistics computed inside a conv forward launch: the conv epilogue
-    writes per-M-tile shifted partial sums and the last-arriving workgroups combine them in f64
-    and finalize mean / invstd / scale / shift and the running statistics -- no separate
-    reduction or finalize launch (csrc/conv_gemm.hip bn_stats_finalize). With SyncBatchNorm
-    (``ws.sync_comm``) the launch stops at f64 totals, which are all-reduced before a small
-    finalize kernel."""
+    """BatchNorm (training) statistics of a conv forward: the conv epilogue writes per-M-tile
+    shifted partial sums, finalized into mean / invstd / scale / shift and the running statistics
+    either by two small parallel launches (:func:`bn_finalize_partials`, the default -- measured
+    ~1.9 ms/step faster on ResNet-50, profiles/ab_r2_inlaunch_bn.md) or inside the conv launch by
+    its last-arriving workgroups (``PDA_INLAUNCH_BN=1|fwd``; csrc/conv_gemm.hip bn_stats_finalize).
+    With SyncBatchNorm (``ws.sync_comm``) the f64 totals are all-reduced before the finalize."""
 
     def __init__(self, ws: "Workspace", gamma, beta, eps: float, momentum: float, mean, invstd,
                  scale, shift, rmean=None, rvar=None, nbt=None, update_running: bool = True):
@@ -137,16 +138,18 @@ def conv_fwd(x: torch.Tensor, w: torch.Tensor, g: ConvGeom, out: torch.Tensor,
              stats: Optional[torch.Tensor] = None, bias: Optional[torch.Tensor] = None,
              relu: bool = False, tile: Optional[Tuple[int, int]] = None,
              pro: Optional[Tuple[torch.Tensor, torch.Tensor]] = None,
-             bn: Optional[BnStats] = None) -> torch.Tensor:
+             bn: Optional[BnStats] = None, inlaunch: Optional[bool] = None) -> torch.Tensor:
     """out[M, Cout] (16-bit or f32) = conv(x, w). w: [Cout, Kpad] 16-bit, Kpad = w.shape[1].
     stats (f32, >= ceil(M/bm)*3*Cout) receives per-M-tile shifted partials (sum(y-s),
     sum((y-s)^2), s) -- see :func:`stats_totals`; ``bn`` (:class:`BnStats`) instead finalizes
     BatchNorm inside the launch. pro = (scale, shift): x is a PRE-BatchNorm tensor and the conv
-    consumes relu(x*scale+shift)."""
+    consumes relu(x*scale+shift). ``inlaunch`` (default: PDA_INLAUNCH_BN) finalizes ``bn`` inside
+    the conv launch instead of in two small follow-up launches."""
     Nb = x.shape[0]
     M = Nb * g.Ho * g.Wo
     Kpad = w.shape[-1] if w.dim() == 2 else w[0].numel()
     bm, bn_ = tile or pick_tile(M, g.Cout, Kpad)
+    inlaunch = _INLAUNCH_BN_FWD if inlaunch is None else inlaunch
     d = g.desc(Nb)
     # direct (unstaged) f32 store + bias: the fc head (16-bit features -> f32 logits, or any conv
     # with a bias); f32 activations of the exact-fp32 engine take the staged path with statistics
@@ -154,7 +157,9 @@ def conv_fwd(x: torch.Tensor, w: torch.Tensor, g: ConvGeom, out: torch.Tensor,
     pitch = out.stride(0) if out.dim() == 2 else g.Cout
     fin = None
     sync = None
-    if bn is not None and not _INLAUNCH_BN_FWD:   # A/B: partials here, finalize in a 2nd launch
+    if bn is not None and not inlaunch:
+        # default: shifted partials here -> parallel f64 prereduce -> finalize (two small launches;
+        # measured cheaper than finalizing inside the conv launch: profiles/ab_r2_inlaunch_bn.md)
         T = math.ceil(M / abs(bm))
         stats = bn.ws.get("fwd_stats", T * 3 * g.Cout)
         rc = ext.lib().pda_conv_fwd(C.byref(d), ptr(x), ptr(w), Kpad, ptr(out), int(out_f32), pitch,
@@ -162,14 +167,7 @@ def conv_fwd(x: torch.Tensor, w: torch.Tensor, g: ConvGeom, out: torch.Tensor,
                                     ptr(pro[1] if pro else None), None, dt_of(x), bm, bn_,
                                     stream(x.device))
         check(rc, "conv_fwd")
-        if getattr(bn.ws, "sync_comm", None) is not None and bn.ws.sync_comm.world_size > 1:
-            raise RuntimeError("PDA_INLAUNCH_BN=0 does not support SyncBatchNorm")
-        rc = ext.lib().pda_bn_finalize_shifted(ptr(stats), T, g.Cout, abs(bm), M, ptr(bn.gamma),
-                                               ptr(bn.beta), bn.eps, bn.momentum, ptr(bn.mean),
-                                               ptr(bn.invstd), ptr(bn.scale), ptr(bn.shift),
-                                               ptr(bn.rmean), ptr(bn.rvar), ptr(bn.nbt),
-                                               int(bn.update), stream(x.device))
-        check(rc, "bn_finalize_shifted")
+        bn_finalize_partials(stats, T, g.Cout, abs(bm), M, bn)
         return out
     if bn is not None:
         ws = bn.ws
@@ -207,6 +205,28 @@ def stats_totals(stats: torch.Tensor, M: int, C_: int, bm: int) -> torch.Tensor:
     rows[-1, 0] = M - (T - 1) * abs(bm)
     d0, d1, sh = p[:, 0], p[:, 1], p[:, 2]
     return torch.stack([(rows * sh + d0).sum(0), (d1 + sh * (2 * d0 + rows * sh)).sum(0)])
+
+
+def bn_finalize_partials(stats: torch.Tensor, T: int, C_: int, bm: int, M: int, bn: BnStats) -> None:
+    """BatchNorm forward finalize from conv_fwd's shifted per-tile partials (two launches): a
+    parallel f64 prereduce into S slabs, then the per-channel finalize. SyncBatchNorm (``ws.sync_comm``):
+    the slabs are summed and all-reduced over the ranks first."""
+    S = max(1, min(T, max(96, min(512, 65536 // (2 * C_)))))
+    slabs = bn.ws.get("bn_slabs", S * 2 * C_, torch.float64)
+    st = stream(stats.device)
+    check(ext.lib().pda_bn_fwd_prereduce(ptr(stats), T, C_, bm, M, S, ptr(slabs), st),
+          "bn_fwd_prereduce")
+    sync = getattr(bn.ws, "sync_comm", None)
+    world = 1
+    if sync is not None and sync.world_size > 1:
+        tot = slabs.view(S, 2 * C_).sum(0)          # fixed-shape f64 reduction
+        sync.all_reduce(tot)
+        slabs, S, world = tot, 1, sync.world_size
+    check(ext.lib().pda_bn_finalize_slabs(ptr(slabs), S, C_, float(M * world), ptr(bn.gamma),
+                                          ptr(bn.beta), bn.eps, bn.momentum, ptr(bn.mean),
+                                          ptr(bn.invstd), ptr(bn.scale), ptr(bn.shift),
+                                          ptr(bn.rmean), ptr(bn.rvar), ptr(bn.nbt), int(bn.update),
+                                          st), "bn_finalize_slabs")
 
 
 def bn_finalize_tot(tot: torch.Tensor, C_: int, count: int, bn: BnStats) -> None:

@@ -159,7 +159,7 @@ def test_bn_forward_finalize_apply():
     assert int(nbt.item()) == 1
 
 
-def _conv_bn_inlaunch(K, x_nhwc, w2d, g, dtype, gamma, beta, tile=None, ws=None):
+def _conv_bn_inlaunch(K, x_nhwc, w2d, g, dtype, gamma, beta, tile=None, ws=None, inlaunch=True):
     ws = ws or K.Workspace(DEV)
     C = g.Cout
     y = torch.empty(x_nhwc.shape[0], g.Ho, g.Wo, C, device=DEV, dtype=dtype)
@@ -167,14 +167,16 @@ def _conv_bn_inlaunch(K, x_nhwc, w2d, g, dtype, gamma, beta, tile=None, ws=None)
     rm, rv = torch.zeros(C, device=DEV), torch.ones(C, device=DEV)
     nbt = torch.zeros(1, dtype=torch.int64, device=DEV)
     bn = K.BnStats(ws, gamma, beta, 1e-5, 0.1, st[0], st[1], st[2], st[3], rm, rv, nbt)
-    K.conv_fwd(x_nhwc, w2d, g, y, bn=bn, tile=tile)
+    K.conv_fwd(x_nhwc, w2d, g, y, bn=bn, tile=tile, inlaunch=inlaunch)
     return y, st, rm, rv, nbt, ws
 
 
+@pytest.mark.parametrize("inlaunch", [True, False])
 @pytest.mark.parametrize("tile", [None, (-128, 128), (128, 64), (64, 128), (-128, 64)])
-def test_conv_fwd_inlaunch_bn_finalize(tile):
-    """BatchNorm statistics finalized INSIDE the conv forward launch (last-arriving workgroups,
-    f64, shifted partials): mean / invstd / scale / shift / running stats / counter against float64
+def test_conv_fwd_inlaunch_bn_finalize(tile, inlaunch):
+    """BatchNorm statistics of the conv forward -- finalized INSIDE the conv launch (last-arriving
+    workgroups, f64, shifted partials) or by the default two follow-up launches (parallel f64
+    prereduce + finalize): mean / invstd / scale / shift / running stats / counter against float64
     statistics of the stored output, on a ragged shape with several column tiles and chunks;
     bit-identical on a second launch (fixed summation order), counters left at zero."""
     K = _k()
@@ -185,8 +187,10 @@ def test_conv_fwd_inlaunch_bn_finalize(tile):
     x = (torch.randn(Nb, H, H, Cin, device=DEV) + 0.2).to(dtype)
     w = (torch.randn(Cout, 3, 3, Cin, device=DEV) / 24).to(dtype)
     gamma, beta = torch.rand(Cout, device=DEV) + 0.5, torch.randn(Cout, device=DEV)
-    y, st, rm, rv, nbt, ws = _conv_bn_inlaunch(K, x, w.view(Cout, -1), g, dtype, gamma, beta, tile)
-    y2, st2, _, _, _, _ = _conv_bn_inlaunch(K, x, w.view(Cout, -1), g, dtype, gamma, beta, tile, ws)
+    y, st, rm, rv, nbt, ws = _conv_bn_inlaunch(K, x, w.view(Cout, -1), g, dtype, gamma, beta, tile,
+                                               inlaunch=inlaunch)
+    y2, st2, _, _, _, _ = _conv_bn_inlaunch(K, x, w.view(Cout, -1), g, dtype, gamma, beta, tile, ws,
+                                            inlaunch=inlaunch)
     torch.cuda.synchronize()
     yd = y.double().reshape(-1, Cout)
     n = yd.shape[0]
@@ -202,8 +206,45 @@ def test_conv_fwd_inlaunch_bn_finalize(tile):
     assert int(ws.counters(64).abs().sum().item()) == 0
 
 
+@pytest.mark.parametrize("C,T", [(64, 3), (192, 700), (512, 97), (1028, 40), (2048, 600)])
+def test_bn_finalize_partials_channel_widths(C, T):
+    """The default forward finalize (parallel f64 prereduce over S slabs + per-channel finalize)
+    on synthetic shifted partials part[T][3][C] for every channel-width regime of the prereduce's
+    (channel quad x slab lane) decomposition, including C/4 > 256 (several quad passes) and a
+    ragged last tile, against a float64 combination."""
+    K = _k()
+    torch.manual_seed(C + T)
+    bm = 128
+    M = T * bm - 37
+    rows = torch.full((T,), float(bm), dtype=torch.float64)
+    rows[-1] = M - (T - 1) * bm
+    shift = torch.randn(T, C, dtype=torch.float64) * 3
+    s1 = torch.randn(T, C, dtype=torch.float64) * 5
+    s2 = torch.rand(T, C, dtype=torch.float64) * 200 + s1 ** 2 / rows[:, None]
+    part = torch.stack([s1, s2, shift], 1).float()
+    p64 = part.double()
+    r = rows[:, None]
+    tot1 = (r * p64[:, 2] + p64[:, 0]).sum(0)
+    tot2 = (p64[:, 1] + p64[:, 2] * (2 * p64[:, 0] + r * p64[:, 2])).sum(0)
+    mean = tot1 / M
+    var = (tot2 / M - mean ** 2).clamp_min(0)
+    ws = K.Workspace(DEV)
+    gamma, beta = torch.rand(C, device=DEV) + 0.5, torch.randn(C, device=DEV)
+    st = torch.zeros(4, C, device=DEV)
+    rm, rv = torch.zeros(C, device=DEV), torch.ones(C, device=DEV)
+    nbt = torch.zeros(1, dtype=torch.long, device=DEV)
+    bn = K.BnStats(ws, gamma, beta, 1e-5, 0.1, st[0], st[1], st[2], st[3], rm, rv, nbt,
+                   update_running=True)
+    K.bn_finalize_partials(part.to(DEV).contiguous(), T, C, bm, M, bn)
+    torch.cuda.synchronize()
+    torch.testing.assert_close(st[0].double().cpu(), mean, rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(st[1].double().cpu(), 1 / torch.sqrt(var + 1e-5), rtol=1e-5, atol=1e-6)
+    assert int(nbt.item()) == 1
+
+
+@pytest.mark.parametrize("inlaunch", [False, True])
 @pytest.mark.parametrize("dtype,std", [(torch.float32, 0.01), (torch.bfloat16, 0.08)])
-def test_bn_statistics_large_offset_layer1_scale(dtype, std):
+def test_bn_statistics_large_offset_layer1_scale(dtype, std, inlaunch):
     """Layer-1 scale (1.25 M rows x 64 channels, batch 400 at 56x56) with mean ~10 and std ~0.01
     (bf16: 0.08, so the stored values -- 1/16 apart at 10 -- still vary): E[y^2] - E[y]^2 from
     f32 partial sums would cancel catastrophically; the shifted per-tile sums + f64 combination
@@ -217,7 +258,8 @@ def test_bn_statistics_large_offset_layer1_scale(dtype, std):
     w = torch.randn(Cout, Cin, device=DEV) * std / 8
     w[:, 0] = 10.0 + torch.rand(Cout, device=DEV)    # y_c ~ 10..11 + N(0, std^2)
     gamma, beta = torch.ones(Cout, device=DEV), torch.zeros(Cout, device=DEV)
-    y, st, rm, rv, nbt, _ = _conv_bn_inlaunch(K, x.to(dtype), w.to(dtype), g, dtype, gamma, beta)
+    y, st, rm, rv, nbt, _ = _conv_bn_inlaunch(K, x.to(dtype), w.to(dtype), g, dtype, gamma, beta,
+                                              inlaunch=inlaunch)
     torch.cuda.synchronize()
     yd = y.double().reshape(-1, Cout)
     mean, var = yd.mean(0), yd.var(0, unbiased=False)
