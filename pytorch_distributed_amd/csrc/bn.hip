@@ -65,9 +65,8 @@ __device__ __forceinline__ void tree_reduce2(double (&red)[2][64][17], int g, in
 }
 
 // ------------------------------------------------------------------ forward finalize
-// From f64 totals tot[2][C] = (sum y, sum y^2) -- the in-launch statistics of the conv forward
-// (conv_gemm.hip bn_stats_finalize, fin_mode 1), after the SyncBatchNorm all-reduce. The
-// single-process path finalizes inside the conv launch itself.
+// From f64 totals tot[2][C] = (sum y, sum y^2) of the conv forward (bn_fwd_stats with a totals
+// buffer), after the SyncBatchNorm all-reduce.
 __global__ __launch_bounds__(256) void bn_finalize_tot_kernel(
     const double* __restrict__ tot, int C, double count, const float* __restrict__ gamma,
     const float* __restrict__ beta, float eps, float momentum, float* __restrict__ mean_out,
@@ -94,97 +93,188 @@ __global__ __launch_bounds__(256) void bn_finalize_tot_kernel(
   if (blockIdx.x == 0 && threadIdx.x == 0 && update_running && nbt) *nbt += 1;
 }
 
-// Forward BatchNorm statistics from the conv epilogue's shifted per-tile partials
-// part[T][3][C] = (sum(y-s), sum((y-s)^2), s) over tiles of `bm` rows (the last one ragged), in
-// two launches: bn_fwd_prereduce (S blocks, each converting a contiguous range of tiles to f64
-// (sum y, sum y^2) for every channel: 16-B loads, (channel quad x slab lane) threads, fixed-order
-// lane combine) -> bn_finalize_slabs (f64 [S][2][C] -> coefficients + running statistics).
-__global__ __launch_bounds__(256) void bn_fwd_prereduce_kernel(const float* __restrict__ part,
-                                                               int T, int C, int bm, int M, int S,
-                                                               double* __restrict__ out) {
-  __shared__ double red[2][1024];   // [q][lane * Q4 + quad] (Q4 * SL <= 256 -> <= 1024 doubles)
-  const int Q4 = C >> 2;
-  const int SL = Q4 >= 256 ? 1 : 256 / Q4;
-  const int t0 = (int)((long long)blockIdx.x * T / S), t1 = (int)((long long)(blockIdx.x + 1) * T / S);
-  for (int qb = 0; qb < Q4; qb += 256 / SL) {
-    const int quad = qb + (int)threadIdx.x % (256 / SL), lane = (int)threadIdx.x / (256 / SL);
-    double a[4] = {0.0, 0.0, 0.0, 0.0}, b[4] = {0.0, 0.0, 0.0, 0.0};
-    if (quad < Q4) {
-      for (int t = t0 + lane; t < t1; t += SL) {
-        const float* pt = part + (size_t)t * 3 * C + quad * 4;
-        const f32x4 d0 = *reinterpret_cast<const f32x4*>(pt);
-        const f32x4 d1 = *reinterpret_cast<const f32x4*>(pt + C);
-        const f32x4 sh = *reinterpret_cast<const f32x4*>(pt + 2 * C);
-        const double rows = (double)min(bm, M - t * bm);
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const double s_ = sh[e], x = d0[e];
-          a[e] += rows * s_ + x;
-          b[e] += (double)d1[e] + s_ * (2.0 * x + rows * s_);
-        }
-      }
-    }
-    __syncthreads();
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      red[0][threadIdx.x * 4 + e] = a[e];
-      red[1][threadIdx.x * 4 + e] = b[e];
-    }
-    __syncthreads();
-    // v < 4 * (256 / SL): column (qb * 4 + v) -- sum the SL lanes in order
-    const int W = 256 / SL;
-    for (int v = threadIdx.x; v < 4 * W; v += 256) {
-      const int qi = v >> 2, e = v & 3, col = (qb + qi) * 4 + e;
-      if (qb + qi < Q4) {
-        double sa = 0.0, sb = 0.0;
-        for (int l = 0; l < SL; ++l) {
-          sa += red[0][(l * W + qi) * 4 + e];
-          sb += red[1][(l * W + qi) * 4 + e];
-        }
-        out[((size_t)blockIdx.x * 2) * C + col] = sa;
-        out[((size_t)blockIdx.x * 2 + 1) * C + col] = sb;
-      }
-    }
-  }
+// BatchNorm statistics from per-tile partial sums, finalized in ONE launch (no separate
+// reduce / finalize launches, no float atomics, deterministic):
+//   KIND 0 (forward): the conv epilogue's SHIFTED partials part[T][3][C] = (sum(y-s), sum((y-s)^2),
+//          s) over tiles of `bm` rows (the last one ragged) -> mean / invstd / scale / shift /
+//          running statistics (or, SyncBatchNorm, f64 totals for the all-reduce);
+//   KIND 1 (backward): the dgrad epilogue's partials part[T][NQ][C] = (sum dz, sum dz*y
+//          [, sum dz*y2]) -> gamma / beta gradients + apply coefficients k of each BN branch.
+// Block (s, g) reduces tiles [s*T/S, (s+1)*T/S) of channel group g (CG = min(C, 256) channels) to
+// an f64 slab -- 16-B loads, (channel quad x slab lane) threads, fixed-order lane combine -- and
+// publishes it write-through (sc1 stores, vmcnt(0), barrier, agent-scope arrival counter); the
+// group's last arriving block (agent acquire) sums the S slabs in slab order and finalizes.
+struct BnFwdOut {  // mirrors ops/ext.py BnFwdOut
+  const float* gamma; const float* beta;
+  float eps, momentum;
+  float* mean; float* invstd; float* scale; float* shift;
+  float* rmean; float* rvar; long long* nbt;
+  int update;
+  double* tot;   // non-null: f64 totals [2][C] instead of the finalize (bn_finalize_tot after)
+};
+
+struct BnBwdOut {  // mirrors ops/ext.py BnBwdOut; branch b = 0: BN of y, 1: shortcut BN of y2
+  float count, gscale;
+  int accumulate;
+  const float* gamma[2]; const float* mean[2]; const float* invstd[2];
+  float* dgamma[2]; float* dbeta[2];
+  float* k;      // [NQ-1][3][C]: dy_b = k0*dz + k1*y_b + k2
+};
+
+__device__ __forceinline__ void st_wt(double* q, double v) {   // write-through (sc1) store
+  __hip_atomic_store(q, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// f64 slabs [S][2][C] (sum y, sum y^2) -> mean, invstd, scale, shift, running stats. One block =
-// 16 channels x 64 slab lanes, fixed-shape tree: deterministic.
-__global__ __launch_bounds__(1024) void bn_finalize_slabs_kernel(
-    const double* __restrict__ slabs, int S, int C, double count, const float* __restrict__ gamma,
-    const float* __restrict__ beta, float eps, float momentum, float* __restrict__ mean_out,
-    float* __restrict__ invstd_out, float* __restrict__ scale, float* __restrict__ shift,
-    float* __restrict__ run_mean, float* __restrict__ run_var, long long* __restrict__ nbt,
-    int update_running) {
-  __shared__ double red[2][64][17];
-  const int cl = threadIdx.x & 15, g = threadIdx.x >> 4;
-  const int c = blockIdx.x * 16 + cl;
-  double s1 = 0.0, s2 = 0.0;
-  if (c < C)
-    for (int t = g; t < S; t += 64) {
-      s1 += slabs[((size_t)t * 2) * C + c];
-      s2 += slabs[((size_t)t * 2 + 1) * C + c];
+template <int KIND, int NQ, class Out>
+__global__ __launch_bounds__(256) void bn_stats_kernel(const float* __restrict__ part, int T, int C,
+                                                       int bm, int M, int CG,
+                                                       double* __restrict__ slabs,
+                                                       int* __restrict__ cnt, Out o) {
+  __shared__ double red[NQ][1024];   // [q][(lane * Q + quad) * 4 + e], then [q][column]
+  __shared__ int flag;
+  const int S = gridDim.x, s = blockIdx.x, g = blockIdx.y, tid = threadIdx.x;
+  const int Q = CG >> 2, SL = 256 / Q;
+  const int quad = tid % Q, lane = tid / Q;
+  const int c = g * CG + quad * 4;
+  const bool act = lane < SL && c < C;
+  // fixed-order sum over the SL lanes of each column v < CG of this group, into red[q][v]
+  auto combine = [&](const double (&a)[NQ][4]) __attribute__((always_inline)) {
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < NQ; ++q)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) red[q][tid * 4 + e] = a[q][e];
+    __syncthreads();
+    double sum[NQ];
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) sum[q] = 0.0;
+    if (tid < CG) {
+      const int qi = tid >> 2, e = tid & 3;
+      for (int l = 0; l < SL; ++l)
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) sum[q] += red[q][(l * Q + qi) * 4 + e];
     }
-  red[0][g][cl] = s1;
-  red[1][g][cl] = s2;
-  tree_reduce2(red, g, cl);
-  if (g == 0 && c < C) {
-    const double mean = red[0][0][cl] / count;
-    double var = red[1][0][cl] / count - mean * mean;
-    if (var < 0.0) var = 0.0;
-    const float inv = (float)(1.0 / sqrt(var + (double)eps));
-    const float sc = gamma[c] * inv;
-    mean_out[c] = (float)mean;
-    invstd_out[c] = inv;
-    scale[c] = sc;
-    shift[c] = beta[c] - (float)mean * sc;
-    if (update_running) {
-      const double unb = count > 1.0 ? var * count / (count - 1.0) : var;
-      run_mean[c] = (1.f - momentum) * run_mean[c] + momentum * (float)mean;
-      run_var[c] = (1.f - momentum) * run_var[c] + momentum * (float)unb;
+    __syncthreads();
+    if (tid < CG)
+#pragma unroll
+      for (int q = 0; q < NQ; ++q) red[q][tid] = sum[q];
+    __syncthreads();
+  };
+  constexpr int PQ = KIND == 0 ? 3 : NQ;   // partial rows per tile
+  {  // level 1: this block's tiles -> slab s
+    double a[NQ][4];
+#pragma unroll
+    for (int q = 0; q < NQ; ++q)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) a[q][e] = 0.0;
+    const int t0 = (int)((long long)s * T / S), t1 = (int)((long long)(s + 1) * T / S);
+    if (act) {
+#pragma unroll 2
+      for (int t = t0 + lane; t < t1; t += SL) {
+        const float* pt = part + (size_t)t * PQ * C + c;
+        f32x4 d[PQ];
+#pragma unroll
+        for (int q = 0; q < PQ; ++q) d[q] = *reinterpret_cast<const f32x4*>(pt + q * C);
+        if constexpr (KIND == 0) {
+          const double rows = (double)min(bm, M - t * bm);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const double s_ = d[2][e], x = d[0][e];
+            a[0][e] += rows * s_ + x;
+            a[1][e] += (double)d[1][e] + s_ * (2.0 * x + rows * s_);
+          }
+        } else {
+#pragma unroll
+          for (int q = 0; q < NQ; ++q)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) a[q][e] += (double)d[q][e];
+        }
+      }
+    }
+    combine(a);
+    const int col = g * CG + tid;
+    if (tid < CG && col < C)
+#pragma unroll
+      for (int q = 0; q < NQ; ++q) st_wt(slabs + ((size_t)s * NQ + q) * C + col, red[q][tid]);
+  }
+  // arrival: this block's slab stores landed (vmcnt(0) in every wave), then the group counter
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (tid == 0) {
+    const int old = __hip_atomic_fetch_add(cnt + g, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    flag = old == S - 1;
+  }
+  __syncthreads();
+  if (!flag) return;
+  if (tid == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __hip_atomic_store(cnt + g, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // reset
+  }
+  __syncthreads();
+  {  // level 2 (the group's last arriver): the S slabs, in slab order per lane
+    double a[NQ][4];
+#pragma unroll
+    for (int q = 0; q < NQ; ++q)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) a[q][e] = 0.0;
+    if (act)
+      for (int t = lane; t < S; t += SL) {
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) {
+          const double* p0 = slabs + ((size_t)t * NQ + q) * C + c;
+          const f64x2 x0 = *reinterpret_cast<const f64x2*>(p0);
+          const f64x2 x1 = *reinterpret_cast<const f64x2*>(p0 + 2);
+          a[q][0] += x0[0]; a[q][1] += x0[1]; a[q][2] += x1[0]; a[q][3] += x1[1];
+        }
+      }
+    combine(a);
+  }
+  const int col = g * CG + tid;
+  if (tid < CG && col < C) {
+    if constexpr (KIND == 0) {
+      const double sx = red[0][tid], sxx = red[1][tid];
+      if (o.tot) {
+        o.tot[col] = sx;
+        o.tot[C + col] = sxx;
+      } else {
+        const double count = (double)M;
+        const double mean = sx / count;
+        double var = sxx / count - mean * mean;
+        if (var < 0.0) var = 0.0;
+        const float inv = (float)(1.0 / sqrt(var + (double)o.eps));
+        const float sc = o.gamma[col] * inv;
+        o.mean[col] = (float)mean;
+        o.invstd[col] = inv;
+        o.scale[col] = sc;
+        o.shift[col] = o.beta[col] - (float)mean * sc;
+        if (o.update) {
+          const double unb = count > 1.0 ? var * count / (count - 1.0) : var;
+          o.rmean[col] = (1.f - o.momentum) * o.rmean[col] + o.momentum * (float)mean;
+          o.rvar[col] = (1.f - o.momentum) * o.rvar[col] + o.momentum * (float)unb;
+        }
+      }
+    } else {
+      const double count = o.count, gs = o.gscale, sdz = red[0][tid];
+#pragma unroll
+      for (int b = 0; b < NQ - 1; ++b) {   // constant member indices (no dynamic param indexing)
+        const double mu = o.mean[b][col], is = o.invstd[b][col], ga = o.gamma[b][col];
+        const double sdzx = (red[1 + b][tid] - mu * sdz) * is;   // sum dz * xhat
+        float* dg = o.dgamma[b];
+        float* db = o.dbeta[b];
+        dg[col] = (float)(sdzx * gs) + (o.accumulate ? dg[col] : 0.f);
+        db[col] = (float)(sdz * gs) + (o.accumulate ? db[col] : 0.f);
+        const double ak = ga * is;
+        const double kk2 = -ak * is * sdzx / count;
+        float* k = o.k + (size_t)b * 3 * C;
+        k[col] = (float)ak;
+        k[C + col] = (float)kk2;
+        k[2 * C + col] = (float)(-ak * sdz / count - kk2 * mu);
+      }
     }
   }
-  if (blockIdx.x == 0 && threadIdx.x == 0 && update_running && nbt) *nbt += 1;
+  if constexpr (KIND == 0)
+    if (g == 0 && tid == 0 && !o.tot && o.update && o.nbt) *o.nbt += 1;
 }
 
 // eval-mode scale/shift from running statistics
@@ -797,20 +887,29 @@ int pda_bn_finalize_tot(const double* tot, int C, double count, const float* gam
   return (int)hipGetLastError();
 }
 
-int pda_bn_fwd_prereduce(const float* part, int T, int C, int bm, int M, int S, double* out,
-                         hipStream_t st) {
-  if ((C & 3) || S <= 0 || S > T) return -2;
-  hipLaunchKernelGGL(bn_fwd_prereduce_kernel, dim3(S), dim3(256), 0, st, part, T, C, bm, M, S, out);
+// Partial statistics -> BatchNorm coefficients in one launch (bn_stats_kernel). slabs: f64 >=
+// S * nq * C; cnt: int32 >= ceil(C / 256), zero (and left zero). Returns -2 on a bad shape.
+int pda_bn_fwd_stats(const float* part, int T, int C, int bm, int M, int S, double* slabs, int* cnt,
+                     const BnFwdOut* o, hipStream_t st) {
+  if ((C & 3) || S <= 0 || S > T || !o || !cnt || !slabs) return -2;
+  const int CG = C < 256 ? C : 256;
+  hipLaunchKernelGGL((bn_stats_kernel<0, 2, BnFwdOut>), dim3(S, (C + CG - 1) / CG), dim3(256), 0, st,
+                     part, T, C, bm, M, CG, slabs, cnt, *o);
   return (int)hipGetLastError();
 }
 
-int pda_bn_finalize_slabs(const double* slabs, int S, int C, double count, const float* gamma,
-                          const float* beta, float eps, float momentum, float* mean, float* invstd,
-                          float* scale, float* shift, float* rmean, float* rvar, long long* nbt,
-                          int update_running, hipStream_t st) {
-  hipLaunchKernelGGL(bn_finalize_slabs_kernel, dim3((C + 15) / 16), dim3(1024), 0, st, slabs, S, C,
-                     count, gamma, beta, eps, momentum, mean, invstd, scale, shift, rmean, rvar, nbt,
-                     update_running);
+int pda_bn_bwd_stats(const float* part, int T, int nq, int C, int S, double* slabs, int* cnt,
+                     const BnBwdOut* o, hipStream_t st) {
+  if ((C & 3) || S <= 0 || S > T || !o || !cnt || !slabs || !o->k || (nq != 2 && nq != 3))
+    return -2;
+  const int CG = C < 256 ? C : 256;
+  const dim3 grid(S, (C + CG - 1) / CG);
+  if (nq == 2)
+    hipLaunchKernelGGL((bn_stats_kernel<1, 2, BnBwdOut>), grid, dim3(256), 0, st, part, T, C, 0, 0, CG,
+                       slabs, cnt, *o);
+  else
+    hipLaunchKernelGGL((bn_stats_kernel<1, 3, BnBwdOut>), grid, dim3(256), 0, st, part, T, C, 0, 0, CG,
+                       slabs, cnt, *o);
   return (int)hipGetLastError();
 }
 

@@ -67,268 +67,10 @@ struct ConvParams {
   const void* eg2;                 // optional second gradient summed into dA
   const uint8_t* emask;            // mode 3: forward ReLU bitmask of a (1 byte per 8 elements)
   float* epart;                    // [ncls*tiles_m][enq][N] partial sums
-  // FWD BatchNorm statistics (stats != nullptr): per-M-tile SHIFTED partials
+  // FWD BatchNorm statistics (stats != nullptr) are per-M-tile SHIFTED partials
   // stats[tile][3][N] = (sum(y - s), sum((y - s)^2), s), s = the tile's first row (no f32
-  // cancellation when |mean| >> std). fin_mode > 0: the last-arriving workgroups combine them in
-  // f64 inside this launch (bn_stats_finalize): 1 = f64 totals only (SyncBN), 2 = full finalize.
-  int fin_mode;
-  int fin_ch;                      // M-tiles per level-1 chunk
-  double* fin_chunk;               // [G1][2][N] chunk sums (sum y, sum y^2)
-  double* fin_tot;                 // [2][N] totals (fin_mode 1)
-  int* fin_cnt;                    // [G1 * tiles_n + tiles_n] arrival counters, zero between launches
-  const float* fin_gamma; const float* fin_beta;
-  float fin_eps, fin_momentum;
-  float* fin_mean; float* fin_invstd; float* fin_scale; float* fin_shift;
-  float* fin_rmean; float* fin_rvar; long long* fin_nbt;
-  int fin_update;
-  // DGRAD BatchNorm-backward finalize inside the launch (bf_mode 1; emode >= 0): index [b] =
-  // 0 for the BN of y, 1 for the shortcut BN of y2 (emode 2); bf_k = [b][3][N] coefficients
-  int bf_mode, bf_ch, bf_accumulate;
-  double* bf_chunk;
-  int* bf_cnt;
-  float bf_count, bf_gscale;
-  const float* bf_gamma[2]; const float* bf_mean[2]; const float* bf_invstd[2];
-  float* bf_dgamma[2]; float* bf_dbeta[2];
-  float* bf_k;
+  // cancellation when |mean| >> std); bn.hip bn_fwd_stats combines and finalizes them.
 };
-
-// ---------------------------------------------------------------- in-launch BN statistics
-// sc1 (write-through / L1-bypassing) accesses for the cross-workgroup hand-off of partial sums
-// (MI355X_MICROARCH.md, inter-workgroup visibility: sc1 stores -> vmcnt(0) -> barrier -> relaxed
-// agent-scope arrival counter; the last arriver: agent acquire -> barrier -> loads).
-template <typename T>
-__device__ __forceinline__ T ld_sc1(const T* q) {
-  return __hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-template <typename T>
-__device__ __forceinline__ void st_sc1(T* q, T v) {
-  __hip_atomic_store(q, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-// Two-level in-launch combine of per-slab partial sums (deterministic, no workgroup ever waits).
-// Every workgroup that wrote slab `slab` (write-through stores) for column tile tn arrives on its
-// chunk's counter; the LAST arriver of a chunk of `ch` consecutive slabs combines them in f64
-// into chunkbuf [G1][NQ][N]; the last chunk-combiner of the column tile sums the chunks and
-// returns true with the column tile's totals in LDS, red[q * BN + c] (f64, at smem + 64).
-// load_add(t, n, acc) adds slab t's contribution to columns n..n+3 into acc[NQ][4]. Both levels
-// spread the work as (slab lane, column quad) with 16-B loads -- many loads in flight per thread
-// -- and combine the slab lanes in a fixed order: sums depend only on slab / chunk indices.
-// Counters are reset by their last arrivers (zero between launches).
-// Level-1 arrival of a workgroup whose partial sums are stored (write-through) by the waves of
-// threads < BN: returns true (block-uniform) in the last arriver of the chunk, after its agent
-// acquire. `flag` is a word of LDS the caller does not need meanwhile.
-template <int BN>
-__device__ __forceinline__ bool inlaunch_arrive(int* flag, int slab, int nslab, int ch, int tn,
-                                                int tiles_n, int* cnt) {
-  const int tid = threadIdx.x;
-  if (tid < BN) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's stores landed
-  __syncthreads();                                                   // ... and every wave's
-  const int chunk = slab / ch, c0 = chunk * ch;
-  const int nin = min(ch, nslab - c0);
-  if (tid == 0) {
-    const int old = __hip_atomic_fetch_add(cnt + chunk * tiles_n + tn, 1, __ATOMIC_RELAXED,
-                                           __HIP_MEMORY_SCOPE_AGENT);
-    flag[0] = old == nin - 1;
-  }
-  __syncthreads();
-  const bool last = flag[0] != 0;
-  if (last && tid == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  }
-  __syncthreads();
-  return last;
-}
-
-// Level-1 combine (by the chunk's last arriver), level-2 arrival and combine: returns true in the
-// column tile's final reducer with the totals at red[q * BN + c] (f64, smem + 64).
-template <int BN, int NQ, class LoadAdd>
-__device__ __forceinline__ bool inlaunch_finish(char* smem, int slab, int nslab, int ch, int N,
-                                                int n0, int tn, int tiles_n, int* cnt,
-                                                double* chunkbuf, LoadAdd load_add) {
-  constexpr int Q4 = BN / 4, SL = NT / Q4;
-  const int tid = threadIdx.x, quad = tid % Q4, sl = tid / Q4;
-  const int nq4 = n0 + quad * 4;
-  int* flag = reinterpret_cast<int*>(smem);
-  double* red = reinterpret_cast<double*>(smem + 64);   // [SL][NQ][BN]
-  const int chunk = slab / ch, c0 = chunk * ch;
-  const int nin = min(ch, nslab - c0);
-  const int G1 = (nslab + ch - 1) / ch;
-  int* cnt1 = cnt + chunk * tiles_n + tn;
-  int* cnt2 = cnt + G1 * tiles_n + tn;
-  auto combine_lanes = [&](double (&acc)[NQ][4]) __attribute__((always_inline)) {   // red[0][q][c] = fixed-order lane sum
-#pragma unroll
-    for (int q = 0; q < NQ; ++q)
-#pragma unroll
-      for (int e = 0; e < 4; ++e) red[(sl * NQ + q) * BN + quad * 4 + e] = acc[q][e];
-    __syncthreads();
-    for (int v = tid; v < NQ * BN; v += NT) {
-      double a = 0.0;
-      for (int l = 0; l < SL; ++l) a += red[l * NQ * BN + v];
-      red[v] = a;   // thread v owns slot v in every lane: in place
-    }
-    __syncthreads();
-  };
-  {  // level 1: the chunk's slabs
-    double acc[NQ][4];
-#pragma unroll
-    for (int q = 0; q < NQ; ++q)
-#pragma unroll
-      for (int e = 0; e < 4; ++e) acc[q][e] = 0.0;
-    if (nq4 < N)
-      for (int t = c0 + sl; t < c0 + nin; t += SL) load_add(t, nq4, acc);
-    combine_lanes(acc);
-    for (int v = tid; v < NQ * BN; v += NT) {
-      const int q = v / BN, n = n0 + (v - q * BN);
-      if (n < N) st_sc1(chunkbuf + ((size_t)chunk * NQ + q) * N + n, red[v]);
-    }
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (tid == 0) {
-    __hip_atomic_store(cnt1, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // chunk complete
-    const int old = __hip_atomic_fetch_add(cnt2, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    flag[0] = old == G1 - 1;
-  }
-  __syncthreads();
-  if (!flag[0]) return false;
-  if (tid == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __hip_atomic_store(cnt2, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-  __syncthreads();
-  {  // level 2: the column tile's chunks
-    double acc[NQ][4];
-#pragma unroll
-    for (int q = 0; q < NQ; ++q)
-#pragma unroll
-      for (int e = 0; e < 4; ++e) acc[q][e] = 0.0;
-    if (nq4 < N)
-      for (int g = sl; g < G1; g += SL) {
-#pragma unroll
-        for (int q = 0; q < NQ; ++q) {
-          const double* src = chunkbuf + ((size_t)g * NQ + q) * N + nq4;
-          const f64x2 a = *reinterpret_cast<const f64x2*>(src);
-          const f64x2 b = *reinterpret_cast<const f64x2*>(src + 2);
-          acc[q][0] += a[0]; acc[q][1] += a[1]; acc[q][2] += b[0]; acc[q][3] += b[1];
-        }
-      }
-    combine_lanes(acc);
-  }
-  return true;
-}
-
-template <int BN, int NQ, class LoadAdd>
-__device__ __forceinline__ bool inlaunch_combine(char* smem, int slab, int nslab, int ch, int N,
-                                                 int n0, int tn, int tiles_n, int* cnt,
-                                                 double* chunkbuf, LoadAdd load_add) {
-  if (!inlaunch_arrive<BN>(reinterpret_cast<int*>(smem), slab, nslab, ch, tn, tiles_n, cnt))
-    return false;
-  return inlaunch_finish<BN, NQ>(smem, slab, nslab, ch, N, n0, tn, tiles_n, cnt, chunkbuf,
-                                 load_add);
-}
-
-// Forward BatchNorm statistics from the conv epilogue's shifted partials (ConvParams fin_*).
-template <int BM, int BN, class PP>
-__device__ __forceinline__ void bn_stats_finalize(PP& p, char* smem, int tm, int tn, int tiles_m,
-                                  int tiles_n, int n0, bool arrived = false) {
-  const float* stats = p.stats;   // (lambdas capture plain values, never the kernel argument)
-  const int N = p.N, M = p.M;
-  auto load_add = [stats, N, M](int t, int n, double (&acc)[2][4]) {
-    const float* pt = stats + (size_t)t * 3 * N + n;
-    const f32x4 d0 = *reinterpret_cast<const f32x4*>(pt);
-    const f32x4 d1 = *reinterpret_cast<const f32x4*>(pt + N);
-    const f32x4 sh = *reinterpret_cast<const f32x4*>(pt + 2 * N);
-    const double rows = (double)min(BM, M - t * BM);
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const double s_ = sh[e], a = d0[e];
-      acc[0][e] += rows * s_ + a;
-      acc[1][e] += (double)d1[e] + s_ * (2.0 * a + rows * s_);
-    }
-  };
-  if (arrived ? !inlaunch_finish<BN, 2>(smem, tm, tiles_m, p.fin_ch, p.N, n0, tn, tiles_n,
-                                        p.fin_cnt, p.fin_chunk, load_add)
-              : !inlaunch_combine<BN, 2>(smem, tm, tiles_m, p.fin_ch, p.N, n0, tn, tiles_n,
-                                         p.fin_cnt, p.fin_chunk, load_add))
-    return;
-  const double* tot = reinterpret_cast<const double*>(smem + 64);
-  const int tid = threadIdx.x;
-  if (tid < BN && n0 + tid < p.N) {
-    const int c = n0 + tid;
-    const double sx = tot[tid], sxx = tot[BN + tid];
-    if (p.fin_mode == 1) {
-      p.fin_tot[c] = sx;
-      p.fin_tot[p.N + c] = sxx;
-    } else {
-      const double count = (double)p.M;
-      const double mean = sx / count;
-      double var = sxx / count - mean * mean;
-      if (var < 0.0) var = 0.0;
-      const float inv = (float)(1.0 / sqrt(var + (double)p.fin_eps));
-      const float sc = p.fin_gamma[c] * inv;
-      p.fin_mean[c] = (float)mean;
-      p.fin_invstd[c] = inv;
-      p.fin_scale[c] = sc;
-      p.fin_shift[c] = p.fin_beta[c] - (float)mean * sc;
-      if (p.fin_update) {
-        const float mo = p.fin_momentum;
-        const double unb = count > 1.0 ? var * count / (count - 1.0) : var;
-        p.fin_rmean[c] = (1.f - mo) * p.fin_rmean[c] + mo * (float)mean;
-        p.fin_rvar[c] = (1.f - mo) * p.fin_rvar[c] + mo * (float)unb;
-      }
-    }
-  }
-  if (tid == 0 && tn == 0 && p.fin_mode == 2 && p.fin_update && p.fin_nbt) *p.fin_nbt += 1;
-}
-
-// Backward BatchNorm finalize from the dgrad epilogue's partials [slab][NQ][N] (q0 = sum dz,
-// q1 = sum dz*y, q2 = sum dz*y2): gamma/beta gradients into the flat gradient buffer and the
-// apply coefficients dy = k1*dz + k2*y + k3 (branch 2, the shortcut BN: k4..k6 for y2).
-template <int BN, int NQ, class PP>
-__device__ __forceinline__ void bn_bwd_finalize_inlaunch(PP& p, char* smem, int slab, int nslab,
-                                         int tn, int tiles_n, int n0) {
-  const float* epart = p.epart;   // (lambdas capture plain values, never the kernel argument)
-  const int N = p.N;
-  auto load_add = [epart, N](int t, int n, double (&acc)[NQ][4]) {
-#pragma unroll
-    for (int q = 0; q < NQ; ++q) {
-      const f32x4 v = *reinterpret_cast<const f32x4*>(epart + ((size_t)t * NQ + q) * N + n);
-#pragma unroll
-      for (int e = 0; e < 4; ++e) acc[q][e] += (double)v[e];
-    }
-  };
-  if (!inlaunch_combine<BN, NQ>(smem, slab, nslab, p.bf_ch, p.N, n0, tn, tiles_n, p.bf_cnt,
-                                p.bf_chunk, load_add))
-    return;
-  const double* tot = reinterpret_cast<const double*>(smem + 64);
-  const int tid = threadIdx.x;
-  if (tid < BN && n0 + tid < p.N) {
-    // (constant member indices only: a dynamically indexed member array of the kernel argument
-    // makes the compiler copy the whole argument block to scratch)
-    const int c = n0 + tid, N = p.N;
-    const double count = p.bf_count, gs = p.bf_gscale, sdz = tot[tid];
-    const bool accum = p.bf_accumulate != 0;
-    auto branch = [=](double sdzy, const float* gam, const float* mean, const float* inv, float* dg,
-                      float* db, float* k) {
-      const double mu = mean[c], is = inv[c], ga = gam[c];
-      const double sdzx = (sdzy - mu * sdz) * is;   // sum dz * xhat
-      dg[c] = (float)(sdzx * gs) + (accum ? dg[c] : 0.f);
-      db[c] = (float)(sdz * gs) + (accum ? db[c] : 0.f);
-      const double a = ga * is;
-      const double kk2 = -a * is * sdzx / count;
-      k[c] = (float)a;
-      k[N + c] = (float)kk2;
-      k[2 * N + c] = (float)(-a * sdz / count - kk2 * mu);
-    };
-    branch(tot[BN + tid], p.bf_gamma[0], p.bf_mean[0], p.bf_invstd[0], p.bf_dgamma[0],
-           p.bf_dbeta[0], p.bf_k);
-    if constexpr (NQ == 3)
-      branch(tot[2 * BN + tid], p.bf_gamma[1], p.bf_mean[1], p.bf_invstd[1], p.bf_dgamma[1],
-             p.bf_dbeta[1], p.bf_k + 3 * (size_t)N);
-  }
-}
 
 // Scalar-f32 pair FMA for the operand prologue, which runs between MFMAs: there a packed
 // v_pk_fma_f32 costs far more issue time than two scalar v_fma_f32 (MI355X_MICROARCH.md, cycle
@@ -470,9 +212,8 @@ __global__ __launch_bounds__(NT, (conv_min_blocks<DT, BM, BN, STAGES>())) void c
   constexpr int BKE = 128 / ES;          // k per tile (one 128-B row)
   constexpr int A_BYTES = BM * 128, B_BYTES = BN * 128;
   constexpr int STAGE = A_BYTES + B_BYTES;
-  // epilogue partial-sum reduction [3][RG][BN] f32; the in-launch combine's [lanes][NQ][BN] f64
-  // (NT * 4 * 3 doubles) behind a 64-B flag word
-  constexpr int RED_BYTES = 3 * NT * 8 * 4 + 64;
+  // epilogue partial-sum reduction [3][RG][BN] f32
+  constexpr int RED_BYTES = 3 * NT * 8 * 4;
   // staged C tile of the epilogue; f32 stages it in two row halves (one per wave row), so the
   // epilogue needs no more LDS than the main loop and f32 tiles keep 3 resident blocks per CU
   constexpr int NH = F32 ? 2 : 1;
@@ -1135,26 +876,19 @@ __global__ __launch_bounds__(NT, (conv_min_blocks<DT, BM, BN, STAGES>())) void c
           }
           const int col = n0 + tid;
           if (col < p.N) {
-            if constexpr (SHIFTED) {   // (sum d, sum d^2, shift), write-through for the hand-off
+            if constexpr (SHIFTED) {   // (sum d, sum d^2, shift)
               float* dst = p.stats + (size_t)tm * 3 * p.N + col;
-              st_sc1(dst, a);
-              st_sc1(dst + p.N, b);
-              st_sc1(dst + 2 * p.N, red[2 * RG * BN + tid]);
-            } else {   // write-through: the in-launch finalize may read them from any XCD
+              dst[0] = a;
+              dst[p.N] = b;
+              dst[2 * p.N] = red[2 * RG * BN + tid];
+            } else {
               float* dst = p.epart;
               const size_t slab = (size_t)split * tiles_m + tm;
-              st_sc1(dst + (slab * NQ + 0) * p.N + col, a);
-              st_sc1(dst + (slab * NQ + 1) * p.N + col, b);
-              if constexpr (NQ > 2) st_sc1(dst + (slab * NQ + 2) * p.N + col, c2);
+              dst[(slab * NQ + 0) * p.N + col] = a;
+              dst[(slab * NQ + 1) * p.N + col] = b;
+              if constexpr (NQ > 2) dst[(slab * NQ + 2) * p.N + col] = c2;
             }
           }
-        }
-        if constexpr (SHIFTED) {
-          if (p.fin_mode > 0) bn_stats_finalize<BM, BN>(p, smem, tm, tn, tiles_m, tiles_n, n0);
-        } else if constexpr (PASS == DGRAD && MODE >= 0) {
-          if (p.bf_mode > 0)
-            bn_bwd_finalize_inlaunch<BN, NQ>(p, smem, split * tiles_m + tm, gridDim.y * tiles_m, tn,
-                                             tiles_n, n0);
         }
       }
     };
@@ -1304,16 +1038,6 @@ static void fill_geom(ConvParams& p, const ConvDesc& d) {
   p.dS = make_div(d.S);
 }
 
-struct BnFin {  // mirrors ops/ext.py BnFin
-  int mode, ch;
-  double* chunk; double* tot; int* cnt;
-  const float* gamma; const float* beta;
-  float eps, momentum;
-  float* mean; float* invstd; float* scale; float* shift;
-  float* rmean; float* rvar; long long* nbt;
-  int update;
-};
-
 extern "C" {
 
 int pda_conv_set_mfma(int mf) {
@@ -1323,10 +1047,10 @@ int pda_conv_set_mfma(int mf) {
 }
 
 // Y[M=Nb*Ho*Wo][Cout] = conv(X, W). W: [Cout][Kpad] 16-bit. stats: [ceil(M/bm)][3][Cout] shifted
-// partials or null; fin (with stats): BatchNorm statistics combined/finalized inside the launch.
+// partials or null.
 int pda_conv_fwd(const ConvDesc* d, const void* x, const void* w, int Kpad, void* y, int out_f32,
                  int out_pitch, const float* bias, float* stats, int relu, const float* pro_sc,
-                 const float* pro_sh, const BnFin* fin, int dt, int bm, int bn, hipStream_t st) {
+                 const float* pro_sh, int dt, int bm, int bn, hipStream_t st) {
   if (!fits32((long long)d->Nb * d->H * d->W * d->Cin, (long long)d->Cout * Kpad,
               (long long)d->Nb * d->Ho * d->Wo * d->Cout, dt) || d->R * d->S > 64)
     return -4;
@@ -1336,17 +1060,6 @@ int pda_conv_fwd(const ConvDesc* d, const void* x, const void* w, int Kpad, void
   p.a = x; p.b = w; p.out = y; p.stats = stats; p.bias = bias;
   p.M = d->Nb * d->Ho * d->Wo; p.N = d->Cout; p.Kpad = Kpad; p.K = Kpad;
   p.out_f32 = out_f32; p.relu = relu; p.out_pitch = out_pitch > 0 ? out_pitch : d->Cout;
-  if (fin && stats) {
-    if (fin->ch <= 0 || !fin->chunk || !fin->cnt || (fin->mode == 1 && !fin->tot) || (d->Cout & 3))
-      return -5;
-    p.fin_mode = fin->mode; p.fin_ch = fin->ch;
-    p.fin_chunk = fin->chunk; p.fin_tot = fin->tot; p.fin_cnt = fin->cnt;
-    p.fin_gamma = fin->gamma; p.fin_beta = fin->beta;
-    p.fin_eps = fin->eps; p.fin_momentum = fin->momentum;
-    p.fin_mean = fin->mean; p.fin_invstd = fin->invstd; p.fin_scale = fin->scale;
-    p.fin_shift = fin->shift; p.fin_rmean = fin->rmean; p.fin_rvar = fin->rvar;
-    p.fin_nbt = fin->nbt; p.fin_update = fin->update;
-  }
   const int abm = bm < 0 ? -bm : bm;
   const int tiles = ((p.M + abm - 1) / abm) * ((p.N + bn - 1) / bn);
   return dispatch<FWD>(dt, bm, bn, p, dim3(tiles, 1), st);
@@ -1359,13 +1072,6 @@ struct BnEpi {  // mirrors ops/ext.py BnEpi
   const void* y2; const float* sc2; const float* sh2;
   const void* g2; float* part;
   const void* mask;
-  // in-launch BN-backward finalize (fin_mode 1) -- see ConvParams bf_*
-  int fin_mode, fin_ch, accumulate;
-  double* chunk; int* cnt;
-  float count, gscale;
-  const float* gamma[2]; const float* mean[2]; const float* invstd[2];
-  float* dgamma[2]; float* dbeta[2];
-  float* k;
 };
 
 int pda_conv_dgrad(const ConvDesc* d, const void* dy, const void* w, void* dx, const BnEpi* epi,
@@ -1383,17 +1089,6 @@ int pda_conv_dgrad(const ConvDesc* d, const void* dy, const void* w, void* dx, c
     p.ey2 = epi->y2; p.esc2 = epi->sc2; p.esh2 = epi->sh2;
     p.eg2 = epi->g2; p.epart = epi->part;
     p.emask = (const uint8_t*)epi->mask;
-    if (epi->fin_mode > 0) {
-      if (epi->fin_ch <= 0 || !epi->chunk || !epi->cnt || !epi->k || (d->Cin & 3)) return -5;
-      p.bf_mode = epi->fin_mode; p.bf_ch = epi->fin_ch; p.bf_accumulate = epi->accumulate;
-      p.bf_chunk = epi->chunk; p.bf_cnt = epi->cnt;
-      p.bf_count = epi->count; p.bf_gscale = epi->gscale;
-      for (int b = 0; b < 2; ++b) {
-        p.bf_gamma[b] = epi->gamma[b]; p.bf_mean[b] = epi->mean[b]; p.bf_invstd[b] = epi->invstd[b];
-        p.bf_dgamma[b] = epi->dgamma[b]; p.bf_dbeta[b] = epi->dbeta[b];
-      }
-      p.bf_k = epi->k;
-    }
   }
   p.N = d->Cin; p.out_pitch = d->Cin;
   const int sd = d->stride;

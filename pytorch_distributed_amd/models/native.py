@@ -675,7 +675,7 @@ class NativeResNet(nn.Module):
                         N * H * W, C_)
         K.check(ext.lib().pda_bn_bwd_reduce(ext.C.byref(a), G, ext.dt_of(dz), ext.stream(dz.device)),
                 "bn_bwd_reduce")
-        return dz, part, G, nq, None
+        return dz, part, G, nq
 
     def _block_backward(self, b: Block, rec, tail, prev, acc):
         """Returns (dx_main, shortcut_grad, prev_tail) -- the last is the fused reduction of the
@@ -687,7 +687,7 @@ class NativeResNet(nn.Module):
         n = len(b.units)
         ul = b.units[-1]
         sl = rec[f"s{n - 1}"]
-        dz, part, G, nq, ktail = tail   # ktail: coefficients if the producing dgrad finalized
+        dz, part, G, nq = tail
         dy = self._empty(*ys[-1].shape)
         sc_ev = None
         if b.ds is not None:
@@ -696,7 +696,7 @@ class NativeResNet(nn.Module):
             K.bn_bwd_finish(ws, part, G, nq, ys[-1], sl[0], sl[1], self.gamma(ul), self.dgamma(ul),
                             self.dbeta(ul), dz, dy, y2=yd, mean2=sd[0], invstd2=sd[1],
                             gamma2=self.gamma(b.ds), dgamma2=self.dgamma(b.ds), dbeta2=self.dbeta(b.ds),
-                            dy2_out=dyd, accumulate=acc, k=ktail)
+                            dy2_out=dyd, accumulate=acc)
             # shortcut branch first: its dX is the second gradient source of the previous tail.
             # On the second stream its dgrad overlaps the conv3/conv2 chain; an event marks it for
             # the conv1 dgrad epilogue (or the stem) that consumes it
@@ -715,7 +715,7 @@ class NativeResNet(nn.Module):
                                                                     accumulate=acc), dyd, x)
         else:
             K.bn_bwd_finish(ws, part, G, nq, ys[-1], sl[0], sl[1], self.gamma(ul), self.dgamma(ul),
-                            self.dbeta(ul), dz, dy, accumulate=acc, k=ktail)
+                            self.dbeta(ul), dz, dy, accumulate=acc)
             shortcut_g = dz
         dx_main = None
         prev_tail = None
@@ -738,36 +738,22 @@ class NativeResNet(nn.Module):
                 up = b.units[j - 1]
                 sp = rec[f"s{j - 1}"]
                 Gp = K.dgrad_slabs(g, Nb)
-                # the dgrad's epilogue reduces AND (last-arriving workgroups) finalizes bn_{j-1}
-                fin = K.BnBwd(self.gamma(up), sp[0], sp[1], self.dgamma(up), self.dbeta(up),
-                              accumulate=acc)
-                epi, part_p, nq_p, kp = K.bn_epilogue(ws, Gp, ys[j - 1], sp[2], sp[3], fin=fin,
-                                                      tiles_n=K.dgrad_tiles_n(g, Nb))
+                # the dgrad's epilogue produces dz and the BN-backward partials of bn_{j-1}
+                epi, part_p, nq_p = K.bn_epilogue(ws, Gp, ys[j - 1], sp[2], sp[3])
                 K.conv_dgrad(dy, self.w16_ohwi(u), g, out, epi=epi)      # out = dz of bn_{j-1}
                 dyp = self._empty(*ys[j - 1].shape)
                 K.bn_bwd_finish(ws, part_p, Gp, nq_p, ys[j - 1], sp[0], sp[1], self.gamma(up),
-                                self.dgamma(up), self.dbeta(up), out, dyp, accumulate=acc, k=kp)
+                                self.dgamma(up), self.dbeta(up), out, dyp, accumulate=acc)
                 dy = dyp
             elif prev is not None:
                 pb, prec = prev
                 if sc_ev is not None:
                     cur.wait_event(sc_ev)
                 Gp = K.dgrad_slabs(g, Nb)
-                ulp = pb.units[-1]
-                slp = prec[f"s{len(pb.units) - 1}"]
-                if pb.ds is not None:
-                    sdp = prec["sd"]
-                    fin = K.BnBwd(self.gamma(ulp), slp[0], slp[1], self.dgamma(ulp), self.dbeta(ulp),
-                                  self.gamma(pb.ds), sdp[0], sdp[1], self.dgamma(pb.ds),
-                                  self.dbeta(pb.ds), accumulate=acc, k_name="bn_kt")
-                else:
-                    fin = K.BnBwd(self.gamma(ulp), slp[0], slp[1], self.dgamma(ulp), self.dbeta(ulp),
-                                  accumulate=acc, k_name="bn_kt")
-                epi, part_p, nq_p, kp = K.bn_epilogue(ws, Gp, g2=shortcut_g, fin=fin,
-                                                      tiles_n=K.dgrad_tiles_n(g, Nb),
-                                                      **self._tail_args(pb, prec, use_mask=True))
+                epi, part_p, nq_p = K.bn_epilogue(ws, Gp, g2=shortcut_g,
+                                                  **self._tail_args(pb, prec, use_mask=True))
                 K.conv_dgrad(dy, self.w16_ohwi(u), g, out, epi=epi)      # out = dz of prev tail
-                prev_tail = (out, part_p, Gp, nq_p, kp)
+                prev_tail = (out, part_p, Gp, nq_p)
             else:
                 K.conv_dgrad(dy, self.w16_ohwi(u), g, out)
                 dx_main = out

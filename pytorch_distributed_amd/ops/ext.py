@@ -15,7 +15,7 @@ from typing import Optional
 
 import torch
 
-__all__ = ["load", "available", "lib", "DT", "dt_of", "ConvDesc", "BwdArgs", "BnEpi", "BnFin",
+__all__ = ["load", "available", "lib", "DT", "dt_of", "ConvDesc", "BwdArgs", "BnEpi", "BnFwdOut", "BnBwdOut",
            "stream", "ptr"]
 
 _LIB: Optional[C.CDLL] = None
@@ -45,40 +45,39 @@ class BwdArgs(C.Structure):
 
 
 class BnEpi(C.Structure):
-    """dgrad epilogue = BatchNorm-backward reduction (+ optional in-launch finalize, fin_mode 1)."""
+    """dgrad epilogue = BatchNorm-backward reduction (csrc/conv_gemm.hip ConvParams e*)."""
     _fields_ = [("mode", C.c_int), ("nq", C.c_int),
                 ("y", C.c_void_p), ("sc", C.c_void_p), ("sh", C.c_void_p),
                 ("y2", C.c_void_p), ("sc2", C.c_void_p), ("sh2", C.c_void_p),
-                ("g2", C.c_void_p), ("part", C.c_void_p), ("mask", C.c_void_p),
-                ("fin_mode", C.c_int), ("fin_ch", C.c_int), ("accumulate", C.c_int),
-                ("chunk", C.c_void_p), ("cnt", C.c_void_p),
-                ("count", C.c_float), ("gscale", C.c_float),
-                ("gamma", C.c_void_p * 2), ("mean", C.c_void_p * 2), ("invstd", C.c_void_p * 2),
-                ("dgamma", C.c_void_p * 2), ("dbeta", C.c_void_p * 2),
-                ("k", C.c_void_p)]
+                ("g2", C.c_void_p), ("part", C.c_void_p), ("mask", C.c_void_p)]
 
 
-class BnFin(C.Structure):
-    """In-launch BatchNorm statistics of a conv forward (csrc/conv_gemm.hip bn_stats_finalize)."""
-    _fields_ = [("mode", C.c_int), ("ch", C.c_int),
-                ("chunk", C.c_void_p), ("tot", C.c_void_p), ("cnt", C.c_void_p),
-                ("gamma", C.c_void_p), ("beta", C.c_void_p),
+class BnFwdOut(C.Structure):
+    """Outputs of the one-launch BatchNorm forward statistics (csrc/bn.hip bn_fwd_stats)."""
+    _fields_ = [("gamma", C.c_void_p), ("beta", C.c_void_p),
                 ("eps", C.c_float), ("momentum", C.c_float),
                 ("mean", C.c_void_p), ("invstd", C.c_void_p), ("scale", C.c_void_p),
                 ("shift", C.c_void_p), ("rmean", C.c_void_p), ("rvar", C.c_void_p),
-                ("nbt", C.c_void_p), ("update", C.c_int)]
+                ("nbt", C.c_void_p), ("update", C.c_int), ("tot", C.c_void_p)]
+
+
+class BnBwdOut(C.Structure):
+    """Outputs of the one-launch BatchNorm backward finalize (csrc/bn.hip bn_stats_kernel<1>):
+    branch 0 = the BN of y, branch 1 = the shortcut BN of y2; k = [branches][3][C]."""
+    _fields_ = [("count", C.c_float), ("gscale", C.c_float), ("accumulate", C.c_int),
+                ("gamma", C.c_void_p * 2), ("mean", C.c_void_p * 2), ("invstd", C.c_void_p * 2),
+                ("dgamma", C.c_void_p * 2), ("dbeta", C.c_void_p * 2), ("k", C.c_void_p)]
 
 
 _V, _I, _F, _L, _U, _D = C.c_void_p, C.c_int, C.c_float, C.c_longlong, C.c_uint, C.c_double
 _SIGS = {
-    "pda_conv_fwd": [C.POINTER(ConvDesc), _V, _V, _I, _V, _I, _I, _V, _V, _I, _V, _V, C.POINTER(BnFin),
-                     _I, _I, _I, _V],
+    "pda_conv_fwd": [C.POINTER(ConvDesc), _V, _V, _I, _V, _I, _I, _V, _V, _I, _V, _V, _I, _I, _I, _V],
     "pda_conv_dgrad": [C.POINTER(ConvDesc), _V, _V, _V, C.POINTER(BnEpi), _I, _I, _I, _V],
     "pda_conv_set_mfma": [_I],
     "pda_conv_wgrad": [C.POINTER(ConvDesc), _V, _V, _V, _I, _I, _V, _V, _I, _I, _I, _V],
     "pda_wgrad_reduce": [_V, _V, _I, _I, _I, _I, _I, _I, _F, _I, _V],
-    "pda_bn_fwd_prereduce": [_V, _I, _I, _I, _I, _I, _V, _V],
-    "pda_bn_finalize_slabs": [_V, _I, _I, _D, _V, _V, _F, _F, _V, _V, _V, _V, _V, _V, _V, _I, _V],
+    "pda_bn_fwd_stats": [_V, _I, _I, _I, _I, _I, _V, _V, C.POINTER(BnFwdOut), _V],
+    "pda_bn_bwd_stats": [_V, _I, _I, _I, _I, _V, _V, C.POINTER(BnBwdOut), _V],
     "pda_bn_finalize_tot": [_V, _I, _D, _V, _V, _F, _F, _V, _V, _V, _V, _V, _V, _V, _I, _V],
     "pda_slab_reduce": [_V, _I, _I, _I, _V, _V],
     "pda_bn_eval_coeffs": [_V, _V, _V, _V, _F, _I, _V, _V, _V],

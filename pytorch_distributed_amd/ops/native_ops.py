@@ -24,7 +24,8 @@ from .ext import ConvDesc, BwdArgs, check, dt_of, ptr, stream
 
 __all__ = [
     "ConvGeom", "conv_fwd", "conv_dgrad", "conv_wgrad", "pick_tile", "wgrad_plan",
-    "BnStats", "BnBwd", "stats_totals", "dgrad_tiles_n", "bn_finalize_tot", "bn_finalize_partials", "bn_eval_coeffs", "bn_apply", "stem_pool", "maxpool_bwd", "tail_pool",
+    "BnStats", "stats_totals", "bn_finalize_tot", "bn_finalize_partials", "bn_eval_coeffs",
+    "bn_apply", "stem_pool", "maxpool_bwd", "tail_pool", "bn_epilogue", "bn_bwd_finish",
     "bn_bwd", "xent", "topk_hits", "col_sum", "sgd_flat", "cast_flat", "amp_scan",
     "pack_stem", "synth_batch", "nchw_to_nhwc8", "Workspace",
 ]
@@ -81,8 +82,8 @@ class Workspace:
         return b[:numel]
 
     def counters(self, numel: int) -> torch.Tensor:
-        """int32 arrival counters of in-launch reductions: zero when allocated, and every kernel
-        that uses them leaves them zero again (its last arrivers reset them)."""
+        """int32 arrival counters of the one-launch statistics kernels: zero when allocated, and
+        every kernel that uses them leaves them zero again (its last arrivers reset them)."""
         b = self._bufs.get("_counters")
         if b is None or b.numel() < numel:
             b = torch.zeros(max(numel, 64), dtype=torch.int32, device=self.device)
@@ -95,11 +96,6 @@ _WGRAD_TARGET = int(os.environ.get("PDA_WGRAD_TARGET", 2 * _NUM_CU))
 
 
 _SINGLE_STAGE = os.environ.get("PDA_SINGLE_STAGE", "1") != "0"
-# BatchNorm reductions inside the producing conv launch (forward statistics / dgrad epilogue
-# backward finalize); 0 = separate finalize launches (A/B)
-_INLAUNCH_BN = os.environ.get("PDA_INLAUNCH_BN", "bwd")     # 1 | 0 | fwd | bwd
-_INLAUNCH_BN_FWD = _INLAUNCH_BN in ("1", "fwd")
-_INLAUNCH_BN_BWD = _INLAUNCH_BN in ("1", "bwd")
 # scale on the split-K block targets (the wgrads run beside the dgrad chain on a second stream)
 _WGRAD_TB_SCALE = float(os.environ.get("PDA_WGRAD_TB_SCALE", "1.0"))
 
@@ -120,11 +116,11 @@ def pick_tile(M: int, N: int, K: Optional[int] = None) -> Tuple[int, int]:
 # ------------------------------------------------------------------ conv
 class BnStats:
     """BatchNorm (training) statistics of a conv forward: the conv epilogue writes per-M-tile
-    shifted partial sums, finalized into mean / invstd / scale / shift and the running statistics
-    either by two small parallel launches (:func:`bn_finalize_partials`, the default -- measured
-    ~1.9 ms/step faster on ResNet-50, profiles/ab_r2_inlaunch_bn.md) or inside the conv launch by
-    its last-arriving workgroups (``PDA_INLAUNCH_BN=1|fwd``; csrc/conv_gemm.hip bn_stats_finalize).
-    With SyncBatchNorm (``ws.sync_comm``) the f64 totals are all-reduced before the finalize."""
+    shifted partial sums, which ONE follow-up launch (:func:`bn_finalize_partials`) combines in f64
+    and finalizes into mean / invstd / scale / shift and the running statistics. (Finalizing inside
+    the conv launch itself measured slower: the finalize code costs the conv epilogue ~2% even when
+    idle -- profiles/ab_r2_inlaunch_bn.md.) With SyncBatchNorm (``ws.sync_comm``) the launch stops
+    at f64 totals, all-reduced before a small finalize kernel."""
 
     def __init__(self, ws: "Workspace", gamma, beta, eps: float, momentum: float, mean, invstd,
                  scale, shift, rmean=None, rvar=None, nbt=None, update_running: bool = True):
@@ -138,62 +134,30 @@ def conv_fwd(x: torch.Tensor, w: torch.Tensor, g: ConvGeom, out: torch.Tensor,
              stats: Optional[torch.Tensor] = None, bias: Optional[torch.Tensor] = None,
              relu: bool = False, tile: Optional[Tuple[int, int]] = None,
              pro: Optional[Tuple[torch.Tensor, torch.Tensor]] = None,
-             bn: Optional[BnStats] = None, inlaunch: Optional[bool] = None) -> torch.Tensor:
+             bn: Optional[BnStats] = None) -> torch.Tensor:
     """out[M, Cout] (16-bit or f32) = conv(x, w). w: [Cout, Kpad] 16-bit, Kpad = w.shape[1].
     stats (f32, >= ceil(M/bm)*3*Cout) receives per-M-tile shifted partials (sum(y-s),
-    sum((y-s)^2), s) -- see :func:`stats_totals`; ``bn`` (:class:`BnStats`) instead finalizes
-    BatchNorm inside the launch. pro = (scale, shift): x is a PRE-BatchNorm tensor and the conv
-    consumes relu(x*scale+shift). ``inlaunch`` (default: PDA_INLAUNCH_BN) finalizes ``bn`` inside
-    the conv launch instead of in two small follow-up launches."""
+    sum((y-s)^2), s) -- see :func:`stats_totals`; ``bn`` (:class:`BnStats`) also finalizes the
+    BatchNorm from them. pro = (scale, shift): x is a PRE-BatchNorm tensor and the conv consumes
+    relu(x*scale+shift)."""
     Nb = x.shape[0]
     M = Nb * g.Ho * g.Wo
     Kpad = w.shape[-1] if w.dim() == 2 else w[0].numel()
     bm, bn_ = tile or pick_tile(M, g.Cout, Kpad)
-    inlaunch = _INLAUNCH_BN_FWD if inlaunch is None else inlaunch
     d = g.desc(Nb)
     # direct (unstaged) f32 store + bias: the fc head (16-bit features -> f32 logits, or any conv
     # with a bias); f32 activations of the exact-fp32 engine take the staged path with statistics
     out_f32 = bias is not None or out.dtype != x.dtype
     pitch = out.stride(0) if out.dim() == 2 else g.Cout
-    fin = None
-    sync = None
-    if bn is not None and not inlaunch:
-        # default: shifted partials here -> parallel f64 prereduce -> finalize (two small launches;
-        # measured cheaper than finalizing inside the conv launch: profiles/ab_r2_inlaunch_bn.md)
-        T = math.ceil(M / abs(bm))
-        stats = bn.ws.get("fwd_stats", T * 3 * g.Cout)
-        rc = ext.lib().pda_conv_fwd(C.byref(d), ptr(x), ptr(w), Kpad, ptr(out), int(out_f32), pitch,
-                                    ptr(bias), ptr(stats), int(relu), ptr(pro[0] if pro else None),
-                                    ptr(pro[1] if pro else None), None, dt_of(x), bm, bn_,
-                                    stream(x.device))
-        check(rc, "conv_fwd")
-        bn_finalize_partials(stats, T, g.Cout, abs(bm), M, bn)
-        return out
+    T = math.ceil(M / abs(bm))
     if bn is not None:
-        ws = bn.ws
-        T = math.ceil(M / abs(bm))
-        tn = math.ceil(g.Cout / bn_)
-        ch = max(1, math.ceil(math.sqrt(T)))
-        G1 = math.ceil(T / ch)
-        stats = ws.get("fwd_stats", T * 3 * g.Cout)
-        chunk = ws.get("bn_chunk", G1 * 2 * g.Cout, torch.float64)
-        cnt = ws.counters(G1 * tn + tn)
-        sync = getattr(ws, "sync_comm", None)
-        if sync is not None and sync.world_size == 1:
-            sync = None
-        tot = ws.get("bn_tot", 2 * g.Cout, torch.float64) if sync is not None else None
-        fin = ext.BnFin(1 if sync is not None else 2, ch, ptr(chunk), ptr(tot), ptr(cnt),
-                        ptr(bn.gamma), ptr(bn.beta), bn.eps, bn.momentum, ptr(bn.mean),
-                        ptr(bn.invstd), ptr(bn.scale), ptr(bn.shift), ptr(bn.rmean), ptr(bn.rvar),
-                        ptr(bn.nbt), int(bn.update))
+        stats = bn.ws.get("fwd_stats", T * 3 * g.Cout)
     rc = ext.lib().pda_conv_fwd(C.byref(d), ptr(x), ptr(w), Kpad, ptr(out), int(out_f32), pitch,
                                 ptr(bias), ptr(stats), int(relu), ptr(pro[0] if pro else None),
-                                ptr(pro[1] if pro else None), C.byref(fin) if fin is not None else None,
-                                dt_of(x), bm, bn_, stream(x.device))
+                                ptr(pro[1] if pro else None), dt_of(x), bm, bn_, stream(x.device))
     check(rc, "conv_fwd")
-    if sync is not None:   # SyncBatchNorm: global f64 totals, then finalize
-        sync.all_reduce(tot)
-        bn_finalize_tot(tot, g.Cout, M * sync.world_size, bn)
+    if bn is not None:
+        bn_finalize_partials(stats, T, g.Cout, abs(bm), M, bn)
     return out
 
 
@@ -208,25 +172,27 @@ def stats_totals(stats: torch.Tensor, M: int, C_: int, bm: int) -> torch.Tensor:
 
 
 def bn_finalize_partials(stats: torch.Tensor, T: int, C_: int, bm: int, M: int, bn: BnStats) -> None:
-    """BatchNorm forward finalize from conv_fwd's shifted per-tile partials (two launches): a
-    parallel f64 prereduce into S slabs, then the per-channel finalize. SyncBatchNorm (``ws.sync_comm``):
-    the slabs are summed and all-reduced over the ranks first."""
-    S = max(1, min(T, max(96, min(512, 65536 // (2 * C_)))))
-    slabs = bn.ws.get("bn_slabs", S * 2 * C_, torch.float64)
-    st = stream(stats.device)
-    check(ext.lib().pda_bn_fwd_prereduce(ptr(stats), T, C_, bm, M, S, ptr(slabs), st),
-          "bn_fwd_prereduce")
-    sync = getattr(bn.ws, "sync_comm", None)
-    world = 1
-    if sync is not None and sync.world_size > 1:
-        tot = slabs.view(S, 2 * C_).sum(0)          # fixed-shape f64 reduction
+    """BatchNorm forward statistics from conv_fwd's shifted per-tile partials in one launch
+    (csrc/bn.hip bn_stats_kernel<0>): S blocks per 256-channel group reduce tile ranges to f64 slabs,
+    the group's last arriving block sums them and finalizes. SyncBatchNorm (``ws.sync_comm``): the
+    launch stops at f64 totals, which are all-reduced before :func:`bn_finalize_tot`."""
+    G = math.ceil(C_ / min(C_, 256))
+    S = _stats_slabs(T, C_)
+    ws = bn.ws
+    slabs = ws.get("bn_slabs", S * 2 * C_, torch.float64)
+    cnt = ws.counters(G)
+    sync = getattr(ws, "sync_comm", None)
+    if sync is not None and sync.world_size == 1:
+        sync = None
+    tot = ws.get("bn_tot", 2 * C_, torch.float64) if sync is not None else None
+    o = ext.BnFwdOut(ptr(bn.gamma), ptr(bn.beta), bn.eps, bn.momentum, ptr(bn.mean),
+                     ptr(bn.invstd), ptr(bn.scale), ptr(bn.shift), ptr(bn.rmean), ptr(bn.rvar),
+                     ptr(bn.nbt), int(bn.update), ptr(tot))
+    check(ext.lib().pda_bn_fwd_stats(ptr(stats), T, C_, bm, M, S, ptr(slabs), ptr(cnt), C.byref(o),
+                                     stream(stats.device)), "bn_fwd_stats")
+    if sync is not None:   # SyncBatchNorm: global f64 totals, then finalize
         sync.all_reduce(tot)
-        slabs, S, world = tot, 1, sync.world_size
-    check(ext.lib().pda_bn_finalize_slabs(ptr(slabs), S, C_, float(M * world), ptr(bn.gamma),
-                                          ptr(bn.beta), bn.eps, bn.momentum, ptr(bn.mean),
-                                          ptr(bn.invstd), ptr(bn.scale), ptr(bn.shift),
-                                          ptr(bn.rmean), ptr(bn.rvar), ptr(bn.nbt), int(bn.update),
-                                          st), "bn_finalize_slabs")
+        bn_finalize_tot(tot, C_, M * sync.world_size, bn)
 
 
 def bn_finalize_tot(tot: torch.Tensor, C_: int, count: int, bn: BnStats) -> None:
@@ -278,25 +244,13 @@ def conv_dgrad(dy: torch.Tensor, w: torch.Tensor, g: ConvGeom, dx: torch.Tensor,
     return dx
 
 
-class BnBwd:
-    """Parameters of the BatchNorm(s) whose backward a dgrad epilogue finalizes in-launch:
-    branch 0 = the BN of y, branch 1 (shortcut tails) = the BN of y2."""
-
-    def __init__(self, gamma, mean, invstd, dgamma, dbeta, gamma2=None, mean2=None, invstd2=None,
-                 dgamma2=None, dbeta2=None, accumulate: bool = False, k_name: str = "bn_k"):
-        self.b = [(gamma, mean, invstd, dgamma, dbeta), (gamma2, mean2, invstd2, dgamma2, dbeta2)]
-        self.accumulate, self.k_name = accumulate, k_name
-
-
 def bn_epilogue(ws: "Workspace", G: int, y, scale, shift, res=None, y2=None, scale2=None,
-                shift2=None, g2=None, mask=None, fin: Optional[BnBwd] = None, tiles_n: int = 0):
+                shift2=None, g2=None, mask=None):
     """Describe the BN-backward reduction a dgrad epilogue performs for a = relu(bn(y) [+res | +bn2(y2)]).
     ``mask`` (the forward's ReLU bitmask of a, see :func:`bn_apply`) replaces ``res``: the epilogue
     then reads one byte per 8 elements instead of the residual tensor (mode 3).
-    ``fin`` (:class:`BnBwd`; not with SyncBatchNorm): the dgrad's last-arriving workgroups also
-    finalize the BN backward (gamma/beta gradients + apply coefficients) inside the launch;
-    ``tiles_n`` = the dgrad's column tiles. Returns (epi, part, nq, k): ``part`` holds G*nq*C
-    partials after the dgrad, ``k`` [nq-1][3][C] the apply coefficients (None without fin)."""
+    Returns (epi, part, nq): ``part`` holds G*nq*C partials after the dgrad (:func:`bn_bwd_finish`
+    finalizes them)."""
     C_ = y.shape[-1]
     mode = 3 if mask is not None else (2 if y2 is not None else (1 if res is not None else 0))
     nq = 3 if mode == 2 else 2
@@ -304,30 +258,7 @@ def bn_epilogue(ws: "Workspace", G: int, y, scale, shift, res=None, y2=None, sca
     epi = ext.BnEpi(mode, nq, ptr(y), ptr(scale), ptr(shift),
                     ptr(y2 if y2 is not None else res), ptr(scale2), ptr(shift2), ptr(g2), ptr(part),
                     ptr(mask))
-    k = None
-    sync = getattr(ws, "sync_comm", None)
-    if (fin is not None and (sync is None or sync.world_size == 1) and tiles_n > 0
-            and _INLAUNCH_BN_BWD):
-        ch = max(1, math.ceil(math.sqrt(G)))
-        G1 = math.ceil(G / ch)
-        chunk = ws.get("bn_chunk", G1 * nq * C_, torch.float64)
-        cnt = ws.counters(G1 * tiles_n + tiles_n)
-        k = ws.get(fin.k_name, (nq - 1) * 3 * C_)
-        epi.fin_mode, epi.fin_ch, epi.accumulate = 1, ch, int(fin.accumulate)
-        epi.chunk, epi.cnt = ptr(chunk), ptr(cnt)
-        epi.count, epi.gscale = float(y.numel() // C_), 1.0
-        for b in range(nq - 1):
-            ga, mu, inv, dg, db = fin.b[b]
-            epi.gamma[b], epi.mean[b], epi.invstd[b] = ptr(ga), ptr(mu), ptr(inv)
-            epi.dgamma[b], epi.dbeta[b] = ptr(dg), ptr(db)
-        epi.k = ptr(k)
-    return epi, part, nq, k
-
-
-def dgrad_tiles_n(g: "ConvGeom", Nb: int, tile: Optional[Tuple[int, int]] = None) -> int:
-    """Column tiles of a dgrad launch (its output channels = the conv's Cin)."""
-    _, bn = tile or dgrad_tile(g, Nb)
-    return math.ceil(g.Cin / bn)
+    return epi, part, nq
 
 
 # Weight-gradient tile / split-K block target per ResNet conv geometry (Cout, R, Cin, stride, Ho),
@@ -541,17 +472,32 @@ def bn_bwd(ws: Workspace, y, mean, invstd, gamma, scale, shift, dgamma, dbeta, d
 
 def bn_bwd_finish(ws: "Workspace", part, G: int, nq: int, y, mean, invstd, gamma, dgamma, dbeta,
                   dz, dy_out, y2=None, mean2=None, invstd2=None, gamma2=None, dgamma2=None,
-                  dbeta2=None, dy2_out=None, gscale: float = 1.0, accumulate: bool = False,
-                  k=None) -> None:
+                  dbeta2=None, dy2_out=None, gscale: float = 1.0, accumulate: bool = False) -> None:
     """Finalize + apply of a BN backward whose reduction a dgrad epilogue already produced
-    (partials ``part`` [G][nq][C], masked gradient ``dz``). ``k`` (from :func:`bn_epilogue` with
-    ``fin``): the dgrad launch already finalized -- only the apply pass(es) run."""
+    (partials ``part`` [G][nq][C], masked gradient ``dz``): ONE finalize launch (csrc/bn.hip
+    bn_stats_kernel<1>: f64 slabs + last-arriver combine -> gamma/beta gradients and the apply
+    coefficients of both branches), then the apply pass(es). SyncBatchNorm takes the separate
+    reduce -> all-reduce -> finalize path."""
     N, H, W, C_ = y.shape
     mode = 2 if nq == 3 else 1   # dz is materialised in both cases
     a = BwdArgs(None, None, None, 0, ptr(y), None, None, ptr(y2), None, None, mode, None, ptr(part),
                 nq, N * H * W, C_)
-    if k is not None:
+    sync = getattr(ws, "sync_comm", None)
+    if sync is None or sync.world_size == 1:
+        k = ws.get("bn_k", 6 * C_)
+        S = _stats_slabs(G, C_)
+        slabs = ws.get("bn_slabs", S * nq * C_, torch.float64)
+        cnt = ws.counters(math.ceil(C_ / min(C_, 256)))
+        o = ext.BnBwdOut(float(N * H * W), float(gscale), int(accumulate))
+        o.gamma[0], o.mean[0], o.invstd[0] = ptr(gamma), ptr(mean), ptr(invstd)
+        o.dgamma[0], o.dbeta[0] = ptr(dgamma), ptr(dbeta)
+        if nq == 3:
+            o.gamma[1], o.mean[1], o.invstd[1] = ptr(gamma2), ptr(mean2), ptr(invstd2)
+            o.dgamma[1], o.dbeta[1] = ptr(dgamma2), ptr(dbeta2)
+        o.k = ptr(k)
         L, st, dt = ext.lib(), stream(y.device), dt_of(y)
+        check(L.pda_bn_bwd_stats(ptr(part), G, nq, C_, S, ptr(slabs), ptr(cnt), C.byref(o), st),
+              "bn_bwd_stats")
         check(L.pda_bn_bwd_apply(C.byref(a), ptr(dz), ptr(y), ptr(k[0:C_]), ptr(k[C_:2 * C_]),
                                  ptr(k[2 * C_:3 * C_]), ptr(dy_out), dt, st), "bn_bwd_apply")
         if mode == 2:
@@ -561,6 +507,13 @@ def bn_bwd_finish(ws: "Workspace", part, G: int, nq: int, y, mean, invstd, gamma
         return
     _bn_bwd_tail(ws, part, G, nq, mode, a, y, mean, invstd, gamma, dgamma, dbeta, dy_out,
                  y2, mean2, invstd2, gamma2, dgamma2, dbeta2, dy2_out, dz, gscale, accumulate)
+
+
+def _stats_slabs(T: int, C_: int) -> int:
+    """Blocks per channel group of the one-launch statistics kernel: level 1 reads T/S tiles per
+    block, the group's last arriver S slabs -- S ~ sqrt(T) balances the two (both run at one CU's
+    bandwidth), at least 8 when T allows so the level-1 reads spread over CUs."""
+    return max(1, min(T, max(8, int(math.sqrt(0.75 * T)))))
 
 
 def _bn_bwd_tail(ws, part, G, nq, mode, a, y, mean, invstd, gamma, dgamma, dbeta, dy_out,

@@ -159,7 +159,7 @@ def test_bn_forward_finalize_apply():
     assert int(nbt.item()) == 1
 
 
-def _conv_bn_inlaunch(K, x_nhwc, w2d, g, dtype, gamma, beta, tile=None, ws=None, inlaunch=True):
+def _conv_bn(K, x_nhwc, w2d, g, dtype, gamma, beta, tile=None, ws=None):
     ws = ws or K.Workspace(DEV)
     C = g.Cout
     y = torch.empty(x_nhwc.shape[0], g.Ho, g.Wo, C, device=DEV, dtype=dtype)
@@ -167,18 +167,17 @@ def _conv_bn_inlaunch(K, x_nhwc, w2d, g, dtype, gamma, beta, tile=None, ws=None,
     rm, rv = torch.zeros(C, device=DEV), torch.ones(C, device=DEV)
     nbt = torch.zeros(1, dtype=torch.int64, device=DEV)
     bn = K.BnStats(ws, gamma, beta, 1e-5, 0.1, st[0], st[1], st[2], st[3], rm, rv, nbt)
-    K.conv_fwd(x_nhwc, w2d, g, y, bn=bn, tile=tile, inlaunch=inlaunch)
+    K.conv_fwd(x_nhwc, w2d, g, y, bn=bn, tile=tile)
     return y, st, rm, rv, nbt, ws
 
 
-@pytest.mark.parametrize("inlaunch", [True, False])
 @pytest.mark.parametrize("tile", [None, (-128, 128), (128, 64), (64, 128), (-128, 64)])
-def test_conv_fwd_inlaunch_bn_finalize(tile, inlaunch):
-    """BatchNorm statistics of the conv forward -- finalized INSIDE the conv launch (last-arriving
-    workgroups, f64, shifted partials) or by the default two follow-up launches (parallel f64
-    prereduce + finalize): mean / invstd / scale / shift / running stats / counter against float64
-    statistics of the stored output, on a ragged shape with several column tiles and chunks;
-    bit-identical on a second launch (fixed summation order), counters left at zero."""
+def test_conv_fwd_bn_finalize(tile):
+    """BatchNorm statistics of the conv forward (shifted per-tile partials in the conv epilogue,
+    then one launch: f64 slabs per block + last-arriver combine and finalize): mean / invstd /
+    scale / shift / running stats / counter against float64 statistics of the stored output, on a
+    ragged shape with several column tiles; bit-identical on a second launch (fixed summation
+    order), arrival counters left at zero."""
     K = _k()
     dtype = torch.bfloat16
     torch.manual_seed(5)
@@ -187,10 +186,8 @@ def test_conv_fwd_inlaunch_bn_finalize(tile, inlaunch):
     x = (torch.randn(Nb, H, H, Cin, device=DEV) + 0.2).to(dtype)
     w = (torch.randn(Cout, 3, 3, Cin, device=DEV) / 24).to(dtype)
     gamma, beta = torch.rand(Cout, device=DEV) + 0.5, torch.randn(Cout, device=DEV)
-    y, st, rm, rv, nbt, ws = _conv_bn_inlaunch(K, x, w.view(Cout, -1), g, dtype, gamma, beta, tile,
-                                               inlaunch=inlaunch)
-    y2, st2, _, _, _, _ = _conv_bn_inlaunch(K, x, w.view(Cout, -1), g, dtype, gamma, beta, tile, ws,
-                                            inlaunch=inlaunch)
+    y, st, rm, rv, nbt, ws = _conv_bn(K, x, w.view(Cout, -1), g, dtype, gamma, beta, tile)
+    y2, st2, _, _, _, _ = _conv_bn(K, x, w.view(Cout, -1), g, dtype, gamma, beta, tile, ws)
     torch.cuda.synchronize()
     yd = y.double().reshape(-1, Cout)
     n = yd.shape[0]
@@ -206,12 +203,22 @@ def test_conv_fwd_inlaunch_bn_finalize(tile, inlaunch):
     assert int(ws.counters(64).abs().sum().item()) == 0
 
 
+class _DoublingComm:
+    """Stand-in SyncBatchNorm communicator of two identical ranks: all_reduce doubles."""
+    world_size = 2
+
+    def all_reduce(self, t):
+        t.mul_(2)
+
+
+@pytest.mark.parametrize("sync", [False, True])
 @pytest.mark.parametrize("C,T", [(64, 3), (192, 700), (512, 97), (1028, 40), (2048, 600)])
-def test_bn_finalize_partials_channel_widths(C, T):
-    """The default forward finalize (parallel f64 prereduce over S slabs + per-channel finalize)
-    on synthetic shifted partials part[T][3][C] for every channel-width regime of the prereduce's
-    (channel quad x slab lane) decomposition, including C/4 > 256 (several quad passes) and a
-    ragged last tile, against a float64 combination."""
+def test_bn_finalize_partials_channel_widths(C, T, sync):
+    """The forward finalize (one launch: f64 slabs per (tile range, 256-channel group) block, the
+    group's last arriver combines and finalizes) on synthetic shifted partials part[T][3][C] for
+    every channel-width regime of its (channel quad x slab lane) decomposition -- several groups,
+    a ragged last group (C = 1028), a ragged last tile -- against a float64 combination; ``sync``:
+    the SyncBatchNorm path (f64 totals -> all-reduce -> finalize) with two identical ranks."""
     K = _k()
     torch.manual_seed(C + T)
     bm = 128
@@ -229,6 +236,8 @@ def test_bn_finalize_partials_channel_widths(C, T):
     mean = tot1 / M
     var = (tot2 / M - mean ** 2).clamp_min(0)
     ws = K.Workspace(DEV)
+    if sync:
+        ws.sync_comm = _DoublingComm()
     gamma, beta = torch.rand(C, device=DEV) + 0.5, torch.randn(C, device=DEV)
     st = torch.zeros(4, C, device=DEV)
     rm, rv = torch.zeros(C, device=DEV), torch.ones(C, device=DEV)
@@ -237,14 +246,16 @@ def test_bn_finalize_partials_channel_widths(C, T):
                    update_running=True)
     K.bn_finalize_partials(part.to(DEV).contiguous(), T, C, bm, M, bn)
     torch.cuda.synchronize()
+    n = M * (2 if sync else 1)
     torch.testing.assert_close(st[0].double().cpu(), mean, rtol=1e-5, atol=1e-6)
     torch.testing.assert_close(st[1].double().cpu(), 1 / torch.sqrt(var + 1e-5), rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(rv.double().cpu(), 0.9 + 0.1 * var * n / (n - 1), rtol=1e-5, atol=1e-6)
     assert int(nbt.item()) == 1
+    assert int(ws.counters(16).abs().sum().item()) == 0
 
 
-@pytest.mark.parametrize("inlaunch", [False, True])
 @pytest.mark.parametrize("dtype,std", [(torch.float32, 0.01), (torch.bfloat16, 0.08)])
-def test_bn_statistics_large_offset_layer1_scale(dtype, std, inlaunch):
+def test_bn_statistics_large_offset_layer1_scale(dtype, std):
     """Layer-1 scale (1.25 M rows x 64 channels, batch 400 at 56x56) with mean ~10 and std ~0.01
     (bf16: 0.08, so the stored values -- 1/16 apart at 10 -- still vary): E[y^2] - E[y]^2 from
     f32 partial sums would cancel catastrophically; the shifted per-tile sums + f64 combination
@@ -258,8 +269,7 @@ def test_bn_statistics_large_offset_layer1_scale(dtype, std, inlaunch):
     w = torch.randn(Cout, Cin, device=DEV) * std / 8
     w[:, 0] = 10.0 + torch.rand(Cout, device=DEV)    # y_c ~ 10..11 + N(0, std^2)
     gamma, beta = torch.ones(Cout, device=DEV), torch.zeros(Cout, device=DEV)
-    y, st, rm, rv, nbt, _ = _conv_bn_inlaunch(K, x.to(dtype), w.to(dtype), g, dtype, gamma, beta,
-                                              inlaunch=inlaunch)
+    y, st, rm, rv, nbt, _ = _conv_bn(K, x.to(dtype), w.to(dtype), g, dtype, gamma, beta)
     torch.cuda.synchronize()
     yd = y.double().reshape(-1, Cout)
     mean, var = yd.mean(0), yd.var(0, unbiased=False)
@@ -531,11 +541,11 @@ def test_synthetic_kernel_matches_torch_generator():
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
 @pytest.mark.parametrize("mode", ["relu", "res", "ds", "mask"])
 @pytest.mark.parametrize("stride", [1, 2])
-@pytest.mark.parametrize("inlaunch", [False, True])
-def test_dgrad_fused_bn_backward(mode, stride, dtype, geo, inlaunch):
-    """dgrad epilogue (mask + BN-backward partial sums) == plain dgrad followed by the standalone
-    BN-backward reduce/apply (16-bit and exact-f32 kernels). ``inlaunch``: the dgrad's
-    last-arriving workgroups also finalize the BN backward (gamma/beta grads, coefficients)."""
+def test_dgrad_fused_bn_backward(mode, stride, dtype, geo):
+    """dgrad epilogue (mask + BN-backward partial sums) + the one-launch finalize (f64 slabs,
+    last-arriver combine: gamma/beta grads and apply coefficients of both branches) == plain dgrad
+    followed by the standalone BN-backward reduce / finalize / apply (16-bit and exact-f32
+    kernels); the arrival counters are left at zero."""
     K = _k()
     tol = 1e-2 if dtype != torch.float32 else 1e-5
     Nb, H, Cin, Cout = geo
@@ -578,13 +588,7 @@ def test_dgrad_fused_bn_backward(mode, stride, dtype, geo, inlaunch):
         K.bn_apply(y, sc, sh, torch.empty_like(y), res=y2, mask=mask)
         kw = dict(mask=mask)
     outs = [torch.zeros(Cin, device=DEV) for _ in range(4)]
-    fin = None
-    if inlaunch:
-        fin = K.BnBwd(gamma, mean, inv, outs[0], outs[1], *((gamma2, mean2, inv2, outs[2], outs[3])
-                                                            if mode == "ds" else ()))
-    epi, part, nq, kc = K.bn_epilogue(ws, G, y, sc, sh, g2=g2 if use_g2 else None, fin=fin,
-                                      tiles_n=K.dgrad_tiles_n(g, Nb), **kw)
-    assert (kc is not None) == inlaunch
+    epi, part, nq = K.bn_epilogue(ws, G, y, sc, sh, g2=g2 if use_g2 else None, **kw)
     dz = torch.empty_like(y)
     K.conv_dgrad(dy, w, g, dz, epi=epi)
     dyf = torch.empty_like(y)
@@ -593,7 +597,7 @@ def test_dgrad_fused_bn_backward(mode, stride, dtype, geo, inlaunch):
     if mode == "ds":
         extra = dict(y2=y2, mean2=mean2, invstd2=inv2, gamma2=gamma2, dgamma2=outs[2], dbeta2=outs[3],
                      dy2_out=dy2f)
-    K.bn_bwd_finish(ws, part, G, nq, y, mean, inv, gamma, outs[0], outs[1], dz, dyf, k=kc, **extra)
+    K.bn_bwd_finish(ws, part, G, nq, y, mean, inv, gamma, outs[0], outs[1], dz, dyf, **extra)
     torch.cuda.synchronize()
     assert int(ws.counters(64).abs().sum().item()) == 0
     if mode != "relu":

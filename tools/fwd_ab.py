@@ -3,7 +3,7 @@
     python tools/fwd_ab.py LIB_A LIB_B [--with-fin-a] [--with-fin-b]
 
 Each library's ``pda_conv_fwd`` is called through its own ctypes binding (``--with-fin-X``: that
-library's launcher takes the BnFin pointer before ``dt``, as from round 2 on), with the same
+library's launcher takes a BnFin pointer before ``dt``, an intermediate round-2 ABI), with the same
 operands, tile (ops.native_ops.pick_tile), BatchNorm partial statistics and operand prologue as in
 the ResNet-50 step; the launches alternate A/B so clock drift hits both alike. Prints the median
 microseconds per shape and the COUNT-weighted total (tools/conv_bench.py SHAPES / COUNT)."""
