@@ -169,7 +169,7 @@ __global__ __launch_bounds__(256) void bn_stats_kernel(const float* __restrict__
       for (int e = 0; e < 4; ++e) a[q][e] = 0.0;
     const int t0 = (int)((long long)s * T / S), t1 = (int)((long long)(s + 1) * T / S);
     if (act) {
-#pragma unroll 2
+#pragma unroll 4
       for (int t = t0 + lane; t < t1; t += SL) {
         const float* pt = part + (size_t)t * PQ * C + c;
         f32x4 d[PQ];
@@ -219,6 +219,7 @@ __global__ __launch_bounds__(256) void bn_stats_kernel(const float* __restrict__
 #pragma unroll
       for (int e = 0; e < 4; ++e) a[q][e] = 0.0;
     if (act)
+#pragma unroll 4
       for (int t = lane; t < S; t += SL) {
 #pragma unroll
         for (int q = 0; q < NQ; ++q) {

@@ -621,9 +621,9 @@ __global__ __launch_bounds__(NT, (conv_min_blocks<DT, BM, BN, STAGES>())) void c
           }
     } else {
 #pragma unroll
-      for (int i = 0; i < MI; ++i)
+      for (int j = 0; j < NI; ++j)   // column-tile outer: measured ~1% faster FWD than row-outer
 #pragma unroll
-        for (int j = 0; j < NI; ++j) fn(i * 16 + lr, j * 16 + 4 * lg, acc[i][j]);
+        for (int i = 0; i < MI; ++i) fn(i * 16 + lr, j * 16 + 4 * lg, acc[i][j]);
     }
   };
   if constexpr (PASS == WGRAD) {

@@ -128,9 +128,12 @@ class NativeResNet(nn.Module):
         self._grads_zero = True
         self._fwd_ctx = None
         self._anchor = torch.zeros((), device=device, requires_grad=True)
-        # BN1/BN2 (+ReLU) applied inside the consumer conv's operand staging (fwd and wgrad)
+        # BN1/BN2 (+ReLU) applied inside the consumer conv's operand staging (fwd and wgrad):
+        # "1" every consumer, "1x1" only 1x1 consumers (a 3x3 consumer gathers each element 9x per
+        # N-tile, so it re-applies the prologue 9-36x: there one materialising pass is cheaper),
+        # "0" none
         import os
-        self.fuse_prologue = os.environ.get("PDA_FUSE_PROLOGUE", "1") != "0"
+        self.fuse_prologue = os.environ.get("PDA_FUSE_PROLOGUE", "1")
         self.fused_stem_bwd = os.environ.get("PDA_FUSED_STEM_BWD", "1") != "0"
         self.tail_mask = os.environ.get("PDA_TAIL_MASK", "1") != "0"
         self.ds_stream = os.environ.get("PDA_DS_STREAM", "1") != "0"
@@ -485,7 +488,10 @@ class NativeResNet(nn.Module):
                     rec[f"s{j}"] = u.state
                 if j < len(b.units) - 1:
                     sc, sh = self._coeffs(u, train)
-                    if self.fuse_prologue:   # next conv applies BN+ReLU while staging its tiles
+                    nxt = b.units[j + 1]
+                    if self.fuse_prologue == "1" or (self.fuse_prologue == "1x1"
+                                                     and nxt.conv.kernel_size == (1, 1)):
+                        # the next conv applies BN+ReLU while staging its tiles
                         a, pro = y, (sc, sh)
                         acts.append(None)
                     else:
