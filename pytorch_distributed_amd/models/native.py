@@ -131,9 +131,9 @@ class NativeResNet(nn.Module):
         # BN1/BN2 (+ReLU) applied inside the consumer conv's operand staging (fwd and wgrad):
         # "1" every consumer, "1x1" only 1x1 consumers (a 3x3 consumer gathers each element 9x per
         # N-tile, so it re-applies the prologue 9-36x: there one materialising pass is cheaper),
-        # "0" none
+        # "1x1:H" also 3x3 consumers of input size >= H, "0" none
         import os
-        self.fuse_prologue = os.environ.get("PDA_FUSE_PROLOGUE", "1")
+        self.fuse_prologue = os.environ.get("PDA_FUSE_PROLOGUE", "1x1:56")
         self.fused_stem_bwd = os.environ.get("PDA_FUSED_STEM_BWD", "1") != "0"
         self.tail_mask = os.environ.get("PDA_TAIL_MASK", "1") != "0"
         self.ds_stream = os.environ.get("PDA_DS_STREAM", "1") != "0"
@@ -422,6 +422,16 @@ class NativeResNet(nn.Module):
         return out
 
     # ------------------------------------------------------------------ forward
+    def _fuse_into(self, u: ConvBN) -> bool:
+        """Whether conv ``u`` applies the previous BN+ReLU in its operand staging (else the
+        activation is materialised by bn_apply) -- the PDA_FUSE_PROLOGUE policy."""
+        mode = self.fuse_prologue
+        if mode in ("1", "0"):
+            return mode == "1"
+        if u.conv.kernel_size == (1, 1):
+            return True
+        return ":" in mode and u.H >= int(mode.split(":")[1])
+
     def _conv_bn(self, u: ConvBN, x: torch.Tensor, train: bool, pro=None, ws=None) -> torch.Tensor:
         """y = conv(x) and BN coefficients (batch stats in training, running stats in eval).
         ``pro=(scale, shift)``: x is the previous PRE-BN tensor; the conv applies BN+ReLU on load."""
@@ -488,9 +498,7 @@ class NativeResNet(nn.Module):
                     rec[f"s{j}"] = u.state
                 if j < len(b.units) - 1:
                     sc, sh = self._coeffs(u, train)
-                    nxt = b.units[j + 1]
-                    if self.fuse_prologue == "1" or (self.fuse_prologue == "1x1"
-                                                     and nxt.conv.kernel_size == (1, 1)):
+                    if self._fuse_into(b.units[j + 1]):
                         # the next conv applies BN+ReLU while staging its tiles
                         a, pro = y, (sc, sh)
                         acts.append(None)

@@ -96,6 +96,7 @@ _WGRAD_TARGET = int(os.environ.get("PDA_WGRAD_TARGET", 2 * _NUM_CU))
 
 
 _SINGLE_STAGE = os.environ.get("PDA_SINGLE_STAGE", "1") != "0"
+_STATS_S = os.environ.get("PDA_STATS_S")   # fixed slab count of the statistics kernels (A/B)
 # scale on the split-K block targets (the wgrads run beside the dgrad chain on a second stream)
 _WGRAD_TB_SCALE = float(os.environ.get("PDA_WGRAD_TB_SCALE", "1.0"))
 
@@ -513,6 +514,8 @@ def _stats_slabs(T: int, C_: int) -> int:
     """Blocks per channel group of the one-launch statistics kernel: level 1 reads T/S tiles per
     block, the group's last arriver S slabs -- S ~ sqrt(T) balances the two (both run at one CU's
     bandwidth), at least 8 when T allows so the level-1 reads spread over CUs."""
+    if _STATS_S is not None:   # A/B override (tools/bnstats_bench.py)
+        return max(1, min(T, int(_STATS_S)))
     return max(1, min(T, max(8, int(math.sqrt(0.75 * T)))))
 
 
