@@ -105,3 +105,28 @@ def test_native_dataparallel_resume_reloads_every_replica():
     assert torch.equal(dp.module.flat_params, ck.flat_params)
     assert torch.equal(dp.replicas[0].flat_params, ck.flat_params)
     assert torch.equal(dp.replicas[0].flat_shadow, ck.flat_shadow)
+
+
+def test_rccl_group_single_device_collectives():
+    """The in-process RCCL group (ncclCommInitAll, the DataParallel gradient path over distinct
+    GPUs) on the one device of the box: all_reduce (sum / avg), broadcast and reduce run through
+    the native C ABI on every dtype the DP step uses, with world-1 semantics (identity), and the
+    group closes cleanly. (The multi-device form runs only where several GPUs are visible.)"""
+    from pytorch_distributed_amd.parallel.rccl import RcclGroup
+    g = RcclGroup([0])
+    try:
+        for dt in (torch.float32, torch.bfloat16, torch.int64):
+            t = (torch.arange(1000, device=DEV) - 300).to(dt)
+            ref = t.clone()
+            g.all_reduce([t], op="sum")
+            g.broadcast([t], root=0)
+            g.reduce([t], root=0, op="sum")
+            torch.cuda.synchronize()
+            assert torch.equal(t, ref), dt
+        f = torch.randn(4096, device=DEV)
+        ref = f.clone()
+        g.all_reduce([f], op="avg")
+        torch.cuda.synchronize()
+        assert torch.equal(f, ref)
+    finally:
+        g.close()
