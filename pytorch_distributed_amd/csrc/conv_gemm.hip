@@ -44,6 +44,7 @@ struct ConvParams {
   int Ho, Wo, Cout;   // output Y geometry
   int R, S, stride, pad;
   int log2Cin;        // channels of the gathered tensor are a power of two (3 is padded to 8)
+  int log2Cout;       // DGRAD: log2(Cout) when a power of two, else -1 (tap of a k-tile: shift)
   int out_f32;
   int relu;           // FWD epilogue relu (fc: 0)
   int k_chunk;        // WGRAD: rows per split
@@ -389,21 +390,40 @@ __global__ __launch_bounds__(NT, (conv_min_blocks<DT, BM, BN, STAGES>())) void c
     const int k0 = kbeg + kt * BKE;
     // ---------------- A
     if constexpr (PASS == FWD) {
-      const int k = k0 + (tid & 7) * EPC;
-      const int tap = k >> p.log2Cin;
-      const int c = k & ((1 << p.log2Cin) - 1);
-      const int r = (int)fdiv(tap, p.dS), q = tap - r * p.S;
-      const int toff = ((r * p.W + q) * p.Cin + c) * ES;
-      const bool tap_ok = tap < p.R * p.S;
+      if (p.Cin >= BKE) {
+        // the k-tile lies in ONE tap (Cin is a power of two >= 64): tap, (r, s) and the tap's
+        // pixel offset are wave-uniform scalar math; per lane only the chunk's channel offset
+        const int tap = k0 >> p.log2Cin;
+        const int c0 = k0 & ((1 << p.log2Cin) - 1);
+        const int r = (int)fdiv(tap, p.dS), q = tap - r * p.S;
+        const int toff = ((r * p.W + q) * p.Cin + c0 + (tid & 7) * EPC) * ES;
+        const uint32_t word = tap >> 5, bit = tap & 31;
 #pragma unroll
-      for (int i = 0; i < AR; ++i) {
-        const bool ok = tap_ok && ((a_mask[i] >> (tap & 63)) & 1ull);
-        ra[i] = bld(rsa, ok ? (uint32_t)(a_base[i] + toff) : OOB);
-        pv[i] = ok;
+        for (int i = 0; i < AR; ++i) {
+          const uint32_t mw = word ? (uint32_t)(a_mask[i] >> 32) : (uint32_t)a_mask[i];
+          const bool ok = (mw >> bit) & 1u;
+          ra[i] = bld(rsa, ok ? (uint32_t)(a_base[i] + toff) : OOB);
+          pv[i] = ok;
+        }
+        if (pro) pro_coeffs(c0 + (tid & 7) * EPC);
+      } else {   // Cin < 64 (the space-to-depth stem): taps change inside the k-tile
+        const int k = k0 + (tid & 7) * EPC;
+        const int tap = k >> p.log2Cin;
+        const int c = k & ((1 << p.log2Cin) - 1);
+        const int r = (int)fdiv(tap, p.dS), q = tap - r * p.S;
+        const int toff = ((r * p.W + q) * p.Cin + c) * ES;
+        const bool tap_ok = tap < p.R * p.S;
+#pragma unroll
+        for (int i = 0; i < AR; ++i) {
+          const bool ok = tap_ok && ((a_mask[i] >> (tap & 63)) & 1ull);
+          ra[i] = bld(rsa, ok ? (uint32_t)(a_base[i] + toff) : OOB);
+          pv[i] = ok;
+        }
+        if (pro) pro_coeffs(c);
       }
-      if (pro) pro_coeffs(c);
     } else if constexpr (PASS == DGRAD) {
-      const int ti = k0 / p.Cout;  // tile lies in one tap (Cout % 64 == 0)
+      // tile lies in one tap (Cout % 64 == 0); scalar shift instead of a scalar division
+      const int ti = p.log2Cout >= 0 ? k0 >> p.log2Cout : k0 / p.Cout;
       const int c = k0 - ti * p.Cout + (tid & 7) * EPC;
       const int tsel = ti < 9 ? ti : 0;
       const int toff = ((p.tdy[split][tsel] * p.Wo + p.tdx[split][tsel]) * p.Cout + c) * ES;
@@ -423,7 +443,7 @@ __global__ __launch_bounds__(NT, (conv_min_blocks<DT, BM, BN, STAGES>())) void c
 #pragma unroll
       for (int i = 0; i < BR; ++i) rb[i] = bld(rsb, b_off[i] + (uint32_t)k0 * (uint32_t)ES);
     } else if constexpr (PASS == DGRAD) {
-      const int ti = k0 / p.Cout;
+      const int ti = p.log2Cout >= 0 ? k0 >> p.log2Cout : k0 / p.Cout;
       const int tap = p.taps[split][ti < 9 ? ti : 0];
       const uint32_t uoff = (uint32_t)(((k0 - ti * p.Cout) * p.R * p.S + tap) * p.Cin) * (uint32_t)ES;
 #pragma unroll
@@ -1033,6 +1053,9 @@ static void fill_geom(ConvParams& p, const ConvDesc& d) {
   int l = 0;
   while ((1 << l) < d.Cin) ++l;
   p.log2Cin = l;
+  int lo = 0;
+  while ((1 << lo) < d.Cout) ++lo;
+  p.log2Cout = (1 << lo) == d.Cout ? lo : -1;
   p.dHoWo = make_div(d.Ho * d.Wo);
   p.dWo = make_div(d.Wo);
   p.dS = make_div(d.S);
