@@ -289,6 +289,16 @@ _WGRAD_TUNED = {
     (512, 1, 2048, 1, 7): ((128, 128), 512),    # C21
     (512, 3, 512, 1, 7): ((-256, 128), 1024),   # C22
 }
+# round-2 re-measurement (profiles/convbench_r2.txt, the round-2 kernels): single-stage tiles at
+# the default block target beat the round-1 entries on these shapes (PDA_WGRAD_TUNE=r1: old table)
+if os.environ.get("PDA_WGRAD_TUNE", "r2") == "r2":
+    _WGRAD_TUNED.update({
+        (64, 1, 64, 1, 56): ((-64, 128), 512),      # C1   69.1 -> 61.0 us
+        (128, 3, 128, 1, 28): ((-64, 128), 512),    # C10 223.9 -> 213.2
+        (256, 3, 256, 2, 14): ((-256, 128), 512),   # C12 198.0 -> 130.2
+        (1024, 1, 256, 1, 14): ((-128, 64), 512),   # C13  83.4 -> 75.3
+        (256, 1, 1024, 1, 14): ((-128, 64), 512),   # C15  82.7 -> 74.8
+    })
 
 
 def wgrad_plan(g: ConvGeom, Nb: int, tile: Optional[Tuple[int, int]] = None,
