@@ -375,14 +375,14 @@ __global__ __launch_bounds__(NT, (conv_min_blocks<DT, BM, BN, STAGES>())) void c
       for (int k = 0; k < 4; ++k)
         v[k] = __float_as_int(fmaxf(__builtin_fmaf(__int_as_float(v[k]), psc[k >> 1][k & 1],
                                                    psh[k >> 1][k & 1]), 0.f));
-      return;
-    }
+    } else {
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const f32x2 u = unpack2<DT>((uint32_t)v[k]);
-      const f32x2 f = fma2(u, psc[k], psh[k]);
-      const s16x2 h = __builtin_bit_cast(s16x2, pack2<DT>(f));
-      v[k] = __builtin_bit_cast(int, __builtin_elementwise_max(h, (s16x2){0, 0}));
+      for (int k = 0; k < 4; ++k) {
+        const f32x2 u = unpack2<DT>((uint32_t)v[k]);
+        const f32x2 f = fma2(u, psc[k], psh[k]);
+        const s16x2 h = __builtin_bit_cast(s16x2, pack2<DT>(f));
+        v[k] = __builtin_bit_cast(int, __builtin_elementwise_max(h, (s16x2){0, 0}));
+      }
     }
   };
 
