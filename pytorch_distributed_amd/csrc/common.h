@@ -17,7 +17,10 @@ typedef unsigned short u16;
 #define LDS_PTR(T, p) ((__attribute__((address_space(3))) T*)(p))
 
 // dtype tags shared with the Python side (ops/ext.py)
-enum DType : int { DT_F32 = 0, DT_BF16 = 1, DT_F16 = 2 };
+// DT_F32S: f32 tensors in memory, products on the bf16 MFMA as a three-term split
+// (a_hi*b_hi + a_hi*b_lo + a_lo*b_hi, hi = bf16(x), lo = bf16(x - hi)): ~16 significant bits
+// per product, above the TF32 (10-bit) convolutions of the reference's "fp32" runs
+enum DType : int { DT_F32 = 0, DT_BF16 = 1, DT_F16 = 2, DT_F32S = 3 };
 
 // ---- 16-bit <-> f32 conversions -------------------------------------------------------------
 __device__ __forceinline__ float bf16_to_f32(u16 v) { return __uint_as_float(((uint32_t)v) << 16); }

@@ -182,6 +182,7 @@ constexpr int conv_min_blocks() {
 #ifdef PDA_CONV_MINB_LEGACY   // A/B: the pre-r2 bounds (tools/build_variant.py)
   return (STAGES == 1 && BM * BN <= 128 * 128) ? 3 : 2;
 #endif
+  if (DT == DT_F32S) return BM * BN <= 64 * 64 ? 4 : 2;   // hi + lo tiles: twice the LDS
   if (DT != DT_F32 && BM * BN <= 64 * 64) return 5;
   if (DT != DT_F32 && STAGES == 1 && BM * BN <= 128 * 64) return 4;
   return (STAGES == 1 && BM * BN <= 128 * 128) ? 3 : 2;
@@ -189,7 +190,8 @@ constexpr int conv_min_blocks() {
 
 template <int PASS, int DT, int BM, int BN, int STAGES, int MF = 16>
 __global__ __launch_bounds__(NT, (conv_min_blocks<DT, BM, BN, STAGES>())) void conv_gemm_kernel(ConvParams p_arg) {
-  static_assert(MF == 16 || (MF == 32 && DT != DT_F32 && BM >= 64 && BN >= 64), "MFMA shape");
+  static_assert(MF == 16 || (MF == 32 && (DT == DT_BF16 || DT == DT_F16) && BM >= 64 && BN >= 64),
+                "MFMA shape");
   // DGRAD / WGRAD read the parameters in place in the kernarg segment (constant address space):
   // binding a reference to the by-value argument makes the compiler copy the whole ~1 KB block to
   // scratch once a member array is indexed dynamically (DGRAD tap tables), and costs WGRAD spills.
@@ -206,18 +208,26 @@ __global__ __launch_bounds__(NT, (conv_min_blocks<DT, BM, BN, STAGES>())) void c
 #endif
   // A tile: FWD/DGRAD ROW [BM][64]; WGRAD COL [64][BM]. B tile: FWD ROW [BN][64]; else COL [64][BN]
   // element geometry: 16-bit operands move 8 elements per 16-B chunk and 64 k per 128-B tile row;
-  // the exact-f32 path (DT_F32, MFMA 16x16x4 f32) moves 4 per chunk and 32 k per row
+  // the exact-f32 path (DT_F32, MFMA 16x16x4 f32) moves 4 per chunk and 32 k per row; the split
+  // path (DT_F32S) reads f32 tensors (two 16-B loads per 8-element chunk) and stages bf16 hi and
+  // lo tiles in the 16-bit LDS layout (the lo images AB_BYTES behind the hi images)
   constexpr bool F32 = DT == DT_F32;
-  constexpr int ES = F32 ? 4 : 2;        // element bytes
-  constexpr int EPC = 16 / ES;           // elements per 16-B chunk
-  constexpr int BKE = 128 / ES;          // k per tile (one 128-B row)
+  constexpr bool SPLIT = DT == DT_F32S;
+  constexpr bool O32 = F32 || SPLIT;     // f32 tensors in memory (operands and C tile)
+  constexpr int MDT = SPLIT ? DT_BF16 : DT;   // MFMA / pack element type of the 16-bit paths
+  constexpr int LES = F32 ? 4 : 2;       // operand element bytes in LDS
+  constexpr int ES = O32 ? 4 : 2;        // element bytes in global memory and in the C tile
+  constexpr int EPC = 16 / LES;          // operand elements per 16-B LDS chunk
+  constexpr int EPO = 16 / ES;           // C-tile elements per 16-B chunk (epilogue)
+  constexpr int BKE = 128 / LES;         // k per tile (one 128-B row)
   constexpr int A_BYTES = BM * 128, B_BYTES = BN * 128;
-  constexpr int STAGE = A_BYTES + B_BYTES;
+  constexpr int AB_BYTES = A_BYTES + B_BYTES;
+  constexpr int STAGE = SPLIT ? 2 * AB_BYTES : AB_BYTES;
   // epilogue partial-sum reduction [3][RG][BN] f32
   constexpr int RED_BYTES = 3 * NT * 8 * 4;
   // staged C tile of the epilogue; f32 stages it in two row halves (one per wave row), so the
   // epilogue needs no more LDS than the main loop and f32 tiles keep 3 resident blocks per CU
-  constexpr int NH = F32 ? 2 : 1;
+  constexpr int NH = O32 ? 2 : 1;
   constexpr int C_BYTES = BM / NH * BN * ES;
   constexpr int LDS_0 = STAGES * STAGE > RED_BYTES ? STAGES * STAGE : RED_BYTES;
   constexpr int LDS_BYTES = LDS_0 > C_BYTES ? LDS_0 : C_BYTES;
@@ -354,6 +364,15 @@ __global__ __launch_bounds__(NT, (conv_min_blocks<DT, BM, BN, STAGES>())) void c
   };
 
   i32x4 ra[AR], rb[BR];
+  i32x4 ra2[SPLIT ? AR : 1], rb2[SPLIT ? BR : 1];   // DT_F32S: elements 4..7 of each chunk
+  auto lda = [&](int i, uint32_t off) __attribute__((always_inline)) {
+    ra[i] = bld(rsa, off);
+    if constexpr (SPLIT) ra2[i] = bld(rsa, off + 16u);   // OOB + 16 stays out of range
+  };
+  auto ldb = [&](int i, uint32_t off) __attribute__((always_inline)) {
+    rb[i] = bld(rsb, off);
+    if constexpr (SPLIT) rb2[i] = bld(rsb, off + 16u);
+  };
   // prologue state: per-chunk validity (padding must stay 0) and the chunk's 8 channel coeffs
   const bool pro = (PASS == FWD || PASS == WGRAD) && p.pro_sc != nullptr;
   bool pv[PASS == FWD ? AR : BR];
@@ -375,7 +394,7 @@ __global__ __launch_bounds__(NT, (conv_min_blocks<DT, BM, BN, STAGES>())) void c
       for (int k = 0; k < 4; ++k)
         v[k] = __float_as_int(fmaxf(__builtin_fmaf(__int_as_float(v[k]), psc[k >> 1][k & 1],
                                                    psh[k >> 1][k & 1]), 0.f));
-    } else {
+    } else if constexpr (!SPLIT) {   // (DT_F32S: pro_apply2)
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
         const f32x2 u = unpack2<DT>((uint32_t)v[k]);
@@ -384,6 +403,32 @@ __global__ __launch_bounds__(NT, (conv_min_blocks<DT, BM, BN, STAGES>())) void c
         v[k] = __builtin_bit_cast(int, __builtin_elementwise_max(h, (s16x2){0, 0}));
       }
     }
+  };
+
+  // DT_F32S: BN+ReLU on the chunk's 8 f32 values (v0: channels 0-3, v1: 4-7)
+  auto pro_apply2 = [&](i32x4& v0, i32x4& v1) __attribute__((always_inline)) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      v0[k] = __float_as_int(fmaxf(__builtin_fmaf(__int_as_float(v0[k]), psc[k >> 1][k & 1],
+                                                  psh[k >> 1][k & 1]), 0.f));
+      v1[k] = __float_as_int(fmaxf(__builtin_fmaf(__int_as_float(v1[k]), psc[2 + (k >> 1)][k & 1],
+                                                  psh[2 + (k >> 1)][k & 1]), 0.f));
+    }
+  };
+  // DT_F32S: 8 f32 -> bf16 hi chunk at base+addr and bf16 lo = bf16(x - hi) chunk AB_BYTES behind
+  auto split_put = [&](char* base, int addr, const i32x4& v0, const i32x4& v1)
+      __attribute__((always_inline)) {
+    i32x4 hi, lo;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const i32x4& v = k < 2 ? v0 : v1;
+      const f32x2 f = f32x2{__int_as_float(v[2 * (k & 1)]), __int_as_float(v[2 * (k & 1) + 1])};
+      const uint32_t h = pack2<DT_BF16>(f);
+      hi[k] = (int)h;
+      lo[k] = (int)pack2<DT_BF16>(f - unpack2<DT_BF16>(h));
+    }
+    *reinterpret_cast<i32x4*>(base + addr) = hi;
+    *reinterpret_cast<i32x4*>(base + AB_BYTES + addr) = lo;
   };
 
   auto load_tile = [&](int kt) __attribute__((always_inline)) {
@@ -402,7 +447,7 @@ __global__ __launch_bounds__(NT, (conv_min_blocks<DT, BM, BN, STAGES>())) void c
         for (int i = 0; i < AR; ++i) {
           const uint32_t mw = word ? (uint32_t)(a_mask[i] >> 32) : (uint32_t)a_mask[i];
           const bool ok = (mw >> bit) & 1u;
-          ra[i] = bld(rsa, ok ? (uint32_t)(a_base[i] + toff) : OOB);
+          lda(i, ok ? (uint32_t)(a_base[i] + toff) : OOB);
           pv[i] = ok;
         }
         if (pro) pro_coeffs(c0 + (tid & 7) * EPC);
@@ -416,7 +461,7 @@ __global__ __launch_bounds__(NT, (conv_min_blocks<DT, BM, BN, STAGES>())) void c
 #pragma unroll
         for (int i = 0; i < AR; ++i) {
           const bool ok = tap_ok && ((a_mask[i] >> (tap & 63)) & 1ull);
-          ra[i] = bld(rsa, ok ? (uint32_t)(a_base[i] + toff) : OOB);
+          lda(i, ok ? (uint32_t)(a_base[i] + toff) : OOB);
           pv[i] = ok;
         }
         if (pro) pro_coeffs(c);
@@ -430,31 +475,31 @@ __global__ __launch_bounds__(NT, (conv_min_blocks<DT, BM, BN, STAGES>())) void c
 #pragma unroll
       for (int i = 0; i < AR; ++i) {
         const bool ok = ((uint32_t)a_mask[i] >> ti) & 1u;
-        ra[i] = bld(rsa, ok ? (uint32_t)(a_base[i] + toff) : OOB);
+        lda(i, ok ? (uint32_t)(a_base[i] + toff) : OOB);
       }
     } else {  // WGRAD A: dY rows m (k), cols n1 (COL tile [64][BM])
       const uint32_t koff = (uint32_t)(kt * BKE * p.Cout) * (uint32_t)ES;
 #pragma unroll
       for (int i = 0; i < AR; ++i)
-        ra[i] = bld(rsa, (k0 + a_krow[i] < kend) ? a_off[i] + koff : OOB);
+        lda(i, (k0 + a_krow[i] < kend) ? a_off[i] + koff : OOB);
     }
     // ---------------- B
     if constexpr (PASS == FWD) {
 #pragma unroll
-      for (int i = 0; i < BR; ++i) rb[i] = bld(rsb, b_off[i] + (uint32_t)k0 * (uint32_t)ES);
+      for (int i = 0; i < BR; ++i) ldb(i, b_off[i] + (uint32_t)k0 * (uint32_t)ES);
     } else if constexpr (PASS == DGRAD) {
       const int ti = p.log2Cout >= 0 ? k0 >> p.log2Cout : k0 / p.Cout;
       const int tap = p.taps[split][ti < 9 ? ti : 0];
       const uint32_t uoff = (uint32_t)(((k0 - ti * p.Cout) * p.R * p.S + tap) * p.Cin) * (uint32_t)ES;
 #pragma unroll
-      for (int i = 0; i < BR; ++i) rb[i] = bld(rsb, b_off[i] + uoff);
+      for (int i = 0; i < BR; ++i) ldb(i, b_off[i] + uoff);
     } else if (wb_direct) {  // WGRAD B, 1x1 stride-1 conv: X rows ARE the GEMM rows
       constexpr int CPR = BN / EPC, RPI = NT / CPR;
 #pragma unroll
       for (int i = 0; i < BR; ++i) {
         const int m = k0 + tid / CPR + RPI * i;
         const bool ok = wb_colok && m < kend;
-        rb[i] = bld(rsb, ok ? (uint32_t)(m * p.Cin + wb_c) * (uint32_t)ES : OOB);
+        ldb(i, ok ? (uint32_t)(m * p.Cin + wb_c) * (uint32_t)ES : OOB);
         pv[i] = ok;
       }
     } else {  // WGRAD B: gathered X rows m, cols (tap, c)
@@ -470,7 +515,7 @@ __global__ __launch_bounds__(NT, (conv_min_blocks<DT, BM, BN, STAGES>())) void c
         const int y = (int)yo * p.stride - p.pad + wb_r, x = (int)xo * p.stride - p.pad + wb_s;
         ok = ok && (unsigned)y < (unsigned)p.H && (unsigned)x < (unsigned)p.W;
         const int off = ((((int)img * p.H + y) * p.W + x) * p.Cin + wb_c) * ES;
-        rb[i] = bld(rsb, ok ? (uint32_t)off : OOB);
+        ldb(i, ok ? (uint32_t)off : OOB);
         if constexpr (PASS == WGRAD) pv[i] = ok;
       }
     }
@@ -483,9 +528,15 @@ __global__ __launch_bounds__(NT, (conv_min_blocks<DT, BM, BN, STAGES>())) void c
 #pragma unroll
       for (int i = 0; i < AR; ++i) {
         if constexpr (PASS == FWD) {
-          if (pro && pv[i]) pro_apply(ra[i]);
+          if constexpr (SPLIT) {
+            if (pro && pv[i]) pro_apply2(ra[i], ra2[i]);
+          } else {
+            if (pro && pv[i]) pro_apply(ra[i]);
+          }
         }
-        *reinterpret_cast<i32x4*>(sa + row_addr((tid >> 3) + 32 * i, tid & 7)) = ra[i];
+        const int addr = row_addr((tid >> 3) + 32 * i, tid & 7);
+        if constexpr (SPLIT) split_put(sa, addr, ra[i], ra2[i]);
+        else *reinterpret_cast<i32x4*>(sa + addr) = ra[i];
       }
     } else {
       constexpr int CPR = BM / EPC, RPI = NT / CPR;
@@ -493,23 +544,32 @@ __global__ __launch_bounds__(NT, (conv_min_blocks<DT, BM, BN, STAGES>())) void c
       for (int i = 0; i < AR; ++i) {
         const int ca = F32 ? col_addr_f32<BM>(tid / CPR + RPI * i, tid % CPR)
                            : col_addr<BM>(tid / CPR + RPI * i, tid % CPR);
-        *reinterpret_cast<i32x4*>(sa + ca) = ra[i];
+        if constexpr (SPLIT) split_put(sa, ca, ra[i], ra2[i]);
+        else *reinterpret_cast<i32x4*>(sa + ca) = ra[i];
       }
     }
     if constexpr (B_ROW) {
 #pragma unroll
-      for (int i = 0; i < BR; ++i)
-        *reinterpret_cast<i32x4*>(sb + row_addr((tid >> 3) + 32 * i, tid & 7)) = rb[i];
+      for (int i = 0; i < BR; ++i) {
+        const int addr = row_addr((tid >> 3) + 32 * i, tid & 7);
+        if constexpr (SPLIT) split_put(sb, addr, rb[i], rb2[i]);
+        else *reinterpret_cast<i32x4*>(sb + addr) = rb[i];
+      }
     } else {
       constexpr int CPR = BN / EPC, RPI = NT / CPR;
 #pragma unroll
       for (int i = 0; i < BR; ++i) {
         if constexpr (PASS == WGRAD) {
-          if (pro && pv[i]) pro_apply(rb[i]);
+          if constexpr (SPLIT) {
+            if (pro && pv[i]) pro_apply2(rb[i], rb2[i]);
+          } else {
+            if (pro && pv[i]) pro_apply(rb[i]);
+          }
         }
         const int cb_ = F32 ? col_addr_f32<BN>(tid / CPR + RPI * i, tid % CPR)
                             : col_addr<BN>(tid / CPR + RPI * i, tid % CPR);
-        *reinterpret_cast<i32x4*>(sb + cb_) = rb[i];
+        if constexpr (SPLIT) split_put(sb, cb_, rb[i], rb2[i]);
+        else *reinterpret_cast<i32x4*>(sb + cb_) = rb[i];
       }
     }
   };
@@ -609,10 +669,37 @@ __global__ __launch_bounds__(NT, (conv_min_blocks<DT, BM, BN, STAGES>())) void c
         if constexpr (B_ROW) fb[j] = frag_row(sb, cbase, s, lane);
         else fb[j] = frag_col<BN>(sb, cbase, s, lane);
       }
+      if constexpr (SPLIT) {   // a*b ~ a_hi*b_hi + a_hi*b_lo + a_lo*b_hi
+        s16x8 fl[NI > MI ? NI : MI];
+#pragma unroll
+        for (int j = 0; j < NI; ++j) {
+          const int cbase = wc * (BN / 2) + j * 16;
+          if constexpr (B_ROW) fl[j] = frag_row(sb + AB_BYTES, cbase, s, lane);
+          else fl[j] = frag_col<BN>(sb + AB_BYTES, cbase, s, lane);
+        }
+#pragma unroll
+        for (int i = 0; i < MI; ++i)
+#pragma unroll
+          for (int j = 0; j < NI; ++j) {
+            acc[i][j] = mfma16<MDT>(fb[j], fa[i], acc[i][j]);
+            acc[i][j] = mfma16<MDT>(fl[j], fa[i], acc[i][j]);
+          }
+#pragma unroll
+        for (int i = 0; i < MI; ++i) {
+          const int rbase = wr * (BM / 2) + i * 16;
+          if constexpr (A_ROW) fl[i] = frag_row(sa + AB_BYTES, rbase, s, lane);
+          else fl[i] = frag_col<BM>(sa + AB_BYTES, rbase, s, lane);
+        }
+#pragma unroll
+        for (int i = 0; i < MI; ++i)
+#pragma unroll
+          for (int j = 0; j < NI; ++j) acc[i][j] = mfma16<MDT>(fb[j], fl[i], acc[i][j]);
+      } else {
 #pragma unroll
       for (int i = 0; i < MI; ++i)
 #pragma unroll
-        for (int j = 0; j < NI; ++j) acc[i][j] = mfma16<DT>(fb[j], fa[i], acc[i][j]);
+        for (int j = 0; j < NI; ++j) acc[i][j] = mfma16<MDT>(fb[j], fa[i], acc[i][j]);
+      }
       }
     }
     }   // MF == 16
@@ -681,7 +768,7 @@ __global__ __launch_bounds__(NT, (conv_min_blocks<DT, BM, BN, STAGES>())) void c
     const bool relu = p.relu != 0;
     // stage the C tile through LDS: [BM][BN], row pitch BN*ES bytes, 16-B chunks swizzled by
     // row; one packed 8-byte store (4 columns) per item per lane (f32: one 16-B store).
-    constexpr int CPR = BN / EPC;
+    constexpr int CPR = BN / EPO;
     auto c_addr = [&](int row, int chunk) { return row * CPR + (chunk ^ (row & (CPR - 1))); };
     // f32: the waves of wave-row h write their tiles to local rows [0, BM/2) of the LDS image
     auto stage_f32 = [&](int h) __attribute__((always_inline)) {
@@ -692,7 +779,7 @@ __global__ __launch_bounds__(NT, (conv_min_blocks<DT, BM, BN, STAGES>())) void c
         *reinterpret_cast<f32x4*>(smem + rl * (BN * 4) + (((col >> 2) ^ (rl & (CPR - 1))) << 4)) = v;
       });
     };
-    if constexpr (!F32) {
+    if constexpr (!O32) {
       for_items([&](int rl, int cl, f32x4 v) {
         const int col = wc * (BN / 2) + cl;
         const int row = wr * (BM / 2) + rl;
@@ -725,7 +812,7 @@ __global__ __launch_bounds__(NT, (conv_min_blocks<DT, BM, BN, STAGES>())) void c
     // which bounds the prefetch registers to PD rows.
     constexpr int PD = RPTH > 4 ? 4 : RPTH;
     char* outb = reinterpret_cast<char*>(p.out);
-    const int gcol = n0 + cc * EPC;
+    const int gcol = n0 + cc * EPO;
     auto row_off = [&](int i, bool& ok) __attribute__((always_inline)) -> uint32_t {
       const int grow = m0 + rg + RG * i;
       ok = grow < p.M && gcol < p.N;
@@ -749,7 +836,7 @@ __global__ __launch_bounds__(NT, (conv_min_blocks<DT, BM, BN, STAGES>())) void c
       if constexpr (MODE >= 0 && MODE != 3) {
         const int cg = gcol < p.N ? gcol : 0;
 #pragma unroll
-        for (int k = 0; k < EPC / 2; ++k) {
+        for (int k = 0; k < EPO / 2; ++k) {
           esc[k] = f32x2{p.esc[cg + 2 * k], p.esc[cg + 2 * k + 1]};
           esh[k] = f32x2{p.esh[cg + 2 * k], p.esh[cg + 2 * k + 1]};
           if constexpr (MODE == 2) {
@@ -785,7 +872,7 @@ __global__ __launch_bounds__(NT, (conv_min_blocks<DT, BM, BN, STAGES>())) void c
       constexpr bool SHIFTED = PASS == FWD && MODE < 0;   // forward statistics: shifted sums
 #pragma unroll
       for (int h = 0; h < NH; ++h) {
-      if constexpr (F32) {
+      if constexpr (O32) {
         if (h > 0) __syncthreads();   // every thread is done reading the previous half
         stage_f32(h);
       }
@@ -793,7 +880,7 @@ __global__ __launch_bounds__(NT, (conv_min_blocks<DT, BM, BN, STAGES>())) void c
       __syncthreads();
       if (SHIFTED && h == 0 && do_stats) {   // shift = the tile's first row (always a valid row)
         const i32x4 v0 = *reinterpret_cast<const i32x4*>(ct + c_addr(0, cc) * 16);
-        if constexpr (F32) {
+        if constexpr (O32) {
 #pragma unroll
           for (int e = 0; e < 4; ++e) shv[e >> 1][e & 1] = __int_as_float(v0[e]);
         } else {
@@ -809,7 +896,7 @@ __global__ __launch_bounds__(NT, (conv_min_blocks<DT, BM, BN, STAGES>())) void c
           const int row = rg + RG * (g0 + j);   // local row of the staged half
           i32x4 v = *reinterpret_cast<const i32x4*>(ct + c_addr(row, cc) * 16);
           if (!eok[j]) continue;
-          if constexpr (F32) {   // one element per dword
+          if constexpr (O32) {   // one element per dword
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
               const int k = e >> 1, h = e & 1;
@@ -877,12 +964,12 @@ __global__ __launch_bounds__(NT, (conv_min_blocks<DT, BM, BN, STAGES>())) void c
         __syncthreads();
         float* red = reinterpret_cast<float*>(smem);  // [NQ][RG][BN] (+ FWD: shift row)
 #pragma unroll
-        for (int k = 0; k < EPC / 2; ++k) {
-          *reinterpret_cast<f32x2*>(red + rg * BN + cc * EPC + 2 * k) = q0[k];
-          *reinterpret_cast<f32x2*>(red + RG * BN + rg * BN + cc * EPC + 2 * k) = q1[k];
-          if constexpr (NQ > 2) *reinterpret_cast<f32x2*>(red + 2 * RG * BN + rg * BN + cc * EPC + 2 * k) = q2[k];
+        for (int k = 0; k < EPO / 2; ++k) {
+          *reinterpret_cast<f32x2*>(red + rg * BN + cc * EPO + 2 * k) = q0[k];
+          *reinterpret_cast<f32x2*>(red + RG * BN + rg * BN + cc * EPO + 2 * k) = q1[k];
+          if constexpr (NQ > 2) *reinterpret_cast<f32x2*>(red + 2 * RG * BN + rg * BN + cc * EPO + 2 * k) = q2[k];
           if constexpr (SHIFTED) {
-            if (rg == 0) *reinterpret_cast<f32x2*>(red + 2 * RG * BN + cc * EPC + 2 * k) = shv[k];
+            if (rg == 0) *reinterpret_cast<f32x2*>(red + 2 * RG * BN + cc * EPO + 2 * k) = shv[k];
           }
         }
         __syncthreads();
@@ -1004,7 +1091,7 @@ static int g_mfma = 16;
 
 template <int PASS, int DT, int BM, int BN, int ST>
 static int launch(const ConvParams& p, dim3 grid, hipStream_t st) {
-  if constexpr (DT != DT_F32) {
+  if constexpr (DT == DT_BF16 || DT == DT_F16) {
     if (g_mfma == 32) {
       hipLaunchKernelGGL((conv_gemm_kernel<PASS, DT, BM, BN, ST, 32>), grid, dim3(NT), 0, st, p);
       return (int)hipGetLastError();
@@ -1026,6 +1113,9 @@ static int dispatch(int dt, int bm, int bn, const ConvParams& p, dim3 grid, hipS
     if constexpr (PASS == WGRAD) { PDA_CASE1(DT_BF16, 256, 128) PDA_CASE1(DT_F16, 256, 128) }
     PDA_CASE1(DT_F16, 128, 128) PDA_CASE1(DT_F16, 128, 64) PDA_CASE1(DT_F16, 64, 128)
     PDA_CASE1(DT_F32, 128, 128) PDA_CASE1(DT_F32, 128, 64) PDA_CASE1(DT_F32, 64, 128)
+    // the split-f32 path stages hi + lo tiles: single-stage only (LDS)
+    PDA_CASE1(DT_F32S, 128, 128) PDA_CASE1(DT_F32S, 128, 64) PDA_CASE1(DT_F32S, 64, 128)
+    PDA_CASE1(DT_F32S, 64, 64)
 #undef PDA_CASE1
     return -1;
   }
@@ -1043,7 +1133,7 @@ static int dispatch(int dt, int bm, int bn, const ConvParams& p, dim3 grid, hipS
 
 // the kernels address operands with 32-bit buffer offsets (range-checked, OOB = 0x80000000)
 static bool fits32(long long a, long long b, long long c, int dt) {
-  const long long lim = 0x7fffffffll, es = dt == DT_F32 ? 4 : 2;
+  const long long lim = 0x7fffffffll, es = (dt == DT_F32 || dt == DT_F32S) ? 4 : 2;
   return a * es < lim && b * es < lim && c * 4 < lim;
 }
 

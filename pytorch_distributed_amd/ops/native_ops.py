@@ -96,9 +96,26 @@ _WGRAD_TARGET = int(os.environ.get("PDA_WGRAD_TARGET", 2 * _NUM_CU))
 
 
 _SINGLE_STAGE = os.environ.get("PDA_SINGLE_STAGE", "1") != "0"
+# f32 convolutions: "exact" = MFMA 16x16x4 f32 (DT_F32); "split" = f32 tensors with the products on
+# the bf16 MFMA as a three-term hi/lo split (DT_F32S, ~16 significant bits per product -- above
+# the TF32 convolutions of the reference's fp32 runs; csrc/common.h DType)
+_F32_CONV = os.environ.get("PDA_F32_CONV", "exact")
 _STATS_S = os.environ.get("PDA_STATS_S")   # fixed slab count of the statistics kernels (A/B)
 # scale on the split-K block targets (the wgrads run beside the dgrad chain on a second stream)
 _WGRAD_TB_SCALE = float(os.environ.get("PDA_WGRAD_TB_SCALE", "1.0"))
+
+
+def _kdt(t: torch.Tensor) -> int:
+    """Kernel dtype code of a conv launch on tensor ``t`` (see _F32_CONV)."""
+    d = dt_of(t)
+    return 3 if d == 0 and _F32_CONV == "split" else d
+
+
+def _ktile(bm: int, bn: int, kdt: int) -> Tuple[int, int]:
+    """The split-f32 kernels stage hi + lo tiles: single-stage tiles of at most 128 x 128."""
+    if kdt != 3:
+        return bm, bn
+    return -min(abs(bm), 128), min(bn, 128)
 
 
 def pick_tile(M: int, N: int, K: Optional[int] = None) -> Tuple[int, int]:
@@ -153,9 +170,11 @@ def conv_fwd(x: torch.Tensor, w: torch.Tensor, g: ConvGeom, out: torch.Tensor,
     T = math.ceil(M / abs(bm))
     if bn is not None:
         stats = bn.ws.get("fwd_stats", T * 3 * g.Cout)
+    kdt = _kdt(x)
+    kbm, kbn = _ktile(bm, bn_, kdt)
     rc = ext.lib().pda_conv_fwd(C.byref(d), ptr(x), ptr(w), Kpad, ptr(out), int(out_f32), pitch,
                                 ptr(bias), ptr(stats), int(relu), ptr(pro[0] if pro else None),
-                                ptr(pro[1] if pro else None), dt_of(x), bm, bn_, stream(x.device))
+                                ptr(pro[1] if pro else None), kdt, kbm, kbn, stream(x.device))
     check(rc, "conv_fwd")
     if bn is not None:
         bn_finalize_partials(stats, T, g.Cout, abs(bm), M, bn)
@@ -238,8 +257,10 @@ def conv_dgrad(dy: torch.Tensor, w: torch.Tensor, g: ConvGeom, dx: torch.Tensor,
     Nb = dy.shape[0]
     bm, bn = tile or dgrad_tile(g, Nb)
     d = g.desc(Nb)
+    kdt = _kdt(dy)
+    kbm, kbn = _ktile(bm, bn, kdt)
     rc = ext.lib().pda_conv_dgrad(C.byref(d), ptr(dy), ptr(w), ptr(dx),
-                                  C.byref(epi) if epi is not None else None, dt_of(dy), bm, bn,
+                                  C.byref(epi) if epi is not None else None, kdt, kbm, kbn,
                                   stream(dy.device))
     check(rc, "conv_dgrad")
     return dx
@@ -341,9 +362,11 @@ def conv_wgrad(dy: torch.Tensor, x: torch.Tensor, g: ConvGeom, grad: torch.Tenso
     slab = ws.get("wgrad_slab", splits * M * N)
     d = g.desc(Nb)
     st = stream(dy.device)
+    kdt = _kdt(dy)
+    kbm, kbn = _ktile(bm, bn, kdt)
     rc = ext.lib().pda_conv_wgrad(C.byref(d), ptr(dy), ptr(x), ptr(slab), splits, k_chunk,
                                   ptr(pro[0] if pro else None), ptr(pro[1] if pro else None),
-                                  dt_of(dy), bm, bn, st)
+                                  kdt, kbm, kbn, st)
     check(rc, "conv_wgrad")
     cr = g.Cin if cin_real is None else cin_real
     rc = ext.lib().pda_wgrad_reduce(ptr(slab), ptr(grad), splits, M, N, int(math.log2(g.Cin)), cr,
