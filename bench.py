@@ -25,8 +25,11 @@ Self-validation for N > 1 (everything below runs AFTER the timed region):
   an error, not a hang.
 
 ``fp32_images_per_sec``: a short pass of the same step in exact fp32 (the reference
-scripts' precision) so the like-for-like number is measured in the same run. For N > 1
-each rank runs it without gradient all-reduce (per-GPU fp32 compute, aggregated).
+scripts' precision) so the like-for-like number is measured in the same run; and
+``fp32_split_images_per_sec``: the same f32 step with the convolutions on the bf16 MFMA as a
+hi/lo three-term split (~16 significant bits per product -- the reference's fp32 runs use TF32
+convolutions, 10 bits). For N > 1 each rank runs them without gradient all-reduce (per-GPU fp32
+compute, aggregated).
 
 Reference metric: images/sec whole node at bs 400/GPU; published
 (derived) 717.0 img/s on 1 GPU (fp32/TF32) and 5,546.7 img/s on 8 GPUs (AMP-DDP "Apex").
@@ -182,20 +185,34 @@ def _verify_consistent(ctx: Ctx, tr) -> dict:
     return {"weights_consistent": ok, "checksum": [int(v) for v in cs.tolist()]}
 
 
-def _fp32_pass(ctx: Ctx, args) -> dict:
-    """Short exact-fp32 pass (reference precision), each rank locally (no all-reduce)."""
+def _fp32_pass(ctx: Ctx, args, mode: str = "exact") -> dict:
+    """Short fp32 pass (reference precision), each rank locally (no all-reduce). ``mode``: the f32
+    convolution math of the native engine -- "exact" (MFMA 16x16x4 f32) or "split" (bf16 MFMA on a
+    hi/lo three-term split, ~16 significant bits per product: above the TF32 convolutions the
+    reference's fp32 runs use by default)."""
     from pytorch_distributed_amd.bench_step import make_trainer
-    tr = make_trainer(args.arch, args.batch, torch.float32, ctx.device, engine=args.engine,
-                      world=1, rank=0, bucket_mb=args.bucket_mb, image_size=args.image_size)
-    for i in range(2):
-        tr.step(i)
-    el = _timed(ctx, tr, 2, args.fp32_steps)
+    from pytorch_distributed_amd.ops import native_ops as K
+    old, K._F32_CONV = K._F32_CONV, mode
+    try:
+        tr = make_trainer(args.arch, args.batch, torch.float32, ctx.device, engine=args.engine,
+                          world=1, rank=0, bucket_mb=args.bucket_mb, image_size=args.image_size)
+        if mode != "exact" and tr.engine != "native":
+            return {}
+        for i in range(2):
+            tr.step(i)
+        el = _timed(ctx, tr, 2, args.fp32_steps)
+    finally:
+        K._F32_CONV = old
     world = ctx.world if ctx.multi else 1
-    res = {"fp32_images_per_sec": round(args.batch * world * args.fp32_steps / el, 2),
-           "fp32_ms_per_step": round(1000.0 * el / args.fp32_steps, 3),
-           "fp32_engine": tr.engine,
-           "fp32_mode": "single" if world == 1 else "per-rank local steps, no all-reduce"}
+    key = "fp32" if mode == "exact" else "fp32_split"
+    res = {f"{key}_images_per_sec": round(args.batch * world * args.fp32_steps / el, 2),
+           f"{key}_ms_per_step": round(1000.0 * el / args.fp32_steps, 3)}
+    if mode == "exact":
+        res.update({"fp32_engine": tr.engine,
+                    "fp32_mode": "single" if world == 1 else "per-rank local steps, no all-reduce"})
     del tr
+    if ctx.cuda:
+        torch.cuda.empty_cache()
     return res
 
 
@@ -262,6 +279,7 @@ def main():
         if ctx.cuda:
             torch.cuda.empty_cache()
         fp32 = _fp32_pass(ctx, args)
+        fp32.update(_fp32_pass(ctx, args, "split"))
     if ctx.rank == 0:
         rec = {
             "metric": METRIC,
@@ -285,6 +303,8 @@ def main():
         }
         if fp32 and base:
             rec["vs_baseline_fp32"] = round(fp32["fp32_images_per_sec"] / base, 3)
+            if "fp32_split_images_per_sec" in fp32:
+                rec["vs_baseline_fp32_split"] = round(fp32["fp32_split_images_per_sec"] / base, 3)
         print(json.dumps(rec), flush=True)
     if consistency.get("weights_consistent") is False:
         print(f"bench: rank {ctx.rank}: parameters differ across ranks after training "

@@ -99,7 +99,9 @@ _SINGLE_STAGE = os.environ.get("PDA_SINGLE_STAGE", "1") != "0"
 # f32 convolutions: "exact" = MFMA 16x16x4 f32 (DT_F32); "split" = f32 tensors with the products on
 # the bf16 MFMA as a three-term hi/lo split (DT_F32S, ~16 significant bits per product -- above
 # the TF32 convolutions of the reference's fp32 runs; csrc/common.h DType)
-_F32_CONV = os.environ.get("PDA_F32_CONV", "exact")
+_F32_CONV = os.environ.get("PDA_F32_CONV", os.environ.get("MX_F32_CONV", "exact"))
+if _F32_CONV not in ("exact", "split"):
+    raise ValueError(f"MX_F32_CONV / PDA_F32_CONV must be exact|split, got {_F32_CONV!r}")
 _STATS_S = os.environ.get("PDA_STATS_S")   # fixed slab count of the statistics kernels (A/B)
 # scale on the split-K block targets (the wgrads run beside the dgrad chain on a second stream)
 _WGRAD_TB_SCALE = float(os.environ.get("PDA_WGRAD_TB_SCALE", "1.0"))
