@@ -102,6 +102,7 @@ _SINGLE_STAGE = os.environ.get("PDA_SINGLE_STAGE", "1") != "0"
 _F32_CONV = os.environ.get("PDA_F32_CONV", os.environ.get("MX_F32_CONV", "exact"))
 if _F32_CONV not in ("exact", "split"):
     raise ValueError(f"MX_F32_CONV / PDA_F32_CONV must be exact|split, got {_F32_CONV!r}")
+_SPLIT_BN = int(os.environ.get("PDA_SPLIT_BN", "128"))   # widest N tile of the split kernels (A/B)
 _STATS_S = os.environ.get("PDA_STATS_S")   # fixed slab count of the statistics kernels (A/B)
 # scale on the split-K block targets (the wgrads run beside the dgrad chain on a second stream)
 _WGRAD_TB_SCALE = float(os.environ.get("PDA_WGRAD_TB_SCALE", "1.0"))
@@ -117,7 +118,7 @@ def _ktile(bm: int, bn: int, kdt: int) -> Tuple[int, int]:
     """The split-f32 kernels stage hi + lo tiles: single-stage tiles of at most 128 x 128."""
     if kdt != 3:
         return bm, bn
-    return -min(abs(bm), 128), min(bn, 128)
+    return -min(abs(bm), 128), min(bn, _SPLIT_BN)
 
 
 def pick_tile(M: int, N: int, K: Optional[int] = None) -> Tuple[int, int]:
