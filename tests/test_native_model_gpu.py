@@ -110,6 +110,8 @@ def test_optimizer_step_and_state_dict():
 
 
 def test_eval_forward_uses_running_stats():
+    """Eval mode normalises with the running statistics (two training forwards first): the native
+    bf16 logits must be as close to the fp32 model as PyTorch's own bf16 autocast is."""
     tm, nm = _pair("resnet18")
     x = torch.randn(4, 3, 64, 64, device=DEV)
     for _ in range(2):
@@ -118,7 +120,12 @@ def test_eval_forward_uses_running_stats():
     tm.eval()
     nm.eval()
     with torch.no_grad():
-        assert rel_err(nm(x), tm(x)) < 0.05
+        ref = tm(x)
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            e_bf16 = rel_err(tm(x), ref)
+        e_nat = rel_err(nm(x), ref)
+    print(f"eval logits vs fp32: native {e_nat:.2e}, torch bf16 autocast {e_bf16:.2e}")
+    assert e_nat < 1.5 * e_bf16 + 2e-3, (e_nat, e_bf16)
 
 
 def test_training_reduces_loss_native():
