@@ -485,7 +485,11 @@ class NativeResNet(nn.Module):
             ys, acts = [], [h]
             pro = None
             yd = None
-            ds_side = b.ds is not None and self._side is not None and self.ds_stream
+            # (SyncBatchNorm: the shortcut BN's all-reduce must not run on a second stream beside
+            # the main chain's -- two streams on one communicator can order its collectives
+            # differently on different ranks and deadlock -- so the shortcut stays on the chain)
+            ds_side = (b.ds is not None and self._side is not None and self.ds_stream
+                       and self.ws.sync_comm is None)
             if ds_side:   # the shortcut conv (+BN stats) runs beside conv1..conv3 on the 2nd stream
                 cur = torch.cuda.current_stream(self.device)
                 self._side.wait_stream(cur)
