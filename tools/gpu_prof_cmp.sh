@@ -1,7 +1,8 @@
 #!/bin/bash
 # GPU-box script: rocprofv3 kernel traces of the round-1 tree (_r1/, a git worktree of 13df5b0
-# with its own in-tree build) and of the current tree under env variants, back to back on one
-# device, for per-kernel regression hunting (tools/prof_cmp.py).
+# with its own in-tree build) and of the current tree under env variants (PROF_VARIANTS: a list of
+# VAR=value, default the current defaults), back to back on one device, for per-kernel regression
+# hunting (tools/prof_cmp.py).
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 cd /tmp && export TMPDIR=/tmp
@@ -13,6 +14,8 @@ run() {  # name dir envs...
 }
 run prof_r1 $R/_r1 PDA_X=1 || exit 1
 EXTRA="--fp32-steps 0"
-for v in ${PROF_VARIANTS:-bwd 1 0}; do
-  run prof_$v $R PDA_INLAUNCH_BN=$v || exit 1
+i=0
+for v in ${PROF_VARIANTS:-PDA_X=1}; do
+  i=$((i+1))
+  run prof_$i $R $v || exit 1
 done
