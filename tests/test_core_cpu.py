@@ -180,3 +180,21 @@ def test_loss_scaler_state_machine_matches_gradscaler():
     s2 = LossScaler()
     s2.load_state_dict(sd)
     assert s2.get_scale() == 16.0
+
+
+def test_f32_conv_mode_dtype_and_tile_mapping(monkeypatch):
+    """MX_F32_CONV / PDA_F32_CONV: f32 tensors map to kernel dtype 0 (exact f32 MFMA) or 3
+    (split bf16 MFMA); the split kernels exist only as single-stage tiles of at most 128 x 128, so
+    every (bm, bn) request is mapped onto one of those; 16-bit tensors are never affected."""
+    import torch
+    from pytorch_distributed_amd.ops import native_ops as K
+    f32, bf16 = torch.zeros(1), torch.zeros(1, dtype=torch.bfloat16)
+    monkeypatch.setattr(K, "_F32_CONV", "exact")
+    assert K._kdt(f32) == 0 and K._kdt(bf16) == 1
+    monkeypatch.setattr(K, "_F32_CONV", "split")
+    assert K._kdt(f32) == 3 and K._kdt(bf16) == 1
+    assert K._ktile(128, 128, 3) == (-128, 128)
+    assert K._ktile(-256, 128, 3) == (-128, 128)
+    assert K._ktile(64, 64, 3) == (-64, 64)
+    assert K._ktile(128, 256, 3) == (-128, 128)
+    assert K._ktile(128, 64, 1) == (128, 64)          # other dtypes untouched
