@@ -143,6 +143,14 @@ class NativeResNet(nn.Module):
         self._side = (torch.cuda.Stream(device) if os.environ.get("PDA_WGRAD_STREAM", "1") != "0"
                       else None)
         self.ws_w = Workspace(device) if self._side is not None else self.ws
+        # "block" (default): queue a block's weight-gradient kernels and fork the wgrad stream ONCE
+        # per residual block instead of once per conv (fewer cross-stream edges; in a captured
+        # graph every fork / join edge becomes a cross-queue barrier packet); "stage": once per
+        # stage; "0": once per conv (profiles/ab_r2_inlaunch_bn.md section 9)
+        self._wbatch_mode = os.environ.get("PDA_WGRAD_BATCH", "block")
+        if self._wbatch_mode not in ("0", "block", "stage"):
+            raise ValueError(f"PDA_WGRAD_BATCH={self._wbatch_mode!r}: expected 0, block or stage")
+        self._wbatch = [] if self._side is not None and self._wbatch_mode != "0" else None
         # optionally run the dgrad/BN-backward chain (the critical path) on a high-priority stream
         self._chain = (torch.cuda.Stream(device, priority=-1)
                        if self._side is not None and os.environ.get("PDA_CHAIN_PRIO", "0") == "1"
@@ -561,10 +569,24 @@ class NativeResNet(nn.Module):
         if self._side is None:
             fn(self.ws)
             return
+        if self._wbatch is not None:
+            self._wbatch.append(fn)
+            self._keep.extend(keep)
+            return
         self._side.wait_stream(torch.cuda.current_stream(self.device))
         with torch.cuda.stream(self._side):
             fn(self.ws_w)
         self._keep.extend(keep)
+
+    def _flush_wgrad(self) -> None:
+        """Run the queued weight-gradient kernels (PDA_WGRAD_BATCH=block) after one fork."""
+        if not self._wbatch:
+            return
+        self._side.wait_stream(torch.cuda.current_stream(self.device))
+        with torch.cuda.stream(self._side):
+            for fn in self._wbatch:
+                fn(self.ws_w)
+        self._wbatch.clear()
 
     def _grads_ready(self, red, upto: int) -> None:
         """DDP bucket readiness: the bucket's BN grads come from the main stream, its conv weight
@@ -572,6 +594,7 @@ class NativeResNet(nn.Module):
         if self._side is None:
             red.grads_ready(upto)
             return
+        self._flush_wgrad()
         self._side.wait_stream(torch.cuda.current_stream(self.device))
         with torch.cuda.stream(self._side):
             red.grads_ready(upto)
@@ -631,6 +654,8 @@ class NativeResNet(nn.Module):
             rec = sv["blocks"][bi]
             prev = (self.blocks[bi - 1], sv["blocks"][bi - 1]) if bi > 0 else None
             dx_main, shortcut_g, tail = self._block_backward(b, rec, tail, prev, acc)
+            if self._wbatch_mode == "block" or b.ds is not None:
+                self._flush_wgrad()
             if red is not None:
                 self._grads_ready(red, self.block_bounds[nblk - bi])
         # ---- stem: maxpool backward of (main + shortcut) gradients, BN backward, wgrad
@@ -655,6 +680,7 @@ class NativeResNet(nn.Module):
             K.conv_wgrad(dy0, x0, g0, self.stem_wgrad, w)
             K.stem_s2d_grad(self.stem_wgrad, self.wgrad_view(u), accumulate=acc)
         self._wgrad(stem_wgrad, dy0, x0)
+        self._flush_wgrad()
         if self._side is not None:   # join: the optimizer step reads every gradient
             torch.cuda.current_stream(self.device).wait_stream(self._side)
             self._keep.clear()
