@@ -842,6 +842,123 @@ __global__ __launch_bounds__(NT) void bn_bwd_apply_dz_kernel(const void* __restr
   }
 }
 
+// 16-bit streaming forms with U independent 16-byte chunks per thread per trip: all U loads of
+// both inputs are issued before the first use, so each lane keeps 2U (apply-dz) / up to 2U (apply)
+// requests in flight instead of 2 -- the per-CU bytes in flight, not the instruction count, set
+// a streaming kernel's HBM rate. The caller guarantees (stride % C8) == 0, so every chunk of a
+// thread shares one channel octet: coefficients are loaded once. NTM bit 0: nontemporal loads,
+// bit 1: nontemporal stores.
+template <int NTL>
+__device__ __forceinline__ i32x4 ldnt(const i32x4* p) {
+  if constexpr (NTL) return __builtin_nontemporal_load(p);
+  else return *p;
+}
+
+template <int DT, int U, int NTM>
+__global__ __launch_bounds__(NT) void bn_bwd_apply_dz_u_kernel(const void* __restrict__ dz_in,
+                                                               const void* __restrict__ ysel,
+                                                               const float* __restrict__ k1,
+                                                               const float* __restrict__ k2,
+                                                               const float* __restrict__ k3,
+                                                               void* __restrict__ dy, int n8, int C) {
+  const int C8 = C >> 3;
+  const int stride = gridDim.x * NT;
+  int i = blockIdx.x * NT + threadIdx.x;
+  if (i >= n8) return;
+  f32x2 A[4], B[4], K3[4];
+  {
+    const int c0 = (i % C8) * 8;
+    ld8p<DT>(k1 + c0, A);
+    ld8p<DT>(k2 + c0, B);
+    ld8p<DT>(k3 + c0, K3);
+  }
+  const i32x4* dzp = reinterpret_cast<const i32x4*>(dz_in);
+  const i32x4* yp = reinterpret_cast<const i32x4*>(ysel);
+  i32x4* op = reinterpret_cast<i32x4*>(dy);
+  for (; i + (U - 1) * stride < n8; i += U * stride) {
+    i32x4 dz[U], yv[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      dz[u] = ldnt<NTM & 1>(dzp + i + u * stride);
+      yv[u] = ldnt<NTM & 1>(yp + i + u * stride);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      i32x4 o;
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+        o[k] = (int)pack2<DT>(A[k] * unpack2<DT>((uint32_t)dz[u][k]) +
+                              B[k] * unpack2<DT>((uint32_t)yv[u][k]) + K3[k]);
+      if constexpr (NTM & 2) __builtin_nontemporal_store(o, op + i + u * stride);
+      else op[i + u * stride] = o;
+    }
+  }
+  for (; i < n8; i += stride) {
+    const i32x4 dz = dzp[i], yv = yp[i];
+    i32x4 o;
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      o[k] = (int)pack2<DT>(A[k] * unpack2<DT>((uint32_t)dz[k]) + B[k] * unpack2<DT>((uint32_t)yv[k]) + K3[k]);
+    op[i] = o;
+  }
+}
+
+// bn_apply_kernel's 16-bit path with U chunks per trip (see bn_bwd_apply_dz_u_kernel).
+template <int DT, int U, int NTM>
+__global__ __launch_bounds__(NT) void bn_apply_u_kernel(
+    const void* __restrict__ y, const float* __restrict__ sc, const float* __restrict__ sh,
+    const void* __restrict__ r2, const float* __restrict__ sc2, const float* __restrict__ sh2,
+    void* __restrict__ out, int n8, int C, int mode, int relu, uint8_t* __restrict__ mask) {
+  const int C8 = C >> 3;
+  const int stride = gridDim.x * NT;
+  int i = blockIdx.x * NT + threadIdx.x;
+  if (i >= n8) return;
+  f32x2 a[4], b[4], a2[4], b2[4];
+  {
+    const int c0 = (i % C8) * 8;
+    ld8p<DT>(sc + c0, a);
+    ld8p<DT>(sh + c0, b);
+    if (mode == 2) {
+      ld8p<DT>(sc2 + c0, a2);
+      ld8p<DT>(sh2 + c0, b2);
+    }
+  }
+  const i32x4* yp = reinterpret_cast<const i32x4*>(y);
+  const i32x4* rp = reinterpret_cast<const i32x4*>(r2);
+  i32x4* op = reinterpret_cast<i32x4*>(out);
+  auto one = [&](const i32x4& yv, const i32x4& rv, int j) {
+    i32x4 o;
+    uint32_t bits = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      f32x2 v = unpack2<DT>((uint32_t)yv[k]) * a[k] + b[k];
+      if (mode) {
+        f32x2 w = unpack2<DT>((uint32_t)rv[k]);
+        if (mode == 2) w = w * a2[k] + b2[k];
+        v += w;
+      }
+      if (relu) v = f32x2{fmaxf(v.x, 0.f), fmaxf(v.y, 0.f)};
+      o[k] = (int)pack2<DT>(v);
+      bits |= (v.x > 0.f ? 1u : 0u) << (2 * k);
+      bits |= (v.y > 0.f ? 1u : 0u) << (2 * k + 1);
+    }
+    if constexpr (NTM & 2) __builtin_nontemporal_store(o, op + j);
+    else op[j] = o;
+    if (mask) mask[j] = (uint8_t)bits;
+  };
+  for (; i + (U - 1) * stride < n8; i += U * stride) {
+    i32x4 yv[U], rv[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      yv[u] = ldnt<NTM & 1>(yp + i + u * stride);
+      rv[u] = mode ? ldnt<NTM & 1>(rp + i + u * stride) : i32x4{0, 0, 0, 0};
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) one(yv[u], rv[u], i + u * stride);
+  }
+  for (; i < n8; i += stride) one(yp[i], mode ? rp[i] : i32x4{0, 0, 0, 0}, i);
+}
+
 // first stage of the statistics reduction: [G][QC] partial slabs -> [S][QC] (S << G), coalesced
 __global__ __launch_bounds__(256) void slab_reduce_kernel(const float* __restrict__ in, int G, int QC,
                                                           int rows_per, float* __restrict__ out) {
@@ -866,9 +983,61 @@ inline int grid_for(long long n, int cap = 8192) {
   return (int)(b < 1 ? 1 : (b > cap ? cap : b));
 }
 
+// Streaming-kernel shape for the 16-bit apply passes: chunks per thread per trip (0 = the plain
+// one-chunk kernels), nontemporal policy (bit 0 loads, bit 1 stores), grid cap in blocks.
+// unroll < 0 (auto): tensors of at least min_mb MiB (past the 256 MB Infinity Cache's useful
+// reach, where nothing is gained by keeping them cached for the consumer) take (4, nt loads +
+// stores, 16384); smaller ones the one-chunk kernels (tools/stream_bench.py,
+// profiles/stream_bench_r2.txt: -11 % isolated on the >= 160 MB passes, +10-15 % on the small).
+struct StreamCfg {
+  int unroll, ntm, cap, min_mb;
+};
+StreamCfg g_stream{0, 0, 8192, 100};
+
+// Launch KER<DT, U, NTM> for the configured (U, NTM); false when the shape does not qualify.
+#define PDA_STREAM_DISPATCH(KER, DT, g, st, ...)                                              \
+  do {                                                                                        \
+    const int u_ = g_stream.unroll < 0 ? 4 : g_stream.unroll;                                 \
+    const int m_ = g_stream.unroll < 0 ? 3 : g_stream.ntm;                                    \
+    if (u_ == 2 && m_ == 0) hipLaunchKernelGGL((KER<DT, 2, 0>), dim3(g), dim3(NT), 0, st, __VA_ARGS__); \
+    else if (u_ == 2 && m_ == 1) hipLaunchKernelGGL((KER<DT, 2, 1>), dim3(g), dim3(NT), 0, st, __VA_ARGS__); \
+    else if (u_ == 2 && m_ == 2) hipLaunchKernelGGL((KER<DT, 2, 2>), dim3(g), dim3(NT), 0, st, __VA_ARGS__); \
+    else if (u_ == 2) hipLaunchKernelGGL((KER<DT, 2, 3>), dim3(g), dim3(NT), 0, st, __VA_ARGS__); \
+    else if (u_ == 4 && m_ == 0) hipLaunchKernelGGL((KER<DT, 4, 0>), dim3(g), dim3(NT), 0, st, __VA_ARGS__); \
+    else if (u_ == 4 && m_ == 1) hipLaunchKernelGGL((KER<DT, 4, 1>), dim3(g), dim3(NT), 0, st, __VA_ARGS__); \
+    else if (u_ == 4 && m_ == 2) hipLaunchKernelGGL((KER<DT, 4, 2>), dim3(g), dim3(NT), 0, st, __VA_ARGS__); \
+    else if (u_ == 4) hipLaunchKernelGGL((KER<DT, 4, 3>), dim3(g), dim3(NT), 0, st, __VA_ARGS__); \
+    else if (m_ == 0) hipLaunchKernelGGL((KER<DT, 1, 0>), dim3(g), dim3(NT), 0, st, __VA_ARGS__); \
+    else if (m_ == 1) hipLaunchKernelGGL((KER<DT, 1, 1>), dim3(g), dim3(NT), 0, st, __VA_ARGS__); \
+    else if (m_ == 2) hipLaunchKernelGGL((KER<DT, 1, 2>), dim3(g), dim3(NT), 0, st, __VA_ARGS__); \
+    else hipLaunchKernelGGL((KER<DT, 1, 3>), dim3(g), dim3(NT), 0, st, __VA_ARGS__);         \
+  } while (0)
+
+// grid for the U-chunk kernels: ~n8/U threads, capped; 0 when a thread's chunks would not share
+// one channel octet (stride % C8 != 0)
+inline int stream_grid(long long n8, int C) {
+  if (g_stream.unroll == 0) return 0;
+  const bool autoc = g_stream.unroll < 0;
+  if (autoc && n8 * 16 < ((long long)g_stream.min_mb << 20)) return 0;
+  const int u = autoc ? 4 : g_stream.unroll;
+  const int g = grid_for((n8 + u - 1) / u, autoc ? 16384 : g_stream.cap);
+  return ((long long)g * NT) % (C >> 3) == 0 ? g : 0;
+}
+
 }  // namespace
 
 extern "C" {
+
+// Streaming apply kernels (see StreamCfg): unroll -1 = auto, 0 = the one-chunk kernels, 1/2/4 =
+// that many chunks for every shape. Returns the previous unroll.
+int pda_set_stream_cfg(int unroll, int ntm, int cap, int min_mb) {
+  const int prev = g_stream.unroll;
+  g_stream.unroll = (unroll == 1 || unroll == 2 || unroll == 4 || unroll == -1) ? unroll : 0;
+  g_stream.ntm = ntm & 3;
+  g_stream.cap = cap > 0 ? cap : 8192;
+  g_stream.min_mb = min_mb >= 0 ? min_mb : 100;
+  return prev;
+}
 
 int pda_slab_reduce(const float* in, int G, int QC, int S, float* out, hipStream_t st) {
   const int rows_per = (G + S - 1) / S;
@@ -941,6 +1110,14 @@ int pda_bn_apply(const void* y, const float* sc, const float* sh, const void* r2
   const int g = grid_for(n8);
 #define ARGS (const void*)y, sc, sh, (const void*)r2, sc2, sh2, (void*)out, n8, C, mode, relu, \
              (uint8_t*)mask
+  if (g_stream.unroll != 0 && dt != DT_F32 && (C & 7) == 0) {
+    const int gs = stream_grid(n8, C);
+    if (gs > 0) {
+      if (dt == DT_BF16) PDA_STREAM_DISPATCH(bn_apply_u_kernel, DT_BF16, gs, st, ARGS);
+      else PDA_STREAM_DISPATCH(bn_apply_u_kernel, DT_F16, gs, st, ARGS);
+      return (int)hipGetLastError();
+    }
+  }
   if (dt == DT_BF16) hipLaunchKernelGGL(bn_apply_kernel<DT_BF16>, dim3(g), dim3(NT), 0, st, ARGS);
   else if (dt == DT_F32) hipLaunchKernelGGL(bn_apply_kernel<DT_F32>, dim3(g), dim3(NT), 0, st, ARGS);
   else hipLaunchKernelGGL(bn_apply_kernel<DT_F16>, dim3(g), dim3(NT), 0, st, ARGS);
@@ -1046,6 +1223,14 @@ int pda_bn_bwd_apply(const BwdArgsC* c, const void* dz_in, const void* ysel, con
   const int g = grid_for(a.rows * (a.C / 8));
   if (dz_in && a.rows * (a.C / 8) < (1ll << 31)) {
     const int n8 = (int)(a.rows * (a.C / 8));
+    const int gs = dt != DT_F32 ? stream_grid(n8, a.C) : 0;
+    if (gs > 0) {
+#define KA (const void*)dz_in, (const void*)ysel, k1, k2, k3, (void*)dy, n8, a.C
+      if (dt == DT_BF16) PDA_STREAM_DISPATCH(bn_bwd_apply_dz_u_kernel, DT_BF16, gs, st, KA);
+      else PDA_STREAM_DISPATCH(bn_bwd_apply_dz_u_kernel, DT_F16, gs, st, KA);
+#undef KA
+      return (int)hipGetLastError();
+    }
 #define K(D) hipLaunchKernelGGL(bn_bwd_apply_dz_kernel<D>, dim3(g), dim3(NT), 0, st, (const void*)dz_in, \
                                 (const void*)ysel, k1, k2, k3, (void*)dy, n8, a.C)
     if (dt == DT_BF16) K(DT_BF16); else if (dt == DT_F32) K(DT_F32); else K(DT_F16);

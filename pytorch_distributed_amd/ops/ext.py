@@ -102,7 +102,20 @@ _SIGS = {
     "pda_nchw_to_s2d": [_V, _I, _I, _I, _V, _I, _V],
     "pda_pack_stem_s2d": [_V, _V, _I, _I, _V],
     "pda_stem_s2d_grad": [_V, _V, _I, _I, _V],
+    "pda_set_stream_cfg": [_I, _I, _I, _I],
 }
+
+
+def stream_cfg() -> tuple:
+    """16-bit BN apply passes (csrc/bn.hip StreamCfg): PDA_STREAM = "auto" (default: 4 chunks per
+    thread + nontemporal loads/stores for tensors >= 100 MiB, the one-chunk kernels below) or
+    "U,NTM,CAP[,MIN_MB]" (or ':'-separated) to force one configuration (U = 0: the one-chunk
+    kernels everywhere). In-step A/B (tools/gpu_ab.sh, one box): 30.02 ms (0) vs 29.41 ms (auto)."""
+    v = os.environ.get("PDA_STREAM", "auto")
+    if v == "auto":
+        return (-1, 3, 16384, 100)
+    f = [int(x) for x in v.replace(":", ",").split(",")][:4]
+    return tuple(f + [0, 0, 8192, 100][len(f):])
 
 
 def load(required: bool = False) -> Optional[C.CDLL]:
@@ -126,6 +139,8 @@ def load(required: bool = False) -> Optional[C.CDLL]:
         if getattr(lib, "pda_conv_set_mfma", None) is not None:
             # MFMA shape of the 16-bit conv kernels: 16 = 16x16x32, 32 = 32x32x16
             lib.pda_conv_set_mfma(int(os.environ.get("PDA_MFMA", "16")))
+        if getattr(lib, "pda_set_stream_cfg", None) is not None:
+            lib.pda_set_stream_cfg(*stream_cfg())
         _LIB = lib
     except OSError as e:
         _ERR = str(e)

@@ -159,6 +159,50 @@ def test_bn_forward_finalize_apply():
     assert int(nbt.item()) == 1
 
 
+@pytest.mark.parametrize("cfg", [(0, 0, 8192, 100), (1, 0, 8192, 100), (2, 0, 8192, 100),
+                                 (4, 3, 8192, 100), (2, 3, 7, 100), (4, 1, 3, 100), (-1, 3, 16384, 0)])
+@pytest.mark.parametrize("C", [64, 256, 2048])
+def test_bn_streaming_apply_configs(cfg, C):
+    """bn_apply (modes 0/1/2 + ReLU bitmask) and bn_bwd_apply (dz read back) under every streaming
+    configuration (chunks per thread U, nontemporal policy, grid cap -- small caps force many
+    trips and the remainder loop; -1 = the auto policy with its size threshold at 0) against plain PyTorch fp32 on the same bf16 inputs."""
+    K = _k()
+    from pytorch_distributed_amd.ops import ext
+    L = ext.lib()
+    rows = 1237 * 8   # ragged against U * stride
+    g = torch.Generator(device=DEV).manual_seed(C)
+    mk = lambda: torch.randn(rows, C, device=DEV, generator=g).to(torch.bfloat16)  # noqa: E731
+    y, r, y2 = mk(), mk(), mk()
+    sc, sh, sc2, sh2, k3 = (torch.randn(C, device=DEV, generator=g) for _ in range(5))
+    out = torch.empty_like(y)
+    mask = torch.empty(rows * C // 8, dtype=torch.uint8, device=DEV)
+    bit = 1 << torch.arange(8, device=DEV)
+    try:
+        L.pda_set_stream_cfg(*cfg)
+        for mode in (0, 1, 2):
+            ref = y.float() * sc + sh
+            if mode == 1:
+                ref = ref + r.float()
+            if mode == 2:
+                ref = ref + y2.float() * sc2 + sh2
+            ref = torch.relu(ref)
+            K.bn_apply(y, sc, sh, out, res=r if mode == 1 else None, y2=y2 if mode == 2 else None,
+                       scale2=sc2 if mode == 2 else None, shift2=sh2 if mode == 2 else None, mask=mask)
+            torch.cuda.synchronize()
+            torch.testing.assert_close(out.float(), ref, rtol=1e-2, atol=1e-2)
+            want = ((out.float().reshape(-1, 8) > 0).int() * bit).sum(1).to(torch.uint8)
+            assert torch.equal(mask, want), (cfg, mode)
+        a = K.BwdArgs(None, None, None, 0, K.ptr(y), None, None, None, None, None, 1, None, None, 2,
+                      rows, C)
+        K.check(L.pda_bn_bwd_apply(ext.C.byref(a), K.ptr(r), K.ptr(y), K.ptr(sc), K.ptr(sh), K.ptr(k3),
+                                   K.ptr(out), 1, K.stream(torch.device(DEV))), "bn_bwd_apply")
+        torch.cuda.synchronize()
+        torch.testing.assert_close(out.float(), sc * r.float() + sh * y.float() + k3, rtol=1e-2,
+                                   atol=2e-2)
+    finally:
+        L.pda_set_stream_cfg(*ext.stream_cfg())
+
+
 def _conv_bn(K, x_nhwc, w2d, g, dtype, gamma, beta, tile=None, ws=None):
     ws = ws or K.Workspace(DEV)
     C = g.Cout
