@@ -795,7 +795,7 @@ __global__ __launch_bounds__(NT) void bn_bwd_apply_kernel(BwdArgs a, const void*
     ld8f(k2 + c0, B);
     ld8f(k3 + c0, Cc);
 #pragma unroll
-    for (int e = 0; e < 8; ++e) o[e] = A[e] * dz[e] + B[e] * yv[e] + Cc[e];
+    for (int e = 0; e < 8; ++e) o[e] = bnb_affine(A[e], B[e], Cc[e], dz[e], yv[e]);
     store8<DT>(dy, (size_t)i * 8, o);
   }
 }
@@ -828,7 +828,7 @@ __global__ __launch_bounds__(NT) void bn_bwd_apply_dz_kernel(const void* __restr
       load8<DT>(ysel, (size_t)i * 8, yv);
 #pragma unroll
       for (int e = 0; e < 8; ++e)
-        o[e] = A[e >> 1][e & 1] * dz[e] + B[e >> 1][e & 1] * yv[e] + K3[e >> 1][e & 1];
+        o[e] = bnb_affine(A[e >> 1][e & 1], B[e >> 1][e & 1], K3[e >> 1][e & 1], dz[e], yv[e]);
       store8<DT>(dy, (size_t)i * 8, o);
       continue;
     }
@@ -837,7 +837,8 @@ __global__ __launch_bounds__(NT) void bn_bwd_apply_dz_kernel(const void* __restr
     i32x4 o;
 #pragma unroll
     for (int k = 0; k < 4; ++k)
-      o[k] = (int)pack2<DT>(A[k] * unpack2<DT>((uint32_t)dz[k]) + B[k] * unpack2<DT>((uint32_t)yv[k]) + K3[k]);
+      o[k] = (int)pack2<DT>(bnb_affine2(A[k], B[k], K3[k], unpack2<DT>((uint32_t)dz[k]),
+                                        unpack2<DT>((uint32_t)yv[k])));
     reinterpret_cast<i32x4*>(dy)[i] = o;
   }
 }
@@ -887,8 +888,8 @@ __global__ __launch_bounds__(NT) void bn_bwd_apply_dz_u_kernel(const void* __res
       i32x4 o;
 #pragma unroll
       for (int k = 0; k < 4; ++k)
-        o[k] = (int)pack2<DT>(A[k] * unpack2<DT>((uint32_t)dz[u][k]) +
-                              B[k] * unpack2<DT>((uint32_t)yv[u][k]) + K3[k]);
+        o[k] = (int)pack2<DT>(bnb_affine2(A[k], B[k], K3[k], unpack2<DT>((uint32_t)dz[u][k]),
+                                          unpack2<DT>((uint32_t)yv[u][k])));
       if constexpr (NTM & 2) __builtin_nontemporal_store(o, op + i + u * stride);
       else op[i + u * stride] = o;
     }
@@ -898,7 +899,8 @@ __global__ __launch_bounds__(NT) void bn_bwd_apply_dz_u_kernel(const void* __res
     i32x4 o;
 #pragma unroll
     for (int k = 0; k < 4; ++k)
-      o[k] = (int)pack2<DT>(A[k] * unpack2<DT>((uint32_t)dz[k]) + B[k] * unpack2<DT>((uint32_t)yv[k]) + K3[k]);
+      o[k] = (int)pack2<DT>(bnb_affine2(A[k], B[k], K3[k], unpack2<DT>((uint32_t)dz[k]),
+                                        unpack2<DT>((uint32_t)yv[k])));
     op[i] = o;
   }
 }

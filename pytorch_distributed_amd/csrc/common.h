@@ -43,6 +43,14 @@ template <> __device__ __forceinline__ uint32_t pack2<DT_BF16>(f32x2 v) {
 template <> __device__ __forceinline__ uint32_t pack2<DT_F16>(f32x2 v) {
   return __builtin_bit_cast(uint32_t, __builtin_convertvector(v, f16x2));
 }
+// BatchNorm-backward apply dy = k1*dz + k2*y + k3 as ONE explicit fma chain, shared by the apply
+// kernels (bn.hip) and the WGRAD_BNA operand staging (conv_gemm.hip) so the two paths round alike.
+__device__ __forceinline__ float bnb_affine(float k1, float k2, float k3, float dz, float y) {
+  return __builtin_fmaf(k1, dz, __builtin_fmaf(k2, y, k3));
+}
+__device__ __forceinline__ f32x2 bnb_affine2(f32x2 k1, f32x2 k2, f32x2 k3, f32x2 dz, f32x2 y) {
+  return f32x2{bnb_affine(k1.x, k2.x, k3.x, dz.x, y.x), bnb_affine(k1.y, k2.y, k3.y, dz.y, y.y)};
+}
 template <int DT> __device__ __forceinline__ f32x2 unpack2(uint32_t w);
 template <> __device__ __forceinline__ f32x2 unpack2<DT_BF16>(uint32_t w) {
   return f32x2{__uint_as_float(w << 16), __uint_as_float(w & 0xffff0000u)};

@@ -28,7 +28,10 @@ namespace {
 
 constexpr int NT = 256;
 
-enum Pass : int { FWD = 0, DGRAD = 1, WGRAD = 2 };
+// WGRAD_BNA: WGRAD whose A operand is the BatchNorm-backward output formed while staging,
+// dY = k1[c]*dz + k2[c]*y + k3[c] (a = dz, a2 = y): the stem's weight gradient is the only consumer
+// of its BN-backward output, so the apply pass (and dY's write + re-read) is skipped.
+enum Pass : int { FWD = 0, DGRAD = 1, WGRAD = 2, WGRAD_BNA = 3 };
 
 template <int V> struct IC { static constexpr int value = V; };
 
@@ -68,6 +71,10 @@ struct ConvParams {
   const void* eg2;                 // optional second gradient summed into dA
   const uint8_t* emask;            // mode 3: forward ReLU bitmask of a (1 byte per 8 elements)
   float* epart;                    // [ncls*tiles_m][enq][N] partial sums
+  const void* a2;                  // WGRAD_BNA: y (the BN input) beside a = dz
+  const float* ak1; const float* ak2; const float* ak3;   // WGRAD_BNA: per-Cout coefficients
+  int ntm;                         // nontemporal policy of this launch: bit 0 epilogue operand
+                                   // loads (DGRAD), bit 1 output stores
   // FWD BatchNorm statistics (stats != nullptr) are per-M-tile SHIFTED partials
   // stats[tile][3][N] = (sum(y - s), sum((y - s)^2), s), s = the tile's first row (no f32
   // cancellation when |mean| >> std); bn.hip bn_fwd_stats combines and finalizes them.
@@ -188,8 +195,13 @@ constexpr int conv_min_blocks() {
   return (STAGES == 1 && BM * BN <= 128 * 128) ? 3 : 2;
 }
 
-template <int PASS, int DT, int BM, int BN, int STAGES, int MF = 16>
-__global__ __launch_bounds__(NT, (conv_min_blocks<DT, BM, BN, STAGES>())) void conv_gemm_kernel(ConvParams p_arg) {
+template <int PASS_T, int DT, int BM, int BN, int STAGES, int MF = 16>
+// WGRAD_BNA holds the fixed column chunk's 24 BN coefficients and the y chunks: 3 blocks per CU
+// (the 16-bit WGRAD budget of 4 spilled 15 VGPRs)
+__global__ __launch_bounds__(NT, (PASS_T == WGRAD_BNA ? 3 : conv_min_blocks<DT, BM, BN, STAGES>())) void conv_gemm_kernel(ConvParams p_arg) {
+  constexpr int PASS = PASS_T == WGRAD_BNA ? WGRAD : PASS_T;
+  constexpr bool ABN = PASS_T == WGRAD_BNA;
+  static_assert(!ABN || DT == DT_BF16 || DT == DT_F16, "WGRAD_BNA: 16-bit operands");
   static_assert(MF == 16 || (MF == 32 && (DT == DT_BF16 || DT == DT_F16) && BM >= 64 && BN >= 64),
                 "MFMA shape");
   // DGRAD / WGRAD read the parameters in place in the kernarg segment (constant address space):
@@ -313,6 +325,19 @@ __global__ __launch_bounds__(NT, (conv_min_blocks<DT, BM, BN, STAGES>())) void c
       a_off[i] = col < p.M ? (uint32_t)((kbeg + a_krow[i]) * p.Cout + col) * (uint32_t)ES : OOB;
     }
   }
+  // WGRAD_BNA: the thread's A column chunk (8 output channels) is fixed: its coefficients once
+  f32x2 bk1[ABN ? 4 : 1], bk2[ABN ? 4 : 1], bk3[ABN ? 4 : 1];
+  if constexpr (ABN) {
+    constexpr int CPR = BM / EPC;
+    const int col = m0 + (tid % CPR) * EPC;
+    const int cs = col < p.M ? col : 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      bk1[k] = *reinterpret_cast<const f32x2*>(p.ak1 + cs + 2 * k);
+      bk2[k] = *reinterpret_cast<const f32x2*>(p.ak2 + cs + 2 * k);
+      bk3[k] = *reinterpret_cast<const f32x2*>(p.ak3 + cs + 2 * k);
+    }
+  }
   // B
   uint32_t b_off[BR];
   if constexpr (PASS == FWD) {
@@ -362,6 +387,12 @@ __global__ __launch_bounds__(NT, (conv_min_blocks<DT, BM, BN, STAGES>())) void c
   auto bld = [&](const __amdgpu_buffer_rsrc_t& r, uint32_t off) __attribute__((always_inline)) -> i32x4 {
     return __builtin_bit_cast(i32x4, __builtin_amdgcn_raw_buffer_load_b128(r, (int)off, 0, 0));
   };
+  // WGRAD_BNA: y beside dz (same geometry), its chunks and the chunks' validity (padding rows must
+  // stay 0, not k3)
+  const __amdgpu_buffer_rsrc_t rsa2 = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<void*>(ABN ? p.a2 : p.a), (short)0, (int)a_bytes, 0x00020000);
+  i32x4 ray[ABN ? AR : 1];
+  bool av[ABN ? AR : 1];
 
   i32x4 ra[AR], rb[BR];
   i32x4 ra2[SPLIT ? AR : 1], rb2[SPLIT ? BR : 1];   // DT_F32S: elements 4..7 of each chunk
@@ -480,8 +511,14 @@ __global__ __launch_bounds__(NT, (conv_min_blocks<DT, BM, BN, STAGES>())) void c
     } else {  // WGRAD A: dY rows m (k), cols n1 (COL tile [64][BM])
       const uint32_t koff = (uint32_t)(kt * BKE * p.Cout) * (uint32_t)ES;
 #pragma unroll
-      for (int i = 0; i < AR; ++i)
-        lda(i, (k0 + a_krow[i] < kend) ? a_off[i] + koff : OOB);
+      for (int i = 0; i < AR; ++i) {
+        const bool ok = k0 + a_krow[i] < kend;
+        lda(i, ok ? a_off[i] + koff : OOB);
+        if constexpr (ABN) {
+          ray[i] = bld(rsa2, ok ? a_off[i] + koff : OOB);
+          av[i] = ok && a_off[i] != OOB;
+        }
+      }
     }
     // ---------------- B
     if constexpr (PASS == FWD) {
@@ -542,6 +579,16 @@ __global__ __launch_bounds__(NT, (conv_min_blocks<DT, BM, BN, STAGES>())) void c
       constexpr int CPR = BM / EPC, RPI = NT / CPR;
 #pragma unroll
       for (int i = 0; i < AR; ++i) {
+        if constexpr (ABN) {   // dY = k1*dz + k2*y + k3 on the valid chunks (padding stays 0)
+          if (av[i]) {
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+              const f32x2 dz = unpack2<DT>((uint32_t)ra[i][k]);
+              const f32x2 yv = unpack2<DT>((uint32_t)ray[i][k]);
+              ra[i][k] = (int)pack2<DT>(bnb_affine2(bk1[k], bk2[k], bk3[k], dz, yv));
+            }
+          }
+        }
         const int ca = F32 ? col_addr_f32<BM>(tid / CPR + RPI * i, tid % CPR)
                            : col_addr<BM>(tid / CPR + RPI * i, tid % CPR);
         if constexpr (SPLIT) split_put(sa, ca, ra[i], ra2[i]);
@@ -855,12 +902,13 @@ __global__ __launch_bounds__(NT, (conv_min_blocks<DT, BM, BN, STAGES>())) void c
         for (int j = 0; j < PD; ++j) {
           eoff[j] = row_off(g0 + j, eok[j]);
           const size_t bo = (size_t)eoff[j] * ES;
-          if constexpr (MODE >= 0)
-            py[j] = eok[j] ? *reinterpret_cast<const i32x4*>(reinterpret_cast<const char*>(p.ey) + bo) : z;
-          if constexpr (G2)
-            pg2[j] = eok[j] ? *reinterpret_cast<const i32x4*>(reinterpret_cast<const char*>(p.eg2) + bo) : z;
-          if constexpr (Y2)
-            py2[j] = eok[j] ? *reinterpret_cast<const i32x4*>(reinterpret_cast<const char*>(p.ey2) + bo) : z;
+          auto ld = [&](const void* base) __attribute__((always_inline)) {
+            const i32x4* q = reinterpret_cast<const i32x4*>(reinterpret_cast<const char*>(base) + bo);
+            return (p.ntm & 1) ? __builtin_nontemporal_load(q) : *q;
+          };
+          if constexpr (MODE >= 0) py[j] = eok[j] ? ld(p.ey) : z;
+          if constexpr (G2) pg2[j] = eok[j] ? ld(p.eg2) : z;
+          if constexpr (Y2) py2[j] = eok[j] ? ld(p.ey2) : z;
           if constexpr (MODE == 3) pm[j] = eok[j] ? (uint32_t)p.emask[eoff[j] >> 3] >> (eoff[j] & 7) : 0u;
         }
       };
@@ -956,7 +1004,9 @@ __global__ __launch_bounds__(NT, (conv_min_blocks<DT, BM, BN, STAGES>())) void c
               q1[k] += dlt * dlt;
             }
           }
-          *reinterpret_cast<i32x4*>(outb + (size_t)eoff[j] * ES) = v;
+          i32x4* dst = reinterpret_cast<i32x4*>(outb + (size_t)eoff[j] * ES);
+          if (p.ntm & 2) __builtin_nontemporal_store(v, dst);
+          else *dst = v;
         }
       }
       }
@@ -1088,17 +1138,29 @@ struct ConvDesc {  // mirrors pytorch_distributed_amd/ops/ext.py ConvDesc
 
 // MFMA shape of the 16-bit kernels (pda_conv_set_mfma): 16 = 16x16x32, 32 = 32x32x16
 static int g_mfma = 16;
+// Nontemporal policy (pda_conv_set_nt): bit 0 DGRAD epilogue operand loads, bit 1 DGRAD output
+// stores, bit 2 FWD output stores, bit 3 only for outputs of >= 100 MiB.
+static int g_conv_nt = 0;
+
+static int conv_ntm(long long out_bytes, bool fwd) {
+  if ((g_conv_nt & 8) && out_bytes < (100ll << 20)) return 0;
+  return fwd ? ((g_conv_nt & 4) ? 2 : 0) : (g_conv_nt & 3);
+}
 
 template <int PASS, int DT, int BM, int BN, int ST>
 static int launch(const ConvParams& p, dim3 grid, hipStream_t st) {
-  if constexpr (DT == DT_BF16 || DT == DT_F16) {
-    if (g_mfma == 32) {
-      hipLaunchKernelGGL((conv_gemm_kernel<PASS, DT, BM, BN, ST, 32>), grid, dim3(NT), 0, st, p);
-      return (int)hipGetLastError();
+  if constexpr (PASS == WGRAD_BNA && DT != DT_BF16 && DT != DT_F16) {
+    return -1;
+  } else {
+    if constexpr (DT == DT_BF16 || DT == DT_F16) {
+      if (g_mfma == 32) {
+        hipLaunchKernelGGL((conv_gemm_kernel<PASS, DT, BM, BN, ST, 32>), grid, dim3(NT), 0, st, p);
+        return (int)hipGetLastError();
+      }
     }
+    hipLaunchKernelGGL((conv_gemm_kernel<PASS, DT, BM, BN, ST, 16>), grid, dim3(NT), 0, st, p);
+    return (int)hipGetLastError();
   }
-  hipLaunchKernelGGL((conv_gemm_kernel<PASS, DT, BM, BN, ST, 16>), grid, dim3(NT), 0, st, p);
-  return (int)hipGetLastError();
 }
 
 // bm < 0 selects the single-buffer (STAGES = 1) variant of tile |bm| x bn (FWD / DGRAD only)
@@ -1153,6 +1215,11 @@ static void fill_geom(ConvParams& p, const ConvDesc& d) {
 
 extern "C" {
 
+int pda_conv_set_nt(int ntm) {
+  g_conv_nt = ntm & 15;
+  return 0;
+}
+
 int pda_conv_set_mfma(int mf) {
   if (mf != 16 && mf != 32) return -1;
   g_mfma = mf;
@@ -1173,6 +1240,7 @@ int pda_conv_fwd(const ConvDesc* d, const void* x, const void* w, int Kpad, void
   p.a = x; p.b = w; p.out = y; p.stats = stats; p.bias = bias;
   p.M = d->Nb * d->Ho * d->Wo; p.N = d->Cout; p.Kpad = Kpad; p.K = Kpad;
   p.out_f32 = out_f32; p.relu = relu; p.out_pitch = out_pitch > 0 ? out_pitch : d->Cout;
+  p.ntm = out_f32 ? 0 : conv_ntm((long long)p.M * p.out_pitch * (dt == DT_F32 || dt == DT_F32S ? 4 : 2), true);
   const int abm = bm < 0 ? -bm : bm;
   const int tiles = ((p.M + abm - 1) / abm) * ((p.N + bn - 1) / bn);
   return dispatch<FWD>(dt, bm, bn, p, dim3(tiles, 1), st);
@@ -1204,6 +1272,7 @@ int pda_conv_dgrad(const ConvDesc* d, const void* dy, const void* w, void* dx, c
     p.emask = (const uint8_t*)epi->mask;
   }
   p.N = d->Cin; p.out_pitch = d->Cin;
+  p.ntm = conv_ntm((long long)d->Nb * d->H * d->W * d->Cin * (dt == DT_F32 || dt == DT_F32S ? 4 : 2), false);
   const int sd = d->stride;
   if (sd != 1 && sd != 2) return -2;
   if ((d->H % sd) || (d->W % sd) || (d->Cout % 64)) return -3;
@@ -1232,6 +1301,34 @@ int pda_conv_dgrad(const ConvDesc* d, const void* dy, const void* w, void* dx, c
   const int abm = bm < 0 ? -bm : bm;
   const int tiles = ((p.M + abm - 1) / abm) * ((p.N + bn - 1) / bn);
   return dispatch<DGRAD>(dt, bm, bn, p, dim3(tiles, ncls), st);
+}
+
+// As pda_conv_wgrad with dY formed while staging from the BatchNorm backward: dY = k1*dz + k2*y + k3
+// (per output channel; the stem: Cout 64). 16-bit, 64x128 tiles only (wider ones spill); -1 otherwise.
+int pda_conv_wgrad_bna(const ConvDesc* d, const void* dz, const void* y, const float* k1,
+                       const float* k2, const float* k3, const void* x, float* slab, int splits,
+                       int k_chunk, const float* pro_sc, const float* pro_sh, int dt, int bm, int bn,
+                       hipStream_t st) {
+  if (dt != DT_BF16 && dt != DT_F16) return -1;
+  if (!fits32((long long)d->Nb * d->Ho * d->Wo * d->Cout, (long long)d->Nb * d->H * d->W * d->Cin,
+              (long long)splits * d->Cout * d->R * d->S * d->Cin, dt) || (d->Cout % 8))
+    return -4;
+  ConvParams p{};
+  fill_geom(p, *d);
+  p.pro_sc = pro_sc; p.pro_sh = pro_sh;
+  p.a = dz; p.a2 = y; p.ak1 = k1; p.ak2 = k2; p.ak3 = k3;
+  p.b = x; p.out = slab;
+  p.M = d->Cout; p.N = d->R * d->S * d->Cin;
+  p.K = d->Nb * d->Ho * d->Wo;
+  p.k_chunk = k_chunk;
+  const int abm = bm < 0 ? -bm : bm;
+  const dim3 grid(((p.M + abm - 1) / abm) * ((p.N + bn - 1) / bn), splits);
+#define PDA_BNA(D, M_, N_, S_) \
+  if (dt == D && bm == (S_ == 1 ? -M_ : M_) && bn == N_) return launch<WGRAD_BNA, D, M_, N_, S_>(p, grid, st);
+  PDA_BNA(DT_BF16, 64, 128, 1) PDA_BNA(DT_BF16, 64, 128, 2)
+  PDA_BNA(DT_F16, 64, 128, 1) PDA_BNA(DT_F16, 64, 128, 2)
+#undef PDA_BNA
+  return -1;
 }
 
 // slab[splits][Cout][R*S*Cin] partial weight gradients (f32). k_chunk must be a multiple of 64.

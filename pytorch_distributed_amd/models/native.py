@@ -135,6 +135,8 @@ class NativeResNet(nn.Module):
         import os
         self.fuse_prologue = os.environ.get("PDA_FUSE_PROLOGUE", "1x1:56")
         self.fused_stem_bwd = os.environ.get("PDA_FUSED_STEM_BWD", "1") != "0"
+        # stem wgrad forms its dY from the BN backward in-kernel (PDA_STEM_BNA=0: apply pass)
+        self.stem_bna = os.environ.get("PDA_STEM_BNA", "1") != "0"
         self.tail_mask = os.environ.get("PDA_TAIL_MASK", "1") != "0"
         self.ds_stream = os.environ.get("PDA_DS_STREAM", "1") != "0"
         # weight gradients on a second HIP stream: nothing in the backward chain consumes them, so
@@ -250,6 +252,7 @@ class NativeResNet(nn.Module):
         self.flat_nbt = self.flat_bufstore[boff * 4:].view(torch.int64)
         self.stem_packed = torch.zeros(64, 256, dtype=self.dtype, device=dev)   # [64][4][4][16]
         self.stem_wgrad = torch.zeros(64 * 256, dtype=torch.float32, device=dev)
+        self._stem_k = torch.zeros(3 * 64, dtype=torch.float32, device=dev)   # fused stem BN-bwd
         self.bn_state = torch.zeros(sum(4 * _align(u.cout) for u in units), dtype=torch.float32,
                                     device=dev)
         so = 0
@@ -662,24 +665,42 @@ class NativeResNet(nn.Module):
         x0, y0, arg = sv["x0"], sv["y0"], sv["arg"]
         st0 = sv["stem_stats"]
         u = self.stem
-        dy0 = self._empty(*y0.shape)
+        g0 = u.geom(Nb)
+        sync = getattr(ws, "sync_comm", None)
+        # the stem's BN-backward output feeds only its weight gradient: with the fused stem
+        # backward, the wgrad forms dy0 = k1*dz0 + k2*y0 + k3 while staging (no apply pass, no
+        # dy0 write + re-read: 2 x 642 MB at batch 400)
+        bna = (self.fused_stem_bwd and self.stem_bna and (sync is None or sync.world_size == 1)
+               and K.wgrad_bna_ok(g0, Nb, y0.dtype))
         if self.fused_stem_bwd:   # maxpool gather + ReLU mask + BN partials in one pass
             dz0 = self._empty(*y0.shape)
             part, G, nq = K.stem_bwd_reduce(ws, dx_main, arg, y0, st0[2], st0[3], dz0,
                                             dout2=shortcut_g)
-            K.bn_bwd_finish(ws, part, G, nq, y0, st0[0], st0[1], self.gamma(u), self.dgamma(u),
-                            self.dbeta(u), dz0, dy0, accumulate=acc)
+            if bna:
+                k0 = self._stem_k
+                K.bn_bwd_finish(ws, part, G, nq, y0, st0[0], st0[1], self.gamma(u), self.dgamma(u),
+                                self.dbeta(u), dz0, None, accumulate=acc, k_out=k0)
+            else:
+                dy0 = self._empty(*y0.shape)
+                K.bn_bwd_finish(ws, part, G, nq, y0, st0[0], st0[1], self.gamma(u), self.dgamma(u),
+                                self.dbeta(u), dz0, dy0, accumulate=acc)
         else:
+            dy0 = self._empty(*y0.shape)
             dA0 = self._empty(*y0.shape)
             K.maxpool_bwd(dx_main, arg, dA0, dout2=shortcut_g)
             K.bn_bwd(ws, y0, st0[0], st0[1], self.gamma(u), st0[2], st0[3], self.dgamma(u),
                      self.dbeta(u), dy0, g1=dA0, accumulate=acc)
-        g0 = u.geom(Nb)
 
-        def stem_wgrad(w):
-            K.conv_wgrad(dy0, x0, g0, self.stem_wgrad, w)
-            K.stem_s2d_grad(self.stem_wgrad, self.wgrad_view(u), accumulate=acc)
-        self._wgrad(stem_wgrad, dy0, x0)
+        if bna:
+            def stem_wgrad(w):
+                K.conv_wgrad(dz0, x0, g0, self.stem_wgrad, w, bna=(y0, k0))
+                K.stem_s2d_grad(self.stem_wgrad, self.wgrad_view(u), accumulate=acc)
+            self._wgrad(stem_wgrad, dz0, y0, x0, k0)
+        else:
+            def stem_wgrad(w):
+                K.conv_wgrad(dy0, x0, g0, self.stem_wgrad, w)
+                K.stem_s2d_grad(self.stem_wgrad, self.wgrad_view(u), accumulate=acc)
+            self._wgrad(stem_wgrad, dy0, x0)
         self._flush_wgrad()
         if self._side is not None:   # join: the optimizer step reads every gradient
             torch.cuda.current_stream(self.device).wait_stream(self._side)

@@ -352,13 +352,28 @@ def wgrad_plan(g: ConvGeom, Nb: int, tile: Optional[Tuple[int, int]] = None,
     return bm, bn, splits, k_chunk
 
 
+def wgrad_bna_ok(g: ConvGeom, Nb: int, dtype: torch.dtype) -> bool:
+    """Whether :func:`conv_wgrad` can form dY from the BN backward in-kernel for this geometry: 16-bit
+    operands on the tile WGRAD_BNA is built for (64x128: the stem's Cout = 64)."""
+    if dtype not in (torch.bfloat16, torch.float16) or g.Cout % 8:
+        return False
+    if getattr(ext.lib(), "pda_conv_wgrad_bna", None) is None:
+        return False
+    bm, bn, _, _ = wgrad_plan(g, Nb)
+    return abs(bm) == 64 and bn == 128
+
+
 def conv_wgrad(dy: torch.Tensor, x: torch.Tensor, g: ConvGeom, grad: torch.Tensor, ws: Workspace,
                cin_real: Optional[int] = None, scale: float = 1.0, accumulate: bool = False,
                tile: Optional[Tuple[int, int]] = None,
                pro: Optional[Tuple[torch.Tensor, torch.Tensor]] = None,
-               target_blocks: Optional[int] = None) -> torch.Tensor:
+               target_blocks: Optional[int] = None,
+               bna: Optional[Tuple[torch.Tensor, torch.Tensor]] = None) -> torch.Tensor:
     """grad (f32, OHWI with cin_real channels, rows of pitch R*S*cin_real) = scale * dW.
-    pro = (scale, shift): x is PRE-BatchNorm; the activation relu(x*scale+shift) is recomputed."""
+    pro = (scale, shift): x is PRE-BatchNorm; the activation relu(x*scale+shift) is recomputed.
+    bna = (y, k) with k = [k1; k2; k3] (3 x Cout f32): ``dy`` is the BN-backward's masked gradient
+    dz and the kernel stages dY = k1*dz + k2*y + k3 itself (csrc/conv_gemm.hip WGRAD_BNA; see
+    :func:`wgrad_bna_ok`)."""
     Nb = dy.shape[0]
     bm, bn, splits, k_chunk = wgrad_plan(g, Nb, tile, target_blocks, f32=dy.dtype == torch.float32)
     M, N = g.Cout, g.R * g.S * g.Cin
@@ -367,10 +382,19 @@ def conv_wgrad(dy: torch.Tensor, x: torch.Tensor, g: ConvGeom, grad: torch.Tenso
     st = stream(dy.device)
     kdt = _kdt(dy)
     kbm, kbn = _ktile(bm, bn, kdt)
-    rc = ext.lib().pda_conv_wgrad(C.byref(d), ptr(dy), ptr(x), ptr(slab), splits, k_chunk,
-                                  ptr(pro[0] if pro else None), ptr(pro[1] if pro else None),
-                                  kdt, kbm, kbn, st)
-    check(rc, "conv_wgrad")
+    if bna is not None:
+        y, k = bna
+        Co = g.Cout
+        rc = ext.lib().pda_conv_wgrad_bna(C.byref(d), ptr(dy), ptr(y), ptr(k[0:Co]), ptr(k[Co:2 * Co]),
+                                          ptr(k[2 * Co:3 * Co]), ptr(x), ptr(slab), splits, k_chunk,
+                                          ptr(pro[0] if pro else None), ptr(pro[1] if pro else None),
+                                          kdt, kbm, kbn, st)
+        check(rc, "conv_wgrad_bna")
+    else:
+        rc = ext.lib().pda_conv_wgrad(C.byref(d), ptr(dy), ptr(x), ptr(slab), splits, k_chunk,
+                                      ptr(pro[0] if pro else None), ptr(pro[1] if pro else None),
+                                      kdt, kbm, kbn, st)
+        check(rc, "conv_wgrad")
     cr = g.Cin if cin_real is None else cin_real
     rc = ext.lib().pda_wgrad_reduce(ptr(slab), ptr(grad), splits, M, N, int(math.log2(g.Cin)), cr,
                                     g.R * g.S * cr, float(scale), int(accumulate), st)
@@ -509,19 +533,25 @@ def bn_bwd(ws: Workspace, y, mean, invstd, gamma, scale, shift, dgamma, dbeta, d
 
 def bn_bwd_finish(ws: "Workspace", part, G: int, nq: int, y, mean, invstd, gamma, dgamma, dbeta,
                   dz, dy_out, y2=None, mean2=None, invstd2=None, gamma2=None, dgamma2=None,
-                  dbeta2=None, dy2_out=None, gscale: float = 1.0, accumulate: bool = False) -> None:
+                  dbeta2=None, dy2_out=None, gscale: float = 1.0, accumulate: bool = False,
+                  k_out: Optional[torch.Tensor] = None) -> None:
     """Finalize + apply of a BN backward whose reduction a dgrad epilogue already produced
     (partials ``part`` [G][nq][C], masked gradient ``dz``): ONE finalize launch (csrc/bn.hip
     bn_stats_kernel<1>: f64 slabs + last-arriver combine -> gamma/beta gradients and the apply
     coefficients of both branches), then the apply pass(es). SyncBatchNorm takes the separate
-    reduce -> all-reduce -> finalize path."""
+    reduce -> all-reduce -> finalize path.
+    ``k_out`` (3 x C f32, single-branch, not SyncBatchNorm): write the apply coefficients
+    [k1; k2; k3] there and skip the apply pass (``dy_out`` unused) -- the consumer forms dy itself
+    (:func:`conv_wgrad` ``bna``)."""
     N, H, W, C_ = y.shape
     mode = 2 if nq == 3 else 1   # dz is materialised in both cases
     a = BwdArgs(None, None, None, 0, ptr(y), None, None, ptr(y2), None, None, mode, None, ptr(part),
                 nq, N * H * W, C_)
     sync = getattr(ws, "sync_comm", None)
+    if k_out is not None and (nq != 2 or (sync is not None and sync.world_size > 1)):
+        raise ValueError("bn_bwd_finish: k_out needs the single-branch, non-synchronised form")
     if sync is None or sync.world_size == 1:
-        k = ws.get("bn_k", 6 * C_)
+        k = ws.get("bn_k", 6 * C_) if k_out is None else k_out
         S = _stats_slabs(G, C_)
         slabs = ws.get("bn_slabs", S * nq * C_, torch.float64)
         cnt = ws.counters(math.ceil(C_ / min(C_, 256)))
@@ -535,6 +565,8 @@ def bn_bwd_finish(ws: "Workspace", part, G: int, nq: int, y, mean, invstd, gamma
         L, st, dt = ext.lib(), stream(y.device), dt_of(y)
         check(L.pda_bn_bwd_stats(ptr(part), G, nq, C_, S, ptr(slabs), ptr(cnt), C.byref(o), st),
               "bn_bwd_stats")
+        if k_out is not None:
+            return
         check(L.pda_bn_bwd_apply(C.byref(a), ptr(dz), ptr(y), ptr(k[0:C_]), ptr(k[C_:2 * C_]),
                                  ptr(k[2 * C_:3 * C_]), ptr(dy_out), dt, st), "bn_bwd_apply")
         if mode == 2:

@@ -107,6 +107,38 @@ def test_conv_stem_padded_cin():
     assert rel_err(dw, wr.grad.permute(0, 2, 3, 1)) < 1e-2
 
 
+@pytest.mark.parametrize("Cout,Cin,k,H", [(64, 64, 3, 9), (64, 16, 4, 11), (64, 16, 4, 60)])
+def test_conv_wgrad_bna_matches_applied(Cout, Cin, k, H):
+    """WGRAD_BNA (the stem wgrad forming dY = k1*dz + k2*y + k3 while staging) against the unfused
+    path (dY materialised in bf16, plain wgrad) and against the fp32 PyTorch weight gradient of the
+    same dY; ragged row counts check that padding rows contribute 0, not k3; H = 60 runs split-K."""
+    K = _k()
+    dtype = torch.bfloat16
+    Nb = 3
+    torch.manual_seed(Cout + k)
+    g = K.ConvGeom(Nb, H, H, Cin, Cout, k, k, 1, k // 2 if k != 4 else 0)
+    if not K.wgrad_bna_ok(g, Nb, dtype):
+        pytest.skip("tile not built for WGRAD_BNA")
+    x = torch.randn(Nb, H, H, Cin, device=DEV).to(dtype)
+    dz = torch.randn(Nb, g.Ho, g.Wo, Cout, device=DEV).to(dtype)
+    y = (torch.randn(Nb, g.Ho, g.Wo, Cout, device=DEV) * 2 + 1).to(dtype)
+    kk = torch.randn(3 * Cout, device=DEV)
+    ws = K.Workspace(DEV)
+    dw_f = torch.zeros(Cout, k, k, Cin, device=DEV)
+    K.conv_wgrad(dz, x, g, dw_f.view(-1), ws, bna=(y, kk))
+    # the kernels' fma chain fma(k1, dz, fma(k2, y, k3)), in f64 then rounded once to f32
+    dy = (kk[:Cout].double() * dz.double() + (kk[Cout:2 * Cout].double() * y.double()
+                                              + kk[2 * Cout:].double()).float().double()).float().to(dtype)
+    dw_u = torch.zeros_like(dw_f)
+    K.conv_wgrad(dy, x, g, dw_u.view(-1), ws)
+    torch.cuda.synchronize()
+    assert rel_err(dw_f, dw_u) < 2e-3
+    wr = torch.zeros(Cout, Cin, k, k, device=DEV, requires_grad=True)
+    out = F.conv2d(x.permute(0, 3, 1, 2).float(), wr, stride=1, padding=g.pad)
+    out.backward(dy.permute(0, 3, 1, 2).float())
+    assert rel_err(dw_f, wr.grad.permute(0, 2, 3, 1)) < 1e-2
+
+
 def test_fc_as_conv():
     K = _k()
     dtype = torch.bfloat16

@@ -80,6 +80,29 @@ def test_forward_backward_matches_reference(arch):
             assert rel_err(bfr, tbuf[name]) < 0.5, name
 
 
+def test_stem_wgrad_bna_matches_apply_path():
+    """The stem weight gradient with dY formed inside the wgrad kernel (WGRAD_BNA, default) equals
+    the apply-pass path (PDA_STEM_BNA=0) on the same forward state: 224 px, so the stem wgrad runs
+    split-K over many row chunks."""
+    _, nm = _pair("resnet50", image=224)
+    torch.manual_seed(3)
+    x = torch.randn(8, 3, 224, 224, device=DEV)
+    y = torch.randint(0, 1000, (8,), device=DEV)
+    nm.train()
+    crit = nm.make_criterion()
+    grads = {}
+    for bna in (False, True):
+        nm.stem_bna = bna
+        nm.zero_grad_flat()
+        crit(nm(x), y).backward()
+        torch.cuda.synchronize()
+        grads[bna] = dict((n, p.grad.detach().float().clone()) for n, p in nm.named_parameters())
+    # both paths evaluate dy = k1*dz + k2*y + k3 with the same fma chain and round it to bf16
+    # before the same MFMA schedule: bitwise-equal gradients
+    for n in grads[True]:
+        assert torch.equal(grads[True][n], grads[False][n]), (n, rel_err(grads[True][n], grads[False][n]))
+
+
 def test_optimizer_step_and_state_dict():
     tm, nm = _pair("resnet18")
     x = torch.randn(4, 3, 64, 64, device=DEV)
