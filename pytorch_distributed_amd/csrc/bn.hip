@@ -905,6 +905,65 @@ __global__ __launch_bounds__(NT) void bn_bwd_apply_dz_u_kernel(const void* __res
   }
 }
 
+// Both branches of a downsample block's tail in one pass: dz (the masked gradient of
+// relu(bn(y) + bn2(y2))) is read ONCE for dy = k[0..3C)(dz, y) and dy2 = k[3C..6C)(dz, y2) --
+// 3 reads + 2 writes per chunk instead of 4 + 2 over two launches. U chunks per trip as above.
+template <int DT, int U, int NTM>
+__global__ __launch_bounds__(NT) void bn_bwd_apply_dz2_u_kernel(const void* __restrict__ dz_in,
+                                                                const void* __restrict__ ysel,
+                                                                const void* __restrict__ y2sel,
+                                                                const float* __restrict__ k,
+                                                                void* __restrict__ dy,
+                                                                void* __restrict__ dy2, int n8, int C) {
+  const int C8 = C >> 3;
+  const int stride = gridDim.x * NT;
+  int i = blockIdx.x * NT + threadIdx.x;
+  if (i >= n8) return;
+  f32x2 A[4], B[4], K3[4], A2[4], B2[4], K32[4];
+  {
+    const int c0 = (i % C8) * 8;
+    ld8p<DT>(k + c0, A);
+    ld8p<DT>(k + C + c0, B);
+    ld8p<DT>(k + 2 * C + c0, K3);
+    ld8p<DT>(k + 3 * C + c0, A2);
+    ld8p<DT>(k + 4 * C + c0, B2);
+    ld8p<DT>(k + 5 * C + c0, K32);
+  }
+  const i32x4* dzp = reinterpret_cast<const i32x4*>(dz_in);
+  const i32x4* yp = reinterpret_cast<const i32x4*>(ysel);
+  const i32x4* y2p = reinterpret_cast<const i32x4*>(y2sel);
+  i32x4* op = reinterpret_cast<i32x4*>(dy);
+  i32x4* op2 = reinterpret_cast<i32x4*>(dy2);
+  auto one = [&](const i32x4& dz, const i32x4& yv, const i32x4& y2v, int j) __attribute__((always_inline)) {
+    i32x4 o, o2;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const f32x2 d = unpack2<DT>((uint32_t)dz[q]);
+      o[q] = (int)pack2<DT>(bnb_affine2(A[q], B[q], K3[q], d, unpack2<DT>((uint32_t)yv[q])));
+      o2[q] = (int)pack2<DT>(bnb_affine2(A2[q], B2[q], K32[q], d, unpack2<DT>((uint32_t)y2v[q])));
+    }
+    if constexpr (NTM & 2) {
+      __builtin_nontemporal_store(o, op + j);
+      __builtin_nontemporal_store(o2, op2 + j);
+    } else {
+      op[j] = o;
+      op2[j] = o2;
+    }
+  };
+  for (; i + (U - 1) * stride < n8; i += U * stride) {
+    i32x4 dz[U], yv[U], y2v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      dz[u] = ldnt<NTM & 1>(dzp + i + u * stride);
+      yv[u] = ldnt<NTM & 1>(yp + i + u * stride);
+      y2v[u] = ldnt<NTM & 1>(y2p + i + u * stride);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) one(dz[u], yv[u], y2v[u], i + u * stride);
+  }
+  for (; i < n8; i += stride) one(dzp[i], yp[i], y2p[i], i);
+}
+
 // bn_apply_kernel's 16-bit path with U chunks per trip (see bn_bwd_apply_dz_u_kernel).
 template <int DT, int U, int NTM>
 __global__ __launch_bounds__(NT) void bn_apply_u_kernel(
@@ -998,9 +1057,11 @@ StreamCfg g_stream{0, 0, 8192, 100};
 
 // Launch KER<DT, U, NTM> for the configured (U, NTM); false when the shape does not qualify.
 #define PDA_STREAM_DISPATCH(KER, DT, g, st, ...)                                              \
+  PDA_STREAM_DISPATCH_UM(KER, DT, g, st, (g_stream.unroll < 0 ? 4 : g_stream.unroll),          \
+                         (g_stream.unroll < 0 ? 3 : g_stream.ntm), __VA_ARGS__)
+#define PDA_STREAM_DISPATCH_UM(KER, DT, g, st, U_, M_, ...)                                    \
   do {                                                                                        \
-    const int u_ = g_stream.unroll < 0 ? 4 : g_stream.unroll;                                 \
-    const int m_ = g_stream.unroll < 0 ? 3 : g_stream.ntm;                                    \
+    const int u_ = (U_), m_ = (M_);                                                           \
     if (u_ == 2 && m_ == 0) hipLaunchKernelGGL((KER<DT, 2, 0>), dim3(g), dim3(NT), 0, st, __VA_ARGS__); \
     else if (u_ == 2 && m_ == 1) hipLaunchKernelGGL((KER<DT, 2, 1>), dim3(g), dim3(NT), 0, st, __VA_ARGS__); \
     else if (u_ == 2 && m_ == 2) hipLaunchKernelGGL((KER<DT, 2, 2>), dim3(g), dim3(NT), 0, st, __VA_ARGS__); \
@@ -1216,6 +1277,28 @@ int pda_bn_bwd_finalize(const float* part, int G, int nq, int qy, int C, float c
                         hipStream_t st) {
   hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 15) / 16), dim3(1024), 0, st, part, G, nq, qy,
                      C, count, gamma, mean, invstd, dgamma, dbeta, k1, k2, k3, gscale, accumulate);
+  return (int)hipGetLastError();
+}
+
+// Both branches of a downsample tail in one pass (16-bit; -1 for other dtypes): k = [2][3][C].
+int pda_bn_bwd_apply2(const void* dz, const void* y, const void* y2, const float* k, void* dy,
+                      void* dy2, long long rows, int C, int dt, hipStream_t st) {
+  if ((dt != DT_BF16 && dt != DT_F16) || (C & 7) || rows * (C / 8) >= (1ll << 31)) return -1;
+  const int n8 = (int)(rows * (C / 8));
+  // streaming config as the one-branch pass (auto: 4 chunks + nontemporal for >= 100 MiB),
+  // else one chunk per trip
+  int gs = stream_grid(n8, C);
+  int u = g_stream.unroll < 0 ? 4 : g_stream.unroll, m = g_stream.unroll < 0 ? 3 : g_stream.ntm;
+  if (gs <= 0) {
+    gs = grid_for(n8);
+    if (((long long)gs * NT) % (C >> 3)) return -1;
+    u = 1;
+    m = 0;
+  }
+#define KA dz, y, y2, k, dy, dy2, n8, C
+  if (dt == DT_BF16) PDA_STREAM_DISPATCH_UM(bn_bwd_apply_dz2_u_kernel, DT_BF16, gs, st, u, m, KA);
+  else PDA_STREAM_DISPATCH_UM(bn_bwd_apply_dz2_u_kernel, DT_F16, gs, st, u, m, KA);
+#undef KA
   return (int)hipGetLastError();
 }
 

@@ -105,6 +105,7 @@ _SIGS = {
     "pda_pack_stem_s2d": [_V, _V, _I, _I, _V],
     "pda_stem_s2d_grad": [_V, _V, _I, _I, _V],
     "pda_set_stream_cfg": [_I, _I, _I, _I],
+    "pda_bn_bwd_apply2": [_V, _V, _V, _V, _V, _V, _L, _I, _I, _V],
     "pda_conv_set_nt": [_I],
 }
 

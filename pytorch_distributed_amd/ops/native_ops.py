@@ -104,6 +104,8 @@ if _F32_CONV not in ("exact", "split"):
     raise ValueError(f"MX_F32_CONV / PDA_F32_CONV must be exact|split, got {_F32_CONV!r}")
 _SPLIT_BN = int(os.environ.get("PDA_SPLIT_BN", "128"))   # widest N tile of the split kernels (A/B)
 _STATS_S = os.environ.get("PDA_STATS_S")   # fixed slab count of the statistics kernels (A/B)
+# downsample-tail BN backward: both branches' apply in one pass over dz (PDA_BWD_APPLY2=0: two)
+_BWD_APPLY2 = os.environ.get("PDA_BWD_APPLY2", "1") != "0"
 # scale on the split-K block targets (the wgrads run beside the dgrad chain on a second stream)
 _WGRAD_TB_SCALE = float(os.environ.get("PDA_WGRAD_TB_SCALE", "1.0"))
 
@@ -567,6 +569,9 @@ def bn_bwd_finish(ws: "Workspace", part, G: int, nq: int, y, mean, invstd, gamma
               "bn_bwd_stats")
         if k_out is not None:
             return
+        if mode == 2 and _BWD_APPLY2 and L.pda_bn_bwd_apply2(
+                ptr(dz), ptr(y), ptr(y2), ptr(k), ptr(dy_out), ptr(dy2_out), N * H * W, C_, dt, st) == 0:
+            return   # both branches in one pass over dz
         check(L.pda_bn_bwd_apply(C.byref(a), ptr(dz), ptr(y), ptr(k[0:C_]), ptr(k[C_:2 * C_]),
                                  ptr(k[2 * C_:3 * C_]), ptr(dy_out), dt, st), "bn_bwd_apply")
         if mode == 2:

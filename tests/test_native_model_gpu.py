@@ -103,6 +103,27 @@ def test_stem_wgrad_bna_matches_apply_path():
         assert torch.equal(grads[True][n], grads[False][n]), (n, rel_err(grads[True][n], grads[False][n]))
 
 
+def test_downsample_tail_dual_apply_matches_two_passes(monkeypatch):
+    """The downsample blocks' tail BN backward applies both branches in one pass over dz
+    (csrc/bn.hip bn_bwd_apply_dz2_u_kernel); gradients are bitwise those of the two-launch path."""
+    from pytorch_distributed_amd.ops import native_ops as K
+    _, nm = _pair("resnet50", image=64)
+    torch.manual_seed(5)
+    x = torch.randn(8, 3, 64, 64, device=DEV)
+    y = torch.randint(0, 1000, (8,), device=DEV)
+    nm.train()
+    crit = nm.make_criterion()
+    grads = {}
+    for dual in (False, True):
+        monkeypatch.setattr(K, "_BWD_APPLY2", dual)
+        nm.zero_grad_flat()
+        crit(nm(x), y).backward()
+        torch.cuda.synchronize()
+        grads[dual] = dict((n, p.grad.detach().float().clone()) for n, p in nm.named_parameters())
+    for n in grads[True]:
+        assert torch.equal(grads[True][n], grads[False][n]), n
+
+
 def test_optimizer_step_and_state_dict():
     tm, nm = _pair("resnet18")
     x = torch.randn(4, 3, 64, 64, device=DEV)
