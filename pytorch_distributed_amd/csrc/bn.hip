@@ -1046,10 +1046,9 @@ inline int grid_for(long long n, int cap = 8192) {
 
 // Streaming-kernel shape for the 16-bit apply passes: chunks per thread per trip (0 = the plain
 // one-chunk kernels), nontemporal policy (bit 0 loads, bit 1 stores), grid cap in blocks.
-// unroll < 0 (auto): tensors of at least min_mb MiB (past the 256 MB Infinity Cache's useful
-// reach, where nothing is gained by keeping them cached for the consumer) take (4, nt loads +
-// stores, 16384); smaller ones the one-chunk kernels (tools/stream_bench.py,
-// profiles/stream_bench_r2.txt: -11 % isolated on the >= 160 MB passes, +10-15 % on the small).
+// unroll < 0 (auto): tensors of at least min_mb MiB (the host passes 50: in-step best of
+// 30-200, ext.stream_cfg) take (4, nt loads + stores, 16384); smaller ones the one-chunk kernels
+// (tools/stream_bench.py, profiles/stream_bench_r2.txt: isolated -11 % on the >= 160 MB passes).
 struct StreamCfg {
   int unroll, ntm, cap, min_mb;
 };
