@@ -1047,7 +1047,8 @@ inline int grid_for(long long n, int cap = 8192) {
 // Streaming-kernel shape for the 16-bit apply passes: chunks per thread per trip (0 = the plain
 // one-chunk kernels), nontemporal policy (bit 0 loads, bit 1 stores), grid cap in blocks.
 // unroll < 0 (auto): tensors of at least min_mb MiB (the host passes 50: in-step best of
-// 30-200, ext.stream_cfg) take (4, nt loads + stores, 16384); smaller ones the one-chunk kernels
+// 30-200, ext.stream_cfg) take -unroll chunks (-1: 4), nontemporal policy ntm and grid cap
+// (host default: nt loads + stores, 16384); smaller ones the one-chunk kernels
 // (tools/stream_bench.py, profiles/stream_bench_r2.txt: isolated -11 % on the >= 160 MB passes).
 struct StreamCfg {
   int unroll, ntm, cap, min_mb;
@@ -1056,8 +1057,7 @@ StreamCfg g_stream{0, 0, 8192, 100};
 
 // Launch KER<DT, U, NTM> for the configured (U, NTM); false when the shape does not qualify.
 #define PDA_STREAM_DISPATCH(KER, DT, g, st, ...)                                              \
-  PDA_STREAM_DISPATCH_UM(KER, DT, g, st, (g_stream.unroll < 0 ? 4 : g_stream.unroll),          \
-                         (g_stream.unroll < 0 ? 3 : g_stream.ntm), __VA_ARGS__)
+  PDA_STREAM_DISPATCH_UM(KER, DT, g, st, stream_chunks(), g_stream.ntm, __VA_ARGS__)
 #define PDA_STREAM_DISPATCH_UM(KER, DT, g, st, U_, M_, ...)                                    \
   do {                                                                                        \
     const int u_ = (U_), m_ = (M_);                                                           \
@@ -1075,14 +1075,19 @@ StreamCfg g_stream{0, 0, 8192, 100};
     else hipLaunchKernelGGL((KER<DT, 1, 3>), dim3(g), dim3(NT), 0, st, __VA_ARGS__);         \
   } while (0)
 
+// chunks per thread per trip: unroll > 0 as given; auto (unroll < 0): -unroll, -1 meaning 4
+inline int stream_chunks() {
+  return g_stream.unroll > 0 ? g_stream.unroll : (g_stream.unroll == -1 ? 4 : -g_stream.unroll);
+}
+
 // grid for the U-chunk kernels: ~n8/U threads, capped; 0 when a thread's chunks would not share
 // one channel octet (stride % C8 != 0)
 inline int stream_grid(long long n8, int C) {
   if (g_stream.unroll == 0) return 0;
   const bool autoc = g_stream.unroll < 0;
   if (autoc && n8 * 16 < ((long long)g_stream.min_mb << 20)) return 0;
-  const int u = autoc ? 4 : g_stream.unroll;
-  const int g = grid_for((n8 + u - 1) / u, autoc ? 16384 : g_stream.cap);
+  const int u = stream_chunks();
+  const int g = grid_for((n8 + u - 1) / u, g_stream.cap);
   return ((long long)g * NT) % (C >> 3) == 0 ? g : 0;
 }
 
@@ -1090,11 +1095,13 @@ inline int stream_grid(long long n8, int C) {
 
 extern "C" {
 
-// Streaming apply kernels (see StreamCfg): unroll -1 = auto, 0 = the one-chunk kernels, 1/2/4 =
-// that many chunks for every shape. Returns the previous unroll.
+// Streaming apply kernels (see StreamCfg): unroll < 0 = auto with -unroll chunks (-1: 4) for
+// tensors >= min_mb MiB, 0 = the one-chunk kernels, 1/2/4 = that many chunks for every shape;
+// ntm / cap apply to the multi-chunk launches. Returns the previous unroll.
 int pda_set_stream_cfg(int unroll, int ntm, int cap, int min_mb) {
   const int prev = g_stream.unroll;
-  g_stream.unroll = (unroll == 1 || unroll == 2 || unroll == 4 || unroll == -1) ? unroll : 0;
+  const int a = unroll < 0 ? -unroll : unroll;
+  g_stream.unroll = (a == 1 || a == 2 || a == 4) ? unroll : 0;
   g_stream.ntm = ntm & 3;
   g_stream.cap = cap > 0 ? cap : 8192;
   g_stream.min_mb = min_mb >= 0 ? min_mb : 100;
@@ -1287,7 +1294,7 @@ int pda_bn_bwd_apply2(const void* dz, const void* y, const void* y2, const float
   // streaming config as the one-branch pass (auto: 4 chunks + nontemporal for >= 100 MiB),
   // else one chunk per trip
   int gs = stream_grid(n8, C);
-  int u = g_stream.unroll < 0 ? 4 : g_stream.unroll, m = g_stream.unroll < 0 ? 3 : g_stream.ntm;
+  int u = stream_chunks(), m = g_stream.ntm;
   if (gs <= 0) {
     gs = grid_for(n8);
     if (((long long)gs * NT) % (C >> 3)) return -1;
