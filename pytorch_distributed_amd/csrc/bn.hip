@@ -1048,7 +1048,7 @@ inline int grid_for(long long n, int cap = 8192) {
 // one-chunk kernels), nontemporal policy (bit 0 loads, bit 1 stores), grid cap in blocks.
 // unroll < 0 (auto): tensors of at least min_mb MiB (the host passes 50: in-step best of
 // 30-200, ext.stream_cfg) take -unroll chunks (-1: 4), nontemporal policy ntm and grid cap
-// (host default: nt loads + stores, 16384); smaller ones the one-chunk kernels
+// (host default: nt loads + stores, 65536); smaller ones the one-chunk kernels
 // (tools/stream_bench.py, profiles/stream_bench_r2.txt: isolated -11 % on the >= 160 MB passes).
 struct StreamCfg {
   int unroll, ntm, cap, min_mb;

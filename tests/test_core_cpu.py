@@ -205,7 +205,7 @@ def test_stream_cfg_parsing(monkeypatch):
     'U,NTM,CAP[,MIN_MB]' (',' or ':' separated) padded with the defaults."""
     from pytorch_distributed_amd.ops import ext
     monkeypatch.delenv("PDA_STREAM", raising=False)
-    assert ext.stream_cfg() == (-1, 3, 16384, 50)
+    assert ext.stream_cfg() == (-1, 3, 65536, 50)
     for v, want in [("0", (0, 0, 8192, 100)), ("2,3", (2, 3, 8192, 100)),
                     ("4:3:16384", (4, 3, 16384, 100)), ("4,1,4096,50", (4, 1, 4096, 50))]:
         monkeypatch.setenv("PDA_STREAM", v)
