@@ -145,20 +145,31 @@ class NativeResNet(nn.Module):
         self._side = (torch.cuda.Stream(device) if os.environ.get("PDA_WGRAD_STREAM", "1") != "0"
                       else None)
         self.ws_w = Workspace(device) if self._side is not None else self.ws
-        # "block" (default): queue a block's weight-gradient kernels and fork the wgrad stream ONCE
-        # per residual block instead of once per conv (fewer cross-stream edges; in a captured
-        # graph every fork / join edge becomes a cross-queue barrier packet); "stage": once per
-        # stage; "0": once per conv (profiles/ab_r2_inlaunch_bn.md section 9)
-        self._wbatch_mode = os.environ.get("PDA_WGRAD_BATCH", "block")
-        if self._wbatch_mode not in ("0", "block", "stage"):
-            raise ValueError(f"PDA_WGRAD_BATCH={self._wbatch_mode!r}: expected 0, block or stage")
-        self._wbatch = [] if self._side is not None and self._wbatch_mode != "0" else None
+        # When the wgrad stream forks: "0" once per conv (eager default: each weight gradient
+        # starts as soon as its inputs exist), "block" queues a residual block's weight-gradient
+        # kernels and forks ONCE per block (graph-capture default: in a captured graph every fork /
+        # join edge becomes a cross-queue barrier packet), "stage" once per stage; PDA_WGRAD_BATCH
+        # overrides both (profiles/ab_r2_inlaunch_bn.md sections 9, 10)
+        self._wbatch_env = os.environ.get("PDA_WGRAD_BATCH")
+        self.set_wgrad_batch(self._wbatch_env or "0")
         # optionally run the dgrad/BN-backward chain (the critical path) on a high-priority stream
         self._chain = (torch.cuda.Stream(device, priority=-1)
                        if self._side is not None and os.environ.get("PDA_CHAIN_PRIO", "0") == "1"
                        else None)
         self._keep: List[torch.Tensor] = []
         self.refresh_shadow()
+
+    def set_wgrad_batch(self, mode: str) -> None:
+        """Wgrad-stream fork granularity ("0" | "block" | "stage", see __init__)."""
+        if mode not in ("0", "block", "stage"):
+            raise ValueError(f"PDA_WGRAD_BATCH={mode!r}: expected 0, block or stage")
+        self._wbatch_mode = mode
+        self._wbatch = [] if self._side is not None and mode != "0" else None
+
+    def use_graph_schedule(self) -> None:
+        """Schedule for HIP-graph capture: fork the wgrad stream once per block (unless
+        PDA_WGRAD_BATCH says otherwise)."""
+        self.set_wgrad_batch(self._wbatch_env or "block")
 
     # ------------------------------------------------------------------ planning
     def _build_plan(self) -> None:

@@ -311,6 +311,7 @@ class _ReplicaGraph:
 
     def __init__(self, m, shape, global_batch: int) -> None:
         self.m = m
+        m.use_graph_schedule()
         self.dev = m.device
         self.gscale = 1.0 / global_batch
         with torch.cuda.device(self.dev):

@@ -68,6 +68,7 @@ class GraphedNativeStep:
     def __init__(self, model, opt, gen: Callable, batch: int, scaler=None,
                  device: Optional[torch.device] = None) -> None:
         self.model, self.opt, self.gen, self.batch, self.scaler = model, opt, gen, batch, scaler
+        model.use_graph_schedule()
         self.device = torch.device(device) if device is not None else model.device
         self.ids_base = torch.arange(batch, dtype=torch.int64, device=self.device)
         self.ids_off = torch.zeros(1, dtype=torch.int64, device=self.device)
