@@ -104,6 +104,7 @@ if _F32_CONV not in ("exact", "split"):
     raise ValueError(f"MX_F32_CONV / PDA_F32_CONV must be exact|split, got {_F32_CONV!r}")
 _SPLIT_BN = int(os.environ.get("PDA_SPLIT_BN", "128"))   # widest N tile of the split kernels (A/B)
 _STATS_S = os.environ.get("PDA_STATS_S")   # fixed slab count of the statistics kernels (A/B)
+_STATS_S_SCALE = float(os.environ.get("PDA_STATS_S_SCALE", "1.0"))   # scale on its heuristic (A/B)
 # downsample-tail BN backward: both branches' apply in one pass over dz (PDA_BWD_APPLY2=0: two)
 _BWD_APPLY2 = os.environ.get("PDA_BWD_APPLY2", "1") != "0"
 # scale on the split-K block targets (the wgrads run beside the dgrad chain on a second stream)
@@ -589,7 +590,7 @@ def _stats_slabs(T: int, C_: int) -> int:
     bandwidth), at least 8 when T allows so the level-1 reads spread over CUs."""
     if _STATS_S is not None:   # A/B override (tools/bnstats_bench.py)
         return max(1, min(T, int(_STATS_S)))
-    return max(1, min(T, max(8, int(math.sqrt(0.75 * T)))))
+    return max(1, min(T, max(8, int(_STATS_S_SCALE * math.sqrt(0.75 * T)))))
 
 
 def _bn_bwd_tail(ws, part, G, nq, mode, a, y, mean, invstd, gamma, dgamma, dbeta, dy_out,
