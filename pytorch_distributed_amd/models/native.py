@@ -147,8 +147,8 @@ class NativeResNet(nn.Module):
         self.ws_w = Workspace(device) if self._side is not None else self.ws
         # When the wgrad stream forks: "0" once per conv (eager default: each weight gradient
         # starts as soon as its inputs exist), "block" queues a residual block's weight-gradient
-        # kernels and forks ONCE per block (graph-capture default: in a captured graph every fork /
-        # join edge becomes a cross-queue barrier packet), "stage" once per stage; PDA_WGRAD_BATCH
+        # kernels and forks ONCE per block, "stage" once per stage (graph-capture default: in a
+        # captured graph every fork / join edge becomes a cross-queue barrier packet); PDA_WGRAD_BATCH
         # overrides both (profiles/ab_r2_inlaunch_bn.md sections 9, 10)
         self._wbatch_env = os.environ.get("PDA_WGRAD_BATCH")
         self.set_wgrad_batch(self._wbatch_env or "0")
@@ -167,9 +167,10 @@ class NativeResNet(nn.Module):
         self._wbatch = [] if self._side is not None and mode != "0" else None
 
     def use_graph_schedule(self) -> None:
-        """Schedule for HIP-graph capture: fork the wgrad stream once per block (unless
-        PDA_WGRAD_BATCH says otherwise)."""
-        self.set_wgrad_batch(self._wbatch_env or "block")
+        """Schedule for HIP-graph capture: fork the wgrad stream once per stage (unless
+        PDA_WGRAD_BATCH says otherwise): replayed 29.16-29.23 ms vs 29.50-29.63 per block and
+        29.85-30.00 per conv (profiles/ab_r2_inlaunch_bn.md section 10)."""
+        self.set_wgrad_batch(self._wbatch_env or "stage")
 
     # ------------------------------------------------------------------ planning
     def _build_plan(self) -> None:
