@@ -105,6 +105,7 @@ if _F32_CONV not in ("exact", "split"):
 _SPLIT_BN = int(os.environ.get("PDA_SPLIT_BN", "128"))   # widest N tile of the split kernels (A/B)
 _STATS_S = os.environ.get("PDA_STATS_S")   # fixed slab count of the statistics kernels (A/B)
 _STATS_S_SCALE = float(os.environ.get("PDA_STATS_S_SCALE", "1.0"))   # scale on its heuristic (A/B)
+_STEM_G = int(os.environ.get("PDA_STEM_G", "4096"))   # block cap of the one-pass stem backward (A/B)
 # downsample-tail BN backward: both branches' apply in one pass over dz (PDA_BWD_APPLY2=0: two)
 _BWD_APPLY2 = os.environ.get("PDA_BWD_APPLY2", "1") != "0"
 # scale on the split-K block targets (the wgrads run beside the dgrad chain on a second stream)
@@ -490,7 +491,7 @@ def stem_bwd_reduce(ws: "Workspace", dout, arg, y, scale, shift, dz_out, dout2=N
     Returns (part, G, nq) for :func:`bn_bwd_finish`."""
     N, H, W, C_ = y.shape
     Ho, Wo = dout.shape[1], dout.shape[2]
-    G = max(1, min(4096, (N * H * W) // 512))   # gather-latency bound: more blocks than a plain reduce
+    G = max(1, min(_STEM_G, (N * H * W) // 512))   # gather-latency bound: more blocks than a reduce
     part = ws.get("bn_part", G * 2 * C_)
     rc = ext.lib().pda_stem_bwd_reduce(ptr(dout), ptr(dout2), ptr(arg), ptr(y), ptr(scale), ptr(shift),
                                        ptr(dz_out), ptr(part), G, N, H, W, C_, Ho, Wo, dt_of(y),
