@@ -47,6 +47,8 @@ import traceback
 
 import torch
 
+from pytorch_distributed_amd.utils.gpu_util import BusySampler
+
 BASELINE = {1: 717.0, 8: 5546.7}      # BASELINE.md derived images/sec (other hardware)
 BASELINE_DP = {1: 717.0, 8: 1301.2}   # the nn.DataParallel bar of result.png
 GRAPH_DEFAULT = os.environ.get("PDA_GRAPH", "0") == "1"
@@ -86,7 +88,44 @@ def parse():
                     help="N>1: extra untimed steps with bucket timing events")
     ap.add_argument("--fp32-steps", type=int, default=5,
                     help="timed steps of the exact-fp32 pass (0: skip)")
+    ap.add_argument("--amp-steps", type=int, default=10,
+                    help="timed steps of the fp16 AMP-DDP pass (resnet_ddp_apex.py config; 0: skip)")
+    ap.add_argument("--dp-steps", type=int, default=10,
+                    help="timed steps of the DataParallel pass (resnet_dp.py config: rank 0 drives "
+                         "all N GPUs in one process; 0: skip)")
+    ap.add_argument("--nccl-channels", type=int, default=0,
+                    help="RCCL channel count (NCCL_MIN_NCHANNELS = NCCL_MAX_NCHANNELS); 0: RCCL's "
+                         "own tuning for the topology")
+    ap.add_argument("--nccl-proto", default="", help="NCCL_PROTO (LL, LL128, Simple; '' = RCCL's choice)")
+    ap.add_argument("--nccl-algo", default="", help="NCCL_ALGO (Ring, Tree; '' = RCCL's choice)")
     return ap.parse_args()
+
+
+def _configure_process(args) -> dict:
+    """Everything that must precede the first HIP call of the process: the IPC mode HSA reads at
+    its initialisation, the RCCL knobs a communicator reads at creation, and the NUMA binding (HIP's
+    runtime threads inherit the affinity the process has when they start). Returns the effective
+    RCCL/HSA settings for the JSON record."""
+    os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    os.environ.setdefault("MX_WATCHDOG", "0")   # timed runs: no polling thread beside the step
+    if args.nccl_channels > 0:
+        os.environ["NCCL_MIN_NCHANNELS"] = os.environ["NCCL_MAX_NCHANNELS"] = str(args.nccl_channels)
+    if args.nccl_proto:
+        os.environ["NCCL_PROTO"] = args.nccl_proto
+    if args.nccl_algo:
+        os.environ["NCCL_ALGO"] = args.nccl_algo
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    numa = False
+    if world > 1 and args.device == "cuda" and os.environ.get("PDA_BIND_NUMA", "1") != "0":
+        # one rank per GPU, pinned to that GPU's NUMA node as the reference's
+        # hfai.multiprocessing.spawn(bind_numa=True) (SURVEY R18); device_count() does not
+        # initialise HIP on this image
+        from pytorch_distributed_amd.launch import bind_numa
+        numa = bind_numa(local_rank % max(torch.cuda.device_count(), 1))
+    env = {k: v for k, v in sorted(os.environ.items())
+           if k.startswith(("NCCL_", "RCCL_", "HSA_ENABLE_IPC", "GPU_MAX_HW_QUEUES"))}
+    return {"comm_env": env, "numa_bound": numa}
 
 
 class Ctx:
@@ -216,19 +255,127 @@ def _fp32_pass(ctx: Ctx, args, mode: str = "exact") -> dict:
     return res
 
 
+def _gather_util(ctx: Ctx, mine):
+    """Average GPU busy % over the ranks' devices (the reference's "Avg GPU Util" panel)."""
+    if not ctx.multi:
+        return mine
+    import torch.distributed as dist
+    dev = ctx.device if dist.get_backend() == "nccl" else torch.device("cpu")
+    t = torch.tensor([mine if mine is not None else 0.0, 1.0 if mine is not None else 0.0],
+                     device=dev, dtype=torch.float64)
+    dist.all_reduce(t)
+    return round(float(t[0] / t[1]), 1) if t[1] > 0 else None
+
+
+def _guarded(ctx: Ctx, name: str, fn, *a) -> dict:
+    """A secondary pass must not cost the headline record: its failure is reported in the JSON
+    (``<name>_error``) on every rank, and the ranks stay in step (the pass ends on a barrier)."""
+    try:
+        return fn(*a)
+    except Exception as e:   # noqa: BLE001
+        traceback.print_exc()
+        return {f"{name}_error": f"{type(e).__name__}: {e}"[:300]}
+
+
+def _amp_pass(ctx: Ctx, args) -> dict:
+    """The resnet_ddp_apex.py configuration (/root/reference/resnet_ddp_apex.py:27-34,107): fp16
+    compute with dynamic loss scaling (native LossScaler: device-side inf scan + scale update, no
+    host sync), DDP gradient all-reduce over RCCL, fp32 master weights. Timed like the headline;
+    then the bit-exact cross-rank checksum of parameters + momentum."""
+    from pytorch_distributed_amd.bench_step import make_trainer
+    tr = make_trainer(args.arch, args.batch, torch.float16, ctx.device, engine=args.engine,
+                      world=ctx.world, rank=ctx.rank, bucket_mb=args.bucket_mb,
+                      image_size=args.image_size)
+    for i in range(3):
+        tr.step(i)
+    with BusySampler([ctx.device.index] if ctx.cuda else []) as busy:
+        el = _timed(ctx, tr, 3, args.amp_steps)
+    cons = _verify_consistent(ctx, tr)
+    world = ctx.world if ctx.multi else 1
+    sc = getattr(tr, "scaler", None)
+    res = {"amp_fp16_images_per_sec": round(args.batch * world * args.amp_steps / el, 2),
+           "amp_fp16_ms_per_step": round(1000.0 * el / args.amp_steps, 3),
+           "amp_config": f"fp16 + dynamic loss scaling, {'DDP over RCCL' if ctx.multi else 'single GPU'}"
+                         f" ({tr.engine}; resnet_ddp_apex.py)",
+           "amp_weights_consistent": cons.get("weights_consistent"),
+           "amp_loss": tr.last_loss(),
+           "amp_loss_scale": float(sc.get_scale()) if sc is not None and hasattr(sc, "get_scale") else None,
+           "amp_max_mem_gb": round(torch.cuda.max_memory_allocated(ctx.device) / 1e9, 2) if ctx.cuda else None,
+           "amp_gpu_util_pct": _gather_util(ctx, busy.overall())}
+    base = BASELINE.get(world)
+    if base:
+        res["amp_vs_baseline"] = round(res["amp_fp16_images_per_sec"] / base, 3)
+    del tr
+    if ctx.cuda:
+        torch.cuda.empty_cache()
+    return res
+
+
+def _dp_pass(ctx: Ctx, args, dtype) -> dict:
+    """The resnet_dp.py configuration (/root/reference/resnet_dp.py:82): ONE process drives all N
+    GPUs (global batch 400 x N), here rank 0 over devices 0..N-1 while the other ranks wait on
+    the TCP store (a host-side wait: an RCCL barrier would occupy their GPUs). Persistent native
+    replicas, per-replica graph-replayed forward/backward, in-process grouped RCCL all-reduce,
+    replicated fused SGD; afterwards every replica's weights must be bit-identical."""
+    n = min(ctx.world if ctx.multi else 1, torch.cuda.device_count())
+    store = None
+    if ctx.multi:
+        import torch.distributed as dist
+        store = dist.distributed_c10d._get_default_store()
+    res = {}
+    if ctx.rank == 0:
+        try:
+            from pytorch_distributed_amd.bench_step import make_dp_trainer
+            tr = make_dp_trainer(args.arch, args.batch, dtype, n, args.image_size)
+            for i in range(3):
+                tr.step(i)
+            devs = list(range(n))
+            for d in devs:
+                torch.cuda.synchronize(d)
+            with BusySampler(devs) as busy:
+                t0 = time.perf_counter()
+                for i in range(args.dp_steps):
+                    tr.step(3 + i)
+                for d in devs:
+                    torch.cuda.synchronize(d)
+                el = time.perf_counter() - t0
+            try:
+                tr.state_checksum()
+                same = True
+            except RuntimeError:
+                same = False
+            res = {"dp_images_per_sec": round(args.batch * n * args.dp_steps / el, 2),
+                   "dp_ms_per_step": round(1000.0 * el / args.dp_steps, 3),
+                   "dp_config": f"dataparallel{n}: one process, {n} GPU(s), global batch "
+                                f"{args.batch * n}, {tr.engine} (resnet_dp.py)",
+                   "dp_replicas_consistent": same,
+                   "dp_loss": tr.last_loss(),
+                   "dp_max_mem_gb": round(max(torch.cuda.max_memory_allocated(d) for d in devs) / 1e9, 2),
+                   "dp_gpu_util_pct": busy.overall()}
+            base = BASELINE_DP.get(n)
+            if base:
+                res["dp_vs_baseline"] = round(res["dp_images_per_sec"] / base, 3)
+            del tr
+            for d in devs:
+                with torch.cuda.device(d):
+                    torch.cuda.empty_cache()
+        finally:
+            if store is not None:
+                store.set("pda_bench_dp_done", json.dumps(res))
+    elif store is not None:
+        timeout = float(os.environ.get("PDA_DIST_TIMEOUT_S", "600"))
+        store.wait(["pda_bench_dp_done"], datetime.timedelta(seconds=timeout))
+        res = json.loads(store.get("pda_bench_dp_done").decode())
+    return res
+
+
 def main():
     args = parse()
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    proc = _configure_process(args)    # before Ctx: Ctx initialises HIP (set_device)
     ctx = Ctx(args)
     if args.gpus != ctx.world and ctx.world > 1:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE {ctx.world}", file=sys.stderr)
-    os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
-    os.environ.setdefault("MX_WATCHDOG", "0")   # timed runs: no polling thread beside the step
-    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
-    if ctx.world > 1 and ctx.cuda and os.environ.get("PDA_BIND_NUMA", "1") != "0":
-        # one rank per GPU, pinned to that GPU's NUMA node as the reference's
-        # hfai.multiprocessing.spawn(bind_numa=True)
-        from pytorch_distributed_amd.launch import bind_numa
-        bind_numa(ctx.local_rank % ctx.ndev)
     if ctx.world > 1:
         import torch.distributed as dist
         timeout = datetime.timedelta(seconds=float(os.environ.get("PDA_DIST_TIMEOUT_S", "600")))
@@ -257,7 +404,9 @@ def main():
     for i in range(args.warmup):
         tr.step(i)
     ctx.sync()
-    elapsed = _timed(ctx, tr, args.warmup, args.steps)   # barrier + sync on both sides, MAX
+    util_devs = list(range(args.gpus)) if args.dp else ([ctx.device.index] if ctx.cuda else [])
+    with BusySampler(util_devs) as busy:
+        elapsed = _timed(ctx, tr, args.warmup, args.steps)   # barrier + sync on both sides, MAX
     loss = tr.last_loss()
     nxt = args.warmup + args.steps
     diag = _diagnostics(ctx, tr, nxt) if ctx.multi else {}
@@ -273,13 +422,19 @@ def main():
            "optimizer": "SGD(lr=0.1, momentum=0.9, wd=1e-4)",
            "bucket_cap_mb": args.bucket_mb if ctx.multi else None}
     max_mem = round(torch.cuda.max_memory_allocated(ctx.device) / 1e9, 2) if ctx.cuda else None
-    fp32 = {}
-    if args.fp32_steps > 0 and args.dtype != "fp32" and not args.dp:
+    util = _gather_util(ctx, busy.overall())
+    extra = {}
+    if not args.dp:
         del tr
         if ctx.cuda:
             torch.cuda.empty_cache()
-        fp32 = _fp32_pass(ctx, args)
-        fp32.update(_fp32_pass(ctx, args, "split"))
+        if args.fp32_steps > 0 and args.dtype != "fp32":
+            extra.update(_fp32_pass(ctx, args))
+            extra.update(_fp32_pass(ctx, args, "split"))
+        if args.amp_steps > 0 and args.dtype != "fp16":
+            extra.update(_guarded(ctx, "amp_fp16", _amp_pass, ctx, args))
+        if args.dp_steps > 0 and ctx.cuda:
+            extra.update(_guarded(ctx, "dp", _dp_pass, ctx, args, dtype))
     if ctx.rank == 0:
         rec = {
             "metric": METRIC,
@@ -299,17 +454,23 @@ def main():
             "config": cfg,
             "loss": loss,
             "max_mem_gb": max_mem,
-            **diag, **consistency, **fp32,
+            "gpu_util_pct": util,
+            **proc, **diag, **consistency, **extra,
         }
-        if fp32 and base:
-            rec["vs_baseline_fp32"] = round(fp32["fp32_images_per_sec"] / base, 3)
-            if "fp32_split_images_per_sec" in fp32:
-                rec["vs_baseline_fp32_split"] = round(fp32["fp32_split_images_per_sec"] / base, 3)
+        if extra.get("fp32_images_per_sec") and base:
+            rec["vs_baseline_fp32"] = round(extra["fp32_images_per_sec"] / base, 3)
+            if "fp32_split_images_per_sec" in extra:
+                rec["vs_baseline_fp32_split"] = round(extra["fp32_split_images_per_sec"] / base, 3)
         print(json.dumps(rec), flush=True)
     if consistency.get("weights_consistent") is False:
         print(f"bench: rank {ctx.rank}: parameters differ across ranks after training "
               f"(checksum {consistency['checksum']})", file=sys.stderr, flush=True)
         sys.stderr.flush()
+        os._exit(3)
+    bad = [k for k in ("amp_weights_consistent", "dp_replicas_consistent") if extra.get(k) is False]
+    if bad:
+        print(f"bench: rank {ctx.rank}: inconsistent state after a secondary pass: {bad}",
+              file=sys.stderr, flush=True)
         os._exit(3)
     if ctx.multi:
         import torch.distributed as dist

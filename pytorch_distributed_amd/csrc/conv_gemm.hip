@@ -28,6 +28,27 @@ namespace {
 
 constexpr int NT = 256;
 
+// STAGES == 3 selects the LDS-DMA main loop: 512 threads (8 waves, one block per CU), operands
+// copied global -> LDS by buffer_load ... lds (16 B per lane, no VGPR round trip) into a 3-slot
+// ring, two k-tiles in flight across ONE barrier per k-tile (counted vmcnt, raw s_barrier).
+template <int STAGES> constexpr int conv_nt() { return STAGES == 3 ? 512 : NT; }
+
+// one LDS-DMA piece: lane l's 16 bytes at byte voff of the buffer land at lds + 16*l (lds must be
+// wave-uniform: it becomes M0). An out-of-range voff (>= the buffer's size) writes zeros.
+__device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t r, char* lds, uint32_t voff) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)lds, 16,
+                                           (int)voff, 0, 0, 0);
+}
+#ifndef PDA_DMA_SCHED   // 0: a k-tile's LDS-DMA pieces issued in one burst after the barrier
+#define PDA_DMA_SCHED 1   // 1: spread over the k-tile's MFMAs
+#endif
+#ifndef PDA_DMA_PRIO      // 1: s_setprio 1 for waves 4-7 (MI355X_MICROARCH.md, two waves per SIMD)
+#define PDA_DMA_PRIO 0
+#endif
+template <int N> __device__ __forceinline__ void vm_wait() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
 // WGRAD_BNA: WGRAD whose A operand is the BatchNorm-backward output formed while staging,
 // dY = k1[c]*dz + k2[c]*y + k3[c] (a = dz, a2 = y): the stem's weight gradient is the only consumer
 // of its BN-backward output, so the apply pass (and dY's write + re-read) is skipped.
@@ -186,9 +207,7 @@ __device__ __forceinline__ f32x4 frag_col_f32(const char* lds, int cb, int s, in
 // MFMA) need ~250 registers and 64 KiB of LDS: two blocks per CU.
 template <int DT, int BM, int BN, int STAGES>
 constexpr int conv_min_blocks() {
-#ifdef PDA_CONV_MINB_LEGACY   // A/B: the pre-r2 bounds (tools/build_variant.py)
-  return (STAGES == 1 && BM * BN <= 128 * 128) ? 3 : 2;
-#endif
+  if (STAGES == 3) return 2;   // one 512-thread block per CU = two waves per SIMD
   if (DT == DT_F32S) return BM * BN <= 64 * 64 ? 4 : 2;   // hi + lo tiles: twice the LDS
   if (DT != DT_F32 && BM * BN <= 64 * 64) return 5;
   if (DT != DT_F32 && STAGES == 1 && BM * BN <= 128 * 64) return 4;
@@ -198,9 +217,15 @@ constexpr int conv_min_blocks() {
 template <int PASS_T, int DT, int BM, int BN, int STAGES, int MF = 16>
 // WGRAD_BNA holds the fixed column chunk's 24 BN coefficients and the y chunks: 3 blocks per CU
 // (the 16-bit WGRAD budget of 4 spilled 15 VGPRs)
-__global__ __launch_bounds__(NT, (PASS_T == WGRAD_BNA ? 3 : conv_min_blocks<DT, BM, BN, STAGES>())) void conv_gemm_kernel(ConvParams p_arg) {
+__global__ __launch_bounds__(conv_nt<STAGES>(), (PASS_T == WGRAD_BNA ? 3 : conv_min_blocks<DT, BM, BN, STAGES>())) void conv_gemm_kernel(ConvParams p_arg) {
   constexpr int PASS = PASS_T == WGRAD_BNA ? WGRAD : PASS_T;
   constexpr bool ABN = PASS_T == WGRAD_BNA;
+  constexpr bool DMA = STAGES == 3;
+  constexpr int NTH = conv_nt<STAGES>();
+  // wave grid: 2x2 (256 threads); DMA: 4x2 or 2x4 so the wave tile stays square-ish
+  constexpr int WM = DMA ? (BM >= BN ? 4 : 2) : 2;
+  constexpr int WN = (NTH / 64) / WM;
+  static_assert(!DMA || ((DT == DT_BF16 || DT == DT_F16) && !ABN && MF == 16), "LDS-DMA: 16-bit");
   static_assert(!ABN || DT == DT_BF16 || DT == DT_F16, "WGRAD_BNA: 16-bit operands");
   static_assert(MF == 16 || (MF == 32 && (DT == DT_BF16 || DT == DT_F16) && BM >= 64 && BN >= 64),
                 "MFMA shape");
@@ -236,24 +261,25 @@ __global__ __launch_bounds__(NT, (PASS_T == WGRAD_BNA ? 3 : conv_min_blocks<DT, 
   constexpr int AB_BYTES = A_BYTES + B_BYTES;
   constexpr int STAGE = SPLIT ? 2 * AB_BYTES : AB_BYTES;
   // epilogue partial-sum reduction [3][RG][BN] f32
-  constexpr int RED_BYTES = 3 * NT * 8 * 4;
+  constexpr int RED_BYTES = 3 * NTH * 8 * 4;
   // staged C tile of the epilogue; f32 stages it in two row halves (one per wave row), so the
   // epilogue needs no more LDS than the main loop and f32 tiles keep 3 resident blocks per CU
   constexpr int NH = O32 ? 2 : 1;
   constexpr int C_BYTES = BM / NH * BN * ES;
   constexpr int LDS_0 = STAGES * STAGE > RED_BYTES ? STAGES * STAGE : RED_BYTES;
   constexpr int LDS_BYTES = LDS_0 > C_BYTES ? LDS_0 : C_BYTES;
-  static_assert(BN <= NT, "stats reduction: one thread per column");
+  static_assert(BN <= NTH, "stats reduction: one thread per column");
   static_assert(C_BYTES <= LDS_BYTES, "C tile must fit in the staging buffers");
-  static_assert(3 * NT * 8 * 4 <= LDS_BYTES, "stats reduction must fit");
+  static_assert(RED_BYTES <= LDS_BYTES, "stats reduction must fit");
   __shared__ __attribute__((aligned(16))) char smem[LDS_BYTES];
 
   constexpr bool A_ROW = (PASS != WGRAD);
   constexpr bool B_ROW = (PASS == FWD);
   constexpr int AR = BM / 32, BR = BN / 32;  // 16-B chunks per thread per tile
 
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int wr = wid >> 1, wc = wid & 1;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = wid / WN, wc = wid % WN;
   const int tiles_n = (p.N + BN - 1) / BN;
   const int tiles_m = (p.M + BM - 1) / BM;
   const int ntile = tiles_m * tiles_n;
@@ -621,13 +647,159 @@ __global__ __launch_bounds__(NT, (PASS_T == WGRAD_BNA ? 3 : conv_min_blocks<DT, 
     }
   };
 
+  // ---- LDS-DMA loader (DMA) ----------------------------------------------------------------
+  // Piece j of a thread is the 16-B chunk q = (wid*G + j)*64 + lane of the operand tile's LDS
+  // image, in LDS order (buffer_load ... lds writes lane-linearly at M0 + 16*lane). The images keep
+  // the register path's XOR swizzles: they are applied to the SOURCE -- the slot of row/krow r holds
+  // logical chunk slot ^ swz(r) -- so the fragment reads are the same code. Everything that does not
+  // change along K is precomputed; a k-tile then costs 1-3 VALU per piece (FWD/DGRAD tap select,
+  // an add) and, for the gathered WGRAD B, one pixel decode per piece.
+  constexpr int GA = DMA ? BM * 8 / NTH : 1, GB = DMA ? BN * 8 / NTH : 1;
+  static_assert(!DMA || (GA >= 1 && GB >= 1 && BM * 8 % NTH == 0 && BN * 8 % NTH == 0), "DMA tile");
+  int da_base[GA];        // A ROW: byte offset of the row's tap-(0,0) pixel + chunk (may be < 0)
+  uint64_t da_mask[GA];   // A ROW: taps of the row inside the image
+  uint32_t da_off[GA];    // A COL (WGRAD): byte offset of (krow, col) at k = kbeg
+  uint32_t db_off[GB];    // B at k = kbeg: FWD W row / DGRAD W k-row / WGRAD direct X row
+  int db_c[GB], db_r[GB], db_s[GB], db_krow[GB];   // WGRAD gathered B: column (tap, c), k row
+  bool db_ok[GB];
+  if constexpr (DMA) {
+    const int rch = (lane & 7) ^ ((lane >> 3) & 7);   // ROW images: chunk of the lane's slot
+    if constexpr (A_ROW) {
+#pragma unroll
+      for (int j = 0; j < GA; ++j) {
+        const int m = m0 + (wid * GA + j) * 8 + (lane >> 3);
+        const bool okm = m < p.M;
+        const uint32_t mm = okm ? m : 0;
+        uint64_t msk = 0;
+        int base;
+        if constexpr (PASS == FWD) {
+          const uint32_t img = fdiv(mm, p.dHoWo), rem = mm - img * p.dHoWo.d;
+          const uint32_t yo = fdiv(rem, p.dWo), xo = rem - yo * p.dWo.d;
+          const int y0 = (int)yo * p.stride - p.pad, x0 = (int)xo * p.stride - p.pad;
+          base = (((int)img * p.H + y0) * p.W + x0) * p.Cin * ES;
+          for (int r = 0, t = 0; r < p.R; ++r) {
+            const bool yok = (unsigned)(y0 + r) < (unsigned)p.H;
+            for (int q = 0; q < p.S; ++q, ++t)
+              if (yok && (unsigned)(x0 + q) < (unsigned)p.W) msk |= 1ull << t;
+          }
+        } else {   // DGRAD class-grid pixel
+          const uint32_t img = fdiv(mm, p.dHcWc), rem = mm - img * p.dHcWc.d;
+          const uint32_t yi = fdiv(rem, p.dWc), xi = rem - yi * p.dWc.d;
+          base = (((int)img * p.Ho + (int)yi) * p.Wo + (int)xi) * p.Cout * ES;
+          for (int t = 0; t < ntap; ++t)
+            if ((unsigned)((int)yi + p.tdy[split][t]) < (unsigned)p.Ho &&
+                (unsigned)((int)xi + p.tdx[split][t]) < (unsigned)p.Wo)
+              msk |= 1ull << t;
+        }
+        da_base[j] = base + rch * 16;
+        da_mask[j] = okm ? msk : 0ull;
+      }
+    } else {   // WGRAD A: dY COL image [64 pixels][BM channels]
+      constexpr int CPR = BM / 8;
+#pragma unroll
+      for (int j = 0; j < GA; ++j) {
+        const int q = (wid * GA + j) * 64 + lane, krow = q / CPR;
+        const int col = m0 + ((q % CPR) ^ col_swz<BM>(krow)) * 8;
+        da_off[j] = col < p.M ? (uint32_t)((kbeg + krow) * p.Cout + col) * (uint32_t)ES : OOB;
+      }
+    }
+    if constexpr (PASS == FWD) {   // B ROW: W [N][Kpad]
+#pragma unroll
+      for (int j = 0; j < GB; ++j) {
+        const int n = n0 + (wid * GB + j) * 8 + (lane >> 3);
+        db_off[j] = n < p.N ? (uint32_t)(n * p.Kpad + rch * 8) * (uint32_t)ES : OOB;
+      }
+    } else {   // B COL [64 k][BN]
+      constexpr int CPR = BN / 8;
+#pragma unroll
+      for (int j = 0; j < GB; ++j) {
+        const int q = (wid * GB + j) * 64 + lane, krow = q / CPR;
+        const int col = n0 + ((q % CPR) ^ col_swz<BN>(krow)) * 8;
+        if constexpr (PASS == DGRAD) {   // W[cout = k][tap][cin = col]
+          db_off[j] = col < p.N ? (uint32_t)(krow * p.R * p.S * p.Cin + col) * (uint32_t)ES : OOB;
+        } else {                         // X gathered at column (tap, c)
+          const int tap = col >> p.log2Cin;
+          db_c[j] = col & ((1 << p.log2Cin) - 1);
+          db_r[j] = (int)fdiv(tap, p.dS);
+          db_s[j] = tap - db_r[j] * p.S;
+          db_ok[j] = col < p.N && tap < p.R * p.S;
+          db_krow[j] = krow;
+          db_off[j] = db_ok[j] ? (uint32_t)((kbeg + krow) * p.Cin + db_c[j]) * (uint32_t)ES : OOB;
+        }
+      }
+    }
+  }
+  // source offsets of the thread's pieces of k-tile kt: voff[0, GA) A, voff[GA, GA+GB) B
+  constexpr int GP = GA + GB;
+  auto dma_offsets = [&](int kt, uint32_t* voff) __attribute__((always_inline)) {
+    const int k0 = kbeg + kt * BKE;
+    if constexpr (PASS == FWD) {   // the k-tile lies in one tap (Cin a power of two >= 64)
+      const int tap = k0 >> p.log2Cin;
+      const int c0 = k0 & ((1 << p.log2Cin) - 1);
+      const int r = (int)fdiv(tap, p.dS), q = tap - r * p.S;
+      const int toff = ((r * p.W + q) * p.Cin + c0) * ES;
+      const uint32_t word = tap >> 5, bit = tap & 31;
+#pragma unroll
+      for (int j = 0; j < GA; ++j) {
+        const uint32_t mw = word ? (uint32_t)(da_mask[j] >> 32) : (uint32_t)da_mask[j];
+        voff[j] = ((mw >> bit) & 1u) ? (uint32_t)(da_base[j] + toff) : OOB;
+      }
+#pragma unroll
+      for (int j = 0; j < GB; ++j) voff[GA + j] = db_off[j] + (uint32_t)k0 * ES;
+    } else if constexpr (PASS == DGRAD) {   // one tap per k-tile (Cout % 64 == 0)
+      const int ti = p.log2Cout >= 0 ? k0 >> p.log2Cout : k0 / p.Cout;
+      const int tsel = ti < 9 ? ti : 0;
+      const int c = k0 - ti * p.Cout;
+      const int toff = ((p.tdy[split][tsel] * p.Wo + p.tdx[split][tsel]) * p.Cout + c) * ES;
+#pragma unroll
+      for (int j = 0; j < GA; ++j)
+        voff[j] = (((uint32_t)da_mask[j] >> ti) & 1u) ? (uint32_t)(da_base[j] + toff) : OOB;
+      const uint32_t uoff = (uint32_t)((c * p.R * p.S + p.taps[split][tsel]) * p.Cin) * (uint32_t)ES;
+#pragma unroll
+      for (int j = 0; j < GB; ++j) voff[GA + j] = db_off[j] + uoff;
+    } else {   // WGRAD: rows past the split's end (ragged last split) are past the buffers' end
+      const uint32_t koff = (uint32_t)(kt * BKE * p.Cout) * (uint32_t)ES;
+#pragma unroll
+      for (int j = 0; j < GA; ++j) voff[j] = da_off[j] + koff;
+      if (wb_direct) {
+        const uint32_t xoff = (uint32_t)(kt * BKE * p.Cin) * (uint32_t)ES;
+#pragma unroll
+        for (int j = 0; j < GB; ++j) voff[GA + j] = db_off[j] + xoff;
+      } else {
+#pragma unroll
+        for (int j = 0; j < GB; ++j) {
+          const int m = k0 + db_krow[j];
+          bool ok = db_ok[j] && m < kend;
+          const uint32_t mm = ok ? m : 0;
+          const uint32_t img = fdiv(mm, p.dHoWo), rem = mm - img * p.dHoWo.d;
+          const uint32_t yo = fdiv(rem, p.dWo), xo = rem - yo * p.dWo.d;
+          const int y = (int)yo * p.stride - p.pad + db_r[j], x = (int)xo * p.stride - p.pad + db_s[j];
+          ok = ok && (unsigned)y < (unsigned)p.H && (unsigned)x < (unsigned)p.W;
+          voff[GA + j] = ok ? (uint32_t)(((((int)img * p.H + y) * p.W + x) * p.Cin + db_c[j]) * ES) : OOB;
+        }
+      }
+    }
+  };
+  // piece i of the thread into ring slot `slot`
+  auto dma_piece = [&](int i, int slot, const uint32_t* voff) __attribute__((always_inline)) {
+    char* sa = smem + slot * STAGE;
+    if (i < GA) dma16(rsa, sa + (wid * GA + i) * 1024, voff[i]);
+    else dma16(rsb, sa + A_BYTES + (wid * GB + i - GA) * 1024, voff[i]);
+  };
+  auto issue_dma = [&](int kt, int slot) __attribute__((always_inline)) {
+    uint32_t voff[GP];
+    dma_offsets(kt, voff);
+#pragma unroll
+    for (int i = 0; i < GP; ++i) dma_piece(i, slot, voff);
+  };
+
   // acc[i][j][e] = C[wr*(BM/2) + i*16 + (lane&15)][wc*(BN/2) + j*16 + 4*(lane>>4) + e].
   // The MFMA runs with its operands swapped (per 16x16 tile D = Bfrag x Afrag^T = C^T), so every
   // lane ends up holding 4 consecutive COLUMNS of one row: the epilogue writes the C tile with one
   // 8-byte packed LDS store per MFMA tile (and the f32 paths with 16-byte stores) instead of
   // per-element 2-byte stores.
-  constexpr int MI = BM / 32, NI = BN / 32;      // 16x16 tiles per wave
-  constexpr int MI2 = BM / 64, NI2 = BN / 64;    // 32x32 tiles per wave
+  constexpr int MI = BM / WM / 16, NI = BN / WN / 16;   // 16x16 tiles per wave
+  constexpr int MI2 = BM / WM / 32, NI2 = BN / WN / 32; // 32x32 tiles per wave
   f32x4 acc[MF == 16 ? MI : 1][MF == 16 ? NI : 1];
   f32x16 acc2[MF == 32 ? MI2 : 1][MF == 32 ? NI2 : 1];
 #pragma unroll
@@ -641,35 +813,21 @@ __global__ __launch_bounds__(NT, (PASS_T == WGRAD_BNA ? 3 : conv_min_blocks<DT, 
 #pragma unroll
       for (int e = 0; e < 16; ++e) acc2[i][j][e] = 0.f;
 
-  if (nk > 0) {
-    load_tile(0);
-    if constexpr (STAGES == 2) {
-      store_tile(0);
-      __syncthreads();
-    }
-  }
-  for (int kt = 0; kt < nk; ++kt) {
-    const int cur = STAGES == 2 ? (kt & 1) : 0;
-    if constexpr (STAGES == 1) {   // registers hold tile kt: publish it, then prefetch kt+1
-      store_tile(0);
-      __syncthreads();
-    }
-    if (kt + 1 < nk) load_tile(kt + 1);
-    const char* sa = smem + cur * STAGE;
-    const char* sb = sa + A_BYTES;
+  // MFMAs of one staged k-tile (A image at sa, B image at sb)
+  auto mma_tile = [&](const char* sa, const char* sb) __attribute__((always_inline)) {
     if constexpr (MF == 32) {
 #pragma unroll
       for (int s = 0; s < 4; ++s) {   // k-steps of 16
         s16x8 fa[MI2], fb[NI2];
 #pragma unroll
         for (int i = 0; i < MI2; ++i) {
-          const int rbase = wr * (BM / 2) + i * 32;
+          const int rbase = wr * (BM / WM) + i * 32;
           if constexpr (A_ROW) fa[i] = frag_row32(sa, rbase, s, lane);
           else fa[i] = frag_col32<BM>(sa, rbase, s, lane);
         }
 #pragma unroll
         for (int j = 0; j < NI2; ++j) {
-          const int cbase = wc * (BN / 2) + j * 32;
+          const int cbase = wc * (BN / WN) + j * 32;
           if constexpr (B_ROW) fb[j] = frag_row32(sb, cbase, s, lane);
           else fb[j] = frag_col32<BN>(sb, cbase, s, lane);
         }
@@ -685,13 +843,13 @@ __global__ __launch_bounds__(NT, (PASS_T == WGRAD_BNA ? 3 : conv_min_blocks<DT, 
         f32x4 fa[MI], fb[NI];
 #pragma unroll
         for (int i = 0; i < MI; ++i) {
-          const int rbase = wr * (BM / 2) + i * 16;
+          const int rbase = wr * (BM / WM) + i * 16;
           if constexpr (A_ROW) fa[i] = __builtin_bit_cast(f32x4, frag_row(sa, rbase, s, lane));
           else fa[i] = frag_col_f32<BM>(sa, rbase, s, lane);
         }
 #pragma unroll
         for (int j = 0; j < NI; ++j) {
-          const int cbase = wc * (BN / 2) + j * 16;
+          const int cbase = wc * (BN / WN) + j * 16;
           if constexpr (B_ROW) fb[j] = __builtin_bit_cast(f32x4, frag_row(sb, cbase, s, lane));
           else fb[j] = frag_col_f32<BN>(sb, cbase, s, lane);
         }
@@ -706,13 +864,13 @@ __global__ __launch_bounds__(NT, (PASS_T == WGRAD_BNA ? 3 : conv_min_blocks<DT, 
       s16x8 fa[MI], fb[NI];
 #pragma unroll
       for (int i = 0; i < MI; ++i) {
-        const int rbase = wr * (BM / 2) + i * 16;
+        const int rbase = wr * (BM / WM) + i * 16;
         if constexpr (A_ROW) fa[i] = frag_row(sa, rbase, s, lane);
         else fa[i] = frag_col<BM>(sa, rbase, s, lane);
       }
 #pragma unroll
       for (int j = 0; j < NI; ++j) {
-        const int cbase = wc * (BN / 2) + j * 16;
+        const int cbase = wc * (BN / WN) + j * 16;
         if constexpr (B_ROW) fb[j] = frag_row(sb, cbase, s, lane);
         else fb[j] = frag_col<BN>(sb, cbase, s, lane);
       }
@@ -720,7 +878,7 @@ __global__ __launch_bounds__(NT, (PASS_T == WGRAD_BNA ? 3 : conv_min_blocks<DT, 
         s16x8 fl[NI > MI ? NI : MI];
 #pragma unroll
         for (int j = 0; j < NI; ++j) {
-          const int cbase = wc * (BN / 2) + j * 16;
+          const int cbase = wc * (BN / WN) + j * 16;
           if constexpr (B_ROW) fl[j] = frag_row(sb + AB_BYTES, cbase, s, lane);
           else fl[j] = frag_col<BN>(sb + AB_BYTES, cbase, s, lane);
         }
@@ -733,7 +891,7 @@ __global__ __launch_bounds__(NT, (PASS_T == WGRAD_BNA ? 3 : conv_min_blocks<DT, 
           }
 #pragma unroll
         for (int i = 0; i < MI; ++i) {
-          const int rbase = wr * (BM / 2) + i * 16;
+          const int rbase = wr * (BM / WM) + i * 16;
           if constexpr (A_ROW) fl[i] = frag_row(sa + AB_BYTES, rbase, s, lane);
           else fl[i] = frag_col<BM>(sa + AB_BYTES, rbase, s, lane);
         }
@@ -750,10 +908,90 @@ __global__ __launch_bounds__(NT, (PASS_T == WGRAD_BNA ? 3 : conv_min_blocks<DT, 
       }
     }
     }   // MF == 16
-    if constexpr (STAGES == 2) {
-      if (kt + 1 < nk) store_tile(cur ^ 1);
+  };
+
+  if constexpr (DMA) {
+    // 3-slot ring: tile kt lives in slot kt % 3. Tile kt+2 is issued right after the barrier that
+    // retires tile kt (each wave's counted vmcnt + the barrier: every wave's DMA of tile kt has
+    // landed) and that proves every wave finished reading slot (kt+2) % 3 = (kt-1) % 3.
+    if (nk > 0) issue_dma(0, 0);
+    if (nk > 1) issue_dma(1, 1);
+#if PDA_DMA_PRIO
+    if (wid >= NTH / 128) __builtin_amdgcn_s_setprio(1);   // younger half: static priority
+#endif
+    int slot = 0;
+    for (int kt = 0; kt < nk; ++kt) {
+      if (kt + 1 < nk) vm_wait<GP>(); else vm_wait<0>();
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      const int nslot = slot == 0 ? 2 : slot - 1;
+      const char* sa = smem + slot * STAGE;
+      const char* sb = sa + A_BYTES;
+#if PDA_DMA_SCHED == 0
+      if (kt + 2 < nk) issue_dma(kt + 2, nslot);
+      mma_tile(sa, sb);
+#else
+      // the pieces of tile kt+2 spread over this tile's MFMAs (a burst of LDS-DMA issues right
+      // after the barrier holds every wave's matrix pipe); past the last tile they are OOB
+      // no-ops (nothing reads that slot again), so the MFMA stream carries no branch
+      uint32_t voff[GP];
+      dma_offsets(kt + 2, voff);
+      const bool pre = kt + 2 < nk;
+#pragma unroll
+      for (int i = 0; i < GP; ++i) voff[i] = pre ? voff[i] : OOB;
+      constexpr int NMF = MI * NI;
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        s16x8 fa[MI], fb[NI];
+#pragma unroll
+        for (int i = 0; i < MI; ++i) {
+          const int rbase = wr * (BM / WM) + i * 16;
+          if constexpr (A_ROW) fa[i] = frag_row(sa, rbase, s, lane);
+          else fa[i] = frag_col<BM>(sa, rbase, s, lane);
+        }
+#pragma unroll
+        for (int j = 0; j < NI; ++j) {
+          const int cbase = wc * (BN / WN) + j * 16;
+          if constexpr (B_ROW) fb[j] = frag_row(sb, cbase, s, lane);
+          else fb[j] = frag_col<BN>(sb, cbase, s, lane);
+        }
+#pragma unroll
+        for (int idx = 0; idx < NMF; ++idx) {
+          const int i = idx / NI, j = idx % NI;
+          acc[i][j] = mfma16<MDT>(fb[j], fa[i], acc[i][j]);
+          const int g = s * NMF + idx;   // piece pc goes after MFMA (pc * 2 * NMF) / GP
+#pragma unroll
+          for (int pc = 0; pc < GP; ++pc)
+            if (g == (pc * 2 * NMF) / GP) dma_piece(pc, nslot, voff);
+        }
+      }
+#endif
+      slot = slot == 2 ? 0 : slot + 1;
     }
-    __syncthreads();
+    vm_wait<0>();
+    __syncthreads();   // the epilogue reuses the ring
+  } else {
+    if (nk > 0) {
+      load_tile(0);
+      if constexpr (STAGES == 2) {
+        store_tile(0);
+        __syncthreads();
+      }
+    }
+    for (int kt = 0; kt < nk; ++kt) {
+      const int cur = STAGES == 2 ? (kt & 1) : 0;
+      if constexpr (STAGES == 1) {   // registers hold tile kt: publish it, then prefetch kt+1
+        store_tile(0);
+        __syncthreads();
+      }
+      if (kt + 1 < nk) load_tile(kt + 1);
+      const char* sa = smem + cur * STAGE;
+      mma_tile(sa, sa + A_BYTES);
+      if constexpr (STAGES == 2) {
+        if (kt + 1 < nk) store_tile(cur ^ 1);
+      }
+      __syncthreads();
+    }
   }
 
   // ================================================================ epilogue
@@ -784,8 +1022,8 @@ __global__ __launch_bounds__(NT, (PASS_T == WGRAD_BNA ? 3 : conv_min_blocks<DT, 
     float* slab = reinterpret_cast<float*>(p.out) + (size_t)split * p.M * p.N;
     const bool vec = (p.N & 3) == 0;
     for_items([&](int rl, int cl, const f32x4& v) {
-      const int row = m0 + wr * (BM / 2) + rl;
-      const int col = n0 + wc * (BN / 2) + cl;
+      const int row = m0 + wr * (BM / WM) + rl;
+      const int col = n0 + wc * (BN / WN) + cl;
       if (row >= p.M) return;
       float* d = slab + (size_t)row * p.N + col;
       if (vec) {
@@ -801,8 +1039,8 @@ __global__ __launch_bounds__(NT, (PASS_T == WGRAD_BNA ? 3 : conv_min_blocks<DT, 
     if (p.out_f32) {  // fc logits: f32 + bias, direct stores
       float* out = reinterpret_cast<float*>(p.out);
       for_items([&](int rl, int cl, const f32x4& v) {
-        const int row = m0 + wr * (BM / 2) + rl;
-        const int col = n0 + wc * (BN / 2) + cl;
+        const int row = m0 + wr * (BM / WM) + rl;
+        const int col = n0 + wc * (BN / WN) + cl;
         if (row >= p.M) return;
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
@@ -821,15 +1059,15 @@ __global__ __launch_bounds__(NT, (PASS_T == WGRAD_BNA ? 3 : conv_min_blocks<DT, 
     auto stage_f32 = [&](int h) __attribute__((always_inline)) {
       if (wr != h) return;
       for_items([&](int rl, int cl, f32x4 v) {
-        const int col = wc * (BN / 2) + cl;
+        const int col = wc * (BN / WN) + cl;
         if (relu) v = __builtin_elementwise_max(v, (f32x4){0.f, 0.f, 0.f, 0.f});
         *reinterpret_cast<f32x4*>(smem + rl * (BN * 4) + (((col >> 2) ^ (rl & (CPR - 1))) << 4)) = v;
       });
     };
     if constexpr (!O32) {
       for_items([&](int rl, int cl, f32x4 v) {
-        const int col = wc * (BN / 2) + cl;
-        const int row = wr * (BM / 2) + rl;
+        const int col = wc * (BN / WN) + cl;
+        const int row = wr * (BM / WM) + rl;
         if (relu) v = __builtin_elementwise_max(v, (f32x4){0.f, 0.f, 0.f, 0.f});
         // row & (CPR-1) == lr & (CPR-1) for CPR <= 16 (folded); BN = 256 needs the full row
         const int cbyte = (((col >> 3) ^ (row & (CPR - 1))) << 4) + ((col & 4) << 1);
@@ -851,7 +1089,7 @@ __global__ __launch_bounds__(NT, (PASS_T == WGRAD_BNA ? 3 : conv_min_blocks<DT, 
     // prologue, the packed form measured faster here.
     const int cc = tid % CPR;          // column chunk
     const int rg = tid / CPR;          // row group
-    constexpr int RG = NT / CPR;       // row groups
+    constexpr int RG = NTH / CPR;      // row groups
     constexpr int RPT = BM / RG;       // rows per thread
     constexpr int RPTH = RPT / NH;     // ... per staged half
     // rows are processed in groups of PD; the fused-epilogue operands of a group are loaded
@@ -1152,20 +1390,35 @@ static int launch(const ConvParams& p, dim3 grid, hipStream_t st) {
   if constexpr (PASS == WGRAD_BNA && DT != DT_BF16 && DT != DT_F16) {
     return -1;
   } else {
-    if constexpr (DT == DT_BF16 || DT == DT_F16) {
+    if constexpr ((DT == DT_BF16 || DT == DT_F16) && ST != 3) {
       if (g_mfma == 32) {
         hipLaunchKernelGGL((conv_gemm_kernel<PASS, DT, BM, BN, ST, 32>), grid, dim3(NT), 0, st, p);
         return (int)hipGetLastError();
       }
     }
-    hipLaunchKernelGGL((conv_gemm_kernel<PASS, DT, BM, BN, ST, 16>), grid, dim3(NT), 0, st, p);
+    hipLaunchKernelGGL((conv_gemm_kernel<PASS, DT, BM, BN, ST, 16>), grid, dim3(conv_nt<ST>()), 0, st, p);
     return (int)hipGetLastError();
   }
 }
 
-// bm < 0 selects the single-buffer (STAGES = 1) variant of tile |bm| x bn (FWD / DGRAD only)
+// Tile codes: bm < 0 selects the single-buffer (STAGES = 1) variant of tile |bm| x bn; bm > 1000
+// the LDS-DMA 8-wave variant (STAGES = 3) of tile (bm - 1000) x bn (16-bit, no operand prologue).
+static int tile_bm(int bm) { return bm > 1000 ? bm - 1000 : (bm < 0 ? -bm : bm); }
+
 template <int PASS>
 static int dispatch(int dt, int bm, int bn, const ConvParams& p, dim3 grid, hipStream_t st) {
+  if (bm > 1000) {
+    if (p.pro_sc != nullptr) return -5;   // the operand prologue needs register staging
+#define PDA_CASE3(D, M_, N_)                                                   \
+  if (dt == D && bm - 1000 == M_ && bn == N_) return launch<PASS, D, M_, N_, 3>(p, grid, st);
+    PDA_CASE3(DT_BF16, 256, 128) PDA_CASE3(DT_BF16, 128, 256) PDA_CASE3(DT_BF16, 128, 128)
+#ifndef PDA_DMA_ONLY
+    PDA_CASE3(DT_F16, 256, 128) PDA_CASE3(DT_F16, 128, 256) PDA_CASE3(DT_F16, 128, 128)
+#endif
+#undef PDA_CASE3
+    return -1;
+  }
+#ifndef PDA_DMA_ONLY   // experiment builds (tools/dma_ab.py): the LDS-DMA kernels only
   if (bm < 0) {
 #define PDA_CASE1(D, M_, N_)                                                   \
   if (dt == D && -bm == M_ && bn == N_) return launch<PASS, D, M_, N_, 1>(p, grid, st);
@@ -1190,6 +1443,7 @@ static int dispatch(int dt, int bm, int bn, const ConvParams& p, dim3 grid, hipS
   PDA_CASE(DT_F32, 128, 128) PDA_CASE(DT_F32, 128, 64) PDA_CASE(DT_F32, 64, 128)
   PDA_CASE(DT_F32, 64, 64)
 #undef PDA_CASE
+#endif
   return -1;
 }
 
@@ -1241,7 +1495,8 @@ int pda_conv_fwd(const ConvDesc* d, const void* x, const void* w, int Kpad, void
   p.M = d->Nb * d->Ho * d->Wo; p.N = d->Cout; p.Kpad = Kpad; p.K = Kpad;
   p.out_f32 = out_f32; p.relu = relu; p.out_pitch = out_pitch > 0 ? out_pitch : d->Cout;
   p.ntm = out_f32 ? 0 : conv_ntm((long long)p.M * p.out_pitch * (dt == DT_F32 || dt == DT_F32S ? 4 : 2), true);
-  const int abm = bm < 0 ? -bm : bm;
+  if (bm > 1000 && (d->Cin < 64 || (d->Cin & (d->Cin - 1)))) return -5;   // DMA: one tap per k-tile
+  const int abm = tile_bm(bm);
   const int tiles = ((p.M + abm - 1) / abm) * ((p.N + bn - 1) / bn);
   return dispatch<FWD>(dt, bm, bn, p, dim3(tiles, 1), st);
 }
@@ -1298,7 +1553,7 @@ int pda_conv_dgrad(const ConvDesc* d, const void* dy, const void* w, void* dx, c
     }
   }
   p.K = 0;
-  const int abm = bm < 0 ? -bm : bm;
+  const int abm = tile_bm(bm);
   const int tiles = ((p.M + abm - 1) / abm) * ((p.N + bn - 1) / bn);
   return dispatch<DGRAD>(dt, bm, bn, p, dim3(tiles, ncls), st);
 }
@@ -1325,8 +1580,10 @@ int pda_conv_wgrad_bna(const ConvDesc* d, const void* dz, const void* y, const f
   const dim3 grid(((p.M + abm - 1) / abm) * ((p.N + bn - 1) / bn), splits);
 #define PDA_BNA(D, M_, N_, S_) \
   if (dt == D && bm == (S_ == 1 ? -M_ : M_) && bn == N_) return launch<WGRAD_BNA, D, M_, N_, S_>(p, grid, st);
+#ifndef PDA_DMA_ONLY
   PDA_BNA(DT_BF16, 64, 128, 1) PDA_BNA(DT_BF16, 64, 128, 2)
   PDA_BNA(DT_F16, 64, 128, 1) PDA_BNA(DT_F16, 64, 128, 2)
+#endif
 #undef PDA_BNA
   return -1;
 }
@@ -1345,7 +1602,7 @@ int pda_conv_wgrad(const ConvDesc* d, const void* dy, const void* x, float* slab
   p.M = d->Cout; p.N = d->R * d->S * d->Cin;
   p.K = d->Nb * d->Ho * d->Wo;
   p.k_chunk = k_chunk;
-  const int abm = bm < 0 ? -bm : bm;
+  const int abm = tile_bm(bm);
   const int tiles = ((p.M + abm - 1) / abm) * ((p.N + bn - 1) / bn);
   return dispatch<WGRAD>(dt, bm, bn, p, dim3(tiles, splits), st);
 }

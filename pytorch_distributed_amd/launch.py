@@ -22,7 +22,7 @@ from typing import Callable, Optional, Sequence
 
 import torch
 
-__all__ = ["DistEnv", "dist_env", "spawn", "free_port", "bind_numa", "init_distributed"]
+__all__ = ["DistEnv", "dist_env", "spawn", "free_port", "bind_numa", "init_distributed", "gpu_pci_bdf"]
 
 
 @dataclass
@@ -62,8 +62,8 @@ def dist_env(local_rank: Optional[int] = None, nprocs: Optional[int] = None) -> 
     return DistEnv(addr, port, nnodes * gpus, node * gpus + lr, lr, gpus, node, nnodes)
 
 
-def _gpu_numa_cpus(local_rank: int) -> Optional[Sequence[int]]:
-    """CPUs of the NUMA node that hosts GPU ``local_rank`` (KFD topology, sysfs)."""
+def gpu_pci_bdf(index: int) -> Optional[str]:
+    """PCI address (``dddd:bb:dd.f``) of GPU ``index`` in HSA agent order (KFD topology, sysfs)."""
     try:
         root = "/sys/class/kfd/kfd/topology/nodes"
         gpus = []
@@ -72,11 +72,21 @@ def _gpu_numa_cpus(local_rank: int) -> Optional[Sequence[int]]:
             kv = dict(l.split(" ", 1) for l in props if " " in l)
             if int(kv.get("simd_count", "0")) > 0:
                 gpus.append(kv)
-        if local_rank >= len(gpus):
+        if index >= len(gpus):
             return None
-        dom = int(gpus[local_rank].get("domain", "0"))
-        bdf_bus = int(gpus[local_rank].get("location_id", "0"))
-        bdf = f"{dom:04x}:{(bdf_bus >> 8) & 0xff:02x}:{(bdf_bus >> 3) & 0x1f:02x}.{bdf_bus & 7}"
+        dom = int(gpus[index].get("domain", "0"))
+        loc = int(gpus[index].get("location_id", "0"))
+        return f"{dom:04x}:{(loc >> 8) & 0xff:02x}:{(loc >> 3) & 0x1f:02x}.{loc & 7}"
+    except (OSError, ValueError, KeyError):
+        return None
+
+
+def _gpu_numa_cpus(local_rank: int) -> Optional[Sequence[int]]:
+    """CPUs of the NUMA node that hosts GPU ``local_rank`` (KFD topology, sysfs)."""
+    try:
+        bdf = gpu_pci_bdf(local_rank)
+        if bdf is None:
+            return None
         numa = int(open(f"/sys/bus/pci/devices/{bdf}/numa_node").read())
         if numa < 0:
             return None

@@ -814,7 +814,7 @@ class NativeResNet(nn.Module):
             if j > 0:
                 up = b.units[j - 1]
                 sp = rec[f"s{j - 1}"]
-                Gp = K.dgrad_slabs(g, Nb)
+                Gp = K.dgrad_slabs(g, Nb, dtype=dy.dtype)
                 # the dgrad's epilogue produces dz and the BN-backward partials of bn_{j-1}
                 epi, part_p, nq_p = K.bn_epilogue(ws, Gp, ys[j - 1], sp[2], sp[3])
                 K.conv_dgrad(dy, self.w16_ohwi(u), g, out, epi=epi)      # out = dz of bn_{j-1}
@@ -826,7 +826,7 @@ class NativeResNet(nn.Module):
                 pb, prec = prev
                 if sc_ev is not None:
                     cur.wait_event(sc_ev)
-                Gp = K.dgrad_slabs(g, Nb)
+                Gp = K.dgrad_slabs(g, Nb, dtype=dy.dtype)
                 epi, part_p, nq_p = K.bn_epilogue(ws, Gp, g2=shortcut_g,
                                                   **self._tail_args(pb, prec, use_mask=True))
                 K.conv_dgrad(dy, self.w16_ohwi(u), g, out, epi=epi)      # out = dz of prev tail

@@ -118,17 +118,35 @@ def _kdt(t: torch.Tensor) -> int:
     return 3 if d == 0 and _F32_CONV == "split" else d
 
 
-def _ktile(bm: int, bn: int, kdt: int) -> Tuple[int, int]:
-    """The split-f32 kernels stage hi + lo tiles: single-stage tiles of at most 128 x 128."""
+def tile_rows(bm: int) -> int:
+    """M rows of a tile code: -bm = single-stage register-staged, bm > 1000 = the LDS-DMA 8-wave
+    variant of (bm - 1000) rows (csrc/conv_gemm.hip dispatch)."""
+    return bm - 1000 if bm > 1000 else abs(bm)
+
+
+def _ktile(bm: int, bn: int, kdt: int, pro: bool = False) -> Tuple[int, int]:
+    """The tile a launch actually uses. The LDS-DMA tiles (bm > 1000) are 16-bit only and cannot
+    apply an operand prologue (the bytes never pass through registers): those launches fall back
+    to the register-staged 128-row tile. The split-f32 kernels stage hi + lo tiles: single-stage
+    tiles of at most 128 x 128."""
+    if bm > 1000 and (kdt not in (1, 2) or pro):
+        bm, bn = -128, min(bn, 128)
     if kdt != 3:
         return bm, bn
     return -min(abs(bm), 128), min(bn, _SPLIT_BN)
 
 
-def pick_tile(M: int, N: int, K: Optional[int] = None) -> Tuple[int, int]:
+def pick_tile(M: int, N: int, K: Optional[int] = None, dma: bool = False) -> Tuple[int, int]:
     """(bm, bn) for an implicit GEMM; a negative bm selects the single-LDS-buffer variant: half the
     LDS admits a third resident block per CU, which hides the global-load latency better than
-    double buffering does at two blocks per CU (measured on all 23 ResNet-50 shapes)."""
+    double buffering does at two blocks per CU (measured on all 23 ResNet-50 shapes). ``dma``
+    (forward launches): the LDS-DMA 128x256 tile where it measured faster -- deep K (>= 1024) and
+    >= 256 output channels with enough tiles for every CU (profiles/convbench_r3_dma.txt: C12 C16
+    C17 C18 C20 C22, 4-9 %); the launch falls back to the 128-row register tile when the operand
+    needs the BN prologue or is not 16-bit (:func:`_ktile`)."""
+    if (dma and _DMA and K is not None and K >= 1024 and N >= 256 and N % 256 == 0
+            and math.ceil(M / 128) * (N // 256) >= _NUM_CU):
+        return 1128, 256
     bn = 64 if N <= 64 else 128
     bm = 128
     if math.ceil(M / 128) * math.ceil(N / bn) < 2 * _NUM_CU:
@@ -168,32 +186,32 @@ def conv_fwd(x: torch.Tensor, w: torch.Tensor, g: ConvGeom, out: torch.Tensor,
     Nb = x.shape[0]
     M = Nb * g.Ho * g.Wo
     Kpad = w.shape[-1] if w.dim() == 2 else w[0].numel()
-    bm, bn_ = tile or pick_tile(M, g.Cout, Kpad)
+    bm, bn_ = tile or pick_tile(M, g.Cout, Kpad, dma=True)
     d = g.desc(Nb)
     # direct (unstaged) f32 store + bias: the fc head (16-bit features -> f32 logits, or any conv
     # with a bias); f32 activations of the exact-fp32 engine take the staged path with statistics
     out_f32 = bias is not None or out.dtype != x.dtype
     pitch = out.stride(0) if out.dim() == 2 else g.Cout
-    T = math.ceil(M / abs(bm))
+    kdt = _kdt(x)
+    kbm, kbn = _ktile(bm, bn_, kdt, pro is not None or g.Cin < 64)
+    T = math.ceil(M / tile_rows(kbm))
     if bn is not None:
         stats = bn.ws.get("fwd_stats", T * 3 * g.Cout)
-    kdt = _kdt(x)
-    kbm, kbn = _ktile(bm, bn_, kdt)
     rc = ext.lib().pda_conv_fwd(C.byref(d), ptr(x), ptr(w), Kpad, ptr(out), int(out_f32), pitch,
                                 ptr(bias), ptr(stats), int(relu), ptr(pro[0] if pro else None),
                                 ptr(pro[1] if pro else None), kdt, kbm, kbn, stream(x.device))
     check(rc, "conv_fwd")
     if bn is not None:
-        bn_finalize_partials(stats, T, g.Cout, abs(bm), M, bn)
+        bn_finalize_partials(stats, T, g.Cout, tile_rows(kbm), M, bn)
     return out
 
 
 def stats_totals(stats: torch.Tensor, M: int, C_: int, bm: int) -> torch.Tensor:
     """f64 [2][C] (sum y, sum y^2) from conv_fwd's shifted per-tile partials (tests, tools)."""
-    T = math.ceil(M / abs(bm))
+    T = math.ceil(M / tile_rows(bm))
     p = stats[:T * 3 * C_].view(T, 3, C_).double()
-    rows = torch.full((T, 1), float(abs(bm)), dtype=torch.float64, device=stats.device)
-    rows[-1, 0] = M - (T - 1) * abs(bm)
+    rows = torch.full((T, 1), float(tile_rows(bm)), dtype=torch.float64, device=stats.device)
+    rows[-1, 0] = M - (T - 1) * tile_rows(bm)
     d0, d1, sh = p[:, 0], p[:, 1], p[:, 2]
     return torch.stack([(rows * sh + d0).sum(0), (d1 + sh * (2 * d0 + rows * sh)).sum(0)])
 
@@ -232,7 +250,7 @@ def bn_finalize_tot(tot: torch.Tensor, C_: int, count: int, bn: BnStats) -> None
 
 def stats_tiles(M: int, Cout: int, tile: Optional[Tuple[int, int]] = None) -> int:
     bm, _ = tile or pick_tile(M, Cout)
-    return math.ceil(M / abs(bm))
+    return math.ceil(M / tile_rows(bm))
 
 
 def dgrad_tile(g: ConvGeom, Nb: int) -> Tuple[int, int]:
@@ -248,11 +266,15 @@ def _max_class_taps(g: ConvGeom) -> int:
                for ph in (0, 1) for pw in (0, 1))
 
 
-def dgrad_slabs(g: ConvGeom, Nb: int, tile: Optional[Tuple[int, int]] = None) -> int:
-    """Number of partial-sum slabs the fused BN epilogue of a dgrad writes (classes x M-tiles)."""
-    bm, _ = tile or dgrad_tile(g, Nb)
+def dgrad_slabs(g: ConvGeom, Nb: int, tile: Optional[Tuple[int, int]] = None,
+                dtype: Optional[torch.dtype] = None) -> int:
+    """Number of partial-sum slabs the fused BN epilogue of a dgrad writes (classes x M-tiles);
+    ``dtype`` = the dgrad's operand dtype (the tile it launches may differ: :func:`_ktile`)."""
+    bm, bn = tile or dgrad_tile(g, Nb)
+    if dtype is not None:
+        bm, _ = _ktile(bm, bn, _kdt(torch.empty(0, dtype=dtype)))
     M = Nb * (g.H // g.stride) * (g.W // g.stride)
-    return g.stride * g.stride * math.ceil(M / abs(bm))
+    return g.stride * g.stride * math.ceil(M / tile_rows(bm))
 
 
 def conv_dgrad(dy: torch.Tensor, w: torch.Tensor, g: ConvGeom, dx: torch.Tensor,
@@ -291,10 +313,11 @@ def bn_epilogue(ws: "Workspace", G: int, y, scale, shift, res=None, y2=None, sca
 
 
 # Weight-gradient tile / split-K block target per ResNet conv geometry (Cout, R, Cin, stride, Ho),
-# measured with tools/wgrad_sweep.py on MI355X at batch 400 (profiles/wgrad_sweep_r1_v2.txt; the
-# 256x128 single-stage tile wins on the 3x3 layers 3-4 and the wide strided/narrowing 1x1s).
+# measured on MI355X at batch 400: tools/wgrad_sweep.py (profiles/wgrad_sweep_r1_v2.txt), then
+# tools/conv_bench.py re-measurements (profiles/convbench_r2.txt; round 3: the LDS-DMA 8-wave tiles,
+# 1000 + rows, win on the 3x3 and strided weight gradients, profiles/convbench_r3_dma.txt).
 _WGRAD_TUNED = {
-    (64, 1, 64, 1, 56): ((64, 64), 1024),       # C1
+    (64, 1, 64, 1, 56): ((-64, 128), 512),      # C1
     (64, 3, 64, 1, 56): ((64, 128), 512),       # C2
     (256, 1, 64, 1, 56): ((-128, 128), 512),    # C3
     (64, 1, 256, 1, 56): ((128, 128), 512),     # C4
@@ -303,12 +326,12 @@ _WGRAD_TUNED = {
     (512, 1, 128, 1, 28): ((128, 128), 512),    # C7
     (512, 1, 256, 2, 28): ((-256, 128), 512),   # C8
     (128, 1, 512, 1, 28): ((-128, 128), 512),   # C9
-    (128, 3, 128, 1, 28): ((64, 128), 2048),    # C10
+    (128, 3, 128, 1, 28): ((-64, 128), 512),    # C10
     (256, 1, 512, 1, 28): ((-256, 128), 1024),  # C11
-    (256, 3, 256, 2, 14): ((128, 128), 2048),   # C12
-    (1024, 1, 256, 1, 14): ((128, 64), 512),    # C13
+    (256, 3, 256, 2, 14): ((-256, 128), 512),   # C12
+    (1024, 1, 256, 1, 14): ((-128, 64), 512),   # C13
     (1024, 1, 512, 2, 14): ((128, 128), 512),   # C14
-    (256, 1, 1024, 1, 14): ((128, 64), 512),    # C15
+    (256, 1, 1024, 1, 14): ((-128, 64), 512),   # C15
     (256, 3, 256, 1, 14): ((-256, 128), 2048),  # C16
     (512, 1, 1024, 1, 14): ((128, 128), 512),   # C17
     (512, 3, 512, 2, 7): ((-256, 128), 4096),   # C18
@@ -317,23 +340,30 @@ _WGRAD_TUNED = {
     (512, 1, 2048, 1, 7): ((128, 128), 512),    # C21
     (512, 3, 512, 1, 7): ((-256, 128), 1024),   # C22
 }
-# round-2 re-measurement (profiles/convbench_r2.txt, the round-2 kernels): single-stage tiles at
-# the default block target beat the round-1 entries on these shapes (PDA_WGRAD_TUNE=r1: old table)
-if os.environ.get("PDA_WGRAD_TUNE", "r2") == "r2":
-    _WGRAD_TUNED.update({
-        (64, 1, 64, 1, 56): ((-64, 128), 512),      # C1   69.1 -> 61.0 us
-        (128, 3, 128, 1, 28): ((-64, 128), 512),    # C10 223.9 -> 213.2
-        (256, 3, 256, 2, 14): ((-256, 128), 512),   # C12 198.0 -> 130.2
-        (1024, 1, 256, 1, 14): ((-128, 64), 512),   # C13  83.4 -> 75.3
-        (256, 1, 1024, 1, 14): ((-128, 64), 512),   # C15  82.7 -> 74.8
-    })
+# LDS-DMA tiles (16-bit, no operand prologue; the register-staged entry above is the fallback)
+_DMA = os.environ.get("PDA_DMA", "1") != "0"
+_WGRAD_DMA = {
+    (128, 3, 128, 2, 28): ((1128, 256), 512),   # C6  221 -> 197 us
+    (512, 1, 256, 2, 28): ((1256, 128), 512),   # C8  193 -> 165
+    (128, 3, 128, 1, 28): ((1128, 256), 512),   # C10 202 -> 165
+    (256, 1, 512, 1, 28): ((1256, 128), 512),   # C11 200 -> 165
+    (256, 3, 256, 2, 14): ((1256, 128), 512),   # C12 160 -> 141
+    (256, 3, 256, 1, 14): ((1256, 128), 512),   # C16 148 -> 131
+    (512, 3, 512, 2, 7): ((1256, 128), 512),    # C18 145 -> 127
+    (512, 3, 512, 1, 7): ((1256, 128), 512),    # C22 140 -> 125
+}
 
 
 def wgrad_plan(g: ConvGeom, Nb: int, tile: Optional[Tuple[int, int]] = None,
                target_blocks: Optional[int] = None, max_slab_bytes: int = 64 << 20,
-               f32: bool = False):
+               f32: bool = False, dma: bool = False):
+    """(bm, bn, splits, k_chunk) of a weight gradient; ``dma``: the launch may use an LDS-DMA tile
+    (16-bit operands, no operand prologue)."""
     M, N, K = g.Cout, g.R * g.S * g.Cin, Nb * g.Ho * g.Wo
-    tuned = _WGRAD_TUNED.get((g.Cout, g.R, g.Cin, g.stride, g.Ho)) if _SINGLE_STAGE else None
+    key = (g.Cout, g.R, g.Cin, g.stride, g.Ho)
+    tuned = _WGRAD_TUNED.get(key) if _SINGLE_STAGE else None
+    if dma and _DMA and key in _WGRAD_DMA:
+        tuned = _WGRAD_DMA[key]
     bn = 128 if N >= 128 else 64
     bm = 128 if M >= 128 else 64
     if _SINGLE_STAGE and (bm == 128 or bn == 128):
@@ -341,14 +371,14 @@ def wgrad_plan(g: ConvGeom, Nb: int, tile: Optional[Tuple[int, int]] = None,
     if tuned and not tile:
         (bm, bn), tb = tuned
         target_blocks = target_blocks or tb
-        if f32 and (abs(bm) > 128 or bn > 128):   # 256-wide tiles are 16-bit only
+        if f32 and (tile_rows(bm) > 128 or bn > 128):   # 256-wide tiles are 16-bit only
             bm, bn = -128, 128
     if target_blocks is None:
         target_blocks = _WGRAD_TARGET
     target_blocks = max(1, int(target_blocks * _WGRAD_TB_SCALE))
     if tile:
         bm, bn = tile
-    tiles = math.ceil(M / abs(bm)) * math.ceil(N / bn)
+    tiles = math.ceil(M / tile_rows(bm)) * math.ceil(N / bn)
     splits = max(1, min(math.ceil(target_blocks / tiles), math.ceil(K / 256),
                         max(1, max_slab_bytes // (M * N * 4))))
     k_chunk = math.ceil(K / splits / 64) * 64
@@ -379,7 +409,8 @@ def conv_wgrad(dy: torch.Tensor, x: torch.Tensor, g: ConvGeom, grad: torch.Tenso
     dz and the kernel stages dY = k1*dz + k2*y + k3 itself (csrc/conv_gemm.hip WGRAD_BNA; see
     :func:`wgrad_bna_ok`)."""
     Nb = dy.shape[0]
-    bm, bn, splits, k_chunk = wgrad_plan(g, Nb, tile, target_blocks, f32=dy.dtype == torch.float32)
+    bm, bn, splits, k_chunk = wgrad_plan(g, Nb, tile, target_blocks, f32=dy.dtype == torch.float32,
+                                         dma=dy.dtype != torch.float32 and pro is None and bna is None)
     M, N = g.Cout, g.R * g.S * g.Cin
     slab = ws.get("wgrad_slab", splits * M * N)
     d = g.desc(Nb)

@@ -61,6 +61,11 @@ def test_bench_cpu_two_ranks_self_validation(tmp_path):
     assert rec["buckets"] >= 1 and len(rec["bucket_bytes"]) == rec["buckets"]
     assert sum(rec["bucket_bytes"]) >= 11_000_000 * 4     # every ResNet-18 gradient is bucketed
     assert rec["comm"] == "ProcessGroupCommunicator"
+    # the resnet_ddp_apex.py configuration, timed after the headline on every rank
+    assert rec["amp_fp16_images_per_sec"] > 0 and rec["amp_weights_consistent"] is True
+    assert "DDP" in rec["amp_config"]
+    assert isinstance(rec["comm_env"], dict) and rec["numa_bound"] is False
+    assert "gpu_util_pct" in rec
 
 
 def test_bench_cpu_diverged_rank_fails(tmp_path):

@@ -49,3 +49,25 @@ def test_bench_torchrun_two_ranks(tmp_path):
     # the like-for-like exact-fp32 pass, and the split-f32 (>= TF32 precision) pass
     assert rec["fp32_images_per_sec"] > 0 and rec["fp32_engine"] == "native"
     assert rec["fp32_split_images_per_sec"] > 0
+    # the other GPU configurations of BASELINE.json, each labelled with its config/dtype:
+    # fp16 AMP-DDP (resnet_ddp_apex.py) on both ranks, DataParallel (resnet_dp.py) by rank 0
+    # over the visible devices (one here) while rank 1 waits on the store
+    assert rec["amp_fp16_images_per_sec"] > 0 and rec["amp_weights_consistent"] is True
+    assert "fp16" in rec["amp_config"] and "DDP" in rec["amp_config"]
+    assert rec["dp_images_per_sec"] > 0 and rec["dp_replicas_consistent"] is True
+    assert rec["dp_config"].startswith("dataparallel1")
+    assert "HSA_ENABLE_IPC_MODE_LEGACY" in rec["comm_env"]
+    assert rec["max_mem_gb"] > 0 and rec["amp_max_mem_gb"] > 0 and rec["dp_max_mem_gb"] > 0
+
+
+def test_bench_torchrun_perturbed_rank_fails(tmp_path):
+    env = dict(os.environ)
+    env.update({"PDA_DIST_BACKEND": "gloo", "PDA_BIND_NUMA": "0", "OMP_NUM_THREADS": "4",
+                "HSA_ENABLE_IPC_MODE_LEGACY": "0", "PDA_BENCH_PERTURB_RANK": "1"})
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(_port()),
+           os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "1", "--warmup", "1",
+           "--batch", "8", "--image-size", "64", "--fp32-steps", "0", "--amp-steps", "0",
+           "--dp-steps", "0"]
+    r = subprocess.run(cmd, cwd=tmp_path, env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode != 0 and "parameters differ across ranks" in r.stderr

@@ -23,7 +23,9 @@ SHAPES = [  # name, H, Cin, Cout, k, stride  
     ("C22", 7, 512, 512, 3, 1),
 ]
 TILES = [(128, 128), (128, 64), (64, 128), (64, 64), (-128, 128), (-128, 64), (-64, 128)]
-WGRAD_TILES = TILES + [(-256, 128)]   # the 256-row single-stage tile exists for wgrad only
+# LDS-DMA 8-wave tiles (bm = 1000 + rows): 16-bit only
+DMA_TILES = [(1256, 128), (1128, 256), (1128, 128)]
+WGRAD_TILES = TILES + DMA_TILES + [(-256, 128)]   # the 256-row single-stage tile: wgrad only
 
 
 def rel_err(a, b):
@@ -56,7 +58,7 @@ def test_resnet50_conv_shape_all_tiles(shape):
     M = Nb * g.Ho * g.Wo
     bad = []
     for t in WGRAD_TILES:
-        if t not in TILES:   # wgrad-only tile
+        if t not in TILES + DMA_TILES:   # wgrad-only tile
             for tb in (64, 512, 4096):
                 dw = torch.full((Cout, k, k, Cin), float("nan"), device=DEV)
                 K.conv_wgrad(dy_nhwc, x_nhwc, g, dw.view(-1), ws, tile=t, target_blocks=tb)
@@ -122,5 +124,50 @@ def test_resnet50_conv_shape_all_tiles_exact_f32(shape):
         for name, a, b in (("fwd", y, yr), ("dgrad", dx, dxr), ("wgrad", dw, dwr)):
             e = rel_err(a.cpu().double(), b)
             if not e < 1e-5:
+                bad.append((t, name, e))
+    assert not bad, bad
+
+
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16], ids=["bf16", "f16"])
+@pytest.mark.parametrize("shape", [SHAPES[i] for i in (1, 5, 6, 11, 15, 17, 20, 21)],
+                         ids=[SHAPES[i][0] for i in (1, 5, 6, 11, 15, 17, 20, 21)])
+def test_dma_tiles_multi_tile(shape, dt):
+    """The LDS-DMA tiles at a batch that gives many full M tiles (the 3-slot ring wraps, every
+    slot is rewritten while other waves still compute): fwd + statistics, dgrad, wgrad vs fp32."""
+    from pytorch_distributed_amd.ops import ext
+    ext.load(required=True)
+    from pytorch_distributed_amd.ops import native_ops as K
+    _, H, Cin, Cout, k, s = shape
+    Nb, pad = 24 if H <= 14 else 6, k // 2
+    torch.manual_seed(2)
+    x = (torch.randn(Nb, Cin, H, H, device=DEV) + 0.1).to(dt).float()
+    w = (torch.randn(Cout, Cin, k, k, device=DEV) / math.sqrt(Cin * k * k)).to(dt).float()
+    xr = x.clone().requires_grad_(True)
+    wr = w.clone().requires_grad_(True)
+    y_ref = F.conv2d(xr, wr, stride=s, padding=pad)
+    dy = torch.randn_like(y_ref).to(dt).float()
+    y_ref.backward(dy)
+    g = K.ConvGeom(Nb, H, H, Cin, Cout, k, k, s, pad)
+    x_nhwc = x.permute(0, 2, 3, 1).contiguous().to(dt)
+    w_ohwi = w.permute(0, 2, 3, 1).contiguous().to(dt)
+    dy_nhwc = dy.permute(0, 2, 3, 1).contiguous().to(dt)
+    yr = y_ref.detach().permute(0, 2, 3, 1)
+    ws = K.Workspace(DEV)
+    M = Nb * g.Ho * g.Wo
+    bad = []
+    for t in DMA_TILES:
+        y = torch.full((Nb, g.Ho, g.Wo, Cout), float("nan"), device=DEV, dtype=dt)
+        stats = torch.zeros(math.ceil(M / 64) * 3 * Cout, device=DEV)
+        K.conv_fwd(x_nhwc, w_ohwi.view(Cout, -1), g, y, stats=stats, tile=t)
+        dx = torch.full((Nb, H, H, Cin), float("nan"), device=DEV, dtype=dt)
+        K.conv_dgrad(dy_nhwc, w_ohwi, g, dx, tile=t)
+        dw = torch.full((Cout, k, k, Cin), float("nan"), device=DEV)
+        K.conv_wgrad(dy_nhwc, x_nhwc, g, dw.view(-1), ws, tile=t, target_blocks=512)
+        torch.cuda.synchronize()
+        st = K.stats_totals(stats, M, Cout, t[0]).float()
+        for name, e in (("fwd", rel_err(y, yr)), ("dgrad", rel_err(dx, xr.grad.permute(0, 2, 3, 1))),
+                        ("wgrad", rel_err(dw, wr.grad.permute(0, 2, 3, 1))),
+                        ("stats", rel_err(st[0], y.float().reshape(-1, Cout).sum(0)))):
+            if not e < 1e-2:
                 bad.append((t, name, e))
     assert not bad, bad

@@ -24,8 +24,10 @@ SHAPES = [  # name, H, Cin, Cout, k, stride
 COUNT = {"C1": 1, "C2": 3, "C3": 4, "C4": 2, "C5": 1, "C6": 1, "C7": 4, "C8": 1, "C9": 3, "C10": 3,
          "C11": 1, "C12": 1, "C13": 6, "C14": 1, "C15": 5, "C16": 5, "C17": 1, "C18": 1, "C19": 3,
          "C20": 1, "C21": 2, "C22": 2}
-TILES = [(128, 128), (128, 64), (64, 128), (64, 64), (-128, 128), (-128, 64), (-64, 128), (-256, 128)]
-# -bm: 1-stage; the 256-row tile is compiled for wgrad only (other passes report n/a)
+TILES = [(128, 128), (128, 64), (64, 128), (64, 64), (-128, 128), (-128, 64), (-64, 128), (-256, 128),
+         (1256, 128), (1128, 256), (1128, 128)]
+# -bm: 1-stage; the -256 tile is compiled for wgrad only (other passes report n/a);
+# 1000 + bm: the LDS-DMA 8-wave tiles
 
 
 def timeit(fn, reps):
@@ -49,7 +51,7 @@ def main():
     ws = K.Workspace(dev)
     total_best = {"fwd": 0.0, "dgrad": 0.0, "wgrad": 0.0}
     total_def = {"fwd": 0.0, "dgrad": 0.0, "wgrad": 0.0}
-    print(f"{'shape':5s} {'pass':6s} " + " ".join(f"{a:4d}x{b:<3d}" for a, b in TILES) + "  default  best")
+    print(f"{'shape':5s} {'pass':6s} " + " ".join(f"{a:5d}x{b:<3d}" for a, b in TILES) + "  default  best")
     for name, H, Cin, Cout, k, s in SHAPES:
         g = K.ConvGeom(B, H, H, Cin, Cout, k, k, s, k // 2)
         x = torch.randn(B, H, H, Cin, device=dev).to(dt)
@@ -86,7 +88,7 @@ def main():
             n = COUNT[name]
             total_best[ps] += tb * n
             total_def[ps] += td * n
-            print(f"{name:5s} {ps:6s} " + " ".join(f"{v:8.1f}" for v in ts) +
+            print(f"{name:5s} {ps:6s} " + " ".join(f"{v:9.1f}" for v in ts) +
                   f"  {td:7.1f}  {TILES[ts.index(tb)]} {flop / tb / 1e6:6.0f}TF")
     print("per-step totals (us, x layer count): default", {k: round(v) for k, v in total_def.items()},
           " best", {k: round(v) for k, v in total_best.items()})
