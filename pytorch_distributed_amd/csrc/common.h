@@ -77,18 +77,6 @@ template <> __device__ __forceinline__ f32x4 mfma16<DT_F16>(s16x8 a, s16x8 b, f3
                                                 __builtin_bit_cast(f16x8, b), c, 0, 0, 0);
 }
 
-// ---- MFMA 32x32x16 (bf16 / f16): lane l holds A[row l&31][k 8(l>>5)+j] / B[k 8(l>>5)+j][col l&31];
-// D: col = lane&31, row = (reg&3) + 8(reg>>2) + 4(lane>>5)
-template <int DT> __device__ __forceinline__ f32x16 mfma32(s16x8 a, s16x8 b, f32x16 c);
-template <> __device__ __forceinline__ f32x16 mfma32<DT_BF16>(s16x8 a, s16x8 b, f32x16 c) {
-  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, a),
-                                                 __builtin_bit_cast(bf16x8, b), c, 0, 0, 0);
-}
-template <> __device__ __forceinline__ f32x16 mfma32<DT_F16>(s16x8 a, s16x8 b, f32x16 c) {
-  return __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8, a),
-                                                __builtin_bit_cast(f16x8, b), c, 0, 0, 0);
-}
-
 // ---- MFMA 16x16x4 f32 (exact fp32 path, MX_DTYPE=fp32) --------------------------------------
 __device__ __forceinline__ f32x4 mfma16_f32(float a, float b, f32x4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);

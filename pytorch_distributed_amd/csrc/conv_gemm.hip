@@ -31,7 +31,7 @@ constexpr int NT = 256;
 // STAGES == 3 selects the LDS-DMA main loop: 512 threads (8 waves, one block per CU), operands
 // copied global -> LDS by buffer_load ... lds (16 B per lane, no VGPR round trip) into a 3-slot
 // ring, two k-tiles in flight across ONE barrier per k-tile (counted vmcnt, raw s_barrier).
-template <int STAGES> constexpr int conv_nt() { return STAGES == 3 ? 512 : NT; }
+template <int STAGES> constexpr int conv_nt() { return STAGES >= 3 ? 512 : NT; }
 
 // one LDS-DMA piece: lane l's 16 bytes at byte voff of the buffer land at lds + 16*l (lds must be
 // wave-uniform: it becomes M0). An out-of-range voff (>= the buffer's size) writes zeros.
@@ -39,12 +39,6 @@ __device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t r, char* lds, uint3
   __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)lds, 16,
                                            (int)voff, 0, 0, 0);
 }
-#ifndef PDA_DMA_SCHED   // 0: a k-tile's LDS-DMA pieces issued in one burst after the barrier
-#define PDA_DMA_SCHED 1   // 1: spread over the k-tile's MFMAs
-#endif
-#ifndef PDA_DMA_PRIO      // 1: s_setprio 1 for waves 4-7 (MI355X_MICROARCH.md, two waves per SIMD)
-#define PDA_DMA_PRIO 0
-#endif
 template <int N> __device__ __forceinline__ void vm_wait() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
@@ -94,8 +88,6 @@ struct ConvParams {
   float* epart;                    // [ncls*tiles_m][enq][N] partial sums
   const void* a2;                  // WGRAD_BNA: y (the BN input) beside a = dz
   const float* ak1; const float* ak2; const float* ak3;   // WGRAD_BNA: per-Cout coefficients
-  int ntm;                         // nontemporal policy of this launch: bit 0 epilogue operand
-                                   // loads (DGRAD), bit 1 output stores
   // FWD BatchNorm statistics (stats != nullptr) are per-M-tile SHIFTED partials
   // stats[tile][3][N] = (sum(y - s), sum((y - s)^2), s), s = the tile's first row (no f32
   // cancellation when |mean| >> std); bn.hip bn_fwd_stats combines and finalizes them.
@@ -149,30 +141,6 @@ __device__ __forceinline__ s16x8 frag_col(const char* lds, int cb, int s, int la
   return r;
 }
 
-// 32x32x16 fragments, k-step s (16 k) of the 64-k tile: lane holds row/col base+(l&31),
-// k 16s + 8(l>>5) .. +7
-__device__ __forceinline__ s16x8 frag_row32(const char* lds, int rb, int s, int lane) {
-  const int row = rb + (lane & 31);
-  const int chunk = s * 2 + (lane >> 5);
-  return *reinterpret_cast<const s16x8*>(lds + row_addr(row, chunk));
-}
-// COL tile: 16-lane group g reads column block cb + 16(g&1), k rows 16s + 8(g>>1) + 0..7 with two
-// transposed reads (ds_read_b64_tr_b16: lane 4q+p addresses row q, columns 4p..4p+3)
-template <int BC>
-__device__ __forceinline__ s16x8 frag_col32(const char* lds, int cb, int s, int lane) {
-  const int g = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3;
-  const int chunk = ((cb + 16 * (g & 1)) >> 3) + (p >> 1);
-  const int k0 = s * 16 + 8 * (g >> 1) + q;
-  const int a0 = col_addr<BC>(k0, chunk) + ((p & 1) << 3);
-  const int a1 = col_addr<BC>(k0 + 4, chunk) + ((p & 1) << 3);
-  s16x4 v0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(s16x4, lds + a0));
-  s16x4 v1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(s16x4, lds + a1));
-  s16x8 r;
-  r[0] = v0[0]; r[1] = v0[1]; r[2] = v0[2]; r[3] = v0[3];
-  r[4] = v1[0]; r[5] = v1[1]; r[6] = v1[2]; r[7] = v1[3];
-  return r;
-}
-
 // COL tile of f32 (exact-fp32 path): 32 k-rows x BC cols of 4 B, 16-B chunks XOR-swizzled by
 // 4 * ((krow >> 2) & 3) so the four k-groups of a fragment read land in disjoint bank quarters.
 template <int BC>
@@ -197,9 +165,6 @@ __device__ __forceinline__ f32x4 frag_col_f32(const char* lds, int cb, int s, in
 // STAGES = 1: single LDS buffer (half the LDS -> one more resident block per CU) for the many
 //             shallow-K layers of ResNet (K = 64..128: nk <= 2), where the per-block
 //             load -> MFMA -> store chain is latency-bound and concurrency matters more.
-// MF = 32: the 16-bit paths issue MFMA 32x32x16 instead of 16x16x32 -- the same FLOP per cycle
-// with half the MFMA instructions and fragment reads, so three times the VALU issue slots per
-// MFMA for the operand gather / BN prologue (the 16x16 main loops are VALU-issue-bound: PMC r1).
 // Resident blocks per CU the register allocation must allow (one wave per SIMD per block): the
 // 16-bit 64x64 and single-stage 128x64 / 64x128 tiles are held to 5 / 4 (<= 96 / 128 VGPRs) --
 // their fused epilogues would otherwise push them a few registers over and cost a wave per SIMD.
@@ -207,28 +172,28 @@ __device__ __forceinline__ f32x4 frag_col_f32(const char* lds, int cb, int s, in
 // MFMA) need ~250 registers and 64 KiB of LDS: two blocks per CU.
 template <int DT, int BM, int BN, int STAGES>
 constexpr int conv_min_blocks() {
-  if (STAGES == 3) return 2;   // one 512-thread block per CU = two waves per SIMD
+  if (STAGES >= 3) return 2;   // one 512-thread block per CU = two waves per SIMD
   if (DT == DT_F32S) return BM * BN <= 64 * 64 ? 4 : 2;   // hi + lo tiles: twice the LDS
   if (DT != DT_F32 && BM * BN <= 64 * 64) return 5;
   if (DT != DT_F32 && STAGES == 1 && BM * BN <= 128 * 64) return 4;
   return (STAGES == 1 && BM * BN <= 128 * 128) ? 3 : 2;
 }
 
-template <int PASS_T, int DT, int BM, int BN, int STAGES, int MF = 16>
+template <int PASS_T, int DT, int BM, int BN, int STAGES>
 // WGRAD_BNA holds the fixed column chunk's 24 BN coefficients and the y chunks: 3 blocks per CU
 // (the 16-bit WGRAD budget of 4 spilled 15 VGPRs)
 __global__ __launch_bounds__(conv_nt<STAGES>(), (PASS_T == WGRAD_BNA ? 3 : conv_min_blocks<DT, BM, BN, STAGES>())) void conv_gemm_kernel(ConvParams p_arg) {
   constexpr int PASS = PASS_T == WGRAD_BNA ? WGRAD : PASS_T;
   constexpr bool ABN = PASS_T == WGRAD_BNA;
-  constexpr bool DMA = STAGES == 3;
+  constexpr bool DMA = STAGES >= 3;
+  // STAGES == 4 (HALO): tap reuse for 3x3 stride-1 FWD / DGRAD -- see the HALO main loop
+  constexpr bool HALO = STAGES == 4;
   constexpr int NTH = conv_nt<STAGES>();
   // wave grid: 2x2 (256 threads); DMA: 4x2 or 2x4 so the wave tile stays square-ish
   constexpr int WM = DMA ? (BM >= BN ? 4 : 2) : 2;
   constexpr int WN = (NTH / 64) / WM;
-  static_assert(!DMA || ((DT == DT_BF16 || DT == DT_F16) && !ABN && MF == 16), "LDS-DMA: 16-bit");
+  static_assert(!DMA || ((DT == DT_BF16 || DT == DT_F16) && !ABN), "LDS-DMA: 16-bit");
   static_assert(!ABN || DT == DT_BF16 || DT == DT_F16, "WGRAD_BNA: 16-bit operands");
-  static_assert(MF == 16 || (MF == 32 && (DT == DT_BF16 || DT == DT_F16) && BM >= 64 && BN >= 64),
-                "MFMA shape");
   // DGRAD / WGRAD read the parameters in place in the kernarg segment (constant address space):
   // binding a reference to the by-value argument makes the compiler copy the whole ~1 KB block to
   // scratch once a member array is indexed dynamically (DGRAD tap tables), and costs WGRAD spills.
@@ -266,7 +231,12 @@ __global__ __launch_bounds__(conv_nt<STAGES>(), (PASS_T == WGRAD_BNA ? 3 : conv_
   // epilogue needs no more LDS than the main loop and f32 tiles keep 3 resident blocks per CU
   constexpr int NH = O32 ? 2 : 1;
   constexpr int C_BYTES = BM / NH * BN * ES;
-  constexpr int LDS_0 = STAGES * STAGE > RED_BYTES ? STAGES * STAGE : RED_BYTES;
+  // HALO: two input-slab slots of BM + 128 rows (any W <= 63: BM + 2W + 2 rows), three weight-tile
+  // slots and one zero row (the fragment source of a tap that falls outside the image)
+  constexpr int SLAB_ROWS = BM + 128, SLAB_BYTES = SLAB_ROWS * 128;
+  constexpr int ZOFF = 2 * SLAB_BYTES + 3 * B_BYTES;
+  constexpr int RING = HALO ? ZOFF + 128 : STAGES * STAGE;
+  constexpr int LDS_0 = RING > RED_BYTES ? RING : RED_BYTES;
   constexpr int LDS_BYTES = LDS_0 > C_BYTES ? LDS_0 : C_BYTES;
   static_assert(BN <= NTH, "stats reduction: one thread per column");
   static_assert(C_BYTES <= LDS_BYTES, "C tile must fit in the staging buffers");
@@ -662,9 +632,38 @@ __global__ __launch_bounds__(conv_nt<STAGES>(), (PASS_T == WGRAD_BNA ? 3 : conv_
   uint32_t db_off[GB];    // B at k = kbeg: FWD W row / DGRAD W k-row / WGRAD direct X row
   int db_c[GB], db_r[GB], db_s[GB], db_krow[GB];   // WGRAD gathered B: column (tap, c), k row
   bool db_ok[GB];
+  constexpr int HA = HALO ? SLAB_ROWS / 64 : 1;     // HALO: slab pieces per thread and chunk
+  uint32_t ha_off[HA];                               // HALO: slab piece sources at channel 0
+  int hrow[HALO ? BM / WM / 16 : 1];                 // HALO: slab row of the fragment's pixel
+  uint32_t hmask[HALO ? BM / WM / 16 : 1];           // HALO: taps inside the image (bit t)
   if constexpr (DMA) {
     const int rch = (lane & 7) ^ ((lane >> 3) & 7);   // ROW images: chunk of the lane's slot
-    if constexpr (A_ROW) {
+    if constexpr (HALO) {
+      // slab piece j: rows j*64 + wid*8 + lane/8 of the slab = pixels m0 - W - 1 + row
+      const int csz = PASS == FWD ? p.Cin : p.Cout;
+#pragma unroll
+      for (int j = 0; j < HA; ++j) {
+        const int pix = m0 - (p.W + 1) + j * 64 + wid * 8 + (lane >> 3);
+        ha_off[j] = (pix >= 0 && pix < p.M) ? (uint32_t)(pix * csz + rch * 8) * (uint32_t)ES : OOB;
+      }
+      // fragment rows: slab row of the tap-centre pixel and the taps that stay inside the image
+#pragma unroll
+      for (int i = 0; i < BM / WM / 16; ++i) {
+        const int rl = wr * (BM / WM) + i * 16 + (lane & 15);
+        const int m = m0 + rl;
+        hrow[i] = rl + p.W + 1;
+        const uint32_t mm = m < p.M ? m : 0;
+        const uint32_t img = fdiv(mm, p.dHoWo), rem = mm - img * p.dHoWo.d;
+        const int y = (int)fdiv(rem, p.dWo), x = (int)(rem - (uint32_t)y * p.dWo.d);
+        uint32_t msk = 0;
+#pragma unroll
+        for (int t = 0; t < 9; ++t) {
+          const int dy = PASS == FWD ? t / 3 - 1 : 1 - t / 3, dx = PASS == FWD ? t % 3 - 1 : 1 - t % 3;
+          if ((unsigned)(y + dy) < (unsigned)p.H && (unsigned)(x + dx) < (unsigned)p.W) msk |= 1u << t;
+        }
+        hmask[i] = m < p.M ? msk : 0u;
+      }
+    } else if constexpr (A_ROW) {
 #pragma unroll
       for (int j = 0; j < GA; ++j) {
         const int m = m0 + (wid * GA + j) * 8 + (lane >> 3);
@@ -799,44 +798,14 @@ __global__ __launch_bounds__(conv_nt<STAGES>(), (PASS_T == WGRAD_BNA ? 3 : conv_
   // 8-byte packed LDS store per MFMA tile (and the f32 paths with 16-byte stores) instead of
   // per-element 2-byte stores.
   constexpr int MI = BM / WM / 16, NI = BN / WN / 16;   // 16x16 tiles per wave
-  constexpr int MI2 = BM / WM / 32, NI2 = BN / WN / 32; // 32x32 tiles per wave
-  f32x4 acc[MF == 16 ? MI : 1][MF == 16 ? NI : 1];
-  f32x16 acc2[MF == 32 ? MI2 : 1][MF == 32 ? NI2 : 1];
+  f32x4 acc[MI][NI];
 #pragma unroll
-  for (int i = 0; i < (MF == 16 ? MI : 1); ++i)
+  for (int i = 0; i < MI; ++i)
 #pragma unroll
-    for (int j = 0; j < (MF == 16 ? NI : 1); ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-  for (int i = 0; i < (MF == 32 ? MI2 : 1); ++i)
-#pragma unroll
-    for (int j = 0; j < (MF == 32 ? NI2 : 1); ++j)
-#pragma unroll
-      for (int e = 0; e < 16; ++e) acc2[i][j][e] = 0.f;
+    for (int j = 0; j < NI; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   // MFMAs of one staged k-tile (A image at sa, B image at sb)
   auto mma_tile = [&](const char* sa, const char* sb) __attribute__((always_inline)) {
-    if constexpr (MF == 32) {
-#pragma unroll
-      for (int s = 0; s < 4; ++s) {   // k-steps of 16
-        s16x8 fa[MI2], fb[NI2];
-#pragma unroll
-        for (int i = 0; i < MI2; ++i) {
-          const int rbase = wr * (BM / WM) + i * 32;
-          if constexpr (A_ROW) fa[i] = frag_row32(sa, rbase, s, lane);
-          else fa[i] = frag_col32<BM>(sa, rbase, s, lane);
-        }
-#pragma unroll
-        for (int j = 0; j < NI2; ++j) {
-          const int cbase = wc * (BN / WN) + j * 32;
-          if constexpr (B_ROW) fb[j] = frag_row32(sb, cbase, s, lane);
-          else fb[j] = frag_col32<BN>(sb, cbase, s, lane);
-        }
-#pragma unroll
-        for (int i = 0; i < MI2; ++i)
-#pragma unroll
-          for (int j = 0; j < NI2; ++j) acc2[i][j] = mfma32<DT>(fb[j], fa[i], acc2[i][j]);
-      }
-    } else {
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
       if constexpr (F32) {   // 16 k per step: lane holds 4 k of its row/col; 4 MFMAs 16x16x4 f32
@@ -907,18 +876,97 @@ __global__ __launch_bounds__(conv_nt<STAGES>(), (PASS_T == WGRAD_BNA ? 3 : conv_
       }
       }
     }
-    }   // MF == 16
   };
 
-  if constexpr (DMA) {
+  if constexpr (HALO) {
+    // Tap reuse (3x3, stride 1, pad 1): the k loop runs over (64-channel chunk cc, tap t). Per chunk
+    // ONE slab of BM + 2W + 2 consecutive input rows (pixels m0-W-1 ..) is DMA'd into LDS; tap t
+    // reads its A fragments from that slab shifted by the tap's pixel offset, and a row whose tap
+    // falls outside the image reads the zero row instead. Only the weight tile streams per tap:
+    // per 9 k-tiles the block takes in one slab + 9 weight tiles instead of 9 gathered A tiles.
+    // Schedule: weight tile of step s+2 and one slab piece of chunk cc+1 (steps t < HA) are issued
+    // during step s; a step starts with a counted vmcnt + ONE barrier (slot reuse as in the DMA
+    // ring: weight slot (s+2)%3 = (s-1)%3, slab slot (cc+1)&1 last read in chunk cc-1).
+    const int csz = PASS == FWD ? p.Cin : p.Cout;
+    const int nch = csz >> 6;
+    const int Wd = p.W;
+    if (tid < 8) *reinterpret_cast<i32x4*>(smem + ZOFF + tid * 16) = i32x4{0, 0, 0, 0};
+    auto a_piece = [&](int cc, int j) __attribute__((always_inline)) {
+      dma16(rsa, smem + (cc & 1) * SLAB_BYTES + (j * 8 + wid) * 1024,
+            cc < nch ? ha_off[j] + (uint32_t)(cc * 64 * ES) : OOB);
+    };
+    auto b_offsets = [&](int cc, int t, uint32_t* voff) __attribute__((always_inline)) {
+      const uint32_t k = PASS == FWD ? (uint32_t)((t * p.Cin + cc * 64) * ES)
+                                     : (uint32_t)((cc * 64 * p.R * p.S + t) * p.Cin * ES);
+#pragma unroll
+      for (int j = 0; j < GB; ++j) voff[j] = cc < nch ? db_off[j] + k : OOB;
+    };
+    auto b_piece = [&](int slot, int j, const uint32_t* voff) __attribute__((always_inline)) {
+      dma16(rsb, smem + 2 * SLAB_BYTES + slot * B_BYTES + (wid * GB + j) * 1024, voff[j]);
+    };
+    {
+#pragma unroll
+      for (int j = 0; j < HA; ++j) a_piece(0, j);
+      uint32_t v0[GB], v1[GB];
+      b_offsets(0, 0, v0);
+      b_offsets(0, 1, v1);
+#pragma unroll
+      for (int j = 0; j < GB; ++j) b_piece(0, j, v0);
+#pragma unroll
+      for (int j = 0; j < GB; ++j) b_piece(1, j, v1);
+    }
+    for (int cc = 0; cc < nch; ++cc) {
+      const char* slab = smem + (cc & 1) * SLAB_BYTES;
+#pragma unroll
+      for (int t = 0; t < 9; ++t) {
+        if (t >= 1 && t <= HA) vm_wait<GB + 1>(); else vm_wait<GB>();
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        const int r = t / 3, q = t % 3;
+        const int toff = PASS == FWD ? (r - 1) * Wd + (q - 1) : (1 - r) * Wd + (1 - q);
+        const char* sb = smem + 2 * SLAB_BYTES + (t % 3) * B_BYTES;
+        uint32_t voff[GB];
+        b_offsets(t >= 7 ? cc + 1 : cc, t >= 7 ? t - 7 : t + 2, voff);
+        constexpr int NMF = MI * NI;
+        constexpr int NP = GB + 1;   // pieces of this step (the slab piece only while t < HA)
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2) {
+          s16x8 fa[MI], fb[NI];
+#pragma unroll
+          for (int i = 0; i < MI; ++i) {
+            const int row = hrow[i] + toff;
+            const int chunk = s2 * 4 + (lane >> 4);
+            const char* src = ((hmask[i] >> t) & 1u) ? slab + row * 128 + ((chunk ^ (row & 7)) << 4)
+                                                     : smem + ZOFF;
+            fa[i] = *reinterpret_cast<const s16x8*>(src);
+          }
+#pragma unroll
+          for (int j = 0; j < NI; ++j) {
+            const int cbase = wc * (BN / WN) + j * 16;
+            if constexpr (B_ROW) fb[j] = frag_row(sb, cbase, s2, lane);
+            else fb[j] = frag_col<BN>(sb, cbase, s2, lane);
+          }
+#pragma unroll
+          for (int idx = 0; idx < NMF; ++idx) {
+            const int i = idx / NI, j = idx % NI;
+            acc[i][j] = mfma16<MDT>(fb[j], fa[i], acc[i][j]);
+            const int g = s2 * NMF + idx;
+#pragma unroll
+            for (int pc = 0; pc < NP; ++pc) {
+              if (g != (pc * 2 * NMF) / NP) continue;
+              if (pc < GB) b_piece((t + 2) % 3, pc, voff);
+              else if (t < HA) a_piece(cc + 1, t);
+            }
+          }
+        }
+      }
+    }
+  } else if constexpr (DMA) {
     // 3-slot ring: tile kt lives in slot kt % 3. Tile kt+2 is issued right after the barrier that
     // retires tile kt (each wave's counted vmcnt + the barrier: every wave's DMA of tile kt has
     // landed) and that proves every wave finished reading slot (kt+2) % 3 = (kt-1) % 3.
     if (nk > 0) issue_dma(0, 0);
     if (nk > 1) issue_dma(1, 1);
-#if PDA_DMA_PRIO
-    if (wid >= NTH / 128) __builtin_amdgcn_s_setprio(1);   // younger half: static priority
-#endif
     int slot = 0;
     for (int kt = 0; kt < nk; ++kt) {
       if (kt + 1 < nk) vm_wait<GP>(); else vm_wait<0>();
@@ -927,13 +975,10 @@ __global__ __launch_bounds__(conv_nt<STAGES>(), (PASS_T == WGRAD_BNA ? 3 : conv_
       const int nslot = slot == 0 ? 2 : slot - 1;
       const char* sa = smem + slot * STAGE;
       const char* sb = sa + A_BYTES;
-#if PDA_DMA_SCHED == 0
-      if (kt + 2 < nk) issue_dma(kt + 2, nslot);
-      mma_tile(sa, sb);
-#else
       // the pieces of tile kt+2 spread over this tile's MFMAs (a burst of LDS-DMA issues right
-      // after the barrier holds every wave's matrix pipe); past the last tile they are OOB
-      // no-ops (nothing reads that slot again), so the MFMA stream carries no branch
+      // after the barrier holds every wave's matrix pipe: +10-20 % time, profiles/ab_r3_dma.md);
+      // past the last tile they are OOB no-ops (nothing reads that slot again), so the MFMA
+      // stream carries no branch
       uint32_t voff[GP];
       dma_offsets(kt + 2, voff);
       const bool pre = kt + 2 < nk;
@@ -965,9 +1010,10 @@ __global__ __launch_bounds__(conv_nt<STAGES>(), (PASS_T == WGRAD_BNA ? 3 : conv_
             if (g == (pc * 2 * NMF) / GP) dma_piece(pc, nslot, voff);
         }
       }
-#endif
       slot = slot == 2 ? 0 : slot + 1;
     }
+  }
+  if constexpr (DMA) {
     vm_wait<0>();
     __syncthreads();   // the epilogue reuses the ring
   } else {
@@ -996,28 +1042,15 @@ __global__ __launch_bounds__(conv_nt<STAGES>(), (PASS_T == WGRAD_BNA ? 3 : conv_
 
   // ================================================================ epilogue
   const int lr = lane & 15, lg = lane >> 4;
-  // every accumulator value as (row, 4 consecutive columns) within the wave tile: both MFMA
-  // shapes run with swapped operands (D = C^T), so a lane holds 4 consecutive C columns per
-  // 16x16 tile (MF 16) or per group of 4 accumulator registers (MF 32)
+  // every accumulator value as (row, 4 consecutive columns) within the wave tile: the MFMA runs
+  // with swapped operands (D = C^T), so a lane holds 4 consecutive C columns per 16x16 tile
   auto for_items = [&](auto&& fn) __attribute__((always_inline)) {
-    if constexpr (MF == 32) {
 #pragma unroll
-      for (int i = 0; i < MI2; ++i)
+    for (int j = 0; j < NI; ++j)   // column-tile outer: measured ~1% faster FWD than row-outer
 #pragma unroll
-        for (int j = 0; j < NI2; ++j)
-#pragma unroll
-          for (int r4 = 0; r4 < 4; ++r4) {
-            const f32x4 v = {acc2[i][j][4 * r4], acc2[i][j][4 * r4 + 1], acc2[i][j][4 * r4 + 2],
-                             acc2[i][j][4 * r4 + 3]};
-            fn(i * 32 + (lane & 31), j * 32 + 8 * r4 + 4 * (lane >> 5), v);
-          }
-    } else {
-#pragma unroll
-      for (int j = 0; j < NI; ++j)   // column-tile outer: measured ~1% faster FWD than row-outer
-#pragma unroll
-        for (int i = 0; i < MI; ++i) fn(i * 16 + lr, j * 16 + 4 * lg, acc[i][j]);
-    }
+      for (int i = 0; i < MI; ++i) fn(i * 16 + lr, j * 16 + 4 * lg, acc[i][j]);
   };
+
   if constexpr (PASS == WGRAD) {
     float* slab = reinterpret_cast<float*>(p.out) + (size_t)split * p.M * p.N;
     const bool vec = (p.N & 3) == 0;
@@ -1142,7 +1175,7 @@ __global__ __launch_bounds__(conv_nt<STAGES>(), (PASS_T == WGRAD_BNA ? 3 : conv_
           const size_t bo = (size_t)eoff[j] * ES;
           auto ld = [&](const void* base) __attribute__((always_inline)) {
             const i32x4* q = reinterpret_cast<const i32x4*>(reinterpret_cast<const char*>(base) + bo);
-            return (p.ntm & 1) ? __builtin_nontemporal_load(q) : *q;
+            return *q;
           };
           if constexpr (MODE >= 0) py[j] = eok[j] ? ld(p.ey) : z;
           if constexpr (G2) pg2[j] = eok[j] ? ld(p.eg2) : z;
@@ -1243,8 +1276,7 @@ __global__ __launch_bounds__(conv_nt<STAGES>(), (PASS_T == WGRAD_BNA ? 3 : conv_
             }
           }
           i32x4* dst = reinterpret_cast<i32x4*>(outb + (size_t)eoff[j] * ES);
-          if (p.ntm & 2) __builtin_nontemporal_store(v, dst);
-          else *dst = v;
+          *dst = v;
         }
       }
       }
@@ -1374,39 +1406,40 @@ struct ConvDesc {  // mirrors pytorch_distributed_amd/ops/ext.py ConvDesc
   int Nb, H, W, Cin, Cout, R, S, stride, pad, Ho, Wo;
 };
 
-// MFMA shape of the 16-bit kernels (pda_conv_set_mfma): 16 = 16x16x32, 32 = 32x32x16
-static int g_mfma = 16;
-// Nontemporal policy (pda_conv_set_nt): bit 0 DGRAD epilogue operand loads, bit 1 DGRAD output
-// stores, bit 2 FWD output stores, bit 3 only for outputs of >= 100 MiB.
-static int g_conv_nt = 0;
-
-static int conv_ntm(long long out_bytes, bool fwd) {
-  if ((g_conv_nt & 8) && out_bytes < (100ll << 20)) return 0;
-  return fwd ? ((g_conv_nt & 4) ? 2 : 0) : (g_conv_nt & 3);
-}
-
 template <int PASS, int DT, int BM, int BN, int ST>
 static int launch(const ConvParams& p, dim3 grid, hipStream_t st) {
   if constexpr (PASS == WGRAD_BNA && DT != DT_BF16 && DT != DT_F16) {
     return -1;
   } else {
-    if constexpr ((DT == DT_BF16 || DT == DT_F16) && ST != 3) {
-      if (g_mfma == 32) {
-        hipLaunchKernelGGL((conv_gemm_kernel<PASS, DT, BM, BN, ST, 32>), grid, dim3(NT), 0, st, p);
-        return (int)hipGetLastError();
-      }
-    }
-    hipLaunchKernelGGL((conv_gemm_kernel<PASS, DT, BM, BN, ST, 16>), grid, dim3(conv_nt<ST>()), 0, st, p);
+    hipLaunchKernelGGL((conv_gemm_kernel<PASS, DT, BM, BN, ST>), grid, dim3(conv_nt<ST>()), 0, st, p);
     return (int)hipGetLastError();
   }
 }
 
 // Tile codes: bm < 0 selects the single-buffer (STAGES = 1) variant of tile |bm| x bn; bm > 1000
 // the LDS-DMA 8-wave variant (STAGES = 3) of tile (bm - 1000) x bn (16-bit, no operand prologue).
-static int tile_bm(int bm) { return bm > 1000 ? bm - 1000 : (bm < 0 ? -bm : bm); }
+// bm > 2000: the tap-reuse (HALO) variant of (bm - 2000) x bn for 3x3 stride-1 FWD / DGRAD.
+static int tile_bm(int bm) { return bm > 2000 ? bm - 2000 : bm > 1000 ? bm - 1000 : (bm < 0 ? -bm : bm); }
+static bool halo_ok(const ConvParams& p, int csz) {
+  return p.R == 3 && p.S == 3 && p.stride == 1 && p.pad == 1 && p.W <= 63 && csz % 64 == 0 &&
+         p.Ho == p.H && p.Wo == p.W;
+}
 
 template <int PASS>
 static int dispatch(int dt, int bm, int bn, const ConvParams& p, dim3 grid, hipStream_t st) {
+  if (bm > 2000) {
+    if constexpr (PASS != WGRAD) {
+      if (p.pro_sc != nullptr || !halo_ok(p, PASS == FWD ? p.Cin : p.Cout)) return -5;
+#define PDA_CASE4(D, M_, N_)                                                   \
+  if (dt == D && bm - 2000 == M_ && bn == N_) return launch<PASS, D, M_, N_, 4>(p, grid, st);
+      PDA_CASE4(DT_BF16, 256, 128) PDA_CASE4(DT_BF16, 256, 64)
+#ifndef PDA_DMA_ONLY
+      PDA_CASE4(DT_F16, 256, 128) PDA_CASE4(DT_F16, 256, 64)
+#endif
+#undef PDA_CASE4
+    }
+    return -1;
+  }
   if (bm > 1000) {
     if (p.pro_sc != nullptr) return -5;   // the operand prologue needs register staging
 #define PDA_CASE3(D, M_, N_)                                                   \
@@ -1469,17 +1502,6 @@ static void fill_geom(ConvParams& p, const ConvDesc& d) {
 
 extern "C" {
 
-int pda_conv_set_nt(int ntm) {
-  g_conv_nt = ntm & 15;
-  return 0;
-}
-
-int pda_conv_set_mfma(int mf) {
-  if (mf != 16 && mf != 32) return -1;
-  g_mfma = mf;
-  return 0;
-}
-
 // Y[M=Nb*Ho*Wo][Cout] = conv(X, W). W: [Cout][Kpad] 16-bit. stats: [ceil(M/bm)][3][Cout] shifted
 // partials or null.
 int pda_conv_fwd(const ConvDesc* d, const void* x, const void* w, int Kpad, void* y, int out_f32,
@@ -1494,7 +1516,6 @@ int pda_conv_fwd(const ConvDesc* d, const void* x, const void* w, int Kpad, void
   p.a = x; p.b = w; p.out = y; p.stats = stats; p.bias = bias;
   p.M = d->Nb * d->Ho * d->Wo; p.N = d->Cout; p.Kpad = Kpad; p.K = Kpad;
   p.out_f32 = out_f32; p.relu = relu; p.out_pitch = out_pitch > 0 ? out_pitch : d->Cout;
-  p.ntm = out_f32 ? 0 : conv_ntm((long long)p.M * p.out_pitch * (dt == DT_F32 || dt == DT_F32S ? 4 : 2), true);
   if (bm > 1000 && (d->Cin < 64 || (d->Cin & (d->Cin - 1)))) return -5;   // DMA: one tap per k-tile
   const int abm = tile_bm(bm);
   const int tiles = ((p.M + abm - 1) / abm) * ((p.N + bn - 1) / bn);
@@ -1527,7 +1548,6 @@ int pda_conv_dgrad(const ConvDesc* d, const void* dy, const void* w, void* dx, c
     p.emask = (const uint8_t*)epi->mask;
   }
   p.N = d->Cin; p.out_pitch = d->Cin;
-  p.ntm = conv_ntm((long long)d->Nb * d->H * d->W * d->Cin * (dt == DT_F32 || dt == DT_F32S ? 4 : 2), false);
   const int sd = d->stride;
   if (sd != 1 && sd != 2) return -2;
   if ((d->H % sd) || (d->W % sd) || (d->Cout % 64)) return -3;

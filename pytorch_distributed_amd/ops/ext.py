@@ -73,7 +73,6 @@ _V, _I, _F, _L, _U, _D = C.c_void_p, C.c_int, C.c_float, C.c_longlong, C.c_uint,
 _SIGS = {
     "pda_conv_fwd": [C.POINTER(ConvDesc), _V, _V, _I, _V, _I, _I, _V, _V, _I, _V, _V, _I, _I, _I, _V],
     "pda_conv_dgrad": [C.POINTER(ConvDesc), _V, _V, _V, C.POINTER(BnEpi), _I, _I, _I, _V],
-    "pda_conv_set_mfma": [_I],
     "pda_conv_wgrad": [C.POINTER(ConvDesc), _V, _V, _V, _I, _I, _V, _V, _I, _I, _I, _V],
     "pda_conv_wgrad_bna": [C.POINTER(ConvDesc), _V, _V, _V, _V, _V, _V, _V, _I, _I, _V, _V, _I, _I, _I,
                            _V],
@@ -106,7 +105,6 @@ _SIGS = {
     "pda_stem_s2d_grad": [_V, _V, _I, _I, _V],
     "pda_set_stream_cfg": [_I, _I, _I, _I],
     "pda_bn_bwd_apply2": [_V, _V, _V, _V, _V, _V, _L, _I, _I, _V],
-    "pda_conv_set_nt": [_I],
 }
 
 
@@ -142,12 +140,6 @@ def load(required: bool = False) -> Optional[C.CDLL]:
                 continue
             fn.argtypes = argt
             fn.restype = C.c_int
-        if getattr(lib, "pda_conv_set_mfma", None) is not None:
-            # MFMA shape of the 16-bit conv kernels: 16 = 16x16x32, 32 = 32x32x16
-            lib.pda_conv_set_mfma(int(os.environ.get("PDA_MFMA", "16")))
-        if getattr(lib, "pda_conv_set_nt", None) is not None:
-            # conv epilogue nontemporal policy (csrc/conv_gemm.hip g_conv_nt bits)
-            lib.pda_conv_set_nt(int(os.environ.get("PDA_CONV_NT", "0")))
         if getattr(lib, "pda_set_stream_cfg", None) is not None:
             lib.pda_set_stream_cfg(*stream_cfg())
         _LIB = lib

@@ -23,7 +23,7 @@ from . import ext
 from .ext import ConvDesc, BwdArgs, check, dt_of, ptr, stream
 
 __all__ = [
-    "ConvGeom", "conv_fwd", "conv_dgrad", "conv_wgrad", "pick_tile", "wgrad_plan",
+    "ConvGeom", "conv_fwd", "conv_dgrad", "conv_wgrad", "pick_tile", "fwd_tile", "wgrad_plan",
     "BnStats", "stats_totals", "bn_finalize_tot", "bn_finalize_partials", "bn_eval_coeffs",
     "bn_apply", "stem_pool", "maxpool_bwd", "tail_pool", "bn_epilogue", "bn_bwd_finish",
     "bn_bwd", "xent", "topk_hits", "col_sum", "sgd_flat", "cast_flat", "amp_scan",
@@ -120,8 +120,9 @@ def _kdt(t: torch.Tensor) -> int:
 
 def tile_rows(bm: int) -> int:
     """M rows of a tile code: -bm = single-stage register-staged, bm > 1000 = the LDS-DMA 8-wave
-    variant of (bm - 1000) rows (csrc/conv_gemm.hip dispatch)."""
-    return bm - 1000 if bm > 1000 else abs(bm)
+    variant of (bm - 1000) rows, bm > 2000 = its tap-reuse form for 3x3 stride-1 fwd / dgrad
+    (csrc/conv_gemm.hip dispatch)."""
+    return bm - 2000 if bm > 2000 else bm - 1000 if bm > 1000 else abs(bm)
 
 
 def _ktile(bm: int, bn: int, kdt: int, pro: bool = False) -> Tuple[int, int]:
@@ -129,7 +130,7 @@ def _ktile(bm: int, bn: int, kdt: int, pro: bool = False) -> Tuple[int, int]:
     apply an operand prologue (the bytes never pass through registers): those launches fall back
     to the register-staged 128-row tile. The split-f32 kernels stage hi + lo tiles: single-stage
     tiles of at most 128 x 128."""
-    if bm > 1000 and (kdt not in (1, 2) or pro):
+    if bm > 1000 and (kdt not in (1, 2) or pro):   # (the HALO tiles too)
         bm, bn = -128, min(bn, 128)
     if kdt != 3:
         return bm, bn
@@ -173,6 +174,20 @@ class BnStats:
         self.rmean, self.rvar, self.nbt, self.update = rmean, rvar, nbt, update_running
 
 
+def fwd_tile(g: ConvGeom, Nb: int, dtype: torch.dtype, pro: bool = False,
+             Kpad: Optional[int] = None) -> Tuple[int, int]:
+    """Default tile of a forward conv. The LDS-DMA tiles take 16-bit operands without the BN
+    prologue (their bytes never pass through registers): tap reuse (HALO) on the 3x3 stride-1
+    layers with >= 128 output channels (C10 118 -> 105 us, C16 114 -> 98, C22 127 -> 109), the
+    128x256 DMA tile on deep-K layers (:func:`pick_tile`); other launches keep the register-staged
+    choice."""
+    dma = _kdt(torch.empty(0, dtype=dtype)) in (1, 2) and not pro and g.Cin >= 64
+    if dma and _DMA and _halo_geom(g) and g.Cout >= 128:
+        return 2256, 128
+    M = Nb * g.Ho * g.Wo
+    return pick_tile(M, g.Cout, Kpad if Kpad is not None else g.R * g.S * g.Cin, dma=dma)
+
+
 def conv_fwd(x: torch.Tensor, w: torch.Tensor, g: ConvGeom, out: torch.Tensor,
              stats: Optional[torch.Tensor] = None, bias: Optional[torch.Tensor] = None,
              relu: bool = False, tile: Optional[Tuple[int, int]] = None,
@@ -186,7 +201,7 @@ def conv_fwd(x: torch.Tensor, w: torch.Tensor, g: ConvGeom, out: torch.Tensor,
     Nb = x.shape[0]
     M = Nb * g.Ho * g.Wo
     Kpad = w.shape[-1] if w.dim() == 2 else w[0].numel()
-    bm, bn_ = tile or pick_tile(M, g.Cout, Kpad, dma=True)
+    bm, bn_ = tile or fwd_tile(g, Nb, x.dtype, pro is not None, Kpad)
     d = g.desc(Nb)
     # direct (unstaged) f32 store + bias: the fc head (16-bit features -> f32 logits, or any conv
     # with a bias); f32 activations of the exact-fp32 engine take the staged path with statistics
@@ -253,7 +268,18 @@ def stats_tiles(M: int, Cout: int, tile: Optional[Tuple[int, int]] = None) -> in
     return math.ceil(M / tile_rows(bm))
 
 
-def dgrad_tile(g: ConvGeom, Nb: int) -> Tuple[int, int]:
+def _halo_geom(g: ConvGeom) -> bool:
+    """3x3 / stride 1 / pad 1 convolutions whose input rows fit the tap-reuse slab (W <= 63)."""
+    return (g.R == 3 and g.S == 3 and g.stride == 1 and g.pad == 1 and g.W <= 63
+            and g.Cin % 64 == 0 and g.Cout % 64 == 0)
+
+
+def dgrad_tile(g: ConvGeom, Nb: int, dma: bool = True) -> Tuple[int, int]:
+    """Data-gradient tile: the tap-reuse (HALO) 256x128 tile on the 3x3 stride-1 layers with 128-256
+    input channels (C10 121 -> 112 us, C16 115 -> 112; C2 / C22 measured slower:
+    profiles/ab_r3_dma.md); otherwise the register-staged tiles."""
+    if dma and _DMA and _halo_geom(g) and 128 <= g.Cin <= 256:
+        return 2256, 128
     M = Nb * (g.H // g.stride) * (g.W // g.stride)
     return pick_tile(M * g.stride * g.stride, g.Cin, g.Cout * _max_class_taps(g))
 
@@ -270,9 +296,9 @@ def dgrad_slabs(g: ConvGeom, Nb: int, tile: Optional[Tuple[int, int]] = None,
                 dtype: Optional[torch.dtype] = None) -> int:
     """Number of partial-sum slabs the fused BN epilogue of a dgrad writes (classes x M-tiles);
     ``dtype`` = the dgrad's operand dtype (the tile it launches may differ: :func:`_ktile`)."""
-    bm, bn = tile or dgrad_tile(g, Nb)
-    if dtype is not None:
-        bm, _ = _ktile(bm, bn, _kdt(torch.empty(0, dtype=dtype)))
+    kdt = 1 if dtype is None else _kdt(torch.empty(0, dtype=dtype))
+    bm, bn = tile or dgrad_tile(g, Nb, dma=kdt in (1, 2))
+    bm, _ = _ktile(bm, bn, kdt)
     M = Nb * (g.H // g.stride) * (g.W // g.stride)
     return g.stride * g.stride * math.ceil(M / tile_rows(bm))
 
@@ -284,9 +310,9 @@ def conv_dgrad(dy: torch.Tensor, w: torch.Tensor, g: ConvGeom, dx: torch.Tensor,
     With ``epi`` (see :func:`bn_epilogue`) the kernel instead stores dz = dA * relu_mask (dA = the
     transposed conv result [+ epi.g2]) and writes the BatchNorm-backward partial sums."""
     Nb = dy.shape[0]
-    bm, bn = tile or dgrad_tile(g, Nb)
-    d = g.desc(Nb)
     kdt = _kdt(dy)
+    bm, bn = tile or dgrad_tile(g, Nb, dma=kdt in (1, 2))
+    d = g.desc(Nb)
     kbm, kbn = _ktile(bm, bn, kdt)
     rc = ext.lib().pda_conv_dgrad(C.byref(d), ptr(dy), ptr(w), ptr(dx),
                                   C.byref(epi) if epi is not None else None, kdt, kbm, kbn,

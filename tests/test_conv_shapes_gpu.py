@@ -171,3 +171,48 @@ def test_dma_tiles_multi_tile(shape, dt):
             if not e < 1e-2:
                 bad.append((t, name, e))
     assert not bad, bad
+
+
+HALO_TILES = [(2256, 128), (2256, 64)]   # tap-reuse tiles: 3x3 stride-1 fwd / dgrad only
+
+
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16], ids=["bf16", "f16"])
+@pytest.mark.parametrize("shape,Nb", [(SHAPES[1], 3), (SHAPES[9], 5), (SHAPES[15], 9), (SHAPES[21], 13),
+                                      (SHAPES[15], 1), (SHAPES[21], 2)],
+                         ids=["C2", "C10", "C16", "C22", "C16-1img", "C22-2img"])
+def test_halo_tiles(shape, Nb, dt):
+    """The tap-reuse tiles (one input slab per 64-channel chunk serves all 9 taps, shifted
+    fragment reads, out-of-image taps read a zero row): every image border, ragged last M tile,
+    tiles spanning several images, fwd + statistics and dgrad (+ BN-backward epilogue) vs fp32."""
+    from pytorch_distributed_amd.ops import ext
+    ext.load(required=True)
+    from pytorch_distributed_amd.ops import native_ops as K
+    _, H, Cin, Cout, k, s = shape
+    torch.manual_seed(3)
+    x = (torch.randn(Nb, Cin, H, H, device=DEV) + 0.1).to(dt).float()
+    w = (torch.randn(Cout, Cin, k, k, device=DEV) / math.sqrt(Cin * k * k)).to(dt).float()
+    xr = x.clone().requires_grad_(True)
+    wr = w.clone().requires_grad_(True)
+    y_ref = F.conv2d(xr, wr, stride=s, padding=1)
+    dy = torch.randn_like(y_ref).to(dt).float()
+    y_ref.backward(dy)
+    g = K.ConvGeom(Nb, H, H, Cin, Cout, k, k, s, 1)
+    x_nhwc = x.permute(0, 2, 3, 1).contiguous().to(dt)
+    w_ohwi = w.permute(0, 2, 3, 1).contiguous().to(dt)
+    dy_nhwc = dy.permute(0, 2, 3, 1).contiguous().to(dt)
+    M = Nb * H * H
+    bad = []
+    for t in HALO_TILES:
+        y = torch.full((Nb, H, H, Cout), float("nan"), device=DEV, dtype=dt)
+        stats = torch.zeros(math.ceil(M / 64) * 3 * Cout, device=DEV)
+        K.conv_fwd(x_nhwc, w_ohwi.view(Cout, -1), g, y, stats=stats, tile=t)
+        dx = torch.full((Nb, H, H, Cin), float("nan"), device=DEV, dtype=dt)
+        K.conv_dgrad(dy_nhwc, w_ohwi, g, dx, tile=t)
+        torch.cuda.synchronize()
+        st = K.stats_totals(stats, M, Cout, t[0]).float()
+        for name, e in (("fwd", rel_err(y, y_ref.detach().permute(0, 2, 3, 1))),
+                        ("dgrad", rel_err(dx, xr.grad.permute(0, 2, 3, 1))),
+                        ("stats", rel_err(st[0], y.float().reshape(-1, Cout).sum(0)))):
+            if not e < 1e-2:
+                bad.append((t, name, e))
+    assert not bad, bad

@@ -55,13 +55,14 @@ def test_conv_fwd_dgrad_wgrad(case, dtype):
     w_ohwi = w.permute(0, 2, 3, 1).contiguous().to(dtype)
     y = torch.empty(Nb, g.Ho, g.Wo, Cout, device=DEV, dtype=dtype)
     M = Nb * g.Ho * g.Wo
-    T = K.stats_tiles(M, Cout)
+    tile = K.fwd_tile(g, Nb, dtype)   # the default tile conv_fwd launches (DMA / HALO included)
+    T = K.stats_tiles(M, Cout, tile)
     stats = torch.zeros(T * 3 * Cout, device=DEV)
     K.conv_fwd(x_nhwc, w_ohwi.view(Cout, -1), g, y, stats=stats)
     torch.cuda.synchronize()
     yr = y_ref.permute(0, 2, 3, 1)
     assert rel_err(y, yr) < 1e-2
-    st = K.stats_totals(stats, M, Cout, K.pick_tile(M, Cout)[0]).float()
+    st = K.stats_totals(stats, M, Cout, tile[0]).float()
     yb = y.float().reshape(-1, Cout)
     torch.testing.assert_close(st[0], yb.sum(0), rtol=1e-3, atol=1e-2)
     torch.testing.assert_close(st[1], (yb * yb).sum(0), rtol=1e-3, atol=1e-2)
@@ -708,12 +709,13 @@ def test_conv_fwd_dgrad_wgrad_exact_f32(case, mode, monkeypatch):
     w_ohwi = w.permute(0, 2, 3, 1).contiguous().to(DEV)
     y = torch.empty(Nb, g.Ho, g.Wo, Cout, device=DEV)
     M = Nb * g.Ho * g.Wo
-    T = K.stats_tiles(M, Cout)
+    tile = K.fwd_tile(g, Nb, torch.float32)
+    T = K.stats_tiles(M, Cout, tile)
     stats = torch.zeros(T * 3 * Cout, device=DEV)
     K.conv_fwd(x_nhwc, w_ohwi.view(Cout, -1), g, y, stats=stats)
     torch.cuda.synchronize()
     assert rel_err(y.cpu().double(), y_ref.permute(0, 2, 3, 1)) < tol
-    st = K.stats_totals(stats, M, Cout, K.pick_tile(M, Cout)[0]).cpu()
+    st = K.stats_totals(stats, M, Cout, tile[0]).cpu()
     yb = y_ref.permute(0, 2, 3, 1).reshape(-1, Cout)
     torch.testing.assert_close(st[0], yb.sum(0), rtol=1e-4, atol=1e-4)
     torch.testing.assert_close(st[1], (yb * yb).sum(0), rtol=1e-4, atol=1e-4)

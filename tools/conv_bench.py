@@ -25,9 +25,9 @@ COUNT = {"C1": 1, "C2": 3, "C3": 4, "C4": 2, "C5": 1, "C6": 1, "C7": 4, "C8": 1,
          "C11": 1, "C12": 1, "C13": 6, "C14": 1, "C15": 5, "C16": 5, "C17": 1, "C18": 1, "C19": 3,
          "C20": 1, "C21": 2, "C22": 2}
 TILES = [(128, 128), (128, 64), (64, 128), (64, 64), (-128, 128), (-128, 64), (-64, 128), (-256, 128),
-         (1256, 128), (1128, 256), (1128, 128)]
+         (1256, 128), (1128, 256), (1128, 128), (2256, 128), (2256, 64)]
 # -bm: 1-stage; the -256 tile is compiled for wgrad only (other passes report n/a);
-# 1000 + bm: the LDS-DMA 8-wave tiles
+# 1000 + bm: the LDS-DMA 8-wave tiles; 2000 + bm: their tap-reuse form (3x3 stride-1 fwd / dgrad)
 
 
 def timeit(fn, reps):
@@ -72,16 +72,19 @@ def main():
                     f = lambda: K.conv_dgrad(dy, w, g, dx, tile=t)
                 else:
                     f = lambda: K.conv_wgrad(dy, x, g, gw, ws, tile=t)
-                if t == (-256, 128) and ps != "wgrad":
+                if (t == (-256, 128) and ps != "wgrad") or (t[0] > 2000 and ps == "wgrad"):
                     ts.append(float("inf"))
                     continue
-                ts.append(timeit(f, reps))
+                try:
+                    ts.append(timeit(f, reps))
+                except RuntimeError:   # geometry the tile does not take (HALO: 3x3 stride 1 only)
+                    ts.append(float("inf"))
             if ps == "fwd":
-                dflt = K.pick_tile(M, Cout)
+                dflt = K.fwd_tile(g, B, dt)
             elif ps == "dgrad":
                 dflt = K.dgrad_tile(g, B)
             else:
-                bm, bn, _, _ = K.wgrad_plan(g, B)
+                bm, bn, _, _ = K.wgrad_plan(g, B, dma=True)
                 dflt = (bm, bn)
             td = ts[TILES.index(dflt)]
             tb = min(ts)

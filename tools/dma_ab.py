@@ -72,7 +72,11 @@ def run(names, cases, rounds, reps):
         for c, f, _ in fns:
             for n in names:
                 ext._LIB = libs[n]
-                f()
+                try:
+                    f()
+                except RuntimeError:   # tile not built into this variant
+                    res[(c, n)].append(float("inf"))
+                    continue
                 torch.cuda.synchronize()
                 ev[0].record()
                 for _ in range(reps):
