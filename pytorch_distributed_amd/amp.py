@@ -94,6 +94,13 @@ class LossScaler:
             return optimizer.step(*args, **kwargs)
         if self._scale is None:
             return optimizer.step(*args, **kwargs)
+        if self._updated_in_step:
+            # the fused native step already scanned for infs AND moved the scale/growth tracker
+            # this iteration; a second optimizer would unscale by the updated scale (GradScaler
+            # updates once per iteration, in update())
+            raise RuntimeError("LossScaler.step() called twice before update(): the fused native "
+                               "step updates the loss scale in-kernel; use one native optimizer per "
+                               "iteration or call update() between steps")
         self._stepped = True
         if hasattr(optimizer, "step_amp") and not self._unscaled:
             # fused: inf check + scale update (one kernel), unscale + conditional step in the SGD

@@ -47,6 +47,7 @@ class RunConfig:
     metrics: bool = False            # write output/<run>/metrics.jsonl
     bucket_mb: float = 0.0           # DDP bucket cap (0 = framework default)
     sync_bn: bool = False            # SyncBatchNorm in DDP (reference: per-GPU statistics)
+    graph: bool = False              # single-GPU native engine: replay each step from a HIP graph
 
     def replace(self, **kw) -> "RunConfig":
         return dataclasses.replace(self, **kw)
@@ -82,6 +83,7 @@ _ENV = {
     "MX_METRICS": ("metrics", lambda s: s not in ("", "0", "false", "False")),
     "MX_BUCKET_MB": ("bucket_mb", float),
     "MX_SYNC_BN": ("sync_bn", lambda s: s not in ("", "0", "false", "False")),
+    "MX_GRAPH": ("graph", lambda s: s not in ("", "0", "false", "False")),
 }
 
 

@@ -197,10 +197,15 @@ __global__ __launch_bounds__(256) void bn_stats_kernel(const float* __restrict__
 #pragma unroll
       for (int q = 0; q < NQ; ++q) st_wt(slabs + ((size_t)s * NQ + q) * C + col, red[q][tid]);
   }
-  // arrival: this block's slab stores landed (vmcnt(0) in every wave), then the group counter
+  // arrival: this block's slab stores landed (vmcnt(0) in every wave), then ONE release-ordered
+  // arrival on the group counter (agent scope: the release fence before the add orders every
+  // store of this workgroup before it in the memory model, not only by the sc1 write-through
+  // lowering; asm vmcnt(0) between fence and add: cdna_hip_programming.md G16 pitfall 12)
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (tid == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     const int old = __hip_atomic_fetch_add(cnt + g, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     flag = old == S - 1;
   }

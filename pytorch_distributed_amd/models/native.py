@@ -27,6 +27,8 @@ re-points their parameters/buffers into the flat storage.
 """
 from __future__ import annotations
 
+import contextlib
+
 import math
 from dataclasses import dataclass
 from typing import Callable, Dict, List, Optional, Tuple
@@ -152,10 +154,6 @@ class NativeResNet(nn.Module):
         # overrides both (profiles/ab_r2_inlaunch_bn.md sections 9, 10)
         self._wbatch_env = os.environ.get("PDA_WGRAD_BATCH")
         self.set_wgrad_batch(self._wbatch_env or "0")
-        # optionally run the dgrad/BN-backward chain (the critical path) on a high-priority stream
-        self._chain = (torch.cuda.Stream(device, priority=-1)
-                       if self._side is not None and os.environ.get("PDA_CHAIN_PRIO", "0") == "1"
-                       else None)
         self._keep: List[torch.Tensor] = []
         self.refresh_shadow()
 
@@ -166,11 +164,24 @@ class NativeResNet(nn.Module):
         self._wbatch_mode = mode
         self._wbatch = [] if self._side is not None and mode != "0" else None
 
-    def use_graph_schedule(self) -> None:
-        """Schedule for HIP-graph capture: fork the wgrad stream once per stage (unless
-        PDA_WGRAD_BATCH says otherwise): replayed 29.16-29.23 ms vs 29.50-29.63 per block and
-        29.85-30.00 per conv (profiles/ab_r2_inlaunch_bn.md section 10)."""
+    @contextlib.contextmanager
+    def graph_schedule(self):
+        """Schedule for HIP-graph capture, for the duration of the block only: fork the wgrad
+        stream once per stage (unless PDA_WGRAD_BATCH says otherwise): replayed 29.16-29.23 ms vs
+        29.50-29.63 per block and 29.85-30.00 per conv (profiles/ab_r2_inlaunch_bn.md section 10).
+        Eager steps before and after keep their schedule (the fork granularity changes no value:
+        tests/test_graph_gpu.py checks the three modes bitwise). Refuses streams of non-default
+        priority: hipStreamEndCapture segfaults on them (ROCm 7, profiles/ab_r3_dma.md §5)."""
+        for st in (self._side,):
+            if st is not None and st.priority != 0:
+                raise RuntimeError("HIP graph capture of a non-default-priority stream crashes the "
+                                   "HIP runtime at capture end; capture with default priorities")
+        prev = self._wbatch_mode
         self.set_wgrad_batch(self._wbatch_env or "stage")
+        try:
+            yield
+        finally:
+            self.set_wgrad_batch(prev)
 
     # ------------------------------------------------------------------ planning
     def _build_plan(self) -> None:
@@ -615,16 +626,6 @@ class NativeResNet(nn.Module):
             red.grads_ready(upto)
 
     def native_backward(self, dlog16: torch.Tensor) -> None:
-        if self._chain is None:
-            return self._native_backward(dlog16)
-        cur = torch.cuda.current_stream(self.device)
-        self._chain.wait_stream(cur)
-        with torch.cuda.stream(self._chain):
-            self._native_backward(dlog16)
-        cur.wait_stream(self._chain)
-        dlog16.record_stream(self._chain)
-
-    def _native_backward(self, dlog16: torch.Tensor) -> None:
         """dlog16: [B, fc_rows] 16-bit d(loss)/d(logits) (zero padded).
 
         Schedule per bottleneck block (last to first): finish the tail BN backward (its reduction

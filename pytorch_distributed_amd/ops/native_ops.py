@@ -72,11 +72,14 @@ class Workspace:
     def __init__(self, device) -> None:
         self.device = device
         self._bufs = {}
+        self._retired = []   # outgrown buffers stay allocated: a captured HIP graph may use them
         self.sync_comm = None
 
     def get(self, name: str, numel: int, dtype=torch.float32) -> torch.Tensor:
         b = self._bufs.get(name)
         if b is None or b.numel() < numel or b.dtype != dtype:
+            if b is not None:
+                self._retired.append(b)
             b = torch.empty(max(numel, 1), dtype=dtype, device=self.device)
             self._bufs[name] = b
         return b[:numel]
@@ -86,6 +89,8 @@ class Workspace:
         every kernel that uses them leaves them zero again (its last arrivers reset them)."""
         b = self._bufs.get("_counters")
         if b is None or b.numel() < numel:
+            if b is not None:
+                self._retired.append(b)
             b = torch.zeros(max(numel, 64), dtype=torch.int32, device=self.device)
             self._bufs["_counters"] = b
         return b[:numel]
@@ -95,7 +100,6 @@ _NUM_CU = 256
 _WGRAD_TARGET = int(os.environ.get("PDA_WGRAD_TARGET", 2 * _NUM_CU))
 
 
-_SINGLE_STAGE = os.environ.get("PDA_SINGLE_STAGE", "1") != "0"
 # f32 convolutions: "exact" = MFMA 16x16x4 f32 (DT_F32); "split" = f32 tensors with the products on
 # the bf16 MFMA as a three-term hi/lo split (DT_F32S, ~16 significant bits per product -- above
 # the TF32 convolutions of the reference's fp32 runs; csrc/common.h DType)
@@ -152,8 +156,8 @@ def pick_tile(M: int, N: int, K: Optional[int] = None, dma: bool = False) -> Tup
     bm = 128
     if math.ceil(M / 128) * math.ceil(N / bn) < 2 * _NUM_CU:
         bm = 64
-    if bm == 128 and _SINGLE_STAGE:
-        bm = -128     # measured faster on every ResNet-50 shape (tools/conv_bench.py)
+    if bm == 128:
+        bm = -128     # single-stage: measured faster on every ResNet-50 shape (tools/conv_bench.py)
     return bm, bn
 
 
@@ -387,12 +391,12 @@ def wgrad_plan(g: ConvGeom, Nb: int, tile: Optional[Tuple[int, int]] = None,
     (16-bit operands, no operand prologue)."""
     M, N, K = g.Cout, g.R * g.S * g.Cin, Nb * g.Ho * g.Wo
     key = (g.Cout, g.R, g.Cin, g.stride, g.Ho)
-    tuned = _WGRAD_TUNED.get(key) if _SINGLE_STAGE else None
+    tuned = _WGRAD_TUNED.get(key)
     if dma and _DMA and key in _WGRAD_DMA:
         tuned = _WGRAD_DMA[key]
     bn = 128 if N >= 128 else 64
     bm = 128 if M >= 128 else 64
-    if _SINGLE_STAGE and (bm == 128 or bn == 128):
+    if bm == 128 or bn == 128:
         bm = -bm      # single-LDS-buffer variants (tools/conv_bench.py: best or within 2%)
     if tuned and not tile:
         (bm, bn), tb = tuned

@@ -276,7 +276,9 @@ class DataParallel(nn.Module):
             # one host thread per device: hipGraphLaunch of a ~500-node step costs ~2 ms of host
             # time, and CUDAGraph.replay releases the GIL, so N replicas enqueue concurrently
             # instead of staggering device i's start by i x 2 ms (captures stay on this thread)
-            list(self._pool().map(lambda j: j[0].run(j[1], j[2], True), jobs))
+            streams = [torch.cuda.current_stream(rg.dev) for rg in self._graphs]
+            list(self._pool().map(lambda j: j[0][0].run(j[0][1], j[0][2], True, j[1]),
+                                  zip(jobs, streams)))
         else:
             for rg, x, y in jobs:
                 rg.run(x, y, graph)
@@ -311,7 +313,6 @@ class _ReplicaGraph:
 
     def __init__(self, m, shape, global_batch: int) -> None:
         self.m = m
-        m.use_graph_schedule()
         self.dev = m.device
         self.gscale = 1.0 / global_batch
         with torch.cuda.device(self.dev):
@@ -333,8 +334,13 @@ class _ReplicaGraph:
         m.native_backward(dlog16)
         self.loss = loss
 
-    def run(self, x: torch.Tensor, y: torch.Tensor, graph: bool = True) -> None:
-        with torch.cuda.device(self.dev):
+    def run(self, x: torch.Tensor, y: torch.Tensor, graph: bool = True,
+            stream: Optional[torch.cuda.Stream] = None) -> None:
+        """``stream``: the caller's current stream on this device. A worker thread's current
+        stream is its own (the default stream), so a replay issued from the DataParallel thread
+        pool runs on the caller's stream explicitly and stays ordered with the input production
+        before it and the gradient reduction / optimizer step after it."""
+        with torch.cuda.device(self.dev), torch.cuda.stream(stream or torch.cuda.current_stream(self.dev)):
             self.x.copy_(x, non_blocking=True)
             self.y.copy_(y, non_blocking=True)
             if not graph:                  # same schedule, launched eagerly (tests / debugging)
@@ -347,12 +353,13 @@ class _ReplicaGraph:
             cur = torch.cuda.current_stream(self.dev)
             side = torch.cuda.Stream(self.dev)
             side.wait_stream(cur)
-            with torch.cuda.stream(side):
-                self._body()               # the real step for this batch (also sizes workspaces)
-            cur.wait_stream(side)
-            eager = self.loss
-            g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g):
-                self._body()
+            with self.m.graph_schedule():
+                with torch.cuda.stream(side):
+                    self._body()               # the real step for this batch (also sizes workspaces)
+                cur.wait_stream(side)
+                eager = self.loss
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g):
+                    self._body()
             self.graph = g
             self._graph_loss, self.loss = self.loss, eager

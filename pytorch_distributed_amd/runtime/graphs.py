@@ -18,7 +18,7 @@ AMP loss-scale update -- into ONE HIP graph, replayed with a single launch per s
   a re-capture when the LR scheduler changes it.
 
 Used by :class:`~pytorch_distributed_amd.models.native.NativeTrainer` (``bench.py --graph``) and the
-entrypoints (``MX_GRAPH=1``).
+single-GPU entrypoint's training loop (``MX_GRAPH=1``, :mod:`pytorch_distributed_amd.trainer`).
 """
 from __future__ import annotations
 
@@ -68,7 +68,6 @@ class GraphedNativeStep:
     def __init__(self, model, opt, gen: Callable, batch: int, scaler=None,
                  device: Optional[torch.device] = None) -> None:
         self.model, self.opt, self.gen, self.batch, self.scaler = model, opt, gen, batch, scaler
-        model.use_graph_schedule()
         self.device = torch.device(device) if device is not None else model.device
         self.ids_base = torch.arange(batch, dtype=torch.int64, device=self.device)
         self.ids_off = torch.zeros(1, dtype=torch.int64, device=self.device)
@@ -78,11 +77,29 @@ class GraphedNativeStep:
         self.captures = 0
 
     def _body(self) -> None:
-        x, y = self.gen(self.ids_base + self.ids_off)
+        if self.gen is None:      # inputs from the caller: static buffers filled by run_batch
+            x, y = self._sx, self._sy
+        else:
+            x, y = self.gen(self.ids_base + self.ids_off)
         self.loss = native_train_step(self.model, self.opt, x, y, self.scaler)
 
-    def run(self, first_id: int) -> None:
-        self.ids_off.fill_(int(first_id))
+    def accepts(self, x: torch.Tensor) -> bool:
+        """Whether :meth:`run_batch` can replay this batch (its shape is the captured one)."""
+        return getattr(self, "_sx", None) is None or tuple(x.shape) == tuple(self._sx.shape)
+
+    def run_batch(self, x: torch.Tensor, y: torch.Tensor) -> None:
+        """One step on a caller-provided batch (``gen=None``): copied into static buffers that the
+        graph reads, then replayed (captured on the first call / after an LR change)."""
+        if getattr(self, "_sx", None) is None:
+            self._sx = torch.empty_like(x, device=self.device)
+            self._sy = torch.empty_like(y, device=self.device)
+        self._sx.copy_(x, non_blocking=True)
+        self._sy.copy_(y, non_blocking=True)
+        self.run(None)
+
+    def run(self, first_id: Optional[int]) -> None:
+        if first_id is not None:
+            self.ids_off.fill_(int(first_id))
         lr = self.opt.param_groups[0]["lr"]
         if self.graph is not None and lr == self._lr:
             self.graph.replay()
@@ -93,14 +110,15 @@ class GraphedNativeStep:
         cur = torch.cuda.current_stream(self.device)
         side = torch.cuda.Stream(self.device)
         side.wait_stream(cur)
-        with torch.cuda.stream(side):
-            self._body()
-        cur.wait_stream(side)
-        eager_loss = self.loss
-        self.graph = None
-        g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g):
-            self._body()
+        with self.model.graph_schedule():
+            with torch.cuda.stream(side):
+                self._body()
+            cur.wait_stream(side)
+            eager_loss = self.loss
+            self.graph = None
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                self._body()
         self.graph = g
         self._graph_loss = self.loss      # written by each replay
         self.loss = eager_loss            # this step's value (the capture executed nothing)

@@ -110,6 +110,24 @@ def _sync_step(ctx: Context) -> None:
             torch.cuda.empty_cache()
 
 
+def _graphed_step(model, optimizer, ctx: Context):
+    """``MX_GRAPH=1`` (single process, native engine, one GPU): the whole training step --
+    forward, loss, backward, fused SGD (+ AMP scale update) -- replayed from ONE HIP graph per step
+    (:class:`~pytorch_distributed_amd.runtime.graphs.GraphedNativeStep`; re-captured when the LR
+    scheduler changes the learning rate, a ragged last batch runs eagerly). Kept on the context so
+    one capture serves every epoch."""
+    if not ctx.cfg.graph or ctx.distributed or ctx.device.type != "cuda" or ctx.engine != "native":
+        return None
+    if not hasattr(model, "native_forward") or hasattr(model, "replicas"):
+        return None
+    g = ctx.extra.get("graphed")
+    if g is None:
+        from .runtime.graphs import GraphedNativeStep
+        g = GraphedNativeStep(model, optimizer, None, ctx.cfg.batch_size, ctx.scaler, ctx.device)
+        ctx.extra["graphed"] = g
+    return g
+
+
 def train(dataloader, model, criterion, optimizer, scheduler, epoch: int, ctx: Context,
           start_step: int, best_acc: float, save_path: Path) -> int:
     """One epoch of training (reference ``restnet_ddp.py:19-47``). Returns steps run."""
@@ -120,12 +138,16 @@ def train(dataloader, model, criterion, optimizer, scheduler, epoch: int, ctx: C
     from .utils.metrics import StepProfiler
     prof = StepProfiler(int(os.environ.get("MX_PROFILE", "0") or 0) if epoch == 0 else 0, save_path,
                         ctx.rank)
+    graphed = _graphed_step(model, optimizer, ctx)
     for step, (samples, labels) in dataloader.iter_from(start_step):
         if ctx.cfg.script == "single" and cfg.log_every and step % cfg.log_every == 0:
             print("epoch: {}, step: {}".format(epoch, step), flush=True)
         samples = samples.to(ctx.device, non_blocking=True)
         labels = labels.to(ctx.device, non_blocking=True)
-        if getattr(model, "graph_step_ok", None) is not None and model.graph_step_ok(scaler):
+        if graphed is not None and graphed.accepts(samples):
+            graphed.run_batch(samples, labels)      # MX_GRAPH=1: the whole step, one graph launch
+            loss = graphed.loss
+        elif getattr(model, "graph_step_ok", None) is not None and model.graph_step_ok(scaler):
             loss = model.train_step(samples, labels, optimizer)     # DP: HIP-graph replay per GPU
         elif scaler is not None and scaler.enabled:
             with _autocast(ctx):

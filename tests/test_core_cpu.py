@@ -210,3 +210,47 @@ def test_stream_cfg_parsing(monkeypatch):
                     ("4:3:16384", (4, 3, 16384, 100)), ("4,1,4096,50", (4, 1, 4096, 50))]:
         monkeypatch.setenv("PDA_STREAM", v)
         assert ext.stream_cfg() == want, v
+
+
+def test_loss_scaler_refuses_second_fused_step():
+    """The fused native step (inf scan + scale update in one kernel) moves the scale inside
+    step(); a second optimizer stepped before update() would unscale by the updated scale, so the
+    scaler refuses it (GradScaler updates once per iteration)."""
+    from pytorch_distributed_amd.amp import LossScaler
+
+    class FusedOpt:
+        param_groups = []
+
+        def __init__(self):
+            self.calls = 0
+
+        def step_amp(self, *a):
+            self.calls += 1
+
+    s = LossScaler(init_scale=8.0)
+    s.scale(torch.ones(1))
+    o1, o2 = FusedOpt(), FusedOpt()
+    s.step(o1)
+    with pytest.raises(RuntimeError, match="twice"):
+        s.step(o2)
+    s.update()
+    s.step(o2)                      # a new iteration is fine
+    assert o1.calls == 1 and o2.calls == 1
+
+
+def test_lds_dma_tile_codes_and_fallback():
+    """Tile codes of the conv launches: 1000 + rows = LDS-DMA 8-wave tile, 2000 + rows = its
+    tap-reuse (HALO) form; they exist for 16-bit operands without the BN prologue only, and any
+    other launch is mapped onto the register-staged 128-row tile."""
+    from pytorch_distributed_amd.ops import native_ops as K
+    assert K.tile_rows(1256) == 256 and K.tile_rows(2256) == 256 and K.tile_rows(-128) == 128
+    assert K._ktile(1256, 128, 1) == (1256, 128) and K._ktile(2256, 128, 2) == (2256, 128)
+    assert K._ktile(1128, 256, 0) == (-128, 128)            # f32: no DMA kernels
+    assert K._ktile(2256, 128, 1, pro=True) == (-128, 128)  # prologue needs register staging
+    g = K.ConvGeom(400, 14, 14, 256, 256, 3, 3, 1, 1)
+    assert K.fwd_tile(g, 400, torch.bfloat16) == (2256, 128)
+    assert K.fwd_tile(g, 400, torch.bfloat16, pro=True)[0] < 1000
+    assert K.fwd_tile(g, 400, torch.float32)[0] < 1000
+    assert K.dgrad_tile(g, 400) == (2256, 128) and K.dgrad_tile(g, 400, dma=False)[0] < 1000
+    assert K.dgrad_slabs(g, 400, dtype=torch.float32) == math.ceil(400 * 196 / K.tile_rows(
+        K.dgrad_tile(g, 400, dma=False)[0]))

@@ -732,3 +732,50 @@ def test_conv_fwd_dgrad_wgrad_exact_f32(case, mode, monkeypatch):
     torch.cuda.synchronize()
     assert rel_err(dx.cpu().double(), xr.grad.permute(0, 2, 3, 1)) < tol
     assert rel_err(dw.cpu().double(), wr.grad.permute(0, 2, 3, 1)) < tol
+
+
+def test_bn_stats_handoff_under_uneven_load():
+    """The BN statistics kernel's cross-workgroup hand-off (f64 slabs written write-through, a
+    release-ordered arrival counter, the last arriver's acquire) under UNEVEN load: a weight-
+    gradient GEMM saturating the CUs on a second stream while the statistics launches run, several
+    sizes, repeated in one process; every channel of every launch is checked against float64
+    (MI355X_MICROARCH.md: test hand-offs under uneven load, consumer L1-warm)."""
+    K = _k()
+    dev = torch.device(DEV)
+    side = torch.cuda.Stream(dev)
+    g = K.ConvGeom(64, 14, 14, 256, 256, 3, 3, 1, 1)
+    dy = torch.randn(64, 14, 14, 256, device=dev).to(torch.bfloat16)
+    x = torch.randn(64, 14, 14, 256, device=dev).to(torch.bfloat16)
+    gw = torch.empty(256 * 9 * 256, device=dev)
+    ws_side = K.Workspace(dev)
+    ws = K.Workspace(dev)
+    bad = []
+    for rep in range(6):
+        for C, T in ((256, 613), (512, 154), (2048, 77), (64, 9800)):
+            torch.manual_seed(rep * 7 + C)
+            bm = 128
+            M = T * bm - 5
+            rows = torch.full((T,), float(bm), dtype=torch.float64)
+            rows[-1] = M - (T - 1) * bm
+            s1 = torch.randn(T, C, dtype=torch.float64)
+            sh = torch.randn(T, C, dtype=torch.float64)
+            s2 = torch.rand(T, C, dtype=torch.float64) * 50 + s1 ** 2 / rows[:, None]
+            part = torch.stack([s1, s2, sh], 1).float()
+            p64 = part.double()
+            mean = ((rows[:, None] * p64[:, 2] + p64[:, 0]).sum(0)) / M
+            with torch.cuda.stream(side):       # the competing load
+                for _ in range(3):
+                    K.conv_wgrad(dy, x, g, gw, ws_side)
+            gamma, beta = torch.ones(C, device=dev), torch.zeros(C, device=dev)
+            st = torch.zeros(4, C, device=dev)
+            bn = K.BnStats(ws, gamma, beta, 1e-5, 0.1, st[0], st[1], st[2], st[3],
+                           update_running=False)
+            pdev = part.to(dev).contiguous()
+            st[0].copy_(pdev[0, 0])              # L1-warm consumer lines with stale values
+            K.bn_finalize_partials(pdev, T, C, bm, M, bn)
+            torch.cuda.synchronize()
+            err = (st[0].double().cpu() - mean).abs().max().item()
+            if not err < 1e-4:
+                bad.append((rep, C, T, err))
+    assert not bad, bad
+    assert int(ws.counters(64).abs().sum().item()) == 0

@@ -80,3 +80,17 @@ def test_native_resume_from_reference_format_checkpoint(tmp_path):
     assert r.returncode == 0, r.stderr[-4000:]
     assert "resume: epoch 1 step 1 (best acc 0.5)" in r.stdout
     assert "epoch: 1, step: 1" in r.stdout and "epoch: 1, step: 0" not in r.stdout
+
+
+def test_single_gpu_graph_mode_matches_eager(tmp_path):
+    """MX_GRAPH=1: resnet_single_gpu.py replays each training step from ONE HIP graph (captured on
+    the first step, re-captured when StepLR changes the LR); the validation losses it prints are
+    bit-identical to the eager run's."""
+    def losses(sub, **kw):
+        d = tmp_path / sub
+        d.mkdir()
+        r = _run("resnet_single_gpu.py", d, MX_DTYPE="bf16", **kw)
+        assert r.returncode == 0, r.stderr[-4000:]
+        return [l for l in r.stdout.splitlines() if l.startswith("Epoch: ")]
+    eager, graph = losses("eager", MX_GRAPH="0"), losses("graph", MX_GRAPH="1")
+    assert len(eager) == 2 and eager == graph, (eager, graph)

@@ -1,9 +1,9 @@
 #!/bin/bash
 # GPU-box script: build in-tree, run GPU tests, smoke, short native bench (+ optional 2-rank rehearsal).
 set -o pipefail
+export PDA_NO_BUILD=1   # the in-tree libraries travel with the snapshot (built on the CPU side)
 mkdir -p gpurun_out
 export PYTHONUNBUFFERED=1
-timeout -k 10 300 python -c "import __graft_entry__ as g; g.build()" > gpurun_out/build.log 2>&1 || { echo BUILD FAIL; tail -30 gpurun_out/build.log; exit 1; }
 timeout -k 10 1000 python -m pytest tests -m gpu -x -q --timeout 700 ${PYTEST_ARGS} > gpurun_out/pytest_gpu.log 2>&1
 rc=$?
 tail -40 gpurun_out/pytest_gpu.log

@@ -2,9 +2,9 @@
 # GPU-box script: hardware counters for representative conv kernels (counters in their own run,
 # kernel-trace only -- never combined with sys/runtime tracing).
 set -o pipefail
+export PDA_NO_BUILD=1   # the in-tree libraries travel with the snapshot (built on the CPU side)
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 mkdir -p $R/gpurun_out/pmc
-timeout -k 10 300 python -c "import __graft_entry__ as g; g.build()" > $R/gpurun_out/build.log 2>&1 || { tail -30 $R/gpurun_out/build.log; exit 1; }
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 120 rocprofv3 -L > $R/gpurun_out/pmc/counters_list.txt 2>&1 || true
 for case in "C16 fwd" "C3 fwd" "C16 dgrad" "C16 wgrad" "C4 dgrad"; do
