@@ -411,7 +411,9 @@ class NativeResNet(nn.Module):
                 len(self.block_bounds), zlib.crc32(desc.encode())]
 
     def zero_grad_flat(self) -> None:
-        self.flat_grad.zero_()
+        """The next backward OVERWRITES the flat gradient (its first write per segment does not
+        accumulate), so no memset is issued: until then the ``.grad`` views keep the last values
+        (torch 2.x's set_to_none leaves no gradient to read either)."""
         self._grads_zero = True
 
     # ------------------------------------------------------------------ input
@@ -881,7 +883,7 @@ class _NativeNetFn(torch.autograd.Function):
             dlog16 = torch.zeros(ctx.B, m.fc_rows, dtype=m.dtype, device=m.device)
             dlog16[:, :m.num_classes].copy_(dlogits)
         m.native_backward(dlog16)
-        return torch.zeros((), device=m.device), None, None
+        return None, None, None   # the anchor only routes autograd here: no gradient, no fill
 
 
 class _XentFn(torch.autograd.Function):

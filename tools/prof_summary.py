@@ -34,6 +34,16 @@ def main():
         print("no kernel_trace.csv under", d)
         return
     rows = list(csv.DictReader(open(files[0])))
+    # restrict to whole training steps: a step starts with its batch generation (synth*_kernel)
+    # and its last kernel precedes the next step's generation; model construction (weight
+    # copies, fills) and the bench's extra passes fall outside the window
+    rows.sort(key=lambda r: int(r["Start_Timestamp"]))
+    starts = [i for i, r in enumerate(rows)
+              if re.match(r"(void )?(\(anonymous namespace\)::)?synth(_s2d)?_kernel",
+                          (r.get("Kernel_Name") or r.get("KernelName") or ""))]
+    if len(starts) >= 2:
+        rows = rows[starts[0]:starts[-1]]      # steps 1 .. n-1 of the trace (the last may be partial)
+        steps = len(starts) - 1
     tot = defaultdict(float)
     cnt = defaultdict(int)
     for r in rows:
@@ -52,8 +62,6 @@ def main():
     # device occupancy over the trace's last `steps` steps' window: union of kernel intervals
     # (kernels of the main and wgrad streams overlap) vs the wall span, and the idle gaps
     iv = sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"])) for r in rows)
-    n_keep = int(len(iv) * steps / max(steps, 1))
-    iv = iv[len(iv) - n_keep:]
     busy, gaps, cur_s, cur_e = 0, [], iv[0][0], iv[0][1]
     for s_, e_ in iv[1:]:
         if s_ > cur_e:

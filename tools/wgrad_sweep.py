@@ -11,8 +11,9 @@ from pytorch_distributed_amd.ops import ext  # noqa: E402
 from pytorch_distributed_amd.ops import native_ops as K  # noqa: E402
 from tools.conv_bench import COUNT, SHAPES, timeit  # noqa: E402
 
-TILES = [(64, 64), (128, 64), (64, 128), (-128, 128), (128, 128), (-256, 128)]
-TARGETS = [512, 1024, 2048, 4096]
+TILES = [tuple(int(v) for v in t.split(":")) for t in os.environ.get(
+    "WS_TILES", "64:64,128:64,64:128,-128:128,128:128,-256:128").split(",")]
+TARGETS = [int(v) for v in os.environ.get("WS_TARGETS", "512,1024,2048,4096").split(",")]
 
 
 def main():
