@@ -47,7 +47,7 @@ import traceback
 
 import torch
 
-from pytorch_distributed_amd.utils.gpu_util import BusySampler
+from pytorch_distributed_amd.utils.gpu_util import BusySampler, kernel_busy
 
 BASELINE = {1: 717.0, 8: 5546.7}      # BASELINE.md derived images/sec (other hardware)
 BASELINE_DP = {1: 717.0, 8: 1301.2}   # the nn.DataParallel bar of result.png
@@ -93,6 +93,8 @@ def parse():
     ap.add_argument("--dp-steps", type=int, default=10,
                     help="timed steps of the DataParallel pass (resnet_dp.py config: rank 0 drives "
                          "all N GPUs in one process; 0: skip)")
+    ap.add_argument("--util-steps", type=int, default=3,
+                    help="untimed steps profiled for the device-busy %% when sysfs is unavailable")
     ap.add_argument("--nccl-channels", type=int, default=0,
                     help="RCCL channel count (NCCL_MIN_NCHANNELS = NCCL_MAX_NCHANNELS); 0: RCCL's "
                          "own tuning for the topology")
@@ -153,20 +155,28 @@ class Ctx:
             else:
                 torch.cuda.synchronize(self.device)
 
+    # host-side collectives on the gloo host group: the only RCCL communicator of the process is
+    # the gradient communicator of the model (launch.host_group)
     def barrier(self):
         if self.multi:
             import torch.distributed as dist
-            dist.barrier()
+            from pytorch_distributed_amd.launch import host_group
+            self.sync()
+            dist.barrier(group=host_group())
         self.sync()
+
+    def allreduce(self, vals, op: str = "max"):
+        import torch.distributed as dist
+        from pytorch_distributed_amd.launch import host_group
+        t = torch.tensor(vals, dtype=torch.float64)
+        dist.all_reduce(t, op={"max": dist.ReduceOp.MAX, "min": dist.ReduceOp.MIN,
+                               "sum": dist.ReduceOp.SUM}[op], group=host_group())
+        return t
 
     def allreduce_max(self, x: float) -> float:
         if not self.multi:
             return x
-        import torch.distributed as dist
-        dev = self.device if dist.get_backend() == "nccl" else torch.device("cpu")
-        t = torch.tensor([x], device=dev, dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        return float(t.item())
+        return float(self.allreduce([x], "max")[0])
 
 
 def _timed(ctx: Ctx, tr, first: int, steps: int) -> float:
@@ -216,10 +226,10 @@ def _verify_consistent(ctx: Ctx, tr) -> dict:
     if not ctx.multi:
         return {"weights_consistent": None, "checksum": [int(v) for v in cs.tolist()]}
     import torch.distributed as dist
-    dev = ctx.device if dist.get_backend() == "nccl" else torch.device("cpu")
-    lo, hi = cs.to(dev).clone(), cs.to(dev).clone()
-    dist.all_reduce(lo, op=dist.ReduceOp.MIN)
-    dist.all_reduce(hi, op=dist.ReduceOp.MAX)
+    from pytorch_distributed_amd.launch import host_group
+    lo, hi = cs.cpu().clone(), cs.cpu().clone()     # int64: exact on the gloo host group
+    dist.all_reduce(lo, op=dist.ReduceOp.MIN, group=host_group())
+    dist.all_reduce(hi, op=dist.ReduceOp.MAX, group=host_group())
     ok = bool(torch.equal(lo, hi))
     return {"weights_consistent": ok, "checksum": [int(v) for v in cs.tolist()]}
 
@@ -259,12 +269,15 @@ def _gather_util(ctx: Ctx, mine):
     """Average GPU busy % over the ranks' devices (the reference's "Avg GPU Util" panel)."""
     if not ctx.multi:
         return mine
-    import torch.distributed as dist
-    dev = ctx.device if dist.get_backend() == "nccl" else torch.device("cpu")
-    t = torch.tensor([mine if mine is not None else 0.0, 1.0 if mine is not None else 0.0],
-                     device=dev, dtype=torch.float64)
-    dist.all_reduce(t)
+    t = ctx.allreduce([mine if mine is not None else 0.0, 1.0 if mine is not None else 0.0], "sum")
     return round(float(t[0] / t[1]), 1) if t[1] > 0 else None
+
+
+def _all_ranks(ctx: Ctx, flag: bool) -> bool:
+    """True iff ``flag`` holds on every rank (a decision that gates collective work)."""
+    if not ctx.multi:
+        return flag
+    return bool(ctx.allreduce([1.0 if flag else 0.0], "min")[0] > 0)
 
 
 def _guarded(ctx: Ctx, name: str, fn, *a) -> dict:
@@ -283,6 +296,8 @@ def _amp_pass(ctx: Ctx, args) -> dict:
     host sync), DDP gradient all-reduce over RCCL, fp32 master weights. Timed like the headline;
     then the bit-exact cross-rank checksum of parameters + momentum."""
     from pytorch_distributed_amd.bench_step import make_trainer
+    if ctx.cuda:
+        torch.cuda.reset_peak_memory_stats(ctx.device)
     tr = make_trainer(args.arch, args.batch, torch.float16, ctx.device, engine=args.engine,
                       world=ctx.world, rank=ctx.rank, bucket_mb=args.bucket_mb,
                       image_size=args.image_size)
@@ -290,6 +305,10 @@ def _amp_pass(ctx: Ctx, args) -> dict:
         tr.step(i)
     with BusySampler([ctx.device.index] if ctx.cuda else []) as busy:
         el = _timed(ctx, tr, 3, args.amp_steps)
+    amp_util = busy.overall()
+    if not _all_ranks(ctx, amp_util is not None) and ctx.cuda and args.util_steps > 0:
+        kb = kernel_busy(lambda i: tr.step(1000 + i), args.util_steps, [ctx.device.index])
+        amp_util = kb.get(ctx.device.index)
     cons = _verify_consistent(ctx, tr)
     world = ctx.world if ctx.multi else 1
     sc = getattr(tr, "scaler", None)
@@ -301,7 +320,7 @@ def _amp_pass(ctx: Ctx, args) -> dict:
            "amp_loss": tr.last_loss(),
            "amp_loss_scale": float(sc.get_scale()) if sc is not None and hasattr(sc, "get_scale") else None,
            "amp_max_mem_gb": round(torch.cuda.max_memory_allocated(ctx.device) / 1e9, 2) if ctx.cuda else None,
-           "amp_gpu_util_pct": _gather_util(ctx, busy.overall())}
+           "amp_gpu_util_pct": _gather_util(ctx, amp_util)}
     base = BASELINE.get(world)
     if base:
         res["amp_vs_baseline"] = round(res["amp_fp16_images_per_sec"] / base, 3)
@@ -313,58 +332,49 @@ def _amp_pass(ctx: Ctx, args) -> dict:
 
 def _dp_pass(ctx: Ctx, args, dtype) -> dict:
     """The resnet_dp.py configuration (/root/reference/resnet_dp.py:82): ONE process drives all N
-    GPUs (global batch 400 x N), here rank 0 over devices 0..N-1 while the other ranks wait on
-    the TCP store (a host-side wait: an RCCL barrier would occupy their GPUs). Persistent native
-    replicas, per-replica graph-replayed forward/backward, in-process grouped RCCL all-reduce,
-    replicated fused SGD; afterwards every replica's weights must be bit-identical."""
+    GPUs (global batch 400 x N). Rank 0 runs it as a child process (``bench.py --dp --gpus N``:
+    persistent native replicas, per-replica graph-replayed forward/backward, in-process grouped
+    RCCL all-reduce, replicated fused SGD, replicas checked bit-identical) under a time limit, while
+    the other ranks wait on the TCP store -- a host-side wait (an RCCL barrier would occupy their
+    GPUs), and a failure or hang of the pass costs its keys, never the headline record."""
+    import subprocess
     n = min(ctx.world if ctx.multi else 1, torch.cuda.device_count())
     store = None
     if ctx.multi:
         import torch.distributed as dist
         store = dist.distributed_c10d._get_default_store()
+    limit = float(os.environ.get("PDA_BENCH_DP_TIMEOUT_S", "420"))
     res = {}
     if ctx.rank == 0:
         try:
-            from pytorch_distributed_amd.bench_step import make_dp_trainer
-            tr = make_dp_trainer(args.arch, args.batch, dtype, n, args.image_size)
-            for i in range(3):
-                tr.step(i)
-            devs = list(range(n))
-            for d in devs:
-                torch.cuda.synchronize(d)
-            with BusySampler(devs) as busy:
-                t0 = time.perf_counter()
-                for i in range(args.dp_steps):
-                    tr.step(3 + i)
-                for d in devs:
-                    torch.cuda.synchronize(d)
-                el = time.perf_counter() - t0
-            try:
-                tr.state_checksum()
-                same = True
-            except RuntimeError:
-                same = False
-            res = {"dp_images_per_sec": round(args.batch * n * args.dp_steps / el, 2),
-                   "dp_ms_per_step": round(1000.0 * el / args.dp_steps, 3),
-                   "dp_config": f"dataparallel{n}: one process, {n} GPU(s), global batch "
-                                f"{args.batch * n}, {tr.engine} (resnet_dp.py)",
-                   "dp_replicas_consistent": same,
-                   "dp_loss": tr.last_loss(),
-                   "dp_max_mem_gb": round(max(torch.cuda.max_memory_allocated(d) for d in devs) / 1e9, 2),
-                   "dp_gpu_util_pct": busy.overall()}
-            base = BASELINE_DP.get(n)
-            if base:
-                res["dp_vs_baseline"] = round(res["dp_images_per_sec"] / base, 3)
-            del tr
-            for d in devs:
-                with torch.cuda.device(d):
-                    torch.cuda.empty_cache()
+            env = {k: v for k, v in os.environ.items()
+                   if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "LOCAL_WORLD_SIZE", "GROUP_RANK",
+                                "ROLE_RANK", "ROLE_WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT")
+                   and not k.startswith("TORCHELASTIC")}
+            cmd = [sys.executable, os.path.abspath(__file__), "--dp", "--gpus", str(n),
+                   "--steps", str(args.dp_steps), "--warmup", "3", "--batch", str(args.batch),
+                   "--arch", args.arch, "--image-size", str(args.image_size), "--dtype", args.dtype,
+                   "--fp32-steps", "0", "--amp-steps", "0", "--dp-steps", "0"]
+            r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=limit)
+            lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+            if r.returncode != 0 or not lines:
+                res = {"dp_error": f"rc={r.returncode}: {r.stderr.strip()[-300:]}"}
+            else:
+                rec = json.loads(lines[-1])
+                res = {"dp_images_per_sec": rec["value"], "dp_ms_per_step": rec["ms_per_step"],
+                       "dp_config": f"{rec['config']['parallelism']}: one process, {n} GPU(s), global "
+                                    f"batch {rec['config']['global_batch']}, {rec['config']['engine']}"
+                                    f" (resnet_dp.py)",
+                       "dp_replicas_consistent": rec.get("replicas_consistent"),
+                       "dp_loss": rec.get("loss"), "dp_max_mem_gb": rec.get("max_mem_gb"),
+                       "dp_gpu_util_pct": rec.get("gpu_util_pct"), "dp_vs_baseline": rec.get("vs_baseline")}
+        except subprocess.TimeoutExpired:
+            res = {"dp_error": f"timeout after {limit:.0f} s"}
         finally:
             if store is not None:
                 store.set("pda_bench_dp_done", json.dumps(res))
     elif store is not None:
-        timeout = float(os.environ.get("PDA_DIST_TIMEOUT_S", "600"))
-        store.wait(["pda_bench_dp_done"], datetime.timedelta(seconds=timeout))
+        store.wait(["pda_bench_dp_done"], datetime.timedelta(seconds=limit + 120))
         res = json.loads(store.get("pda_bench_dp_done").decode())
     return res
 
@@ -381,10 +391,11 @@ def main():
         timeout = datetime.timedelta(seconds=float(os.environ.get("PDA_DIST_TIMEOUT_S", "600")))
         backend = os.environ.get("PDA_DIST_BACKEND", "nccl" if ctx.cuda else "gloo")
         os.environ.setdefault("PDA_RCCL_INIT_TIMEOUT_S", str(timeout.total_seconds()))
-        if backend == "nccl":
-            dist.init_process_group("nccl", device_id=ctx.device, timeout=timeout)
-        else:
-            dist.init_process_group(backend, timeout=timeout)
+        # no device_id: torch's NCCL communicator stays uncreated; gradients go through the
+        # model's own RCCL communicator, host-side values through the gloo host group
+        dist.init_process_group(backend, timeout=timeout)
+        from pytorch_distributed_amd.launch import host_group
+        host_group()
 
     from pytorch_distributed_amd.bench_step import make_trainer
     dtype = {"bf16": torch.bfloat16, "fp16": torch.float16, "fp32": torch.float32}[args.dtype]
@@ -410,7 +421,14 @@ def main():
     loss = tr.last_loss()
     nxt = args.warmup + args.steps
     diag = _diagnostics(ctx, tr, nxt) if ctx.multi else {}
-    consistency = _verify_consistent(ctx, tr) if hasattr(tr, "state_checksum") else {}
+    if args.dp:   # every replica must hold bit-identical weights (the replicated fused SGD)
+        try:
+            tr.state_checksum()
+            consistency = {"replicas_consistent": True}
+        except RuntimeError:
+            consistency = {"replicas_consistent": False}
+    else:
+        consistency = _verify_consistent(ctx, tr) if hasattr(tr, "state_checksum") else {}
     ms = 1000.0 * elapsed / max(args.steps, 1)
     value = args.batch * world * args.steps / elapsed
     base = (BASELINE_DP if args.dp else BASELINE).get(world)
@@ -422,7 +440,15 @@ def main():
            "optimizer": "SGD(lr=0.1, momentum=0.9, wd=1e-4)",
            "bucket_cap_mb": args.bucket_mb if ctx.multi else None}
     max_mem = round(torch.cuda.max_memory_allocated(ctx.device) / 1e9, 2) if ctx.cuda else None
-    util = _gather_util(ctx, busy.overall())
+    mine = busy.overall()
+    util_method = "sysfs gpu_busy_percent" if mine is not None else None
+    if not _all_ranks(ctx, mine is not None) and ctx.cuda and args.util_steps > 0:
+        # no sysfs counter (on some rank): the kernels' own records, on every rank alike
+        kb = kernel_busy(lambda i: tr.step(nxt + 100 + i), args.util_steps, util_devs)
+        v = [x for x in kb.values() if x is not None]
+        mine = round(sum(v) / len(v), 1) if v else None
+        util_method = f"kernel-interval union over {args.util_steps} untimed steps (torch.profiler)"
+    util = _gather_util(ctx, mine)
     extra = {}
     if not args.dp:
         del tr
@@ -455,6 +481,7 @@ def main():
             "loss": loss,
             "max_mem_gb": max_mem,
             "gpu_util_pct": util,
+            "gpu_util_method": util_method,
             **proc, **diag, **consistency, **extra,
         }
         if extra.get("fp32_images_per_sec") and base:
@@ -468,6 +495,8 @@ def main():
         sys.stderr.flush()
         os._exit(3)
     bad = [k for k in ("amp_weights_consistent", "dp_replicas_consistent") if extra.get(k) is False]
+    if consistency.get("replicas_consistent") is False:
+        bad.append("replicas_consistent")
     if bad:
         print(f"bench: rank {ctx.rank}: inconsistent state after a secondary pass: {bad}",
               file=sys.stderr, flush=True)

@@ -1061,9 +1061,9 @@ struct StreamCfg {
 StreamCfg g_stream{0, 0, 8192, 100};
 
 // Launch KER<DT, U, NTM> for the configured (U, NTM); false when the shape does not qualify.
-#define PDA_STREAM_DISPATCH(KER, DT, g, st, ...)                                              \
-  PDA_STREAM_DISPATCH_UM(KER, DT, g, st, stream_chunks(), g_stream.ntm, __VA_ARGS__)
-#define PDA_STREAM_DISPATCH_UM(KER, DT, g, st, U_, M_, ...)                                    \
+#define STREAM_DISPATCH(KER, DT, g, st, ...)                                              \
+  STREAM_DISPATCH_UM(KER, DT, g, st, stream_chunks(), g_stream.ntm, __VA_ARGS__)
+#define STREAM_DISPATCH_UM(KER, DT, g, st, U_, M_, ...)                                    \
   do {                                                                                        \
     const int u_ = (U_), m_ = (M_);                                                           \
     if (u_ == 2 && m_ == 0) hipLaunchKernelGGL((KER<DT, 2, 0>), dim3(g), dim3(NT), 0, st, __VA_ARGS__); \
@@ -1187,8 +1187,8 @@ int pda_bn_apply(const void* y, const float* sc, const float* sh, const void* r2
   if (g_stream.unroll != 0 && dt != DT_F32 && (C & 7) == 0) {
     const int gs = stream_grid(n8, C);
     if (gs > 0) {
-      if (dt == DT_BF16) PDA_STREAM_DISPATCH(bn_apply_u_kernel, DT_BF16, gs, st, ARGS);
-      else PDA_STREAM_DISPATCH(bn_apply_u_kernel, DT_F16, gs, st, ARGS);
+      if (dt == DT_BF16) STREAM_DISPATCH(bn_apply_u_kernel, DT_BF16, gs, st, ARGS);
+      else STREAM_DISPATCH(bn_apply_u_kernel, DT_F16, gs, st, ARGS);
       return (int)hipGetLastError();
     }
   }
@@ -1307,8 +1307,8 @@ int pda_bn_bwd_apply2(const void* dz, const void* y, const void* y2, const float
     m = 0;
   }
 #define KA dz, y, y2, k, dy, dy2, n8, C
-  if (dt == DT_BF16) PDA_STREAM_DISPATCH_UM(bn_bwd_apply_dz2_u_kernel, DT_BF16, gs, st, u, m, KA);
-  else PDA_STREAM_DISPATCH_UM(bn_bwd_apply_dz2_u_kernel, DT_F16, gs, st, u, m, KA);
+  if (dt == DT_BF16) STREAM_DISPATCH_UM(bn_bwd_apply_dz2_u_kernel, DT_BF16, gs, st, u, m, KA);
+  else STREAM_DISPATCH_UM(bn_bwd_apply_dz2_u_kernel, DT_F16, gs, st, u, m, KA);
 #undef KA
   return (int)hipGetLastError();
 }
@@ -1322,8 +1322,8 @@ int pda_bn_bwd_apply(const BwdArgsC* c, const void* dz_in, const void* ysel, con
     const int gs = dt != DT_F32 ? stream_grid(n8, a.C) : 0;
     if (gs > 0) {
 #define KA (const void*)dz_in, (const void*)ysel, k1, k2, k3, (void*)dy, n8, a.C
-      if (dt == DT_BF16) PDA_STREAM_DISPATCH(bn_bwd_apply_dz_u_kernel, DT_BF16, gs, st, KA);
-      else PDA_STREAM_DISPATCH(bn_bwd_apply_dz_u_kernel, DT_F16, gs, st, KA);
+      if (dt == DT_BF16) STREAM_DISPATCH(bn_bwd_apply_dz_u_kernel, DT_BF16, gs, st, KA);
+      else STREAM_DISPATCH(bn_bwd_apply_dz_u_kernel, DT_F16, gs, st, KA);
 #undef KA
       return (int)hipGetLastError();
     }

@@ -1430,52 +1430,52 @@ static int dispatch(int dt, int bm, int bn, const ConvParams& p, dim3 grid, hipS
   if (bm > 2000) {
     if constexpr (PASS != WGRAD) {
       if (p.pro_sc != nullptr || !halo_ok(p, PASS == FWD ? p.Cin : p.Cout)) return -5;
-#define PDA_CASE4(D, M_, N_)                                                   \
+#define TILE_CASE4(D, M_, N_)                                                   \
   if (dt == D && bm - 2000 == M_ && bn == N_) return launch<PASS, D, M_, N_, 4>(p, grid, st);
-      PDA_CASE4(DT_BF16, 256, 128) PDA_CASE4(DT_BF16, 256, 64)
-#ifndef PDA_DMA_ONLY
-      PDA_CASE4(DT_F16, 256, 128) PDA_CASE4(DT_F16, 256, 64)
+      TILE_CASE4(DT_BF16, 256, 128) TILE_CASE4(DT_BF16, 256, 64)
+#ifndef CONV_DMA_ONLY
+      TILE_CASE4(DT_F16, 256, 128) TILE_CASE4(DT_F16, 256, 64)
 #endif
-#undef PDA_CASE4
+#undef TILE_CASE4
     }
     return -1;
   }
   if (bm > 1000) {
     if (p.pro_sc != nullptr) return -5;   // the operand prologue needs register staging
-#define PDA_CASE3(D, M_, N_)                                                   \
+#define TILE_CASE3(D, M_, N_)                                                   \
   if (dt == D && bm - 1000 == M_ && bn == N_) return launch<PASS, D, M_, N_, 3>(p, grid, st);
-    PDA_CASE3(DT_BF16, 256, 128) PDA_CASE3(DT_BF16, 128, 256) PDA_CASE3(DT_BF16, 128, 128)
-#ifndef PDA_DMA_ONLY
-    PDA_CASE3(DT_F16, 256, 128) PDA_CASE3(DT_F16, 128, 256) PDA_CASE3(DT_F16, 128, 128)
+    TILE_CASE3(DT_BF16, 256, 128) TILE_CASE3(DT_BF16, 128, 256) TILE_CASE3(DT_BF16, 128, 128)
+#ifndef CONV_DMA_ONLY
+    TILE_CASE3(DT_F16, 256, 128) TILE_CASE3(DT_F16, 128, 256) TILE_CASE3(DT_F16, 128, 128)
 #endif
-#undef PDA_CASE3
+#undef TILE_CASE3
     return -1;
   }
-#ifndef PDA_DMA_ONLY   // experiment builds (tools/dma_ab.py): the LDS-DMA kernels only
+#ifndef CONV_DMA_ONLY   // experiment builds (tools/dma_ab.py): the LDS-DMA kernels only
   if (bm < 0) {
-#define PDA_CASE1(D, M_, N_)                                                   \
+#define TILE_CASE1(D, M_, N_)                                                   \
   if (dt == D && -bm == M_ && bn == N_) return launch<PASS, D, M_, N_, 1>(p, grid, st);
-    PDA_CASE1(DT_BF16, 128, 128) PDA_CASE1(DT_BF16, 128, 64) PDA_CASE1(DT_BF16, 64, 128)
+    TILE_CASE1(DT_BF16, 128, 128) TILE_CASE1(DT_BF16, 128, 64) TILE_CASE1(DT_BF16, 64, 128)
     // 256-wide tiles only where they measured faster (profiles/convbench_r1_v6.txt): wgrad 256x128
     // (3x3 layers 3-4; the dgrad 128x256 tile never beat 128x128 in the step and is not built)
-    if constexpr (PASS == WGRAD) { PDA_CASE1(DT_BF16, 256, 128) PDA_CASE1(DT_F16, 256, 128) }
-    PDA_CASE1(DT_F16, 128, 128) PDA_CASE1(DT_F16, 128, 64) PDA_CASE1(DT_F16, 64, 128)
-    PDA_CASE1(DT_F32, 128, 128) PDA_CASE1(DT_F32, 128, 64) PDA_CASE1(DT_F32, 64, 128)
+    if constexpr (PASS == WGRAD) { TILE_CASE1(DT_BF16, 256, 128) TILE_CASE1(DT_F16, 256, 128) }
+    TILE_CASE1(DT_F16, 128, 128) TILE_CASE1(DT_F16, 128, 64) TILE_CASE1(DT_F16, 64, 128)
+    TILE_CASE1(DT_F32, 128, 128) TILE_CASE1(DT_F32, 128, 64) TILE_CASE1(DT_F32, 64, 128)
     // the split-f32 path stages hi + lo tiles: single-stage only (LDS)
-    PDA_CASE1(DT_F32S, 128, 128) PDA_CASE1(DT_F32S, 128, 64) PDA_CASE1(DT_F32S, 64, 128)
-    PDA_CASE1(DT_F32S, 64, 64)
-#undef PDA_CASE1
+    TILE_CASE1(DT_F32S, 128, 128) TILE_CASE1(DT_F32S, 128, 64) TILE_CASE1(DT_F32S, 64, 128)
+    TILE_CASE1(DT_F32S, 64, 64)
+#undef TILE_CASE1
     return -1;
   }
-#define PDA_CASE(D, M_, N_)                                                    \
+#define TILE_CASE(D, M_, N_)                                                    \
   if (dt == D && bm == M_ && bn == N_) return launch<PASS, D, M_, N_, 2>(p, grid, st);
-  PDA_CASE(DT_BF16, 128, 128) PDA_CASE(DT_BF16, 128, 64) PDA_CASE(DT_BF16, 64, 128)
-  PDA_CASE(DT_BF16, 64, 64)
-  PDA_CASE(DT_F16, 128, 128) PDA_CASE(DT_F16, 128, 64) PDA_CASE(DT_F16, 64, 128)
-  PDA_CASE(DT_F16, 64, 64)
-  PDA_CASE(DT_F32, 128, 128) PDA_CASE(DT_F32, 128, 64) PDA_CASE(DT_F32, 64, 128)
-  PDA_CASE(DT_F32, 64, 64)
-#undef PDA_CASE
+  TILE_CASE(DT_BF16, 128, 128) TILE_CASE(DT_BF16, 128, 64) TILE_CASE(DT_BF16, 64, 128)
+  TILE_CASE(DT_BF16, 64, 64)
+  TILE_CASE(DT_F16, 128, 128) TILE_CASE(DT_F16, 128, 64) TILE_CASE(DT_F16, 64, 128)
+  TILE_CASE(DT_F16, 64, 64)
+  TILE_CASE(DT_F32, 128, 128) TILE_CASE(DT_F32, 128, 64) TILE_CASE(DT_F32, 64, 128)
+  TILE_CASE(DT_F32, 64, 64)
+#undef TILE_CASE
 #endif
   return -1;
 }
@@ -1598,13 +1598,13 @@ int pda_conv_wgrad_bna(const ConvDesc* d, const void* dz, const void* y, const f
   p.k_chunk = k_chunk;
   const int abm = bm < 0 ? -bm : bm;
   const dim3 grid(((p.M + abm - 1) / abm) * ((p.N + bn - 1) / bn), splits);
-#define PDA_BNA(D, M_, N_, S_) \
+#define BNA_CASE(D, M_, N_, S_) \
   if (dt == D && bm == (S_ == 1 ? -M_ : M_) && bn == N_) return launch<WGRAD_BNA, D, M_, N_, S_>(p, grid, st);
-#ifndef PDA_DMA_ONLY
-  PDA_BNA(DT_BF16, 64, 128, 1) PDA_BNA(DT_BF16, 64, 128, 2)
-  PDA_BNA(DT_F16, 64, 128, 1) PDA_BNA(DT_F16, 64, 128, 2)
+#ifndef CONV_DMA_ONLY
+  BNA_CASE(DT_BF16, 64, 128, 1) BNA_CASE(DT_BF16, 64, 128, 2)
+  BNA_CASE(DT_F16, 64, 128, 1) BNA_CASE(DT_F16, 64, 128, 2)
 #endif
-#undef PDA_BNA
+#undef BNA_CASE
   return -1;
 }
 
@@ -1634,14 +1634,14 @@ int pda_wgrad_reduce(const float* slab, float* grad, int splits, int M, int N, i
     int epb = 256;
     while (epb > 16 && total / epb < 1024) epb >>= 1;
     const dim3 grid((total + epb - 1) / epb);
-#define PDA_RED(E)                                                                              \
+#define RED_CASE(E)                                                                              \
   if (epb == E) {                                                                               \
     hipLaunchKernelGGL(wgrad_reduce4_kernel<E>, grid, dim3(256), 0, st, slab, grad, splits, M, N, \
                        cin_pad_log2, cin_real, dst_pitch, scale, accumulate);                   \
     return (int)hipGetLastError();                                                              \
   }
-    PDA_RED(256) PDA_RED(128) PDA_RED(64) PDA_RED(32) PDA_RED(16)
-#undef PDA_RED
+    RED_CASE(256) RED_CASE(128) RED_CASE(64) RED_CASE(32) RED_CASE(16)
+#undef RED_CASE
   }
   int blocks = (total + 255) / 256;
   if (blocks > 4096) blocks = 4096;

@@ -22,7 +22,8 @@ from typing import Callable, Optional, Sequence
 
 import torch
 
-__all__ = ["DistEnv", "dist_env", "spawn", "free_port", "bind_numa", "init_distributed", "gpu_pci_bdf"]
+__all__ = ["DistEnv", "dist_env", "spawn", "free_port", "bind_numa", "init_distributed", "gpu_pci_bdf",
+           "host_group"]
 
 
 @dataclass
@@ -138,18 +139,35 @@ def spawn(fn: Callable, args: tuple = (), nprocs: Optional[int] = None, bind_num
     return mp.spawn(_child, args=(fn, args, bind_numa), nprocs=nprocs, join=join)
 
 
+_HOST_GROUP = None
+
+
+def host_group():
+    """Process group for HOST-side collectives (suspend flag, validation counters, barriers, bench
+    bookkeeping): gloo over TCP. Device collectives go through the framework's own RCCL
+    communicator (:mod:`~pytorch_distributed_amd.parallel.rccl`), so each process holds ONE RCCL
+    communicator: torch's NCCL process group is only the rendezvous (its communicator is created
+    lazily, i.e. never). Must be called by every rank (it creates the group collectively the first
+    time); :func:`init_distributed` does so."""
+    global _HOST_GROUP
+    import torch.distributed as dist
+    if _HOST_GROUP is None:
+        _HOST_GROUP = (dist.group.WORLD if dist.get_backend() == "gloo"
+                       else dist.new_group(backend="gloo"))
+    return _HOST_GROUP
+
+
 def init_distributed(env: DistEnv, backend: str, timeout_s: float = 1800.0,
                      device: Optional[torch.device] = None) -> None:
-    """TCP rendezvous (reference ``restnet_ddp.py:94``). With ``device`` the RCCL communicator is
-    created eagerly here (``device_id``), not lazily inside the first collective of the timed
-    epoch loop."""
+    """TCP rendezvous (reference ``restnet_ddp.py:94``) + the gloo host group. The gradient
+    communicator is the framework's native RCCL one (created by DistributedDataParallel), so no
+    ``device_id`` here: torch's own NCCL communicator is never instantiated."""
     import datetime
     import torch.distributed as dist
     if dist.is_initialized():
         return
-    kw = {"device_id": device} if (backend == "nccl" and device is not None
-                                   and device.type == "cuda") else {}
     dist.init_process_group(backend=backend,
                             init_method=f"tcp://{env.master_addr}:{env.master_port}",
                             world_size=env.world_size, rank=env.rank,
-                            timeout=datetime.timedelta(seconds=timeout_s), **kw)
+                            timeout=datetime.timedelta(seconds=timeout_s))
+    host_group()

@@ -136,11 +136,11 @@ class NativeResNet(nn.Module):
         # "1x1:H" also 3x3 consumers of input size >= H, "0" none
         import os
         self.fuse_prologue = os.environ.get("PDA_FUSE_PROLOGUE", "1x1:56")
-        self.fused_stem_bwd = os.environ.get("PDA_FUSED_STEM_BWD", "1") != "0"
+        self.fused_stem_bwd = True    # maxpool gather + ReLU mask + BN partials in one pass
         # stem wgrad forms its dY from the BN backward in-kernel (PDA_STEM_BNA=0: apply pass)
         self.stem_bna = os.environ.get("PDA_STEM_BNA", "1") != "0"
-        self.tail_mask = os.environ.get("PDA_TAIL_MASK", "1") != "0"
-        self.ds_stream = os.environ.get("PDA_DS_STREAM", "1") != "0"
+        self.tail_mask = True         # tails store the ReLU bitmask the backward reads
+        self.ds_stream = True         # the shortcut conv runs on the second stream
         # weight gradients on a second HIP stream: nothing in the backward chain consumes them, so
         # the (compute-bound) wgrad GEMMs fill the CUs left idle by the (HBM-bound) BN-backward
         # passes and small finalize launches of the dgrad chain on the main stream
@@ -396,8 +396,21 @@ class NativeResNet(nn.Module):
         self.refresh_shadow()
 
     @torch.no_grad()
-    def broadcast_buffers_from_rank0(self, comm) -> None:
-        comm.broadcast(self.flat_bufstore, 0)     # running stats + counters: one collective
+    def broadcast_buffers_from_rank0(self, comm, overlap: bool = False) -> None:
+        """Running stats + counters from rank 0: ONE collective over the flat buffer store (DDP's
+        per-forward buffer sync, SURVEY §2.8 M4). ``overlap``: issued on the communicator's stream;
+        the forward joins it right before the first BatchNorm finalize (the stem's), the first
+        kernel that writes the store, so the batch generation and the stem conv run meanwhile."""
+        if overlap:
+            self._bufsync = (comm, comm.broadcast_async(self.flat_bufstore, 0))
+            return
+        comm.broadcast(self.flat_bufstore, 0)
+
+    def _join_bufsync(self) -> None:
+        pend = getattr(self, "_bufsync", None)
+        if pend is not None:
+            self._bufsync = None
+            pend[0].wait(pend[1])
 
     def layout_signature(self) -> List[int]:
         """Integers every DDP rank must agree on before any collective (torch DDP's
@@ -468,9 +481,11 @@ class NativeResNet(nn.Module):
             return True
         return ":" in mode and u.H >= int(mode.split(":")[1])
 
-    def _conv_bn(self, u: ConvBN, x: torch.Tensor, train: bool, pro=None, ws=None) -> torch.Tensor:
+    def _conv_bn(self, u: ConvBN, x: torch.Tensor, train: bool, pro=None, ws=None,
+                 before_finalize=None) -> torch.Tensor:
         """y = conv(x) and BN coefficients (batch stats in training, running stats in eval).
-        ``pro=(scale, shift)``: x is the previous PRE-BN tensor; the conv applies BN+ReLU on load."""
+        ``pro=(scale, shift)``: x is the previous PRE-BN tensor; the conv applies BN+ReLU on load.
+        ``before_finalize``: called between the conv launch and the BN finalize launch."""
         ws = self.ws if ws is None else ws
         Nb = x.shape[0]
         g = u.geom(Nb)
@@ -481,9 +496,11 @@ class NativeResNet(nn.Module):
                            u.bn.momentum if u.bn.momentum is not None else 0.1,
                            st[0], st[1], st[2], st[3], self.rmean(u), self.rvar(u),
                            self.flat_nbt[u.nbt_idx:u.nbt_idx + 1], update_running=True)
-            K.conv_fwd(x, self.w16(u), g, y, pro=pro, bn=bn)
+            K.conv_fwd(x, self.w16(u), g, y, pro=pro, bn=bn, before_finalize=before_finalize)
         else:
             K.conv_fwd(x, self.w16(u), g, y, pro=pro)
+            if before_finalize is not None:
+                before_finalize()
             K.bn_eval_coeffs(self.gamma(u), self.beta(u), self.rmean(u), self.rvar(u), u.bn.eps,
                              st[2], st[3])
         return y
@@ -500,8 +517,9 @@ class NativeResNet(nn.Module):
         # context; any later forward overwrites it, which the generation check in backward catches
         self._state_gen = getattr(self, "_state_gen", 0) + 1
         saved: Dict = {"x0": x, "gen": self._state_gen} if save else None
-        # stem: conv -> bn -> relu -> maxpool (fused)
-        y0 = self._conv_bn(self.stem, x, train)
+        # stem: conv -> bn -> relu -> maxpool (fused); a pending DDP buffer broadcast joins
+        # before the stem's BN finalize (the first write of the running statistics)
+        y0 = self._conv_bn(self.stem, x, train, before_finalize=self._join_bufsync)
         ph = self.pool_hw
         p = self._empty(Nb, ph, ph, self.stem.cout)
         arg = torch.empty(Nb, ph, ph, self.stem.cout, dtype=torch.uint8, device=self.device)

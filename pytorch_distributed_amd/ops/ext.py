@@ -109,17 +109,12 @@ _SIGS = {
 
 
 def stream_cfg() -> tuple:
-    """16-bit BN apply passes (csrc/bn.hip StreamCfg): PDA_STREAM = "auto" (default: 4 chunks per
-    thread + nontemporal loads/stores for tensors >= 50 MiB, the one-chunk kernels below) or
-    "U,NTM,CAP[,MIN_MB]" (or ':'-separated): U > 0 forces U chunks for every size, U < 0 is the
-    auto policy with -U chunks (-1: 4) from MIN_MB up, U = 0 the one-chunk kernels everywhere. In-step A/B (tools/gpu_ab.sh, one box): 30.02 ms (0) vs 29.41 ms (auto, 100 MiB);
-    size threshold 200 / 100 / 50 / 30 MiB: 29.38-29.53 / 29.16 / 29.06-29.11 / 29.02-29.13 ms;
-    grid cap 8192 / 16384 / 32768 / 65536 blocks: 29.53 / 29.15-29.27 / 28.90-29.09 / 28.86-28.97 ms."""
-    v = os.environ.get("PDA_STREAM", "auto")
-    if v == "auto":
-        return (-1, 3, 65536, 50)
-    f = [int(x) for x in v.replace(":", ",").split(",")][:4]
-    return tuple(f + [0, 0, 8192, 100][len(f):])
+    """16-bit BN apply passes (csrc/bn.hip StreamCfg): 4 chunks per thread + nontemporal loads /
+    stores for tensors >= 50 MiB, the one-chunk kernels below, grid cap 65536 blocks. In-step A/B
+    (tools/gpu_ab.sh, one box): 30.02 ms (one-chunk everywhere) vs 29.41 ms (100 MiB threshold);
+    threshold 200 / 100 / 50 / 30 MiB: 29.38-29.53 / 29.16 / 29.06-29.11 / 29.02-29.13 ms; grid cap
+    8192 / 16384 / 32768 / 65536: 29.53 / 29.15-29.27 / 28.90-29.09 / 28.86-28.97 ms."""
+    return (-1, 3, 65536, 50)
 
 
 def load(required: bool = False) -> Optional[C.CDLL]:

@@ -97,7 +97,7 @@ class Workspace:
 
 
 _NUM_CU = 256
-_WGRAD_TARGET = int(os.environ.get("PDA_WGRAD_TARGET", 2 * _NUM_CU))
+_WGRAD_TARGET = 2 * _NUM_CU   # default split-K block target of the weight gradients
 
 
 # f32 convolutions: "exact" = MFMA 16x16x4 f32 (DT_F32); "split" = f32 tensors with the products on
@@ -106,14 +106,11 @@ _WGRAD_TARGET = int(os.environ.get("PDA_WGRAD_TARGET", 2 * _NUM_CU))
 _F32_CONV = os.environ.get("PDA_F32_CONV", os.environ.get("MX_F32_CONV", "exact"))
 if _F32_CONV not in ("exact", "split"):
     raise ValueError(f"MX_F32_CONV / PDA_F32_CONV must be exact|split, got {_F32_CONV!r}")
-_SPLIT_BN = int(os.environ.get("PDA_SPLIT_BN", "128"))   # widest N tile of the split kernels (A/B)
-_STATS_S = os.environ.get("PDA_STATS_S")   # fixed slab count of the statistics kernels (A/B)
-_STATS_S_SCALE = float(os.environ.get("PDA_STATS_S_SCALE", "1.0"))   # scale on its heuristic (A/B)
-_STEM_G = int(os.environ.get("PDA_STEM_G", "4096"))   # block cap of the one-pass stem backward (A/B)
-# downsample-tail BN backward: both branches' apply in one pass over dz (PDA_BWD_APPLY2=0: two)
-_BWD_APPLY2 = os.environ.get("PDA_BWD_APPLY2", "1") != "0"
-# scale on the split-K block targets (the wgrads run beside the dgrad chain on a second stream)
-_WGRAD_TB_SCALE = float(os.environ.get("PDA_WGRAD_TB_SCALE", "1.0"))
+_SPLIT_BN = 128      # widest N tile of the split kernels
+_STEM_G = 4096       # block cap of the one-pass stem backward (profiles/ab_r2_inlaunch_bn.md)
+# downsample-tail BN backward: both branches' apply in one pass over dz (False: two launches, kept
+# for tests/test_native_model_gpu.py's bitwise parity test of the two forms)
+_BWD_APPLY2 = True
 
 
 def _kdt(t: torch.Tensor) -> int:
@@ -196,7 +193,7 @@ def conv_fwd(x: torch.Tensor, w: torch.Tensor, g: ConvGeom, out: torch.Tensor,
              stats: Optional[torch.Tensor] = None, bias: Optional[torch.Tensor] = None,
              relu: bool = False, tile: Optional[Tuple[int, int]] = None,
              pro: Optional[Tuple[torch.Tensor, torch.Tensor]] = None,
-             bn: Optional[BnStats] = None) -> torch.Tensor:
+             bn: Optional[BnStats] = None, before_finalize=None) -> torch.Tensor:
     """out[M, Cout] (16-bit or f32) = conv(x, w). w: [Cout, Kpad] 16-bit, Kpad = w.shape[1].
     stats (f32, >= ceil(M/bm)*3*Cout) receives per-M-tile shifted partials (sum(y-s),
     sum((y-s)^2), s) -- see :func:`stats_totals`; ``bn`` (:class:`BnStats`) also finalizes the
@@ -220,6 +217,8 @@ def conv_fwd(x: torch.Tensor, w: torch.Tensor, g: ConvGeom, out: torch.Tensor,
                                 ptr(bias), ptr(stats), int(relu), ptr(pro[0] if pro else None),
                                 ptr(pro[1] if pro else None), kdt, kbm, kbn, stream(x.device))
     check(rc, "conv_fwd")
+    if before_finalize is not None:
+        before_finalize()
     if bn is not None:
         bn_finalize_partials(stats, T, g.Cout, tile_rows(kbm), M, bn)
     return out
@@ -412,7 +411,7 @@ def wgrad_plan(g: ConvGeom, Nb: int, tile: Optional[Tuple[int, int]] = None,
             bm, bn = -128, 128
     if target_blocks is None:
         target_blocks = _WGRAD_TARGET
-    target_blocks = max(1, int(target_blocks * _WGRAD_TB_SCALE))
+    target_blocks = max(1, int(target_blocks))
     if tile:
         bm, bn = tile
     tiles = math.ceil(M / tile_rows(bm)) * math.ceil(N / bn)
@@ -657,9 +656,7 @@ def _stats_slabs(T: int, C_: int) -> int:
     """Blocks per channel group of the one-launch statistics kernel: level 1 reads T/S tiles per
     block, the group's last arriver S slabs -- S ~ sqrt(T) balances the two (both run at one CU's
     bandwidth), at least 8 when T allows so the level-1 reads spread over CUs."""
-    if _STATS_S is not None:   # A/B override (tools/bnstats_bench.py)
-        return max(1, min(T, int(_STATS_S)))
-    return max(1, min(T, max(8, int(_STATS_S_SCALE * math.sqrt(0.75 * T)))))
+    return max(1, min(T, max(8, int(math.sqrt(0.75 * T)))))
 
 
 def _bn_bwd_tail(ws, part, G, nq, mode, a, y, mean, invstd, gamma, dgamma, dbeta, dy_out,

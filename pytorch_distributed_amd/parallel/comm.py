@@ -40,6 +40,12 @@ class Communicator:
     def broadcast(self, t: torch.Tensor, src: int = 0) -> None:
         raise NotImplementedError
 
+    def broadcast_async(self, t: torch.Tensor, src: int = 0) -> Any:
+        """Broadcast that may complete later; the returned handle goes to :meth:`wait`. Default:
+        synchronous (returns None)."""
+        self.broadcast(t, src)
+        return None
+
     def barrier(self) -> None:
         raise NotImplementedError
 

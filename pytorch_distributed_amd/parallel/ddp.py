@@ -214,7 +214,9 @@ class DistributedDataParallel(nn.Module):
 
     def _sync_buffers(self) -> None:
         if self._native:
-            self.module.broadcast_buffers_from_rank0(self.comm)
+            # on the comm stream, joined before the stem's BN finalize (no stall of the compute
+            # stream at the top of every forward); SyncBN keeps every collective on one stream
+            self.module.broadcast_buffers_from_rank0(self.comm, overlap=self.bn_comm is None)
             return
         with torch.no_grad():
             for b in self.module.buffers():

@@ -164,6 +164,20 @@ class RcclCommunicator(Communicator):
         t.record_stream(self.stream)
         return done
 
+    def broadcast_async(self, t: torch.Tensor, src: int = 0):
+        """Broadcast on the comm stream, ordered after the current stream's work; returns the
+        completion event (join with :meth:`wait` where ``t`` is next read or written)."""
+        cur = torch.cuda.current_stream(self.device)
+        ready = torch.cuda.Event()
+        ready.record(cur)
+        self.stream.wait_event(ready)
+        _check(load().pda_broadcast(self._live(), t.data_ptr(), t.data_ptr(), t.numel(), _DT[t.dtype],
+                                    src, self.stream.cuda_stream), "broadcast")
+        done = torch.cuda.Event()
+        done.record(self.stream)
+        t.record_stream(self.stream)
+        return done
+
     def make_bucket_reducer(self, flat: torch.Tensor, buckets) -> "RcclBucketReducer":
         """Native bucket reducer over contiguous ``(begin, end)`` element ranges of ``flat``."""
         return RcclBucketReducer(self, flat, buckets)

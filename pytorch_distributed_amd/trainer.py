@@ -208,8 +208,12 @@ def validate(dataloader, model, criterion, epoch: int, ctx: Context) -> float:
                 stats[2] += hit.sum()
             stats[3] += samples.size(0)
     if ctx.distributed:
-        import torch.distributed as dist
-        dist.all_reduce(stats)
+        comm = getattr(model, "comm", None)
+        if comm is not None and stats.is_cuda:
+            comm.all_reduce(stats)        # the DDP's own RCCL communicator (M6: one 4-element call)
+        else:
+            import torch.distributed as dist
+            dist.all_reduce(stats)
     loss, c1, c5, total = stats.tolist()
     nb = max(len(dataloader), 1)
     loss_val = loss / ctx.world / nb
@@ -345,8 +349,14 @@ def run(cfg: RunConfig, mode: str, local_rank: int = 0, nprocs: Optional[int] = 
         t1 = time.time()
         if train_sampler is not None:
             train_sampler.set_epoch(epoch)
-        steps = train(train_loader, model, criterion, optimizer, scheduler, epoch, ctx,
-                      start_step, best_acc, save_path)
+        from .utils.gpu_util import BusySampler
+        devs = ([ctx.device.index if ctx.device.index is not None else torch.cuda.current_device()]
+                if ctx.device.type == "cuda" else [])
+        if hasattr(model, "device_ids"):     # DataParallel: every replica's device
+            devs = list(model.device_ids)
+        with BusySampler(devs) as busy:       # the reference's "Avg GPU Util" panel (README:33-40)
+            steps = train(train_loader, model, criterion, optimizer, scheduler, epoch, ctx,
+                          start_step, best_acc, save_path)
         start_step = 0
         scheduler.step()
         acc = validate(val_loader, model, criterion, epoch, ctx)
@@ -357,6 +367,7 @@ def run(cfg: RunConfig, mode: str, local_rank: int = 0, nprocs: Optional[int] = 
             print("cost time per epoch: {:.4f} s".format(t2 - t1), flush=True)
             ctx.metrics.write(epoch=epoch, steps=steps, epoch_s=t2 - t1, acc1=acc,
                               images=steps * per_rank_batch * ctx.world, gpu_mem_gb=gpu_mem_gb(),
+                              gpu_util_pct=busy.overall(),
                               engine=engine, dtype=str(dtype))
             if acc > best_acc:
                 best_acc = acc
@@ -364,6 +375,7 @@ def run(cfg: RunConfig, mode: str, local_rank: int = 0, nprocs: Optional[int] = 
                 save_best(save_path, _unwrap(model).state_dict())
     if distributed:
         import torch.distributed as dist
-        dist.barrier()
+        from .launch import host_group
+        dist.barrier(group=host_group())
         dist.destroy_process_group()
     return best_acc

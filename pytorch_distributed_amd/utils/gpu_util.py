@@ -14,7 +14,7 @@ from typing import Dict, List, Optional, Sequence
 
 from ..launch import gpu_pci_bdf
 
-__all__ = ["BusySampler", "busy_path"]
+__all__ = ["BusySampler", "busy_path", "kernel_busy"]
 
 
 def busy_path(index: int) -> Optional[str]:
@@ -66,3 +66,44 @@ class BusySampler:
     def overall(self) -> Optional[float]:
         v = [x for x in self.mean().values() if x is not None]
         return round(sum(v) / len(v), 1) if v else None
+
+
+def kernel_busy(step_fn, steps: int, devices: Sequence[int]) -> Dict[int, Optional[float]]:
+    """Device-busy % measured from the kernels themselves, for hosts where the driver's sysfs
+    counter is not readable (e.g. inside a container): ``steps`` calls of ``step_fn(i)`` under
+    torch.profiler (ROCm: roctracer kernel records), then per device the union of kernel intervals
+    over the span from its first kernel start to its last kernel end -- the same quantity
+    (fraction of time any kernel is running) that ``gpu_busy_percent`` samples."""
+    import torch
+    from torch.autograd import DeviceType
+    from torch.profiler import ProfilerActivity, profile
+    for d in devices:
+        torch.cuda.synchronize(d)
+    with profile(activities=[ProfilerActivity.CUDA]) as prof:
+        for i in range(steps):
+            step_fn(i)
+        for d in devices:
+            torch.cuda.synchronize(d)
+    per: Dict[int, list] = {d: [] for d in devices}
+    for e in prof.events():
+        if e.device_type != DeviceType.CUDA or e.time_range.end <= e.time_range.start:
+            continue
+        if e.device_index in per:
+            per[e.device_index].append((e.time_range.start, e.time_range.end))
+    out: Dict[int, Optional[float]] = {}
+    for d, iv in per.items():
+        if not iv:
+            out[d] = None
+            continue
+        iv.sort()
+        busy, cs, ce = 0, iv[0][0], iv[0][1]
+        for s_, e_ in iv[1:]:
+            if s_ > ce:
+                busy += ce - cs
+                cs, ce = s_, e_
+            else:
+                ce = max(ce, e_)
+        busy += ce - cs
+        span = iv[-1][1] - iv[0][0]
+        out[d] = round(100.0 * busy / span, 1) if span > 0 else None
+    return out

@@ -75,10 +75,11 @@ class SuspendMonitor:
             return False
         if dist.is_available() and dist.is_initialized():
             import torch
-            backend = dist.get_backend(group)
-            dev = torch.device("cuda", torch.cuda.current_device()) if backend == "nccl" else "cpu"
-            t = torch.tensor([1.0 if local else 0.0], device=dev)
-            dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
+            from ..launch import host_group
+            # a host value: all-reduced on the gloo host group (no device collective, no stall of
+            # the compute stream)
+            t = torch.tensor([1.0 if local else 0.0])
+            dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group if group is not None else host_group())
             return bool(t.item() > 0)
         return local
 

@@ -200,16 +200,10 @@ def test_f32_conv_mode_dtype_and_tile_mapping(monkeypatch):
     assert K._ktile(128, 64, 1) == (128, 64)          # other dtypes untouched
 
 
-def test_stream_cfg_parsing(monkeypatch):
-    """PDA_STREAM (BN apply streaming policy, csrc/bn.hip StreamCfg): 'auto' by default, explicit
-    'U,NTM,CAP[,MIN_MB]' (',' or ':' separated) padded with the defaults."""
+def test_stream_cfg_is_fixed():
+    """The BN apply streaming policy (csrc/bn.hip StreamCfg) is the measured one, no env knob."""
     from pytorch_distributed_amd.ops import ext
-    monkeypatch.delenv("PDA_STREAM", raising=False)
     assert ext.stream_cfg() == (-1, 3, 65536, 50)
-    for v, want in [("0", (0, 0, 8192, 100)), ("2,3", (2, 3, 8192, 100)),
-                    ("4:3:16384", (4, 3, 16384, 100)), ("4,1,4096,50", (4, 1, 4096, 50))]:
-        monkeypatch.setenv("PDA_STREAM", v)
-        assert ext.stream_cfg() == want, v
 
 
 def test_loss_scaler_refuses_second_fused_step():

@@ -2,7 +2,7 @@
 
 Build (CPU):  python tools/dma_ab.py build NAME [-DFLAG=V ...] [--full]
     -> pytorch_distributed_amd/_lib/variants/libconv_NAME.so (conv_gemm.hip only; without --full
-       only the LDS-DMA instantiations: -DPDA_DMA_ONLY, a ~10 s build)
+       only the LDS-DMA instantiations: -DCONV_DMA_ONLY, a ~10 s build)
 Run (GPU):    python tools/dma_ab.py run NAME[,NAME...] SHAPE:PASS:BM:BN [...] [--rounds R] [--reps N]
     times every (case, variant) interleaved over R rounds; prints the median and min (us, TF/s).
     NAME "main" = the in-tree libpda_kernels.so."""
@@ -22,7 +22,7 @@ def build(name, flags, full):
     out = _build.OUT / "variants"
     out.mkdir(parents=True, exist_ok=True)
     obj = out / f"conv_{name}.o"
-    extra = list(flags) + ([] if full else ["-DPDA_DMA_ONLY"])
+    extra = list(flags) + ([] if full else ["-DCONV_DMA_ONLY"])
     _build._compile(_build.CSRC / "conv_gemm.hip", obj, extra, verbose=True)
     lib = out / f"libconv_{name}.so"
     _build._link([obj], lib, [], verbose=False)
