@@ -84,12 +84,20 @@ def kernel_busy(step_fn, steps: int, devices: Sequence[int]) -> Dict[int, Option
             step_fn(i)
         for d in devices:
             torch.cuda.synchronize(d)
-    per: Dict[int, list] = {d: [] for d in devices}
+    # ROCTracer labels device records with the HSA agent index (CPU agents first), not the torch
+    # device index: agents are mapped onto the requested devices in enumeration order
+    by_agent: Dict[int, list] = {}
     for e in prof.events():
         if e.device_type != DeviceType.CUDA or e.time_range.end <= e.time_range.start:
             continue
-        if e.device_index in per:
-            per[e.device_index].append((e.time_range.start, e.time_range.end))
+        by_agent.setdefault(e.device_index, []).append((e.time_range.start, e.time_range.end))
+    per: Dict[int, list] = {d: [] for d in devices}
+    agents = sorted(by_agent)
+    if len(devices) == 1:
+        per[devices[0]] = [iv for a in agents for iv in by_agent[a]]
+    elif len(agents) == len(devices):
+        for d, a in zip(sorted(devices), agents):
+            per[d] = by_agent[a]
     out: Dict[int, Optional[float]] = {}
     for d, iv in per.items():
         if not iv:
