@@ -221,8 +221,12 @@ __global__ __launch_bounds__(conv_nt<STAGES>(), (PASS_T == WGRAD_BNA ? 3 : conv_
   constexpr int ES = O32 ? 4 : 2;        // element bytes in global memory and in the C tile
   constexpr int EPC = 16 / LES;          // operand elements per 16-B LDS chunk
   constexpr int EPO = 16 / ES;           // C-tile elements per 16-B chunk (epilogue)
-  constexpr int BKE = 128 / LES;         // k per tile (one 128-B row)
-  constexpr int A_BYTES = BM * 128, B_BYTES = BN * 128;
+  // k per tile: one 128-B row; the 256x256 LDS-DMA tile (weight gradient: both images k-major)
+  // takes 32 k per tile so that four ring slots (128 KiB) keep three tiles in flight
+  constexpr bool BK32 = DMA && !HALO && BM * BN >= 256 * 256;
+  constexpr int BKE = BK32 ? 32 : 128 / LES;
+  static_assert(!BK32 || PASS == WGRAD, "the 32-k tile has k-major (COL) images only");
+  constexpr int A_BYTES = BM * BKE * LES, B_BYTES = BN * BKE * LES;
   constexpr int AB_BYTES = A_BYTES + B_BYTES;
   constexpr int STAGE = SPLIT ? 2 * AB_BYTES : AB_BYTES;
   // epilogue partial-sum reduction [3][RG][BN] f32
@@ -235,7 +239,9 @@ __global__ __launch_bounds__(conv_nt<STAGES>(), (PASS_T == WGRAD_BNA ? 3 : conv_
   // slots and one zero row (the fragment source of a tap that falls outside the image)
   constexpr int SLAB_ROWS = BM + 128, SLAB_BYTES = SLAB_ROWS * 128;
   constexpr int ZOFF = 2 * SLAB_BYTES + 3 * B_BYTES;
-  constexpr int RING = HALO ? ZOFF + 128 : STAGES * STAGE;
+  // LDS-DMA ring slots: 4 when they fit in 144 KiB (three tiles in flight), else 3
+  constexpr int NSLOT = DMA && !HALO ? (4 * STAGE <= 144 * 1024 ? 4 : 3) : STAGES;
+  constexpr int RING = HALO ? ZOFF + 128 : NSLOT * STAGE;
   constexpr int LDS_0 = RING > RED_BYTES ? RING : RED_BYTES;
   constexpr int LDS_BYTES = LDS_0 > C_BYTES ? LDS_0 : C_BYTES;
   static_assert(BN <= NTH, "stats reduction: one thread per column");
@@ -624,8 +630,9 @@ __global__ __launch_bounds__(conv_nt<STAGES>(), (PASS_T == WGRAD_BNA ? 3 : conv_
   // logical chunk slot ^ swz(r) -- so the fragment reads are the same code. Everything that does not
   // change along K is precomputed; a k-tile then costs 1-3 VALU per piece (FWD/DGRAD tap select,
   // an add) and, for the gathered WGRAD B, one pixel decode per piece.
-  constexpr int GA = DMA ? BM * 8 / NTH : 1, GB = DMA ? BN * 8 / NTH : 1;
-  static_assert(!DMA || (GA >= 1 && GB >= 1 && BM * 8 % NTH == 0 && BN * 8 % NTH == 0), "DMA tile");
+  constexpr int GA = DMA ? A_BYTES / (NTH * 16) : 1, GB = DMA ? B_BYTES / (NTH * 16) : 1;
+  static_assert(!DMA || (GA >= 1 && GB >= 1 && A_BYTES % (NTH * 16) == 0 &&
+                         B_BYTES % (NTH * 16) == 0), "DMA tile");
   int da_base[GA];        // A ROW: byte offset of the row's tap-(0,0) pixel + chunk (may be < 0)
   uint64_t da_mask[GA];   // A ROW: taps of the row inside the image
   uint32_t da_off[GA];    // A COL (WGRAD): byte offset of (krow, col) at k = kbeg
@@ -965,14 +972,20 @@ __global__ __launch_bounds__(conv_nt<STAGES>(), (PASS_T == WGRAD_BNA ? 3 : conv_
     // 3-slot ring: tile kt lives in slot kt % 3. Tile kt+2 is issued right after the barrier that
     // retires tile kt (each wave's counted vmcnt + the barrier: every wave's DMA of tile kt has
     // landed) and that proves every wave finished reading slot (kt+2) % 3 = (kt-1) % 3.
-    if (nk > 0) issue_dma(0, 0);
-    if (nk > 1) issue_dma(1, 1);
+#pragma unroll
+    for (int t = 0; t < NSLOT - 1; ++t)
+      if (t < nk) issue_dma(t, t);
     int slot = 0;
     for (int kt = 0; kt < nk; ++kt) {
-      if (kt + 1 < nk) vm_wait<GP>(); else vm_wait<0>();
+      // tile kt must have landed: the younger tiles kt+1 .. kt+NSLOT-2 may stay in flight
+      if constexpr (NSLOT == 4) {
+        if (kt + 2 < nk) vm_wait<2 * GP>(); else if (kt + 1 < nk) vm_wait<GP>(); else vm_wait<0>();
+      } else {
+        if (kt + 1 < nk) vm_wait<GP>(); else vm_wait<0>();
+      }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();
-      const int nslot = slot == 0 ? 2 : slot - 1;
+      const int nslot = slot == 0 ? NSLOT - 1 : slot - 1;   // = (kt + NSLOT - 1) % NSLOT
       const char* sa = smem + slot * STAGE;
       const char* sb = sa + A_BYTES;
       // the pieces of tile kt+2 spread over this tile's MFMAs (a burst of LDS-DMA issues right
@@ -980,13 +993,14 @@ __global__ __launch_bounds__(conv_nt<STAGES>(), (PASS_T == WGRAD_BNA ? 3 : conv_
       // past the last tile they are OOB no-ops (nothing reads that slot again), so the MFMA
       // stream carries no branch
       uint32_t voff[GP];
-      dma_offsets(kt + 2, voff);
-      const bool pre = kt + 2 < nk;
+      dma_offsets(kt + NSLOT - 1, voff);
+      const bool pre = kt + NSLOT - 1 < nk;
 #pragma unroll
       for (int i = 0; i < GP; ++i) voff[i] = pre ? voff[i] : OOB;
       constexpr int NMF = MI * NI;
+      constexpr int NKS = BKE / 32;   // MFMA k-steps per tile
 #pragma unroll
-      for (int s = 0; s < 2; ++s) {
+      for (int s = 0; s < NKS; ++s) {
         s16x8 fa[MI], fb[NI];
 #pragma unroll
         for (int i = 0; i < MI; ++i) {
@@ -1004,13 +1018,13 @@ __global__ __launch_bounds__(conv_nt<STAGES>(), (PASS_T == WGRAD_BNA ? 3 : conv_
         for (int idx = 0; idx < NMF; ++idx) {
           const int i = idx / NI, j = idx % NI;
           acc[i][j] = mfma16<MDT>(fb[j], fa[i], acc[i][j]);
-          const int g = s * NMF + idx;   // piece pc goes after MFMA (pc * 2 * NMF) / GP
+          const int g = s * NMF + idx;   // piece pc goes after MFMA (pc * NKS * NMF) / GP
 #pragma unroll
           for (int pc = 0; pc < GP; ++pc)
-            if (g == (pc * 2 * NMF) / GP) dma_piece(pc, nslot, voff);
+            if (g == (pc * NKS * NMF) / GP) dma_piece(pc, nslot, voff);
         }
       }
-      slot = slot == 2 ? 0 : slot + 1;
+      slot = slot == NSLOT - 1 ? 0 : slot + 1;
     }
   }
   if constexpr (DMA) {
@@ -1445,8 +1459,10 @@ static int dispatch(int dt, int bm, int bn, const ConvParams& p, dim3 grid, hipS
 #define TILE_CASE3(D, M_, N_)                                                   \
   if (dt == D && bm - 1000 == M_ && bn == N_) return launch<PASS, D, M_, N_, 3>(p, grid, st);
     TILE_CASE3(DT_BF16, 256, 128) TILE_CASE3(DT_BF16, 128, 256) TILE_CASE3(DT_BF16, 128, 128)
+    if constexpr (PASS == WGRAD) { TILE_CASE3(DT_BF16, 256, 256) }
 #ifndef CONV_DMA_ONLY
     TILE_CASE3(DT_F16, 256, 128) TILE_CASE3(DT_F16, 128, 256) TILE_CASE3(DT_F16, 128, 128)
+    if constexpr (PASS == WGRAD) { TILE_CASE3(DT_F16, 256, 256) }
 #endif
 #undef TILE_CASE3
     return -1;

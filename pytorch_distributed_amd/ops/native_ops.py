@@ -371,22 +371,26 @@ _WGRAD_TUNED = {
 }
 # LDS-DMA tiles (16-bit, no operand prologue; the register-staged entry above is the fallback)
 _DMA = os.environ.get("PDA_DMA", "1") != "0"
-_WGRAD_DMA = {   # tools/wgrad_sweep.py, kernel + slab reduce (profiles/wgrad_sweep_r3.txt)
+_WGRAD_DMA = {   # tools/wgrad_sweep.py, kernel + slab reduce (profiles/wgrad_sweep_r3{,b}.txt)
     (256, 1, 64, 1, 56): ((1256, 128), 256),    # C3  159 -> 153 us (the downsample; conv3: prologue)
     (64, 1, 256, 1, 56): ((1128, 256), 256),    # C4  160 -> 151
     (128, 1, 256, 1, 56): ((1128, 256), 256),   # C5  206 -> 182
     (128, 3, 128, 2, 28): ((1128, 256), 512),   # C6  200 -> 200 (conv_bench: 221 -> 197)
     (512, 1, 128, 1, 28): ((1256, 128), 256),   # C7  113 ->  98
-    (512, 1, 256, 2, 28): ((1256, 128), 256),   # C8  168 -> 154
+    (512, 1, 256, 2, 28): ((1256, 256), 512),   # C8  168 -> 137
     (128, 1, 512, 1, 28): ((1128, 256), 256),   # C9  115 ->  96
     (128, 3, 128, 1, 28): ((1128, 256), 512),   # C10 171 -> 168
-    (256, 1, 512, 1, 28): ((1256, 128), 256),   # C11 165 -> 151
-    (512, 1, 1024, 1, 14): ((1256, 128), 256),  # C17 130 -> 123
+    (256, 1, 512, 1, 28): ((1256, 256), 256),   # C11 165 -> 140
+    (256, 3, 256, 2, 14): ((1256, 256), 512),   # C12 171 -> 124
+    (1024, 1, 512, 2, 14): ((1256, 256), 512),  # C14 133 -> 121
+    (256, 1, 1024, 1, 14): ((1256, 256), 256),  # C15  78 ->  75
+    (256, 3, 256, 1, 14): ((1256, 256), 256),   # C16 161 -> 120
+    (512, 1, 1024, 1, 14): ((1256, 256), 256),  # C17 130 -> 122
+    (512, 3, 512, 2, 7): ((1256, 256), 512),    # C18 134 -> 119
     (2048, 1, 512, 1, 7): ((1128, 256), 256),   # C19  67 ->  60
-    (2048, 1, 1024, 2, 7): ((1256, 128), 256),  # C20 118 -> 115
-    (512, 1, 2048, 1, 7): ((1256, 128), 256),   # C21  70 ->  62
-    (512, 3, 512, 2, 7): ((1256, 128), 1024),   # C18 131 -> 131
-    (512, 3, 512, 1, 7): ((1256, 128), 512),    # C22 129 -> 127
+    (2048, 1, 1024, 2, 7): ((1256, 256), 512),  # C20 118 -> 111
+    (512, 1, 2048, 1, 7): ((1256, 128), 256),   # C21  70 ->  61
+    (512, 3, 512, 1, 7): ((1256, 256), 512),    # C22 129 -> 116
 }
 
 

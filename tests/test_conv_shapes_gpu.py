@@ -25,7 +25,8 @@ SHAPES = [  # name, H, Cin, Cout, k, stride  
 TILES = [(128, 128), (128, 64), (64, 128), (64, 64), (-128, 128), (-128, 64), (-64, 128)]
 # LDS-DMA 8-wave tiles (bm = 1000 + rows): 16-bit only
 DMA_TILES = [(1256, 128), (1128, 256), (1128, 128)]
-WGRAD_TILES = TILES + DMA_TILES + [(-256, 128)]   # the 256-row single-stage tile: wgrad only
+# wgrad only: the 256-row single-stage tile and the 256x256 LDS-DMA tile (32 k per ring slot)
+WGRAD_TILES = TILES + DMA_TILES + [(-256, 128), (1256, 256)]
 
 
 def rel_err(a, b):
@@ -170,6 +171,13 @@ def test_dma_tiles_multi_tile(shape, dt):
                         ("stats", rel_err(st[0], y.float().reshape(-1, Cout).sum(0)))):
             if not e < 1e-2:
                 bad.append((t, name, e))
+    for tb in (64, 256, 1024):   # the 256x256 weight-gradient tile, several split-K depths
+        dw = torch.full((Cout, k, k, Cin), float("nan"), device=DEV)
+        K.conv_wgrad(dy_nhwc, x_nhwc, g, dw.view(-1), ws, tile=(1256, 256), target_blocks=tb)
+        torch.cuda.synchronize()
+        e = rel_err(dw, wr.grad.permute(0, 2, 3, 1))
+        if not e < 1e-2:
+            bad.append(((1256, 256), f"wgrad/{tb}", e))
     assert not bad, bad
 
 
