@@ -130,35 +130,32 @@ __global__ __launch_bounds__(256) void bn_stats_kernel(const float* __restrict__
                                                        int bm, int M, int CG,
                                                        double* __restrict__ slabs,
                                                        int* __restrict__ cnt, Out o) {
-  __shared__ double red[NQ][1024];   // [q][(lane * Q + quad) * 4 + e], then [q][column]
+  // 8 KiB of LDS whatever NQ: the kernel runs on the main stream beside the weight-gradient
+  // GEMMs, whose LDS-DMA tiles hold 144 KiB of a CU's 160 KiB -- a larger footprint could only be
+  // placed on CUs with no weight-gradient block resident (measured: 150-180 us instead of ~15 us)
+  __shared__ double red[1024];   // [(lane * Q + quad) * 4 + e] of one q at a time
   __shared__ int flag;
   const int S = gridDim.x, s = blockIdx.x, g = blockIdx.y, tid = threadIdx.x;
   const int Q = CG >> 2, SL = 256 / Q;
   const int quad = tid % Q, lane = tid / Q;
   const int c = g * CG + quad * 4;
   const bool act = lane < SL && c < C;
-  // fixed-order sum over the SL lanes of each column v < CG of this group, into red[q][v]
+  // fixed-order sum over the SL lanes of each column v < CG of this group: thread v gets tot[q]
+  double tot[NQ];
   auto combine = [&](const double (&a)[NQ][4]) __attribute__((always_inline)) {
-    __syncthreads();
 #pragma unroll
-    for (int q = 0; q < NQ; ++q)
+    for (int q = 0; q < NQ; ++q) {
+      __syncthreads();
 #pragma unroll
-      for (int e = 0; e < 4; ++e) red[q][tid * 4 + e] = a[q][e];
-    __syncthreads();
-    double sum[NQ];
-#pragma unroll
-    for (int q = 0; q < NQ; ++q) sum[q] = 0.0;
-    if (tid < CG) {
-      const int qi = tid >> 2, e = tid & 3;
-      for (int l = 0; l < SL; ++l)
-#pragma unroll
-        for (int q = 0; q < NQ; ++q) sum[q] += red[q][(l * Q + qi) * 4 + e];
+      for (int e = 0; e < 4; ++e) red[tid * 4 + e] = a[q][e];
+      __syncthreads();
+      double sum = 0.0;
+      if (tid < CG) {
+        const int qi = tid >> 2, e = tid & 3;
+        for (int l = 0; l < SL; ++l) sum += red[(l * Q + qi) * 4 + e];
+      }
+      tot[q] = sum;
     }
-    __syncthreads();
-    if (tid < CG)
-#pragma unroll
-      for (int q = 0; q < NQ; ++q) red[q][tid] = sum[q];
-    __syncthreads();
   };
   constexpr int PQ = KIND == 0 ? 3 : NQ;   // partial rows per tile
   {  // level 1: this block's tiles -> slab s
@@ -195,7 +192,7 @@ __global__ __launch_bounds__(256) void bn_stats_kernel(const float* __restrict__
     const int col = g * CG + tid;
     if (tid < CG && col < C)
 #pragma unroll
-      for (int q = 0; q < NQ; ++q) st_wt(slabs + ((size_t)s * NQ + q) * C + col, red[q][tid]);
+      for (int q = 0; q < NQ; ++q) st_wt(slabs + ((size_t)s * NQ + q) * C + col, tot[q]);
   }
   // arrival: this block's slab stores landed (vmcnt(0) in every wave), then ONE release-ordered
   // arrival on the group counter (agent scope: the release fence before the add orders every
@@ -239,7 +236,7 @@ __global__ __launch_bounds__(256) void bn_stats_kernel(const float* __restrict__
   const int col = g * CG + tid;
   if (tid < CG && col < C) {
     if constexpr (KIND == 0) {
-      const double sx = red[0][tid], sxx = red[1][tid];
+      const double sx = tot[0], sxx = tot[1];
       if (o.tot) {
         o.tot[col] = sx;
         o.tot[C + col] = sxx;
@@ -261,11 +258,11 @@ __global__ __launch_bounds__(256) void bn_stats_kernel(const float* __restrict__
         }
       }
     } else {
-      const double count = o.count, gs = o.gscale, sdz = red[0][tid];
+      const double count = o.count, gs = o.gscale, sdz = tot[0];
 #pragma unroll
       for (int b = 0; b < NQ - 1; ++b) {   // constant member indices (no dynamic param indexing)
         const double mu = o.mean[b][col], is = o.invstd[b][col], ga = o.gamma[b][col];
-        const double sdzx = (red[1 + b][tid] - mu * sdz) * is;   // sum dz * xhat
+        const double sdzx = (tot[1 + b] - mu * sdz) * is;   // sum dz * xhat
         float* dg = o.dgamma[b];
         float* db = o.dbeta[b];
         dg[col] = (float)(sdzx * gs) + (o.accumulate ? dg[col] : 0.f);
