@@ -367,7 +367,9 @@ def _dp_pass(ctx: Ctx, args, dtype) -> dict:
                                     f" (resnet_dp.py)",
                        "dp_replicas_consistent": rec.get("replicas_consistent"),
                        "dp_loss": rec.get("loss"), "dp_max_mem_gb": rec.get("max_mem_gb"),
-                       "dp_gpu_util_pct": rec.get("gpu_util_pct"), "dp_vs_baseline": rec.get("vs_baseline")}
+                       "dp_gpu_util_pct": rec.get("gpu_util_pct"), "dp_vs_baseline": rec.get("vs_baseline"),
+                       "dp_exposed_comm_ms": rec.get("exposed_comm_ms"),
+                       "dp_segments": rec.get("dp_segments")}
         except subprocess.TimeoutExpired:
             res = {"dp_error": f"timeout after {limit:.0f} s"}
         finally:
@@ -421,6 +423,18 @@ def main():
     loss = tr.last_loss()
     nxt = args.warmup + args.steps
     diag = _diagnostics(ctx, tr, nxt) if ctx.multi else {}
+    if args.dp and getattr(tr.dp, "replicas", None):
+        # one more (untimed) step with HIP events at the end of backward and after the last
+        # gradient all-reduce (per-stage slices overlapped with the backward's later segments)
+        tr.dp.timing = True
+        tr.step(nxt)
+        for d in tr.dp.device_ids:
+            torch.cuda.synchronize(d)
+        tr.dp.timing = False
+        ex = tr.dp.exposed_comm_ms()
+        diag["exposed_comm_ms"] = None if ex is None else round(ex, 4)
+        diag["dp_segments"] = len(tr.dp._graphs[0].graphs)
+        nxt += 1
     if args.dp:   # every replica must hold bit-identical weights (the replicated fused SGD)
         try:
             tr.state_checksum()

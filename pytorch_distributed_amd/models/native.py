@@ -155,6 +155,9 @@ class NativeResNet(nn.Module):
         self._wbatch_env = os.environ.get("PDA_WGRAD_BATCH")
         self.set_wgrad_batch(self._wbatch_env or "0")
         self._keep: List[torch.Tensor] = []
+        # called on the main stream with the flat-gradient offset below which every gradient is
+        # final, after each residual block's backward (DataParallel splits its replica graphs there)
+        self.segment_hook: Optional[Callable[[int], None]] = None
         self.refresh_shadow()
 
     def set_wgrad_batch(self, mode: str) -> None:
@@ -381,6 +384,20 @@ class NativeResNet(nn.Module):
 
     def attach_reducer(self, reducer) -> None:
         self._reducer = reducer
+
+    def stage_bounds(self) -> List[int]:
+        """Flat-gradient offsets at which a stage's backward is complete (after layer4.0, layer3.0,
+        layer2.0: the gradient below each offset is final), in backward order."""
+        nblk = len(self.blocks)
+        return [self.block_bounds[nblk - bi] for bi, b in enumerate(self.blocks)
+                if bi > 0 and b.name.endswith(".0")][::-1]
+
+    def join_side(self) -> None:
+        """Make the current stream wait for everything queued on the weight-gradient stream
+        (pending batched weight gradients are launched first)."""
+        self._flush_wgrad()
+        if self._side is not None:
+            torch.cuda.current_stream(self.device).wait_stream(self._side)
 
     @torch.no_grad()
     def set_sync_bn(self, comm) -> None:
@@ -694,6 +711,8 @@ class NativeResNet(nn.Module):
                 self._flush_wgrad()
             if red is not None:
                 self._grads_ready(red, self.block_bounds[nblk - bi])
+            if self.segment_hook is not None:
+                self.segment_hook(self.block_bounds[nblk - bi])
         # ---- stem: maxpool backward of (main + shortcut) gradients, BN backward, wgrad
         x0, y0, arg = sv["x0"], sv["y0"], sv["arg"]
         st0 = sv["stem_stats"]

@@ -13,11 +13,14 @@ statistics follow replica 0) but is built for a fully connected xGMI node:
 
 * replicas are *persistent*. For the native engine each GPU holds a full
   :class:`~pytorch_distributed_amd.models.native.NativeResNet` (flat buffers);
-* after backward the flat gradients are SUM-all-reduced across the local GPUs by
-  ONE grouped in-process RCCL collective (``ncclCommInitAll`` communicator,
-  :class:`~pytorch_distributed_amd.parallel.rccl.RcclGroup`), and every replica
-  runs the fused SGD itself (replicated update: mathematically identical to
-  reduce-to-GPU0 + step + broadcast, with no per-step weight broadcast);
+* the flat gradients are SUM-all-reduced across the local GPUs by grouped
+  in-process RCCL collectives (``ncclCommInitAll`` communicator,
+  :class:`~pytorch_distributed_amd.parallel.rccl.RcclGroup`) -- with the
+  graph-replayed step, one per stage slice of the flat gradient on per-device
+  comm streams, overlapped with the replay of the next backward segment
+  (``PDA_DP_SEGMENTS``) -- and every replica runs the fused SGD itself
+  (replicated update: mathematically identical to reduce-to-GPU0 + step +
+  broadcast, with no per-step weight broadcast);
 * BN buffers (213 KB) are broadcast from replica 0 before each training forward,
   which is what torch's per-step ``replicate`` achieves for them.
 
@@ -27,7 +30,9 @@ reduction into replica 0 after backward -- the same math as ``nn.DataParallel``.
 """
 from __future__ import annotations
 
+import contextlib
 import copy
+import os
 from typing import List, Optional, Sequence
 
 import torch
@@ -181,18 +186,27 @@ class DataParallel(nn.Module):
                 t.copy_(s, non_blocking=True)
 
     @torch.no_grad()
+    def _reduce_slice(self, lo: int, hi: int, streams=None) -> None:
+        """SUM-all-reduce ``flat_grad[lo:hi]`` over the replicas, on ``streams`` (one per replica;
+        default: the devices' current streams)."""
+        ts = [m.flat_grad[lo:hi] for m in self.all_modules]
+        if self.group is not None:
+            self.group.all_reduce(ts, streams=streams)
+            return
+        # replicas sharing a device (tests): plain copies, on replica 0's stream
+        ctx = torch.cuda.stream(streams[0]) if streams is not None else contextlib.nullcontext()
+        with ctx:
+            total = ts[0].clone()
+            for t in ts[1:]:
+                total.add_(t.to(total.device))
+            for t in ts:
+                t.copy_(total, non_blocking=True)
+
+    @torch.no_grad()
     def _reduce_grads(self) -> None:
         self._armed = False
         if self._native:
-            ts = [m.flat_grad for m in self.all_modules]
-            if self.group is not None:
-                self.group.all_reduce(ts)
-            else:
-                total = ts[0].clone()
-                for t in ts[1:]:
-                    total.add_(t.to(total.device))
-                for t in ts:
-                    t.copy_(total, non_blocking=True)
+            self._reduce_slice(0, self.module.numel)
             for m in self.all_modules:
                 m._grads_zero = False
             return
@@ -256,7 +270,8 @@ class DataParallel(nn.Module):
         launch-bound; see ``tools/host_overhead.py``). Same math as ``crit(dp(x), y).backward();
         optimizer.step()``: the loss is the mean over the GLOBAL batch (each replica's gradient
         is scaled by 1/B_global), BN statistics are per replica, BN buffers follow replica 0,
-        gradients are SUM-all-reduced by one grouped RCCL call, then the replicated fused SGD."""
+        gradients are SUM-all-reduced by grouped RCCL calls (one per stage slice, overlapped with
+        the rest of the backward: :meth:`_replay_overlapped`), then the replicated fused SGD."""
         xs = torch.chunk(samples, len(self.device_ids), 0)
         ys = torch.chunk(labels, len(self.device_ids), 0)
         return self.train_step_chunks(xs, ys, optimizer, graph)
@@ -267,31 +282,87 @@ class DataParallel(nn.Module):
         self._broadcast_state()
         B = sum(x.shape[0] for x in xs)
         if getattr(self, "_graphs", None) is None or [x.shape for x in xs] != self._graph_shapes:
-            self._graphs = [_ReplicaGraph(m, x.shape, B) for m, x in zip(self.all_modules, xs)]
+            splits = self._segment_bounds()
+            self._graphs = [_ReplicaGraph(m, x.shape, B, splits) for m, x in zip(self.all_modules, xs)]
             self._graph_shapes = [x.shape for x in xs]
         jobs = list(zip(self._graphs, xs, ys))
-        import os
-        if (graph and len(jobs) > 1 and all(rg.graph is not None for rg in self._graphs)
-                and os.environ.get("PDA_DP_THREADS", "1") != "0"):
-            # one host thread per device: hipGraphLaunch of a ~500-node step costs ~2 ms of host
-            # time, and CUDAGraph.replay releases the GIL, so N replicas enqueue concurrently
-            # instead of staggering device i's start by i x 2 ms (captures stay on this thread)
-            streams = [torch.cuda.current_stream(rg.dev) for rg in self._graphs]
-            list(self._pool().map(lambda j: j[0][0].run(j[0][1], j[0][2], True, j[1]),
-                                  zip(jobs, streams)))
+        streams = [torch.cuda.current_stream(rg.dev) for rg in self._graphs]
+        replay = graph and all(rg.graphs for rg in self._graphs)
+        if replay and self.replicas:
+            self._replay_overlapped(jobs, streams)
         else:
             for rg, x, y in jobs:
                 rg.run(x, y, graph)
-        if self.replicas:
-            self._reduce_grads()
-        else:
-            self.module._grads_zero = False
+            if self.replicas:
+                self._reduce_grads()
+            else:
+                self.module._grads_zero = False
         optimizer.step()
         dev0 = torch.device("cuda", self.output_device)
         loss = torch.zeros((), dtype=torch.float32, device=dev0)
         for rg, x in zip(self._graphs, xs):
             loss += rg.loss.to(dev0, non_blocking=True) * (x.shape[0] / B)
         return loss
+
+    def _segment_bounds(self) -> List[int]:
+        """Where each replica graph is split (``PDA_DP_SEGMENTS``): "stage" (default) after the
+        backward of layer4, layer3 and layer2 -- the fc+layer4 slice (~68 MB of the 102 MB f32
+        gradient of ResNet-50) is all-reduced while layer3..1 run backward, the exposed tail is
+        the ~1 MB layer1+stem slice; "0": one graph, one all-reduce after backward."""
+        mode = os.environ.get("PDA_DP_SEGMENTS", "stage")
+        if mode not in ("stage", "0"):
+            raise ValueError(f"PDA_DP_SEGMENTS={mode!r}: expected stage or 0")
+        if mode == "0" or not self.replicas or not hasattr(self.module, "stage_bounds"):
+            return []
+        return self.module.stage_bounds()
+
+    def _comm_streams(self):
+        if getattr(self, "_cstreams", None) is None:
+            self._cstreams = [torch.cuda.Stream(torch.device("cuda", d)) for d in self.device_ids]
+        return self._cstreams
+
+    def _replay_overlapped(self, jobs, streams) -> None:
+        """Replay segment s of every replica, then all-reduce the gradient slice it completed on
+        per-device comm streams while segment s+1 replays; the replicas' streams join the comm
+        streams before the optimizer step. ``self.timing``: HIP events at the end of backward and
+        after the last all-reduce (``exposed_comm_ms``)."""
+        cs = self._comm_streams()
+        nseg = len(jobs[0][0].graphs)
+        bounds = [0] + jobs[0][0].splits + [self.module.numel]
+        threaded = len(jobs) > 1 and os.environ.get("PDA_DP_THREADS", "1") != "0"
+        timing = getattr(self, "timing", False)
+        for s in range(nseg):
+            if threaded:
+                # one host thread per device: hipGraphLaunch of a ~150-node segment costs ~0.5 ms
+                # of host time and CUDAGraph.replay releases the GIL, so the N replicas enqueue
+                # concurrently instead of staggering device i's start by i launches
+                list(self._pool().map(lambda a: a[0][0].replay(s, a[0][1], a[0][2], a[1]),
+                                      zip(jobs, streams)))
+            else:
+                for (rg, x, y), st in zip(jobs, streams):
+                    rg.replay(s, x, y, st)
+            if timing and s == nseg - 1:
+                self._ev_bwd = [torch.cuda.Event(enable_timing=True) for _ in streams]
+                for e, st in zip(self._ev_bwd, streams):
+                    e.record(st)
+            for c, st in zip(cs, streams):
+                c.wait_stream(st)
+            self._reduce_slice(bounds[s], bounds[s + 1], streams=cs)
+        if timing:
+            self._ev_comm = [torch.cuda.Event(enable_timing=True) for _ in cs]
+            for e, c in zip(self._ev_comm, cs):
+                e.record(c)
+        for c, st in zip(cs, streams):
+            st.wait_stream(c)
+        for m in self.all_modules:
+            m._grads_zero = False
+
+    def exposed_comm_ms(self) -> Optional[float]:
+        """After a step with ``timing = True`` has completed: max over devices of (last gradient
+        all-reduce done - backward done)."""
+        if getattr(self, "_ev_comm", None) is None:
+            return None
+        return max(b.elapsed_time(c) for b, c in zip(self._ev_bwd, self._ev_comm))
 
     def _pool(self):
         if getattr(self, "_executor", None) is None:
@@ -308,18 +379,43 @@ class DataParallel(nn.Module):
 
 
 class _ReplicaGraph:
-    """forward + CE loss/gradient + backward of one native replica, captured in a HIP graph on
-    the replica's device; inputs are copied into static buffers before each replay."""
+    """forward + CE loss/gradient + backward of one native replica, captured as HIP graphs on the
+    replica's device; inputs are copied into static buffers before each replay.
 
-    def __init__(self, m, shape, global_batch: int) -> None:
+    ``splits`` (flat-gradient offsets, ``NativeResNet.stage_bounds``): the capture ends and a new
+    graph (same memory pool, replayed in capture order) begins when the backward has finished the
+    gradient below each offset -- after joining the weight-gradient stream, so every kernel
+    writing that slice is inside the ended segment. Between segment replays DataParallel
+    all-reduces the completed slice on a comm stream."""
+
+    def __init__(self, m, shape, global_batch: int, splits: Sequence[int] = ()) -> None:
         self.m = m
         self.dev = m.device
         self.gscale = 1.0 / global_batch
+        self.splits = list(splits)
         with torch.cuda.device(self.dev):
             self.x = torch.empty(shape, dtype=m.dtype, device=self.dev)
             self.y = torch.empty(shape[0], dtype=torch.int64, device=self.dev)
-        self.graph = None
+        self.graphs: List[torch.cuda.CUDAGraph] = []
         self.loss = None
+        self._capturing = False
+
+    @property
+    def graph(self):
+        return self.graphs[0] if self.graphs else None
+
+    def _split(self, upto: int) -> None:
+        """NativeResNet.segment_hook: at a split offset join the weight-gradient stream (eager and
+        captured schedules alike) and, while capturing, start the next segment's graph."""
+        if upto not in self.splits:
+            return
+        self.m.join_side()
+        if self._capturing:
+            g0 = self.graphs[-1]
+            g0.capture_end()
+            g = torch.cuda.CUDAGraph()
+            g.capture_begin(pool=self.graphs[0].pool())
+            self.graphs.append(g)
 
     def _body(self) -> None:
         from ..ops import native_ops as K
@@ -331,25 +427,40 @@ class _ReplicaGraph:
         dlog16 = torch.empty(B, m.fc_rows, dtype=m.dtype, device=self.dev)
         K.xent(logits, self.y, rows, loss, dlog=dlog16, gscale=self.gscale)
         m._grads_zero = True          # every step overwrites the flat gradient
-        m.native_backward(dlog16)
+        m.segment_hook = self._split if self.splits else None
+        try:
+            m.native_backward(dlog16)
+        finally:
+            m.segment_hook = None
         self.loss = loss
+
+    def replay(self, s: int, x: torch.Tensor, y: torch.Tensor,
+               stream: Optional[torch.cuda.Stream] = None) -> None:
+        """Replay segment ``s`` on ``stream`` (the caller's current stream on this device: a
+        worker thread's own current stream is the default stream); segment 0 first takes the
+        inputs."""
+        with torch.cuda.device(self.dev), torch.cuda.stream(stream or torch.cuda.current_stream(self.dev)):
+            if s == 0:
+                self.x.copy_(x, non_blocking=True)
+                self.y.copy_(y, non_blocking=True)
+            self.graphs[s].replay()
+            self.loss = self._graph_loss
 
     def run(self, x: torch.Tensor, y: torch.Tensor, graph: bool = True,
             stream: Optional[torch.cuda.Stream] = None) -> None:
-        """``stream``: the caller's current stream on this device. A worker thread's current
-        stream is its own (the default stream), so a replay issued from the DataParallel thread
-        pool runs on the caller's stream explicitly and stays ordered with the input production
-        before it and the gradient reduction / optimizer step after it."""
+        """The whole step: eagerly (``graph=False``), by replaying every segment, or -- the first
+        time -- eagerly for this batch and then captured for the next replays."""
+        if graph and self.graphs:
+            for s in range(len(self.graphs)):
+                self.replay(s, x, y, stream)
+            return
         with torch.cuda.device(self.dev), torch.cuda.stream(stream or torch.cuda.current_stream(self.dev)):
             self.x.copy_(x, non_blocking=True)
             self.y.copy_(y, non_blocking=True)
             if not graph:                  # same schedule, launched eagerly (tests / debugging)
                 self._body()
                 return
-            if self.graph is not None:
-                self.graph.replay()
-                self.loss = self._graph_loss
-                return
+            import gc
             cur = torch.cuda.current_stream(self.dev)
             side = torch.cuda.Stream(self.dev)
             side.wait_stream(cur)
@@ -358,8 +469,25 @@ class _ReplicaGraph:
                     self._body()               # the real step for this batch (also sizes workspaces)
                 cur.wait_stream(side)
                 eager = self.loss
-                g = torch.cuda.CUDAGraph()
-                with torch.cuda.graph(g):
-                    self._body()
-            self.graph = g
+                # what torch.cuda.graph does on entry, with capture_begin / capture_end by hand so
+                # the backward can end one segment's graph and begin the next
+                torch.cuda.synchronize(self.dev)
+                gc.collect()
+                torch.cuda.empty_cache()
+                cap = torch.cuda.Stream(self.dev)
+                cap.wait_stream(cur)
+                with torch.cuda.stream(cap):
+                    g = torch.cuda.CUDAGraph()
+                    self.graphs = [g]
+                    self._capturing = True
+                    try:
+                        g.capture_begin()
+                        self._body()
+                        self.graphs[-1].capture_end()
+                    except BaseException:
+                        self.graphs = []
+                        raise
+                    finally:
+                        self._capturing = False
+                cur.wait_stream(cap)
             self._graph_loss, self.loss = self.loss, eager

@@ -357,16 +357,24 @@ class RcclGroup:
         self._h = C.c_void_p()
         _check(lib.pda_comm_init_all(arr, n, C.byref(self._h)), "init_all")
 
-    def _streams(self):
+    def _streams(self, streams=None):
         n = len(self.devices)
-        return (C.c_void_p * n)(*[torch.cuda.current_stream(d).cuda_stream for d in self.devices])
+        if streams is None:
+            streams = [torch.cuda.current_stream(d) for d in self.devices]
+        if len(streams) != n:
+            raise ValueError(f"{len(streams)} streams for a group of {n} devices")
+        return (C.c_void_p * n)(*[s.cuda_stream for s in streams])
 
     def _bufs(self, ts: List[torch.Tensor]):
+        if len(ts) != len(self.devices) or len({t.numel() for t in ts}) != 1:
+            raise ValueError("one tensor of equal size per device of the group")
         return (C.c_void_p * len(ts))(*[t.data_ptr() for t in ts])
 
-    def all_reduce(self, ts: List[torch.Tensor], op: str = "sum") -> None:
+    def all_reduce(self, ts: List[torch.Tensor], op: str = "sum", streams=None) -> None:
+        """Grouped all-reduce, one tensor per device, enqueued on ``streams`` (default: each
+        device's current stream)."""
         _check(load().pda_group_allreduce(self._h, self._bufs(ts), ts[0].numel(), _DT[ts[0].dtype],
-                                          _OPS[op], self._streams()), "group_allreduce")
+                                          _OPS[op], self._streams(streams)), "group_allreduce")
 
     def broadcast(self, ts: List[torch.Tensor], root: int = 0) -> None:
         _check(load().pda_group_broadcast(self._h, self._bufs(ts), ts[0].numel(), _DT[ts[0].dtype],

@@ -43,10 +43,14 @@ def test_native_dataparallel_matches_single_model():
     assert torch.equal(dp.module.flat_params, dp.replicas[0].flat_params)
 
 
-def test_native_dataparallel_graph_step_matches_eager():
+@pytest.mark.parametrize("segments", ["stage", "0"])
+def test_native_dataparallel_graph_step_matches_eager(segments, monkeypatch):
     """train_step replayed from per-replica HIP graphs == the same schedule launched eagerly (bit
     for bit, 4 steps incl. SGD), and its first step == crit(dp(x), y).backward() (autograd DP with
-    ATen's cross-entropy: equal up to the 16-bit rounding of dlogits)."""
+    ATen's cross-entropy: equal up to the 16-bit rounding of dlogits). ``stage``: each replica's
+    graph is split after layer4 / layer3 / layer2 and the completed gradient slice is reduced on a
+    comm stream while the next segment replays (4 segments, 4 reductions)."""
+    monkeypatch.setenv("PDA_DP_SEGMENTS", segments)
     from pytorch_distributed_amd.data import SyntheticImageNet
     from pytorch_distributed_amd.models import build_model
     from pytorch_distributed_amd.models.native import NativeResNet
@@ -71,6 +75,7 @@ def test_native_dataparallel_graph_step_matches_eager():
     og = graphed.make_optimizer(lr=0.05, momentum=0.9, weight_decay=1e-4)
     for step in range(4):
         x, y = gen(torch.arange(16) + 16 * step)
+        graphed.timing = step == 3
         le = eager.train_step(x, y, oe, graph=False)
         lg = graphed.train_step(x, y, og)
         torch.cuda.synchronize()
@@ -85,6 +90,10 @@ def test_native_dataparallel_graph_step_matches_eager():
         assert torch.equal(graphed.module.flat_params, graphed.replicas[0].flat_params)
         assert torch.equal(eager.module.flat_buffers, graphed.module.flat_buffers)
     assert graphed._graphs[0].graph is not None and eager._graphs[0].graph is None
+    assert len(graphed._graphs[0].graphs) == (4 if segments == "stage" else 1)
+    assert len(graphed._graphs[0].splits) == len(graphed._graphs[0].graphs) - 1
+    ex = graphed.exposed_comm_ms()
+    assert ex is not None and 0.0 <= ex < 1000.0, ex
 
 
 def test_native_dataparallel_resume_reloads_every_replica():
