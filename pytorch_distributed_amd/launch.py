@@ -133,6 +133,7 @@ def spawn(fn: Callable, args: tuple = (), nprocs: Optional[int] = None, bind_num
     if "MASTER_PORT" not in os.environ:
         os.environ["MASTER_PORT"] = str(free_port())
     os.environ.setdefault("MASTER_IP", os.environ.get("MASTER_ADDR", "127.0.0.1"))
+    bind_numa = bind_numa and os.environ.get("PDA_BIND_NUMA", "1") != "0"
     if nprocs == 1:
         _child(0, fn, args, bind_numa)
         return None

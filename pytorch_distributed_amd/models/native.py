@@ -158,6 +158,9 @@ class NativeResNet(nn.Module):
         # called on the main stream with the flat-gradient offset below which every gradient is
         # final, after each residual block's backward (DataParallel splits its replica graphs there)
         self.segment_hook: Optional[Callable[[int], None]] = None
+        # diagnostics (tools/layer_times.py): called on the main stream as probe(phase, name) after
+        # the stem and after each residual block, forward and backward
+        self.probe: Optional[Callable[[str, str], None]] = None
         self.refresh_shadow()
 
     def set_wgrad_batch(self, mode: str) -> None:
@@ -542,6 +545,8 @@ class NativeResNet(nn.Module):
         arg = torch.empty(Nb, ph, ph, self.stem.cout, dtype=torch.uint8, device=self.device)
         sc, sh = self._coeffs(self.stem, train)
         K.stem_pool(y0, sc, sh, p, arg)
+        if self.probe is not None:
+            self.probe("fwd", "stem")
         if save:
             saved["y0"], saved["arg"] = y0, arg
             saved["stem_stats"] = self.stem.state
@@ -613,6 +618,8 @@ class NativeResNet(nn.Module):
                 rec["ys"], rec["acts"], rec["yd"] = ys, acts, yd
                 saved["blocks"].append(rec)
             h = out
+            if self.probe is not None:
+                self.probe("fwd", b.name)
         logits = torch.empty(Nb, self.num_classes, dtype=torch.float32, device=self.device)
         g = ConvGeom(Nb, 1, 1, self.feat_dim, self.num_classes, 1, 1, 1, 0)
         K.conv_fwd(feat, self.fc_w16, g, logits,
@@ -713,6 +720,8 @@ class NativeResNet(nn.Module):
                 self._grads_ready(red, self.block_bounds[nblk - bi])
             if self.segment_hook is not None:
                 self.segment_hook(self.block_bounds[nblk - bi])
+            if self.probe is not None:
+                self.probe("bwd", b.name)
         # ---- stem: maxpool backward of (main + shortcut) gradients, BN backward, wgrad
         x0, y0, arg = sv["x0"], sv["y0"], sv["arg"]
         st0 = sv["stem_stats"]

@@ -139,9 +139,12 @@ def train(dataloader, model, criterion, optimizer, scheduler, epoch: int, ctx: C
     prof = StepProfiler(int(os.environ.get("MX_PROFILE", "0") or 0) if epoch == 0 else 0, save_path,
                         ctx.rank)
     graphed = _graphed_step(model, optimizer, ctx)
+    sb = ctx.extra.get("step_busy")     # device-busy fallback (utils/gpu_util.py StepBusy)
     for step, (samples, labels) in dataloader.iter_from(start_step):
         if ctx.cfg.script == "single" and cfg.log_every and step % cfg.log_every == 0:
             print("epoch: {}, step: {}".format(epoch, step), flush=True)
+        if sb is not None:
+            sb.begin()
         samples = samples.to(ctx.device, non_blocking=True)
         labels = labels.to(ctx.device, non_blocking=True)
         if graphed is not None and graphed.accepts(samples):
@@ -164,6 +167,8 @@ def train(dataloader, model, criterion, optimizer, scheduler, epoch: int, ctx: C
             loss = criterion(outputs.float() if outputs.dtype != torch.float32 else outputs, labels)
             loss.backward()
             optimizer.step()
+        if sb is not None:
+            sb.end()
         _sync_step(ctx)
         steps += 1
         prof.step()
@@ -349,14 +354,20 @@ def run(cfg: RunConfig, mode: str, local_rank: int = 0, nprocs: Optional[int] = 
         t1 = time.time()
         if train_sampler is not None:
             train_sampler.set_epoch(epoch)
-        from .utils.gpu_util import BusySampler
+        from .utils.gpu_util import BusySampler, StepBusy, busy_path
         devs = ([ctx.device.index if ctx.device.index is not None else torch.cuda.current_device()]
                 if ctx.device.type == "cuda" else [])
         if hasattr(model, "device_ids"):     # DataParallel: every replica's device
             devs = list(model.device_ids)
-        with BusySampler(devs) as busy:       # the reference's "Avg GPU Util" panel (README:33-40)
+        # where the driver's sysfs counter is unreadable (containers), HIP events around the steps
+        sbusy = StepBusy(torch.device("cuda", devs[0]) if devs else None)
+        ctx.extra["step_busy"] = sbusy if not any(busy_path(d) is not None for d in devs) else None
+        with BusySampler(devs) as busy, sbusy:   # the reference's "Avg GPU Util" panel (README:33-40)
             steps = train(train_loader, model, criterion, optimizer, scheduler, epoch, ctx,
                           start_step, best_acc, save_path)
+        util, util_method = busy.overall(), "sysfs gpu_busy_percent"
+        if util is None:
+            util, util_method = sbusy.overall(), "step intervals (HIP events) / wall time"
         start_step = 0
         scheduler.step()
         acc = validate(val_loader, model, criterion, epoch, ctx)
@@ -367,7 +378,7 @@ def run(cfg: RunConfig, mode: str, local_rank: int = 0, nprocs: Optional[int] = 
             print("cost time per epoch: {:.4f} s".format(t2 - t1), flush=True)
             ctx.metrics.write(epoch=epoch, steps=steps, epoch_s=t2 - t1, acc1=acc,
                               images=steps * per_rank_batch * ctx.world, gpu_mem_gb=gpu_mem_gb(),
-                              gpu_util_pct=busy.overall(),
+                              gpu_util_pct=util, gpu_util_method=util_method if util is not None else None,
                               engine=engine, dtype=str(dtype))
             if acc > best_acc:
                 best_acc = acc

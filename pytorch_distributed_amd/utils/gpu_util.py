@@ -14,7 +14,7 @@ from typing import Dict, List, Optional, Sequence
 
 from ..launch import gpu_pci_bdf
 
-__all__ = ["BusySampler", "busy_path", "kernel_busy"]
+__all__ = ["BusySampler", "StepBusy", "busy_path", "kernel_busy"]
 
 
 def busy_path(index: int) -> Optional[str]:
@@ -66,6 +66,63 @@ class BusySampler:
     def overall(self) -> Optional[float]:
         v = [x for x in self.mean().values() if x is not None]
         return round(sum(v) / len(v), 1) if v else None
+
+
+class StepBusy:
+    """Device-busy % where the sysfs counter is not readable: HIP events on the compute stream at
+    the start and end of every training step (``begin`` / ``end``), read after the step's
+    synchronize, summed over the region and divided by its wall time. The trainer synchronises
+    after every step (as the reference), so the intervals do not overlap and the remainder is the
+    time the device waits for the host; within a step the kernels keep the device busy (98.6 % by
+    the kernel-interval union, ``bench.py``), so this slightly over-counts, never under."""
+
+    def __init__(self, device) -> None:
+        import torch
+        self.on = device is not None and device.type == "cuda"
+        self.device = device
+        self._t = torch
+        self.dev_ms = 0.0
+        self.wall_s = 0.0
+        self._pending = []
+        self._e0 = None
+
+    def __enter__(self) -> "StepBusy":
+        self._w0 = time.perf_counter()
+        return self
+
+    def __exit__(self, *exc) -> None:
+        if self.on:
+            self._t.cuda.synchronize(self.device)
+            self._collect()
+        self.wall_s += time.perf_counter() - self._w0
+
+    def begin(self) -> None:
+        if self.on:
+            self._e0 = self._t.cuda.Event(enable_timing=True)
+            self._e0.record(self._t.cuda.current_stream(self.device))
+
+    def end(self) -> None:
+        if self.on and self._e0 is not None:
+            e1 = self._t.cuda.Event(enable_timing=True)
+            e1.record(self._t.cuda.current_stream(self.device))
+            self._pending.append((self._e0, e1))
+            self._e0 = None
+            if len(self._pending) > 64:
+                self._collect()
+
+    def _collect(self) -> None:
+        keep = []
+        for a, b in self._pending:
+            if b.query():
+                self.dev_ms += a.elapsed_time(b)
+            else:
+                keep.append((a, b))
+        self._pending = keep
+
+    def overall(self) -> Optional[float]:
+        if not self.on or self.wall_s <= 0 or self.dev_ms <= 0:
+            return None
+        return round(min(100.0, 100.0 * self.dev_ms / (1e3 * self.wall_s)), 1)
 
 
 def kernel_busy(step_fn, steps: int, devices: Sequence[int]) -> Dict[int, Optional[float]]:

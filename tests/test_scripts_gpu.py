@@ -38,6 +38,12 @@ def test_entrypoint_native(tmp_path, script, outdir):
     assert '"engine": "native"' in m
     if script == "resnet_ddp_apex.py":
         assert "float16" in m
+    # the reference's three report panels per epoch: time, avg GPU util, GPU memory
+    import json
+    for line in m.strip().splitlines():
+        rec = json.loads(line)
+        assert rec["epoch_s"] > 0 and rec["gpu_mem_gb"] > 0
+        assert rec["gpu_util_pct"] is not None and 0 < rec["gpu_util_pct"] <= 100, rec
 
 
 def test_suspend_resume_native(tmp_path):
