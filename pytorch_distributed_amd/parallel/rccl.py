@@ -2,7 +2,7 @@
 
 Multi-process: the ``ncclUniqueId`` of rank 0 is exchanged through the default
 ``torch.distributed`` TCPStore, then every rank runs ``ncclCommInitRank``.
-Collectives run on a dedicated high-priority HIP stream: ``all_reduce_async``
+Collectives run on a dedicated HIP stream (default priority, see ``__init__``): ``all_reduce_async``
 records an event on the compute stream, makes the comm stream wait on it,
 enqueues ``ncclAllReduce`` and returns a completion event; ``wait`` makes the
 *current* stream wait on that event (the host never blocks). This is how DDP
@@ -114,7 +114,12 @@ class RcclCommunicator(Communicator):
             uid = store.get(key)
         self._h = C.c_void_p()
         self._init_rank(lib, uid)
-        self.stream = torch.cuda.Stream(self.device, priority=-1)
+        # default priority: a high-priority comm stream (priority -1) made every DDP step 13-15 ms
+        # slower at the image's GPU_MAX_HW_QUEUES=4 (28.8 -> 43.3 ms/step, ResNet-50 bs 400; fine
+        # at 3, 6 or 8 queues, 32.0 at 5): the HIP runtime's queue mapping for a second priority
+        # level, not the collectives, cost it (tools/ddp_sync_diag.py, profiles/ddp_overhead_r3.md).
+        # PDA_COMM_PRIO=-1 restores the high-priority stream for A/B runs.
+        self.stream = torch.cuda.Stream(self.device, priority=int(os.environ.get("PDA_COMM_PRIO", "0")))
         self._watchdog_error = None
         self._watchdog = None
         self._watchdog_stop = None

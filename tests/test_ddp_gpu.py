@@ -284,3 +284,23 @@ def test_native_ddp_sync_batchnorm_two_ranks():
         assert err_sync < 1e-4, (rank, err_sync, err_half, err_rm, segs)
         assert err_half > 20 * err_sync, (rank, err_sync, err_half)
         assert err_rm < 1e-5, (rank, err_rm)
+
+
+def test_ddp_step_costs_no_more_than_bare_step(tmp_path):
+    """Each rank's DDP step (native RCCL communicator, C++ bucket reducer, torch's own NCCL
+    communicator NOT created -- the bench / trainer configuration) must cost about what the bare
+    native step costs. A high-priority comm stream made it +13-15 ms (28.8 -> 43.3 ms per
+    ResNet-50 step at GPU_MAX_HW_QUEUES=4; profiles/ddp_overhead_r3.md): checked in a fresh process
+    so no earlier HIP stream or communicator changes the queue mapping."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, os.path.join(root, "tools", "ddp_sync_diag.py"), "--steps", "8",
+                        "--port", str(_port())], capture_output=True, text=True, timeout=300,
+                       env={**os.environ, "PYTHONPATH": root})
+    assert r.returncode == 0, r.stderr[-3000:]
+    res = {l.split(" ", 1)[0]: json.loads(l.split(" ", 1)[1]) for l in r.stdout.splitlines()
+           if l.startswith(("bare_", "ddp_"))}
+    bare, ddp = res["bare_nosync"]["ms"], res["ddp_nosync"]["ms"]
+    assert ddp < 1.1 * bare + 1.0, res

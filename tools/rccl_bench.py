@@ -38,6 +38,10 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--max-mb", type=float, default=128)
     ap.add_argument("--reps", type=int, default=20)
+    ap.add_argument("--op", default="sum", choices=["sum", "avg"])
+    ap.add_argument("--backend", default="gloo", help="torch.distributed backend of the rendezvous")
+    ap.add_argument("--device-id", action="store_true",
+                    help="pass device_id: torch creates ITS NCCL communicator eagerly (nccl backend)")
     a = ap.parse_args()
     rank = int(os.environ.get("RANK", 0))
     world = int(os.environ.get("WORLD_SIZE", 1))
@@ -47,7 +51,8 @@ def main():
     if world == 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         os.environ.setdefault("MASTER_PORT", "29681")
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    kw = {"device_id": dev} if a.device_id else {}
+    dist.init_process_group(a.backend, rank=rank, world_size=world, **kw)
     from pytorch_distributed_amd.parallel.rccl import RcclCommunicator, RcclGroup
     comm = RcclCommunicator(dev)
     sizes = []
@@ -61,12 +66,12 @@ def main():
         for nbytes in sizes:
             t = buf[:nbytes // 4]
             for _ in range(3):
-                comm.all_reduce(t)
-            ms = timeit(lambda: comm.all_reduce(t), comm.stream, a.reps)
+                comm.all_reduce(t, op=a.op)
+            ms = timeit(lambda: comm.all_reduce(t, op=a.op), comm.stream, a.reps)
             # bus bandwidth convention: 2 (n-1)/n S / t; at world 1 the algorithm bandwidth S / t
             algbw = nbytes / (ms * 1e-3) / 1e9
             busbw = algbw * (2 * (world - 1) / world if world > 1 else 1.0)
-            rows.append({"op": "allreduce", "bytes": nbytes, "us": round(ms * 1e3, 2),
+            rows.append({"op": f"allreduce_{a.op}", "bytes": nbytes, "us": round(ms * 1e3, 2),
                          "algbw_GBs": round(algbw, 1), "busbw_GBs": round(busbw, 1)})
     if world == 1:
         grp = RcclGroup([local])
@@ -79,7 +84,7 @@ def main():
                          "algbw_GBs": round(nbytes / (ms * 1e-3) / 1e9, 1)})
         grp.close()
     # alpha / beta fit on the all-reduce rows: t = alpha + S / bw (least squares over the sizes)
-    ar = [r for r in rows if r["op"] == "allreduce"]
+    ar = [r for r in rows if r["op"].startswith("allreduce")]
     xs = [r["bytes"] for r in ar]
     ys = [r["us"] for r in ar]
     n = len(xs)
