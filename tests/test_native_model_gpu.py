@@ -326,3 +326,31 @@ def test_amp_overflow_skips_step_on_device():
     assert scaler.found_inf.item() == 0.0
     assert not torch.equal(nm.flat_params, p0)
     assert scaler.get_scale() == 2048.0 and scaler._growth_tracker.item() == 0
+
+
+def test_probe_and_segment_hooks_fire_per_block_and_change_nothing():
+    """The diagnostics probe (tools/layer_times.py) fires after the stem and after every residual
+    block in the forward and again per block in the backward; the DataParallel segment hook sees
+    exactly the stage bounds among the block bounds; neither changes the gradient (bitwise)."""
+    _, nm = _pair("resnet50", image=64)
+    from pytorch_distributed_amd.data import SyntheticImageNet
+    gen = nm.input_generator(SyntheticImageNet("train", image_size=64))
+    x, y = gen(torch.arange(8))
+    crit = nm.make_criterion()
+    nm.zero_grad_flat()
+    crit(nm(x), y).backward()
+    torch.cuda.synchronize()
+    g0 = nm.flat_grad.clone()
+    calls, bounds = [], []
+    nm.probe = lambda phase, name: calls.append((phase, name))
+    nm.segment_hook = bounds.append
+    nm.zero_grad_flat()
+    crit(nm(x), y).backward()
+    torch.cuda.synchronize()
+    nm.probe = nm.segment_hook = None
+    names = [b.name for b in nm.blocks]
+    assert calls == [("fwd", "stem")] + [("fwd", n) for n in names] + [("bwd", n) for n in reversed(names)]
+    assert bounds == nm.block_bounds[1:len(names) + 1]
+    sb = nm.stage_bounds()
+    assert len(sb) == 3 and all(b in bounds for b in sb) and sb == sorted(sb)
+    assert torch.equal(nm.flat_grad, g0)

@@ -1,0 +1,58 @@
+"""Stem (4x4/1 space-to-depth conv, M = B*112*112, N = 64, K = 256) forward with every register
+tile, with the BN-statistics epilogue as in the step; median of 5 interleaved rounds x 5 reps (us).
+Usage (GPU box): python tools/stem_bench.py"""
+import math
+import os
+import statistics
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from pytorch_distributed_amd.ops import ext  # noqa: E402
+from pytorch_distributed_amd.ops import native_ops as K  # noqa: E402
+
+
+def main():
+    ext.load(required=True)
+    B = 400
+    dev = torch.device("cuda", 0)
+    g = K.stem_s2d_geom(B, 224)
+    x = (torch.randn(B, 112, 112, 16, device=dev) * 0.5).to(torch.bfloat16)
+    w = (torch.randn(64, 256, device=dev) * 0.05).to(torch.bfloat16)
+    y = torch.empty(B, g.Ho, g.Wo, 64, device=dev, dtype=torch.bfloat16)
+    M = B * g.Ho * g.Wo
+    stats = torch.empty(math.ceil(M / 64) * 3 * 64, device=dev)
+    tiles = [(-128, 64), (128, 64), (64, 64), (-64, 64), (-128, 128), (64, 128), (-64, 128)]
+    ref = None
+    times = {t: [] for t in tiles}
+    ok = {}
+    for t in tiles:
+        try:
+            K.conv_fwd(x, w, g, y, stats=stats, tile=t)
+            torch.cuda.synchronize()
+            if ref is None:
+                ref = y.clone()
+            ok[t] = torch.equal(y, ref) or (y.float() - ref.float()).abs().max().item() < 1e-2
+        except Exception as e:  # noqa: BLE001
+            ok[t] = f"err {e}"[:80]
+    tiles = [t for t in tiles if ok[t] is True]
+    st, en = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    for _ in range(5):
+        for t in tiles:
+            st.record()
+            for _ in range(5):
+                K.conv_fwd(x, w, g, y, stats=stats, tile=t)
+            en.record()
+            en.synchronize()
+            times[t].append(st.elapsed_time(en) / 5 * 1e3)
+    print(f"stem fwd M={M} N=64 K=256 default tile {K.fwd_tile(g, B, torch.bfloat16, False, 256)}")
+    for t in tiles:
+        print(f"  tile {t}: {statistics.median(times[t]):8.1f} us")
+    for t, v in ok.items():
+        if v is not True:
+            print(f"  tile {t}: {v}")
+
+
+if __name__ == "__main__":
+    main()
