@@ -445,7 +445,9 @@ def main():
         consistency = _verify_consistent(ctx, tr) if hasattr(tr, "state_checksum") else {}
     ms = 1000.0 * elapsed / max(args.steps, 1)
     value = args.batch * world * args.steps / elapsed
-    base = (BASELINE_DP if args.dp else BASELINE).get(world)
+    # the reference's bars are ResNet-50 on GPUs: no ratio for other models or the CPU config
+    base = ((BASELINE_DP if args.dp else BASELINE).get(world)
+            if args.arch == "resnet50" and ctx.cuda else None)
     cfg = {"model": args.arch, "global_batch": args.batch * world,
            "per_gpu_batch": args.batch, "seq_len": None,
            "parallelism": (f"dataparallel{world}" if args.dp else f"dp{world}"),
@@ -490,7 +492,8 @@ def main():
             "vs_baseline_precision": (f"{args.dtype} (this run) vs the reference's fp32/TF32 bar"
                                       if args.dtype != "fp32" else "fp32 vs fp32/TF32"),
             "dtype": args.dtype,
-            "data": "synthetic (on-device generated 3x224x224, random-init weights)",
+            "data": (f"synthetic ({'on-device' if ctx.cuda else 'host'} generated 3x{args.image_size}x"
+                     f"{args.image_size}, random-init weights)"),
             "config": cfg,
             "loss": loss,
             "max_mem_gb": max_mem,
