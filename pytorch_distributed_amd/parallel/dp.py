@@ -133,6 +133,10 @@ class DataParallel(nn.Module):
             self.group = RcclGroup(self.device_ids)
         # (replicas sharing a device -- used by the 1-GPU tests -- sync through plain copies)
         self._armed = False
+        # HIP events at the end of backward and after the last gradient all-reduce of the next
+        # graph-replayed step (exposed_comm_ms); diagnostics only
+        self.timing = False
+        self._ev_bwd = self._ev_comm = None
 
     # ------------------------------------------------------------------ construction
     def _native_replica(self, dev: torch.device):
@@ -330,7 +334,7 @@ class DataParallel(nn.Module):
         nseg = len(jobs[0][0].graphs)
         bounds = [0] + jobs[0][0].splits + [self.module.numel]
         threaded = len(jobs) > 1 and os.environ.get("PDA_DP_THREADS", "1") != "0"
-        timing = getattr(self, "timing", False)
+        timing = self.timing
         for s in range(nseg):
             if threaded:
                 # one host thread per device: hipGraphLaunch of a ~150-node segment costs ~0.5 ms
@@ -360,7 +364,7 @@ class DataParallel(nn.Module):
     def exposed_comm_ms(self) -> Optional[float]:
         """After a step with ``timing = True`` has completed: max over devices of (last gradient
         all-reduce done - backward done)."""
-        if getattr(self, "_ev_comm", None) is None:
+        if self._ev_comm is None:
             return None
         return max(b.elapsed_time(c) for b, c in zip(self._ev_bwd, self._ev_comm))
 
