@@ -98,6 +98,11 @@ class Workspace:
 
 _NUM_CU = 256
 _WGRAD_TARGET = 2 * _NUM_CU   # default split-K block target of the weight gradients
+# every weight-gradient block target x 0.7 in the step: the targets above were tuned per kernel in
+# isolation, but a weight gradient shares the device with the main-stream chain, and fewer,
+# longer split-K blocks leave it more CUs (bench.py, 5 alternating rounds on one box: x1.0 28.20,
+# x0.85 28.15, x0.7 28.04, x0.6 28.11, x0.4 28.24, x1.5 28.34 ms/step; profiles/ab_r3_dma.md)
+_WGRAD_SCALE = float(os.environ.get("PDA_WGRAD_SCALE", "0.7"))
 
 
 # f32 convolutions: "exact" = MFMA 16x16x4 f32 (DT_F32); "split" = f32 tensors with the products on
@@ -418,7 +423,7 @@ def wgrad_plan(g: ConvGeom, Nb: int, tile: Optional[Tuple[int, int]] = None,
             bm, bn = -128, 128
     if target_blocks is None:
         target_blocks = _WGRAD_TARGET
-    target_blocks = max(1, int(target_blocks))
+    target_blocks = max(1, int(target_blocks * _WGRAD_SCALE))
     if tile:
         bm, bn = tile
     tiles = math.ceil(M / tile_rows(bm)) * math.ceil(N / bn)
