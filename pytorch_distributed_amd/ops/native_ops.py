@@ -283,11 +283,12 @@ def _halo_geom(g: ConvGeom) -> bool:
 
 
 def dgrad_tile(g: ConvGeom, Nb: int, dma: bool = True) -> Tuple[int, int]:
-    """Data-gradient tile: the tap-reuse (HALO) 256x128 tile on the 3x3 stride-1 layers with 128-256
-    input channels (C10 121 -> 112 us, C16 115 -> 112; C2 / C22 measured slower:
-    profiles/ab_r3_dma.md); otherwise the register-staged tiles."""
-    if dma and _DMA and _halo_geom(g) and 128 <= g.Cin <= 256:
-        return 2256, 128
+    """Data-gradient tile: the register-staged tiles. (The tap-reuse (HALO) 256x128 LDS-DMA tile is
+    faster in isolation on C10 / C16 -- 121 -> 112, 115 -> 112 us -- but slower in the step: its
+    block takes a whole CU beside the weight-gradient stream's tiles, and the data gradients are
+    the step's critical path: 28.03 -> 27.88 ms/step without it, profiles/ab_r3_dma.md section 11.
+    ``dma`` is kept for callers that pass the operand dtype; pass tile=(2256, 128) explicitly to
+    run the HALO kernel.)"""
     M = Nb * (g.H // g.stride) * (g.W // g.stride)
     return pick_tile(M * g.stride * g.stride, g.Cin, g.Cout * _max_class_taps(g))
 
