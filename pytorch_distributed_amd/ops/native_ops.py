@@ -378,6 +378,7 @@ _WGRAD_TUNED = {
     # default -- it runs alone at the end of the backward (tools/stem_wgrad_sweep.py)
     (64, 4, 16, 1, 112): ((-64, 128), 1536),
 }
+_WGRAD_ALONE = {(64, 4, 16, 1, 112)}   # weight gradients with nothing beside them (no x0.7)
 # LDS-DMA tiles (16-bit, no operand prologue; the register-staged entry above is the fallback)
 _DMA = os.environ.get("PDA_DMA", "1") != "0"
 _WGRAD_DMA = {   # tools/wgrad_sweep.py, kernel + slab reduce (profiles/wgrad_sweep_r3{,b}.txt)
@@ -424,7 +425,8 @@ def wgrad_plan(g: ConvGeom, Nb: int, tile: Optional[Tuple[int, int]] = None,
             bm, bn = -128, 128
     if target_blocks is None:
         target_blocks = _WGRAD_TARGET
-    target_blocks = max(1, int(target_blocks * _WGRAD_SCALE))
+    # (the stem's weight gradient runs alone at the end of the backward: its isolated optimum holds)
+    target_blocks = max(1, int(target_blocks * (1.0 if key in _WGRAD_ALONE else _WGRAD_SCALE)))
     if tile:
         bm, bn = tile
     tiles = math.ceil(M / tile_rows(bm)) * math.ceil(N / bn)
