@@ -184,14 +184,17 @@ def fwd_tile(g: ConvGeom, Nb: int, dtype: torch.dtype, pro: bool = False,
              Kpad: Optional[int] = None) -> Tuple[int, int]:
     """Default tile of a forward conv. The LDS-DMA tiles take 16-bit operands without the BN
     prologue (their bytes never pass through registers): tap reuse (HALO) on the 3x3 stride-1
-    layers with >= 128 output channels (C10 118 -> 105 us, C16 114 -> 98, C22 127 -> 109), the
-    128x256 DMA tile on deep-K layers (:func:`pick_tile`); other launches keep the register-staged
-    choice."""
+    layers with >= 128 output channels (C10 118 -> 105 us, C16 114 -> 98, C22 127 -> 109); other
+    launches keep the register-staged choice (PDA_FWD_DMA256=1: the 128x256 DMA tile on deep-K
+    layers, :func:`pick_tile`)."""
     dma = _kdt(torch.empty(0, dtype=dtype)) in (1, 2) and not pro and g.Cin >= 64
     if dma and _DMA and _halo_geom(g) and g.Cout >= 128:
         return 2256, 128
     M = Nb * g.Ho * g.Wo
-    return pick_tile(M, g.Cout, Kpad if Kpad is not None else g.R * g.S * g.Cin, dma=dma)
+    # (the 128x256 LDS-DMA tile wins 4-9 % per kernel on the deep-K layers but loses in the step:
+    # 28.65 -> 28.52 ms/step without it, profiles/ab_r3_dma.md section 12; explicit tile only)
+    return pick_tile(M, g.Cout, Kpad if Kpad is not None else g.R * g.S * g.Cin,
+                     dma=dma and os.environ.get("PDA_FWD_DMA256", "0") != "0")
 
 
 def conv_fwd(x: torch.Tensor, w: torch.Tensor, g: ConvGeom, out: torch.Tensor,
