@@ -249,3 +249,32 @@ def test_lds_dma_tile_codes_and_fallback():
     assert K.dgrad_tile(g, 400)[0] < 1000 and K.dgrad_tile(g, 400, dma=False)[0] < 1000
     assert K.dgrad_slabs(g, 400, dtype=torch.float32) == math.ceil(400 * 196 / K.tile_rows(
         K.dgrad_tile(g, 400, dma=False)[0]))
+
+
+def test_dataparallel_segment_bounds_and_step_busy(monkeypatch):
+    """DataParallel's graph-split policy (PDA_DP_SEGMENTS: stage bounds of a native module, none
+    for a single device or mode 0, a clear error otherwise) and the HIP-event busy fallback of the
+    epoch metrics (no device: no value, never a made-up one)."""
+    from pytorch_distributed_amd.parallel.dp import DataParallel
+    from pytorch_distributed_amd.utils.gpu_util import StepBusy
+
+    class Fake:
+        def stage_bounds(self):
+            return [100, 200, 300]
+
+    dp = DataParallel.__new__(DataParallel)     # no devices here: only the policy's inputs
+    dp.__dict__.update(module=Fake(), replicas=[object()])
+    monkeypatch.setenv("PDA_DP_SEGMENTS", "stage")
+    assert dp._segment_bounds() == [100, 200, 300]
+    monkeypatch.setenv("PDA_DP_SEGMENTS", "0")
+    assert dp._segment_bounds() == []
+    monkeypatch.setenv("PDA_DP_SEGMENTS", "stage")
+    dp.__dict__["replicas"] = []
+    assert dp._segment_bounds() == []
+    monkeypatch.setenv("PDA_DP_SEGMENTS", "block")
+    with pytest.raises(ValueError):
+        dp._segment_bounds()
+    with StepBusy(None) as sb:
+        sb.begin()
+        sb.end()
+    assert sb.overall() is None
