@@ -484,11 +484,18 @@ class _ReplicaGraph:
                     g = torch.cuda.CUDAGraph()
                     self.graphs = [g]
                     self._capturing = True
+                    ended = False
                     try:
                         g.capture_begin()
                         self._body()
                         self.graphs[-1].capture_end()
+                        ended = True
                     except BaseException:
+                        if not ended:   # leave no capture open on the stream
+                            try:
+                                self.graphs[-1].capture_end()
+                            except Exception:   # noqa: BLE001 (already invalidated)
+                                pass
                         self.graphs = []
                         raise
                     finally:
