@@ -181,8 +181,9 @@ constexpr int conv_min_blocks() {
 
 template <int PASS_T, int DT, int BM, int BN, int STAGES>
 // WGRAD_BNA holds the fixed column chunk's 24 BN coefficients and the y chunks: 3 blocks per CU
-// (the 16-bit WGRAD budget of 4 spilled 15 VGPRs)
-__global__ __launch_bounds__(conv_nt<STAGES>(), (PASS_T == WGRAD_BNA ? 3 : conv_min_blocks<DT, BM, BN, STAGES>())) void conv_gemm_kernel(ConvParams p_arg) {
+// (the 16-bit WGRAD budget of 4 spilled 15 VGPRs); its 256-column tile (the stem's whole N: dz and
+// y staged and transformed once instead of once per 128-column tile) needs 246: 2 blocks per CU
+__global__ __launch_bounds__(conv_nt<STAGES>(), (PASS_T == WGRAD_BNA ? (BN >= 256 ? 2 : 3) : conv_min_blocks<DT, BM, BN, STAGES>())) void conv_gemm_kernel(ConvParams p_arg) {
   constexpr int PASS = PASS_T == WGRAD_BNA ? WGRAD : PASS_T;
   constexpr bool ABN = PASS_T == WGRAD_BNA;
   constexpr bool DMA = STAGES >= 3;
@@ -1617,8 +1618,8 @@ int pda_conv_wgrad_bna(const ConvDesc* d, const void* dz, const void* y, const f
 #define BNA_CASE(D, M_, N_, S_) \
   if (dt == D && bm == (S_ == 1 ? -M_ : M_) && bn == N_) return launch<WGRAD_BNA, D, M_, N_, S_>(p, grid, st);
 #ifndef CONV_DMA_ONLY
-  BNA_CASE(DT_BF16, 64, 128, 1) BNA_CASE(DT_BF16, 64, 128, 2)
-  BNA_CASE(DT_F16, 64, 128, 1) BNA_CASE(DT_F16, 64, 128, 2)
+  BNA_CASE(DT_BF16, 64, 128, 1) BNA_CASE(DT_BF16, 64, 128, 2) BNA_CASE(DT_BF16, 64, 256, 1)
+  BNA_CASE(DT_F16, 64, 128, 1) BNA_CASE(DT_F16, 64, 128, 2) BNA_CASE(DT_F16, 64, 256, 1)
 #endif
 #undef BNA_CASE
   return -1;

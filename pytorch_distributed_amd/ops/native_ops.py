@@ -377,9 +377,10 @@ _WGRAD_TUNED = {
     (2048, 1, 1024, 2, 7): ((-128, 128), 512),  # C20
     (512, 1, 2048, 1, 7): ((128, 128), 512),    # C21
     (512, 3, 512, 1, 7): ((-256, 128), 1024),   # C22
-    # stem (4x4/1 on the space-to-depth image, WGRAD_BNA): 1536 blocks 437 us vs 490 at the 512
+    # stem (4x4/1 on the space-to-depth image, WGRAD_BNA): the 64x256 tile (the whole N: dz and y
+    # staged once) at ~1024 splits, 404 us vs 440 for 64x128 at 1536 blocks and 490 at the 512
     # default -- it runs alone at the end of the backward (tools/stem_wgrad_sweep.py)
-    (64, 4, 16, 1, 112): ((-64, 128), 1536),
+    (64, 4, 16, 1, 112): ((-64, 256), 1536),
 }
 _WGRAD_ALONE = {(64, 4, 16, 1, 112)}   # weight gradients with nothing beside them (no x0.7)
 # LDS-DMA tiles (16-bit, no operand prologue; the register-staged entry above is the fallback)
@@ -442,13 +443,13 @@ def wgrad_plan(g: ConvGeom, Nb: int, tile: Optional[Tuple[int, int]] = None,
 
 def wgrad_bna_ok(g: ConvGeom, Nb: int, dtype: torch.dtype) -> bool:
     """Whether :func:`conv_wgrad` can form dY from the BN backward in-kernel for this geometry: 16-bit
-    operands on the tile WGRAD_BNA is built for (64x128: the stem's Cout = 64)."""
+    operands on the tiles WGRAD_BNA is built for (64x128, 64x256: the stem's Cout = 64)."""
     if dtype not in (torch.bfloat16, torch.float16) or g.Cout % 8:
         return False
     if getattr(ext.lib(), "pda_conv_wgrad_bna", None) is None:
         return False
     bm, bn, _, _ = wgrad_plan(g, Nb)
-    return abs(bm) == 64 and bn == 128
+    return abs(bm) == 64 and bn in (128, 256)
 
 
 def conv_wgrad(dy: torch.Tensor, x: torch.Tensor, g: ConvGeom, grad: torch.Tensor, ws: Workspace,
@@ -465,6 +466,10 @@ def conv_wgrad(dy: torch.Tensor, x: torch.Tensor, g: ConvGeom, grad: torch.Tenso
     Nb = dy.shape[0]
     bm, bn, splits, k_chunk = wgrad_plan(g, Nb, tile, target_blocks, f32=dy.dtype == torch.float32,
                                          dma=dy.dtype != torch.float32 and pro is None and bna is None)
+    if bna is None and bm == -64 and bn == 256:
+        # 64x256 is a WGRAD_BNA tile: the plain weight gradient of that plan runs 64x128 tiles over
+        # the same split-K chunks (same accumulation order per element: bitwise the same result)
+        bn = 128
     M, N = g.Cout, g.R * g.S * g.Cin
     slab = ws.get("wgrad_slab", splits * M * N)
     d = g.desc(Nb)

@@ -108,8 +108,9 @@ def test_conv_stem_padded_cin():
     assert rel_err(dw, wr.grad.permute(0, 2, 3, 1)) < 1e-2
 
 
+@pytest.mark.parametrize("tile", [None, (-64, 128), (-64, 256)])
 @pytest.mark.parametrize("Cout,Cin,k,H", [(64, 64, 3, 9), (64, 16, 4, 11), (64, 16, 4, 60)])
-def test_conv_wgrad_bna_matches_applied(Cout, Cin, k, H):
+def test_conv_wgrad_bna_matches_applied(Cout, Cin, k, H, tile):
     """WGRAD_BNA (the stem wgrad forming dY = k1*dz + k2*y + k3 while staging) against the unfused
     path (dY materialised in bf16, plain wgrad) and against the fp32 PyTorch weight gradient of the
     same dY; ragged row counts check that padding rows contribute 0, not k3; H = 60 runs split-K."""
@@ -126,7 +127,7 @@ def test_conv_wgrad_bna_matches_applied(Cout, Cin, k, H):
     kk = torch.randn(3 * Cout, device=DEV)
     ws = K.Workspace(DEV)
     dw_f = torch.zeros(Cout, k, k, Cin, device=DEV)
-    K.conv_wgrad(dz, x, g, dw_f.view(-1), ws, bna=(y, kk))
+    K.conv_wgrad(dz, x, g, dw_f.view(-1), ws, bna=(y, kk), tile=tile)
     # the kernels' fma chain fma(k1, dz, fma(k2, y, k3)), in f64 then rounded once to f32
     dy = (kk[:Cout].double() * dz.double() + (kk[Cout:2 * Cout].double() * y.double()
                                               + kk[2 * Cout:].double()).float().double()).float().to(dtype)

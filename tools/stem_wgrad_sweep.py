@@ -24,27 +24,29 @@ def main():
     k = torch.randn(3 * 64, device=dev) * 0.1
     ws = K.Workspace(dev)
     out = torch.empty(64 * 256, device=dev)
-    targets = [512, 1024, 1536, 2048, 3072]
+    targets = [((-64, 128), 1536), ((-64, 256), 512), ((-64, 256), 768), ((-64, 256), 1024),
+               ((-64, 256), 1536)]
     res = {}
     for tb in targets:
-        K.conv_wgrad(dz, x, g, out, ws, bna=(y, k), target_blocks=tb)
+        K.conv_wgrad(dz, x, g, out, ws, bna=(y, k), tile=tb[0], target_blocks=tb[1])
         torch.cuda.synchronize()
         res[tb] = out.clone()
-    ref = res[512]
+    ref = res[targets[0]]
     st, en = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     times = {tb: [] for tb in targets}
     for _ in range(5):
         for tb in targets:
             st.record()
             for _ in range(3):
-                K.conv_wgrad(dz, x, g, out, ws, bna=(y, k), target_blocks=tb)
+                K.conv_wgrad(dz, x, g, out, ws, bna=(y, k), tile=tb[0], target_blocks=tb[1])
             en.record()
             en.synchronize()
             times[tb].append(st.elapsed_time(en) / 3 * 1e3)
     for tb in targets:
-        plan = K.wgrad_plan(g, B, target_blocks=tb)
+        plan = K.wgrad_plan(g, B, tile=tb[0], target_blocks=tb[1])
         err = ((res[tb] - ref).norm() / ref.norm()).item()
-        print(f"target {tb:5d} plan {plan}: {statistics.median(times[tb]):8.1f} us  rel diff vs 512: {err:.2e}")
+        print(f"tile {tb[0]} target {tb[1]:5d} plan {plan}: {statistics.median(times[tb]):8.1f} us  "
+              f"rel diff vs the first: {err:.2e}")
 
 
 if __name__ == "__main__":
