@@ -28,8 +28,8 @@ re-points their parameters/buffers into the flat storage.
 from __future__ import annotations
 
 import contextlib
-
 import math
+import os
 from dataclasses import dataclass
 from typing import Callable, Dict, List, Optional, Tuple
 
@@ -134,7 +134,6 @@ class NativeResNet(nn.Module):
         # "1" every consumer, "1x1" only 1x1 consumers (a 3x3 consumer gathers each element 9x per
         # N-tile, so it re-applies the prologue 9-36x: there one materialising pass is cheaper),
         # "1x1:H" also 3x3 consumers of input size >= H, "0" none
-        import os
         self.fuse_prologue = os.environ.get("PDA_FUSE_PROLOGUE", "1x1:56")
         self.fused_stem_bwd = True    # maxpool gather + ReLU mask + BN partials in one pass
         # stem wgrad forms its dY from the BN backward in-kernel (PDA_STEM_BNA=0: apply pass)
@@ -184,10 +183,18 @@ class NativeResNet(nn.Module):
                                    "HIP runtime at capture end; capture with default priorities")
         prev = self._wbatch_mode
         self.set_wgrad_batch(self._wbatch_env or "stage")
+        # the HIP runtime replays a captured two-stream step almost serially
+        # (profiles/rocprof_r3_graph_replay.md), so the weight gradients keep the per-kernel
+        # split-K targets instead of the x0.7 of the concurrent eager step (DataParallel replay
+        # 29.03 -> 28.85 ms/step, profiles/ab_r3_dma.md section 18)
+        prev_scale = K._WGRAD_SCALE
+        if "PDA_WGRAD_SCALE" not in os.environ:
+            K._WGRAD_SCALE = 1.0
         try:
             yield
         finally:
             self.set_wgrad_batch(prev)
+            K._WGRAD_SCALE = prev_scale
 
     # ------------------------------------------------------------------ planning
     def _build_plan(self) -> None:
