@@ -22,3 +22,17 @@ def test_parity_map_references_exist():
         if not os.path.exists(os.path.join(ROOT, path)):
             missing.append(path)
     assert not missing, missing
+
+
+def test_every_runtime_knob_is_documented():
+    """Every PDA_* environment variable the package or bench.py reads has a README row."""
+    readme = open(os.path.join(ROOT, "README.md")).read()
+    table = readme.split("## Runtime knobs", 1)[1].split("\n## ", 1)[0]
+    knobs = set()
+    files = [os.path.join(ROOT, "bench.py")]
+    for d, _, names in os.walk(os.path.join(ROOT, "pytorch_distributed_amd")):
+        files += [os.path.join(d, n) for n in names if n.endswith(".py")]
+    for f in files:
+        knobs |= set(re.findall(r"environ(?:\.get\(|\[)\"(PDA_[A-Z0-9_]+)\"", open(f).read()))
+    assert len(knobs) > 15
+    assert not sorted(k for k in knobs if f"`{k}`" not in table)
