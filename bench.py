@@ -86,6 +86,9 @@ def parse():
                          "on for 1 GPU)")
     ap.add_argument("--diag-steps", type=int, default=3,
                     help="N>1: extra untimed steps with bucket timing events")
+    ap.add_argument("--comm-probe", type=int, default=1,
+                    help="N>1: measure all-reduce latency / bus bandwidth of the gradient "
+                         "communicator after the timed region (xgmi_probe in the JSON; 0: skip)")
     ap.add_argument("--fp32-steps", type=int, default=5,
                     help="timed steps of the exact-fp32 pass (0: skip)")
     ap.add_argument("--amp-steps", type=int, default=10,
@@ -215,6 +218,48 @@ def _diagnostics(ctx: Ctx, tr, first: int) -> dict:
         out["exposed_comm_ms"] = round(statistics.median(exp), 4)
         out["bucket_allreduce_ms"] = [round(statistics.median(c), 4) for c in zip(*per)]
     return out
+
+
+PROBE_BYTES = (16 << 10, 256 << 10, 2 << 20, 8 << 20, 32 << 20)
+
+
+def _comm_probe(ctx: Ctx, tr) -> dict:
+    """N>1, after the timed region: f32 all-reduce time of the communicator the gradient buckets
+    use (the native RCCL one on GPU), at sizes spanning the bucket plan, so the xGMI cost model
+    behind the bucket caps (parallel/reducer.py: T(S) = alpha + 2(n-1)/n S / busbw, alpha and
+    eta assumed) is measured on the node the driver runs: alpha = T(16 KiB), bus bandwidth and
+    eta = busbw / (7 x 153 GB/s) from T(32 MiB). Wall clock around REPS back-to-back calls with
+    a device sync on both sides, ranks aligned by a barrier; the MAX over ranks."""
+    net = getattr(tr, "net", None)
+    comm = getattr(net, "comm", None)
+    if comm is None or not ctx.args.comm_probe:
+        return {}
+    import torch.distributed as dist
+    from pytorch_distributed_amd.launch import host_group
+    n = ctx.world
+    ms = []
+    for b in PROBE_BYTES:
+        t = torch.zeros(b // 4, device=ctx.device)
+        reps = 20 if b <= (2 << 20) else 8
+        for _ in range(3):
+            comm.all_reduce(t)
+        ctx.sync()
+        comm.barrier()
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            comm.all_reduce(t)
+        ctx.sync()
+        ms.append(1000.0 * (time.perf_counter() - t0) / reps)
+        del t
+    worst = torch.tensor(ms, dtype=torch.float64)
+    dist.all_reduce(worst, op=dist.ReduceOp.MAX, group=host_group())
+    ms = [round(float(v), 4) for v in worst]
+    big = PROBE_BYTES[-1]
+    busbw = 2.0 * (n - 1) / n * big / (ms[-1] * 1e-3) / 1e9
+    return {"xgmi_probe": {"comm": type(comm).__name__, "bytes": list(PROBE_BYTES), "ms": ms,
+                           "alpha_us": round(1000.0 * ms[0], 1),
+                           "busbw_GBs": round(busbw, 1),
+                           "eta_vs_7x153GBs": round(busbw / (7 * 153.0), 3)}}
 
 
 def _verify_consistent(ctx: Ctx, tr) -> dict:
@@ -423,6 +468,8 @@ def main():
     loss = tr.last_loss()
     nxt = args.warmup + args.steps
     diag = _diagnostics(ctx, tr, nxt) if ctx.multi else {}
+    if ctx.multi:
+        diag.update(_comm_probe(ctx, tr))
     if args.dp and getattr(tr.dp, "replicas", None):
         # one more (untimed) step with HIP events at the end of backward and after the last
         # gradient all-reduce (per-stage slices overlapped with the backward's later segments)

@@ -30,8 +30,9 @@ Design (MI355X-first):
        8 ranks x 7 links x 256 B (``models/native.py`` BUCKET_QUANTUM), so RCCL's per-rank /
        per-channel chunks are equal and 256-B aligned for any world size dividing 8.
   ``bench.py`` reports the measured per-bucket all-reduce time and the exposed tail
-  (``bucket_allreduce_ms``, ``exposed_comm_ms``) for N > 1, so the model can be checked on a
-  real node;
+  (``bucket_allreduce_ms``, ``exposed_comm_ms``) for N > 1, and ``xgmi_probe``: alpha, bus
+  bandwidth and eta measured through the same communicator at 16 KiB-32 MiB, so the model's
+  constants come from the node the driver runs;
 * readiness: ``Tensor.register_post_accumulate_grad_hook`` (generic modules) or
   the native engine's ``on_grads_ready(offset)`` callback; a ready bucket is
   pre-scaled by 1/world and all-reduced (SUM) asynchronously through a

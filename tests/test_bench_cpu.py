@@ -61,6 +61,10 @@ def test_bench_cpu_two_ranks_self_validation(tmp_path):
     assert rec["buckets"] >= 1 and len(rec["bucket_bytes"]) == rec["buckets"]
     assert sum(rec["bucket_bytes"]) >= 11_000_000 * 4     # every ResNet-18 gradient is bucketed
     assert rec["comm"] == "ProcessGroupCommunicator"
+    # measured all-reduce cost of the gradient communicator (the reducer's alpha / bandwidth)
+    pr = rec["xgmi_probe"]
+    assert pr["comm"] == "ProcessGroupCommunicator" and len(pr["ms"]) == len(pr["bytes"])
+    assert all(v > 0 for v in pr["ms"]) and pr["alpha_us"] > 0 and pr["busbw_GBs"] > 0
     # the resnet_ddp_apex.py configuration, timed after the headline on every rank
     assert rec["amp_fp16_images_per_sec"] > 0 and rec["amp_weights_consistent"] is True
     assert "DDP" in rec["amp_config"]

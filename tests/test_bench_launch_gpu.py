@@ -46,6 +46,8 @@ def test_bench_torchrun_two_ranks(tmp_path):
     assert rec["buckets"] >= 3 and len(rec["bucket_bytes"]) == rec["buckets"]
     assert all(b % (8 * 7 * 256) == 0 for b in rec["bucket_bytes"])
     assert rec["comm"] == "ProcessGroupCommunicator" and rec["rccl_world"] is None   # gloo here
+    pr = rec["xgmi_probe"]                    # device tensors through the gradient communicator
+    assert len(pr["ms"]) == len(pr["bytes"]) and all(v > 0 for v in pr["ms"])
     # the like-for-like exact-fp32 pass, and the split-f32 (>= TF32 precision) pass
     assert rec["fp32_images_per_sec"] > 0 and rec["fp32_engine"] == "native"
     assert rec["fp32_split_images_per_sec"] > 0
