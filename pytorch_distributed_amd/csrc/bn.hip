@@ -647,6 +647,9 @@ __global__ __launch_bounds__(NT) void stem_bwd_reduce_kernel(
     ld8f(sc + c0, s);
     ld8f(sh + c0, h);
     if (threadIdx.x < tpr * rpi) {
+      // two quads in flight per thread: 520-529 vs 540-554 us in the step (x4: 572-593 us,
+      // tools/gpu_kernel_ab.sh; profiles/ab_r3_dma.md section 20)
+#pragma unroll 2
       for (long long qd = r0 + rsub; qd < r1; qd += rpi) {
         const uint32_t p2 = fdiv((uint32_t)qd, dWo), xo = (uint32_t)qd - p2 * Wo;
         const uint32_t n = fdiv(p2, dHo), yo = p2 - n * Ho;
