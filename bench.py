@@ -124,10 +124,11 @@ def _configure_process(args) -> dict:
     numa = False
     if world > 1 and args.device == "cuda" and os.environ.get("PDA_BIND_NUMA", "1") != "0":
         # one rank per GPU, pinned to that GPU's NUMA node as the reference's
-        # hfai.multiprocessing.spawn(bind_numa=True); device_count() does not
-        # initialise HIP on this image
-        from pytorch_distributed_amd.launch import bind_numa
-        numa = bind_numa(local_rank % max(torch.cuda.device_count(), 1))
+        # hfai.multiprocessing.spawn(bind_numa=True); the GPU count comes from the
+        # KFD topology in sysfs, so no HIP call precedes the binding
+        # (tests/test_bench_cpu.py::test_numa_binding_precedes_any_hip_call)
+        from pytorch_distributed_amd.launch import bind_numa, visible_gpu_count
+        numa = bind_numa(local_rank % max(visible_gpu_count(), 1))
     env = {k: v for k, v in sorted(os.environ.items())
            if k.startswith(("NCCL_", "RCCL_", "HSA_ENABLE_IPC", "GPU_MAX_HW_QUEUES"))}
     return {"comm_env": env, "numa_bound": numa}
@@ -149,6 +150,7 @@ class Ctx:
             self.device = torch.device("cpu")
         self.ndev = ndev
         self.multi = self.world > 1 and not args.dp
+        self.spread = {}
 
     def sync(self):
         if self.cuda:
@@ -182,13 +184,32 @@ class Ctx:
         return float(self.allreduce([x], "max")[0])
 
 
-def _timed(ctx: Ctx, tr, first: int, steps: int) -> float:
+def _timed(ctx: Ctx, tr, first: int, steps: int, key: str = "headline") -> float:
+    """``steps`` timed steps between barrier + device sync on both sides; returns the MAX elapsed
+    over ranks and keeps the per-rank spread (min, max) in ``ctx.spread[key]`` so a straggler rank
+    shows up in the record."""
     ctx.barrier()
     t0 = time.perf_counter()
     for i in range(steps):
         tr.step(first + i)
     ctx.barrier()
-    return ctx.allreduce_max(time.perf_counter() - t0)
+    el = time.perf_counter() - t0
+    if not ctx.multi:
+        ctx.spread[key] = (el, el)
+        return el
+    lo, hi = (float(v) for v in ctx.allreduce([-el, el], "max"))
+    ctx.spread[key] = (-lo, hi)
+    return hi
+
+
+def _spread_record(ctx: Ctx) -> dict:
+    """Per-rank timed-region spread of every timed pass: min / max seconds over ranks and the
+    max-over-min excess in percent (0 on one rank)."""
+    out = {}
+    for k, (lo, hi) in ctx.spread.items():
+        out[k] = {"min_s": round(lo, 4), "max_s": round(hi, 4),
+                  "spread_pct": round(100.0 * (hi - lo) / lo, 2) if lo > 0 else None}
+    return {"rank_time_spread": out}
 
 
 def _diagnostics(ctx: Ctx, tr, first: int) -> dict:
@@ -294,7 +315,7 @@ def _fp32_pass(ctx: Ctx, args, mode: str = "exact") -> dict:
             return {}
         for i in range(2):
             tr.step(i)
-        el = _timed(ctx, tr, 2, args.fp32_steps)
+        el = _timed(ctx, tr, 2, args.fp32_steps, "fp32" if mode == "exact" else "fp32_split")
     finally:
         K._F32_CONV = old
     world = ctx.world if ctx.multi else 1
@@ -349,7 +370,7 @@ def _amp_pass(ctx: Ctx, args) -> dict:
     for i in range(3):
         tr.step(i)
     with BusySampler([ctx.device.index] if ctx.cuda else []) as busy:
-        el = _timed(ctx, tr, 3, args.amp_steps)
+        el = _timed(ctx, tr, 3, args.amp_steps, "amp_fp16")
     amp_util = busy.overall()
     if not _all_ranks(ctx, amp_util is not None) and ctx.cuda and args.util_steps > 0:
         kb = kernel_busy(lambda i: tr.step(1000 + i), args.util_steps, [ctx.device.index])
@@ -361,6 +382,7 @@ def _amp_pass(ctx: Ctx, args) -> dict:
            "amp_fp16_ms_per_step": round(1000.0 * el / args.amp_steps, 3),
            "amp_config": f"fp16 + dynamic loss scaling, {'DDP over RCCL' if ctx.multi else 'single GPU'}"
                          f" ({tr.engine}; resnet_ddp_apex.py)",
+           "amp_dtype": "fp16",
            "amp_weights_consistent": cons.get("weights_consistent"),
            "amp_loss": tr.last_loss(),
            "amp_loss_scale": float(sc.get_scale()) if sc is not None and hasattr(sc, "get_scale") else None,
@@ -369,6 +391,8 @@ def _amp_pass(ctx: Ctx, args) -> dict:
     base = BASELINE.get(world)
     if base:
         res["amp_vs_baseline"] = round(res["amp_fp16_images_per_sec"] / base, 3)
+        # the reference's "Apex" bar is fp16 autocast AMP too: like for like
+        res["amp_vs_baseline_precision"] = "fp16 AMP vs the reference's fp16 AMP (Apex) bar"
     del tr
     if ctx.cuda:
         torch.cuda.empty_cache()
@@ -408,8 +432,10 @@ def _dp_pass(ctx: Ctx, args, dtype) -> dict:
                 rec = json.loads(lines[-1])
                 res = {"dp_images_per_sec": rec["value"], "dp_ms_per_step": rec["ms_per_step"],
                        "dp_config": f"{rec['config']['parallelism']}: one process, {n} GPU(s), global "
-                                    f"batch {rec['config']['global_batch']}, {rec['config']['engine']}"
-                                    f" (resnet_dp.py)",
+                                    f"batch {rec['config']['global_batch']}, {rec['config']['engine']}, "
+                                    f"{rec['dtype']} (resnet_dp.py)",
+                       "dp_dtype": rec.get("dtype"),
+                       "dp_vs_baseline_precision": rec.get("vs_baseline_precision"),
                        "dp_replicas_consistent": rec.get("replicas_consistent"),
                        "dp_loss": rec.get("loss"), "dp_max_mem_gb": rec.get("max_mem_gb"),
                        "dp_gpu_util_pct": rec.get("gpu_util_pct"), "dp_vs_baseline": rec.get("vs_baseline"),
@@ -548,6 +574,7 @@ def main():
             "gpu_util_method": util_method,
             **proc, **diag, **consistency, **extra,
         }
+        rec.update(_spread_record(ctx))
         if extra.get("fp32_images_per_sec") and base:
             rec["vs_baseline_fp32"] = round(extra["fp32_images_per_sec"] / base, 3)
             if "fp32_split_images_per_sec" in extra:

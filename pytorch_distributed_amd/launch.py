@@ -23,7 +23,56 @@ from typing import Callable, Optional, Sequence
 import torch
 
 __all__ = ["DistEnv", "dist_env", "spawn", "free_port", "bind_numa", "init_distributed", "gpu_pci_bdf",
-           "host_group"]
+           "host_group", "visible_gpu_count"]
+
+# KFD topology (sysfs): the GPU list in HSA agent order, readable without initialising HIP
+_KFD_ROOT = "/sys/class/kfd/kfd/topology/nodes"
+
+
+def _kfd_gpus():
+    """Property dicts of the GPU nodes of the KFD topology (simd_count > 0), in HSA agent order;
+    None when the topology is not readable."""
+    try:
+        gpus = []
+        for n in sorted((d for d in os.listdir(_KFD_ROOT) if d.isdigit()), key=int):
+            with open(f"{_KFD_ROOT}/{n}/properties") as f:
+                kv = dict(l.split(" ", 1) for l in f.read().split("\n") if " " in l)
+            if int(kv.get("simd_count", "0")) > 0:
+                gpus.append(kv)
+        return gpus
+    except (OSError, ValueError):
+        return None
+
+
+def _visible_list() -> Optional[list]:
+    """Physical GPU indices selected by ROCR_/HIP_/CUDA_VISIBLE_DEVICES (applied in that order, each
+    one indexing the devices the previous left), or None when none is set. Non-integer entries
+    (UUIDs) make the mapping unknown: None."""
+    sel = None
+    for var in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        v = os.environ.get(var)
+        if v is None:
+            continue
+        try:
+            ids = [int(x) for x in v.split(",") if x.strip() != ""]
+        except ValueError:
+            return None
+        sel = ids if sel is None else [sel[i] for i in ids if 0 <= i < len(sel)]
+    return sel
+
+
+def visible_gpu_count() -> int:
+    """GPUs this process will see, counted from the KFD topology and the *_VISIBLE_DEVICES
+    variables -- no HIP call, so the launcher can bind a rank's NUMA node BEFORE the HIP runtime
+    starts its threads (they inherit the affinity the process has then). Falls back to
+    ``torch.cuda.device_count()`` only where the topology is not readable (no ROCm driver)."""
+    gpus = _kfd_gpus()
+    if gpus is None:
+        return torch.cuda.device_count()
+    sel = _visible_list()
+    if sel is None:
+        return len(gpus)
+    return sum(1 for i in sel if 0 <= i < len(gpus))
 
 
 @dataclass
@@ -59,27 +108,29 @@ def dist_env(local_rank: Optional[int] = None, nprocs: Optional[int] = None) -> 
     nnodes = int(env.get("WORLD_SIZE", "1"))
     node = int(env.get("RANK", "0"))
     lr = 0 if local_rank is None else local_rank
-    gpus = nprocs if nprocs is not None else max(torch.cuda.device_count(), 1)
+    gpus = nprocs if nprocs is not None else max(visible_gpu_count(), 1)
     return DistEnv(addr, port, nnodes * gpus, node * gpus + lr, lr, gpus, node, nnodes)
 
 
 def gpu_pci_bdf(index: int) -> Optional[str]:
-    """PCI address (``dddd:bb:dd.f``) of GPU ``index`` in HSA agent order (KFD topology, sysfs)."""
-    try:
-        root = "/sys/class/kfd/kfd/topology/nodes"
-        gpus = []
-        for n in sorted(os.listdir(root), key=int):
-            props = open(f"{root}/{n}/properties").read().split("\n")
-            kv = dict(l.split(" ", 1) for l in props if " " in l)
-            if int(kv.get("simd_count", "0")) > 0:
-                gpus.append(kv)
-        if index >= len(gpus):
+    """PCI address (``dddd:bb:dd.f``) of the ``index``-th VISIBLE GPU (KFD topology in HSA agent
+    order, remapped through *_VISIBLE_DEVICES)."""
+    gpus = _kfd_gpus()
+    if not gpus:
+        return None
+    sel = _visible_list()
+    if sel is not None:
+        if not 0 <= index < len(sel):
             return None
+        index = sel[index]
+    if not 0 <= index < len(gpus):
+        return None
+    try:
         dom = int(gpus[index].get("domain", "0"))
         loc = int(gpus[index].get("location_id", "0"))
-        return f"{dom:04x}:{(loc >> 8) & 0xff:02x}:{(loc >> 3) & 0x1f:02x}.{loc & 7}"
-    except (OSError, ValueError, KeyError):
+    except ValueError:
         return None
+    return f"{dom:04x}:{(loc >> 8) & 0xff:02x}:{(loc >> 3) & 0x1f:02x}.{loc & 7}"
 
 
 def _gpu_numa_cpus(local_rank: int) -> Optional[Sequence[int]]:
@@ -128,7 +179,7 @@ def spawn(fn: Callable, args: tuple = (), nprocs: Optional[int] = None, bind_num
           join: bool = True):
     """``hfai.multiprocessing.spawn`` equivalent: ``fn(local_rank, *args)`` in ``nprocs`` procs."""
     import torch.multiprocessing as mp
-    nprocs = nprocs if nprocs is not None else max(torch.cuda.device_count(), 1)
+    nprocs = nprocs if nprocs is not None else max(visible_gpu_count(), 1)
     os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
     if "MASTER_PORT" not in os.environ:
         os.environ["MASTER_PORT"] = str(free_port())

@@ -152,6 +152,8 @@ class NativeResNet(nn.Module):
         # captured graph every fork / join edge becomes a cross-queue barrier packet); PDA_WGRAD_BATCH
         # overrides both (profiles/ab_r2_inlaunch_bn.md sections 9, 10)
         self._wbatch_env = os.environ.get("PDA_WGRAD_BATCH")
+        # split-K block-target factor of this model's weight gradients (None: PDA_WGRAD_SCALE)
+        self.wgrad_scale: Optional[float] = None
         self.set_wgrad_batch(self._wbatch_env or "0")
         self._keep: List[torch.Tensor] = []
         # called on the main stream with the flat-gradient offset below which every gradient is
@@ -186,15 +188,16 @@ class NativeResNet(nn.Module):
         # the HIP runtime replays a captured two-stream step almost serially
         # (profiles/rocprof_r3_graph_replay.md), so the weight gradients keep the per-kernel
         # split-K targets instead of the x0.7 of the concurrent eager step (DataParallel replay
-        # 29.03 -> 28.85 ms/step, profiles/ab_r3_dma.md section 18)
-        prev_scale = K._WGRAD_SCALE
+        # 29.03 -> 28.85 ms/step, profiles/ab_r3_dma.md section 18). Per model: another model
+        # running eagerly meanwhile keeps its own plans.
+        prev_scale = self.wgrad_scale
         if "PDA_WGRAD_SCALE" not in os.environ:
-            K._WGRAD_SCALE = 1.0
+            self.wgrad_scale = 1.0
         try:
             yield
         finally:
             self.set_wgrad_batch(prev)
-            K._WGRAD_SCALE = prev_scale
+            self.wgrad_scale = prev_scale
 
     # ------------------------------------------------------------------ planning
     def _build_plan(self) -> None:
@@ -703,7 +706,8 @@ class NativeResNet(nn.Module):
         def fc_wgrad(w):
             K.col_sum(dlog16, self.num_classes,
                       self.flat_grad[self.fc_b_off:self.fc_b_off + self.num_classes], accumulate=acc)
-            K.conv_wgrad(dlog16, sv["feat"], gfc, self.fc_wgrad_full, w, accumulate=acc)
+            K.conv_wgrad(dlog16, sv["feat"], gfc, self.fc_wgrad_full, w, accumulate=acc,
+                          wscale=self.wgrad_scale)
         self._wgrad(fc_wgrad, dlog16, sv["feat"])
         dfeat = self._empty(Nb, 1, 1, self.feat_dim)
         fc_w_ohwi = self.fc_w16.view(self.fc_rows, 1, 1, self.feat_dim)
@@ -761,12 +765,12 @@ class NativeResNet(nn.Module):
 
         if bna:
             def stem_wgrad(w):
-                K.conv_wgrad(dz0, x0, g0, self.stem_wgrad, w, bna=(y0, k0))
+                K.conv_wgrad(dz0, x0, g0, self.stem_wgrad, w, bna=(y0, k0), wscale=self.wgrad_scale)
                 K.stem_s2d_grad(self.stem_wgrad, self.wgrad_view(u), accumulate=acc)
             self._wgrad(stem_wgrad, dz0, y0, x0, k0)
         else:
             def stem_wgrad(w):
-                K.conv_wgrad(dy0, x0, g0, self.stem_wgrad, w)
+                K.conv_wgrad(dy0, x0, g0, self.stem_wgrad, w, wscale=self.wgrad_scale)
                 K.stem_s2d_grad(self.stem_wgrad, self.wgrad_view(u), accumulate=acc)
             self._wgrad(stem_wgrad, dy0, x0)
         self._flush_wgrad()
@@ -845,7 +849,8 @@ class NativeResNet(nn.Module):
             else:
                 K.conv_dgrad(dyd, self.w16_ohwi(b.ds), g, shortcut_g)
             self._wgrad(lambda w, u=b.ds, g=g, dyd=dyd: K.conv_wgrad(dyd, x, g, self.wgrad_view(u), w,
-                                                                    accumulate=acc), dyd, x)
+                                                                    accumulate=acc,
+                                                                    wscale=self.wgrad_scale), dyd, x)
         else:
             K.bn_bwd_finish(ws, part, G, nq, ys[-1], sl[0], sl[1], self.gamma(ul), self.dgamma(ul),
                             self.dbeta(ul), dz, dy, accumulate=acc)
@@ -861,11 +866,13 @@ class NativeResNet(nn.Module):
                 sp_ = rec[f"s{j - 1}"]
                 a_in = ys[j - 1]
                 self._wgrad(lambda w, u=u, g=g, dy=dy, a=a_in, pro=(sp_[2], sp_[3]):
-                            K.conv_wgrad(dy, a, g, self.wgrad_view(u), w, accumulate=acc, pro=pro),
+                            K.conv_wgrad(dy, a, g, self.wgrad_view(u), w, accumulate=acc, pro=pro,
+                                         wscale=self.wgrad_scale),
                             dy, a_in)
             else:
                 self._wgrad(lambda w, u=u, g=g, dy=dy, a=a_in:
-                            K.conv_wgrad(dy, a, g, self.wgrad_view(u), w, accumulate=acc), dy, a_in)
+                            K.conv_wgrad(dy, a, g, self.wgrad_view(u), w, accumulate=acc,
+                                         wscale=self.wgrad_scale), dy, a_in)
             out = self._empty(*a_in.shape)
             if j > 0:
                 up = b.units[j - 1]
@@ -1020,6 +1027,11 @@ class NativeSGD(torch.optim.Optimizer):
     def _launch(self, inv_scale=None, found_inf=None) -> None:
         g = self.param_groups[0]
         m = self.model
+        if m._grads_zero:
+            # zero_grad() and no backward since: torch 2.x's set_to_none leaves every .grad None,
+            # and SGD skips parameters without a gradient -- the flat gradient still holds the
+            # previous step's values (no memset), so applying it would be a stale update
+            return
         K.sgd_flat(m.flat_params, m.flat_grad, self.flat_mom, None if m.f32 else m.flat_shadow,
                    g["lr"], g["momentum"], g["weight_decay"], self._initialized, inv_scale=inv_scale,
                    found_inf=found_inf)

@@ -410,9 +410,10 @@ _WGRAD_DMA = {   # tools/wgrad_sweep.py, kernel + slab reduce (profiles/wgrad_sw
 
 def wgrad_plan(g: ConvGeom, Nb: int, tile: Optional[Tuple[int, int]] = None,
                target_blocks: Optional[int] = None, max_slab_bytes: int = 64 << 20,
-               f32: bool = False, dma: bool = False):
+               f32: bool = False, dma: bool = False, wscale: Optional[float] = None):
     """(bm, bn, splits, k_chunk) of a weight gradient; ``dma``: the launch may use an LDS-DMA tile
-    (16-bit operands, no operand prologue)."""
+    (16-bit operands, no operand prologue); ``wscale``: the split-K block-target factor of the
+    caller's schedule (None: ``PDA_WGRAD_SCALE``, the concurrent eager step's x0.7)."""
     M, N, K = g.Cout, g.R * g.S * g.Cin, Nb * g.Ho * g.Wo
     key = (g.Cout, g.R, g.Cin, g.stride, g.Ho)
     tuned = _WGRAD_TUNED.get(key)
@@ -430,7 +431,8 @@ def wgrad_plan(g: ConvGeom, Nb: int, tile: Optional[Tuple[int, int]] = None,
     if target_blocks is None:
         target_blocks = _WGRAD_TARGET
     # (the stem's weight gradient runs alone at the end of the backward: its isolated optimum holds)
-    target_blocks = max(1, int(target_blocks * (1.0 if key in _WGRAD_ALONE else _WGRAD_SCALE)))
+    sc = _WGRAD_SCALE if wscale is None else wscale
+    target_blocks = max(1, int(target_blocks * (1.0 if key in _WGRAD_ALONE else sc)))
     if tile:
         bm, bn = tile
     tiles = math.ceil(M / tile_rows(bm)) * math.ceil(N / bn)
@@ -457,7 +459,8 @@ def conv_wgrad(dy: torch.Tensor, x: torch.Tensor, g: ConvGeom, grad: torch.Tenso
                tile: Optional[Tuple[int, int]] = None,
                pro: Optional[Tuple[torch.Tensor, torch.Tensor]] = None,
                target_blocks: Optional[int] = None,
-               bna: Optional[Tuple[torch.Tensor, torch.Tensor]] = None) -> torch.Tensor:
+               bna: Optional[Tuple[torch.Tensor, torch.Tensor]] = None,
+               wscale: Optional[float] = None) -> torch.Tensor:
     """grad (f32, OHWI with cin_real channels, rows of pitch R*S*cin_real) = scale * dW.
     pro = (scale, shift): x is PRE-BatchNorm; the activation relu(x*scale+shift) is recomputed.
     bna = (y, k) with k = [k1; k2; k3] (3 x Cout f32): ``dy`` is the BN-backward's masked gradient
@@ -465,7 +468,8 @@ def conv_wgrad(dy: torch.Tensor, x: torch.Tensor, g: ConvGeom, grad: torch.Tenso
     :func:`wgrad_bna_ok`)."""
     Nb = dy.shape[0]
     bm, bn, splits, k_chunk = wgrad_plan(g, Nb, tile, target_blocks, f32=dy.dtype == torch.float32,
-                                         dma=dy.dtype != torch.float32 and pro is None and bna is None)
+                                         dma=dy.dtype != torch.float32 and pro is None and bna is None,
+                                         wscale=wscale)
     if bna is None and bm == -64 and bn == 256:
         # 64x256 is a WGRAD_BNA tile: the plain weight gradient of that plan runs 64x128 tiles over
         # the same split-K chunks (same accumulation order per element: bitwise the same result)

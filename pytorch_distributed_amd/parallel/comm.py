@@ -19,7 +19,24 @@ from typing import Any, Optional
 import torch
 import torch.distributed as dist
 
-__all__ = ["Communicator", "ProcessGroupCommunicator", "make_communicator"]
+__all__ = ["Communicator", "ProcessGroupCommunicator", "make_communicator", "register_default",
+           "default_communicator"]
+
+# the process's device communicator per device (set by DistributedDataParallel on the default
+# group): the hfai-compatible ``platform.nccl.distributed`` collectives use it, so a ported script
+# calling ``dist.reduce`` does not create torch's NCCL communicator beside it
+_DEFAULTS = {}
+
+
+def register_default(comm: "Communicator", device: torch.device) -> None:
+    _DEFAULTS[str(torch.device(device))] = comm
+
+
+def default_communicator(device: torch.device) -> Optional["Communicator"]:
+    c = _DEFAULTS.get(str(torch.device(device)))
+    if c is not None and getattr(c, "aborted", False):
+        return None
+    return c
 
 
 class Communicator:

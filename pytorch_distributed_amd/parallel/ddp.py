@@ -23,7 +23,7 @@ from typing import List, Optional, Sequence, Tuple
 import torch
 from torch import nn
 
-from .comm import Communicator, make_communicator
+from .comm import Communicator, make_communicator, register_default
 from .reducer import MiB, Reducer, plan_buckets
 
 __all__ = ["DistributedDataParallel", "NativeReducer", "convert_sync_batchnorm",
@@ -164,6 +164,10 @@ class DistributedDataParallel(nn.Module):
         self.broadcast_buffers = broadcast_buffers
         dev = next(module.parameters()).device
         self.comm = comm if comm is not None else make_communicator(dev, process_group)
+        if process_group is None and hasattr(self.comm, "make_bucket_reducer"):
+            # the process's ONE RCCL communicator also serves platform.nccl.distributed's
+            # reduce / all_reduce / broadcast (reference restnet_ddp.py:63-64)
+            register_default(self.comm, dev)
         # failure detection: poll the RCCL communicator's async error state from a
         # daemon thread; a dead peer aborts the communicator so collectives return (and the next
         # bucket wait raises) instead of hanging the job. MX_WATCHDOG=0 disables.

@@ -294,6 +294,9 @@ class DataParallel(nn.Module):
         replay = graph and all(rg.graphs for rg in self._graphs)
         if replay and self.replicas:
             self._replay_overlapped(jobs, streams)
+            if len(jobs[0][0].graphs) > 1 and not getattr(self, "_segments_verified", False):
+                self._verify_segmented_reduce(optimizer)
+                return self._step_loss(xs, B)
         else:
             for rg, x, y in jobs:
                 rg.run(x, y, graph)
@@ -302,11 +305,49 @@ class DataParallel(nn.Module):
             else:
                 self.module._grads_zero = False
         optimizer.step()
+        return self._step_loss(xs, B)
+
+    def _step_loss(self, xs, B: int) -> torch.Tensor:
         dev0 = torch.device("cuda", self.output_device)
         loss = torch.zeros((), dtype=torch.float32, device=dev0)
         for rg, x in zip(self._graphs, xs):
             loss += rg.loss.to(dev0, non_blocking=True) * (x.shape[0] / B)
         return loss
+
+    @torch.no_grad()
+    def _verify_segmented_reduce(self, optimizer) -> None:
+        """First segmented step of a DataParallel: every replica must now hold the SAME summed flat
+        gradient (bit-exact; each slice went through one grouped all-reduce). On a mismatch -- a
+        slice that was never reduced, or reduced out of order -- the per-stage overlap is turned off
+        (``PDA_DP_SEGMENTS=0`` behaviour: one graph, one all-reduce after backward), this step's
+        update is taken from replica 0 (its state is copied to every replica after the step), and a
+        warning says so: training continues consistent instead of silently diverging."""
+        from ..bench_step import tensor_checksum
+        for d in self.device_ids:
+            torch.cuda.synchronize(d)
+        sums = [tensor_checksum([m.flat_grad]).cpu() for m in self.all_modules]
+        ok = all(torch.equal(sums[0], c) for c in sums[1:])
+        optimizer.step()
+        self._segments_verified = True
+        if ok:
+            return
+        import warnings
+        warnings.warn("DataParallel: the per-stage gradient all-reduce left replicas with different "
+                      "gradients; falling back to one all-reduce after backward (PDA_DP_SEGMENTS=0) "
+                      "and re-syncing every replica from replica 0", RuntimeWarning)
+        self._force_single_segment = True
+        self._graphs = None      # re-captured without split points at the next step
+        m0 = self.module
+        opt0 = optimizer.opts[0] if hasattr(optimizer, "opts") else None
+        for i, r in enumerate(self.replicas):
+            with torch.cuda.device(r.device):
+                r.flat_params.copy_(m0.flat_params)
+                r.flat_bufstore.copy_(m0.flat_bufstore)
+                if opt0 is not None:
+                    optimizer.opts[i + 1].flat_mom.copy_(opt0.flat_mom)
+                r.refresh_shadow()
+        for d in self.device_ids:
+            torch.cuda.synchronize(d)
 
     def _segment_bounds(self) -> List[int]:
         """Where each replica graph is split (``PDA_DP_SEGMENTS``): "stage" (default) after the
@@ -316,7 +357,8 @@ class DataParallel(nn.Module):
         mode = os.environ.get("PDA_DP_SEGMENTS", "stage")
         if mode not in ("stage", "0"):
             raise ValueError(f"PDA_DP_SEGMENTS={mode!r}: expected stage or 0")
-        if mode == "0" or not self.replicas or not hasattr(self.module, "stage_bounds"):
+        if (mode == "0" or getattr(self, "_force_single_segment", False) or not self.replicas
+                or not hasattr(self.module, "stage_bounds")):
             return []
         return self.module.stage_bounds()
 
@@ -490,6 +532,11 @@ class _ReplicaGraph:
                         self._body()
                         self.graphs[-1].capture_end()
                         ended = True
+                        if len(self.graphs) != len(self.splits) + 1:
+                            # a split offset the backward never reported: the gradient past the
+                            # last segment bound would never be all-reduced
+                            raise RuntimeError(f"replica capture produced {len(self.graphs)} "
+                                               f"segments for {len(self.splits)} split points")
                     except BaseException:
                         if not ended:   # leave no capture open on the stream
                             try:

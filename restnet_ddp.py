@@ -18,10 +18,15 @@ def main(local_rank, script="ddp", nprocs=None):
 def launch(script="ddp"):
     os.environ.update(parse_cli(sys.argv[1:]))   # optional flags -> MX_* env (inherited by ranks)
     if "LOCAL_RANK" in os.environ:            # started by torchrun
-        main(int(os.environ["LOCAL_RANK"]), script)
+        lr = int(os.environ["LOCAL_RANK"])
+        if os.environ.get("PDA_BIND_NUMA", "1") != "0":
+            from pytorch_distributed_amd.launch import bind_numa
+            bind_numa(lr)                     # before any HIP call (sysfs only)
+        main(lr, script)
         return
-    import torch
-    nprocs = int(os.environ.get("MX_NPROCS", "0")) or max(torch.cuda.device_count(), 1)
+    from pytorch_distributed_amd.launch import visible_gpu_count
+    # counted from sysfs: no HIP call before each rank binds its NUMA node
+    nprocs = int(os.environ.get("MX_NPROCS", "0")) or max(visible_gpu_count(), 1)
     spawn(main, args=(script, nprocs), nprocs=nprocs, bind_numa=True)
 
 

@@ -21,16 +21,16 @@ def _port():
     return p
 
 
-def _run(nproc, extra_env=None, tmp=None):
+def _run(nproc, extra_env=None, tmp=None, extra_args=()):
     env = dict(os.environ)
     env.update({"OMP_NUM_THREADS": "2", "PDA_BIND_NUMA": "0"})
     env.update(extra_env or {})
     if nproc == 1:
-        cmd = [sys.executable, os.path.join(ROOT, "bench.py"), *ARGS]
+        cmd = [sys.executable, os.path.join(ROOT, "bench.py"), *ARGS, *extra_args]
     else:
         cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node",
                str(nproc), "--master-addr", "127.0.0.1", "--master-port", str(_port()),
-               os.path.join(ROOT, "bench.py"), "--gpus", str(nproc), *ARGS]
+               os.path.join(ROOT, "bench.py"), "--gpus", str(nproc), *ARGS, *extra_args]
     return subprocess.run(cmd, cwd=tmp, env=env, capture_output=True, text=True, timeout=600)
 
 
@@ -70,6 +70,66 @@ def test_bench_cpu_two_ranks_self_validation(tmp_path):
     assert "DDP" in rec["amp_config"]
     assert isinstance(rec["comm_env"], dict) and rec["numa_bound"] is False
     assert "gpu_util_pct" in rec
+    # per-rank timed-region spread of each timed pass (a straggler rank is visible)
+    sp = rec["rank_time_spread"]
+    for k in ("headline", "amp_fp16"):
+        assert 0 < sp[k]["min_s"] <= sp[k]["max_s"] and sp[k]["spread_pct"] >= 0
+    assert abs(sp["headline"]["max_s"] * 1000.0 / rec["steps"] - rec["ms_per_step"]) < 0.1
+    assert rec["amp_dtype"] == "fp16"
+
+
+def test_bench_cpu_four_ranks(tmp_path):
+    """World 4 (the driver's 8-GPU run has more ranks than any other rehearsal): one record, every
+    rank in the timing spread, weights bit-identical on all four ranks."""
+    r = _run(4, tmp=tmp_path, extra_args=("--amp-steps", "0", "--comm-probe", "0"))
+    assert r.returncode == 0, r.stderr[-4000:]
+    rec = _record(r)
+    assert rec["n_gpus"] == 4 and rec["config"]["global_batch"] == 8
+    assert rec["config"]["parallelism"] == "dp4"
+    assert rec["weights_consistent"] is True
+    assert abs(rec["value"] - 8 * 1000.0 / rec["ms_per_step"]) / rec["value"] < 1e-2
+    sp = rec["rank_time_spread"]["headline"]
+    assert 0 < sp["min_s"] <= sp["max_s"]
+
+
+def test_numa_binding_precedes_any_hip_call(monkeypatch, tmp_path):
+    """bench.py binds a rank to its GPU's NUMA node before HIP starts (its runtime threads inherit
+    the affinity the process has then): the GPU count comes from the KFD topology in sysfs, and no
+    torch.cuda entry point that initialises HIP runs before bind_numa."""
+    import importlib.util
+    import torch
+    from pytorch_distributed_amd import launch
+    # a fake KFD topology: one CPU node, two GPU nodes
+    for i, simd in enumerate((0, 304, 304)):
+        d = tmp_path / "nodes" / str(i)
+        d.mkdir(parents=True)
+        (d / "properties").write_text(f"simd_count {simd}\ndomain 0\nlocation_id {256 * (i + 1)}\n")
+    monkeypatch.setattr(launch, "_KFD_ROOT", str(tmp_path / "nodes"))
+    for var in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        monkeypatch.delenv(var, raising=False)
+    calls = []
+
+    def no_hip(name):
+        def f(*a, **k):
+            raise AssertionError(f"torch.cuda.{name} called before the NUMA binding")
+        return f
+    for name in ("device_count", "is_available", "init", "_lazy_init", "set_device",
+                 "current_device", "synchronize"):
+        monkeypatch.setattr(torch.cuda, name, no_hip(name))
+    monkeypatch.setattr(launch, "bind_numa", lambda lr: calls.append(lr) or True)
+    monkeypatch.setenv("WORLD_SIZE", "2")
+    monkeypatch.setenv("LOCAL_RANK", "1")
+    monkeypatch.delenv("PDA_BIND_NUMA", raising=False)
+    spec = importlib.util.spec_from_file_location("bench_under_test", os.path.join(ROOT, "bench.py"))
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+    args = type("A", (), {"nccl_channels": 0, "nccl_proto": "", "nccl_algo": "", "device": "cuda"})()
+    out = bench._configure_process(args)
+    assert calls == [1] and out["numa_bound"] is True
+    assert launch.visible_gpu_count() == 2
+    monkeypatch.setenv("HIP_VISIBLE_DEVICES", "1")
+    assert launch.visible_gpu_count() == 1
+    assert launch.gpu_pci_bdf(0) == "0000:03:00.0"     # visible 0 = physical GPU 1 (node 2)
 
 
 def test_bench_cpu_diverged_rank_fails(tmp_path):

@@ -303,4 +303,8 @@ def test_ddp_step_costs_no_more_than_bare_step(tmp_path):
     res = {l.split(" ", 1)[0]: json.loads(l.split(" ", 1)[1]) for l in r.stdout.splitlines()
            if l.startswith(("bare_", "ddp_"))}
     bare, ddp = res["bare_nosync"]["ms"], res["ddp_nosync"]["ms"]
-    assert ddp < 1.1 * bare + 1.0, res
+    # the ratio itself is a measurement (printed; profiles/ddp_overhead_r3.md records +0.5 %); the
+    # assertion only guards the regression it targets (+13-15 ms/step), so a shared or loaded box
+    # cannot fail it with no code change
+    print(f"DDP step {ddp:.2f} ms vs bare {bare:.2f} ms ({100.0 * (ddp / bare - 1.0):+.1f} %)")
+    assert ddp < bare + 8.0, res

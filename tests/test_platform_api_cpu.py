@@ -78,3 +78,35 @@ def test_bind_numa_respects_allowed_cpus():
     if not changed:
         assert after == before
     os.sched_setaffinity(0, before)
+
+
+def test_nccl_shim_uses_the_framework_communicator(monkeypatch):
+    """Once DDP has registered the process's device communicator, ``hfai.nccl.distributed``'s
+    reduce / all_reduce / broadcast on that device go through it (no second communicator); a
+    ``group`` argument or an op it lacks goes to torch."""
+    from pytorch_distributed_amd.parallel import comm as C
+    calls = []
+
+    class Fake:
+        def reduce(self, t, dst, op):
+            calls.append(("reduce", dst, op))
+
+        def all_reduce(self, t, op="sum"):
+            calls.append(("all_reduce", op))
+
+        def broadcast(self, t, src=0):
+            calls.append(("broadcast", src))
+
+    monkeypatch.setattr(C, "_DEFAULTS", {})
+    C.register_default(Fake(), torch.device("cpu"))
+    x = torch.zeros(4)
+    dist.reduce(x, 0)
+    dist.all_reduce(x, op=dist.ReduceOp.MAX)
+    assert dist.broadcast(x, 1, async_op=True).wait()
+    assert calls == [("reduce", 0, "sum"), ("all_reduce", "max"), ("broadcast", 1)]
+    torch_calls = []
+    monkeypatch.setattr(torch.distributed, "all_reduce",
+                        lambda t, op=None, group=None, async_op=False: torch_calls.append(op))
+    dist.all_reduce(x, op=dist.ReduceOp.PRODUCT)          # not a native op -> torch
+    dist.all_reduce(x, group=object())                     # explicit group -> torch
+    assert len(torch_calls) == 2 and len(calls) == 3
