@@ -1133,20 +1133,29 @@ int pda_bn_finalize_tot(const double* tot, int C, double count, const float* gam
 
 // Partial statistics -> BatchNorm coefficients in one launch (bn_stats_kernel). slabs: f64 >=
 // S * nq * C; cnt: int32 >= ceil(C / 256), zero (and left zero). Returns -2 on a bad shape.
+// cg: channels per block group (a power of two in [4, 256]; 0 = 256). Fewer channels per group
+// give each channel quad more lanes (SL = 1024 / cg): shorter serial chains in both levels.
+static int stats_cg(int C, int cg) {
+  if (cg <= 0 || cg > 256 || (cg & (cg - 1)) || cg < 4) cg = 256;
+  return C < cg ? C : cg;
+}
+
 int pda_bn_fwd_stats(const float* part, int T, int C, int bm, int M, int S, double* slabs, int* cnt,
-                     const BnFwdOut* o, hipStream_t st) {
+                     const BnFwdOut* o, int cg, hipStream_t st) {
   if ((C & 3) || S <= 0 || S > T || !o || !cnt || !slabs) return -2;
-  const int CG = C < 256 ? C : 256;
+  const int CG = stats_cg(C, cg);
+  if (C % CG) return -2;
   hipLaunchKernelGGL((bn_stats_kernel<0, 2, BnFwdOut>), dim3(S, (C + CG - 1) / CG), dim3(256), 0, st,
                      part, T, C, bm, M, CG, slabs, cnt, *o);
   return (int)hipGetLastError();
 }
 
 int pda_bn_bwd_stats(const float* part, int T, int nq, int C, int S, double* slabs, int* cnt,
-                     const BnBwdOut* o, hipStream_t st) {
+                     const BnBwdOut* o, int cg, hipStream_t st) {
   if ((C & 3) || S <= 0 || S > T || !o || !cnt || !slabs || !o->k || (nq != 2 && nq != 3))
     return -2;
-  const int CG = C < 256 ? C : 256;
+  const int CG = stats_cg(C, cg);
+  if (C % CG) return -2;
   const dim3 grid(S, (C + CG - 1) / CG);
   if (nq == 2)
     hipLaunchKernelGGL((bn_stats_kernel<1, 2, BnBwdOut>), grid, dim3(256), 0, st, part, T, C, 0, 0, CG,

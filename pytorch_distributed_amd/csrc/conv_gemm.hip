@@ -46,7 +46,15 @@ template <int N> __device__ __forceinline__ void vm_wait() {
 // WGRAD_BNA: WGRAD whose A operand is the BatchNorm-backward output formed while staging,
 // dY = k1[c]*dz + k2[c]*y + k3[c] (a = dz, a2 = y): the stem's weight gradient is the only consumer
 // of its BN-backward output, so the apply pass (and dY's write + re-read) is skipped.
-enum Pass : int { FWD = 0, DGRAD = 1, WGRAD = 2, WGRAD_BNA = 3 };
+//
+// DGRAD_BNF: DGRAD of a 1x1 conv whose dY is a BatchNorm-backward output that is never
+// materialised (the consumer-side fold of a bottleneck tail, csrc/conv_gemm.hip bn_fold_kernel):
+// dY = k1*dz + k2*y + k3 with y = a2 . W^T (the conv's own forward), so
+//   dX = dz . (k1 o W) + a2 . G + b,   G = W^T diag(k2) W,  b = W^T k3:
+// the K loop runs over dz's Cout channels against rows [0, Cout) of B = [k1 o W ; G] and then over
+// xa_c channels of the Gram operand xa (a2, formed by the BN+ReLU prologue of the forward when
+// xa_sc is set) read at the dX pixel against rows [Cout, Cout + xa_c); the epilogue adds b.
+enum Pass : int { FWD = 0, DGRAD = 1, WGRAD = 2, WGRAD_BNA = 3, DGRAD_BNF = 4 };
 
 template <int V> struct IC { static constexpr int value = V; };
 
@@ -88,6 +96,10 @@ struct ConvParams {
   float* epart;                    // [ncls*tiles_m][enq][N] partial sums
   const void* a2;                  // WGRAD_BNA: y (the BN input) beside a = dz
   const float* ak1; const float* ak2; const float* ak3;   // WGRAD_BNA: per-Cout coefficients
+  // DGRAD_BNF: the Gram operand (xa_c channels at the dX pixel; BN+ReLU applied when xa_sc is set)
+  // and the epilogue bias b[N]
+  const void* xa; const float* xa_sc; const float* xa_sh; const float* dbias;
+  int xa_c;
   // FWD BatchNorm statistics (stats != nullptr) are per-M-tile SHIFTED partials
   // stats[tile][3][N] = (sum(y - s), sum((y - s)^2), s), s = the tile's first row (no f32
   // cancellation when |mean| >> std); bn.hip bn_fwd_stats combines and finalizes them.
@@ -183,9 +195,11 @@ template <int PASS_T, int DT, int BM, int BN, int STAGES>
 // WGRAD_BNA holds the fixed column chunk's 24 BN coefficients and the y chunks: 3 blocks per CU
 // (the 16-bit WGRAD budget of 4 spilled 15 VGPRs); its 256-column tile (the stem's whole N: dz and
 // y staged and transformed once instead of once per 128-column tile) needs 246: 2 blocks per CU
-__global__ __launch_bounds__(conv_nt<STAGES>(), (PASS_T == WGRAD_BNA ? (BN >= 256 ? 2 : 3) : conv_min_blocks<DT, BM, BN, STAGES>())) void conv_gemm_kernel(ConvParams p_arg) {
-  constexpr int PASS = PASS_T == WGRAD_BNA ? WGRAD : PASS_T;
+// (the 128x128 WGRAD_BNA tile of the bottleneck conv3 fold: 2 blocks, 3 spilled 89 VGPRs)
+__global__ __launch_bounds__(conv_nt<STAGES>(), (PASS_T == WGRAD_BNA ? (BN >= 256 || BM * BN >= 128 * 128 ? 2 : 3) : conv_min_blocks<DT, BM, BN, STAGES>())) void conv_gemm_kernel(ConvParams p_arg) {
+  constexpr int PASS = PASS_T == WGRAD_BNA ? WGRAD : PASS_T == DGRAD_BNF ? DGRAD : PASS_T;
   constexpr bool ABN = PASS_T == WGRAD_BNA;
+  constexpr bool BNF = PASS_T == DGRAD_BNF;
   constexpr bool DMA = STAGES >= 3;
   // STAGES == 4 (HALO): tap reuse for 3x3 stride-1 FWD / DGRAD -- see the HALO main loop
   constexpr bool HALO = STAGES == 4;
@@ -195,6 +209,7 @@ __global__ __launch_bounds__(conv_nt<STAGES>(), (PASS_T == WGRAD_BNA ? (BN >= 25
   constexpr int WN = (NTH / 64) / WM;
   static_assert(!DMA || ((DT == DT_BF16 || DT == DT_F16) && !ABN), "LDS-DMA: 16-bit");
   static_assert(!ABN || DT == DT_BF16 || DT == DT_F16, "WGRAD_BNA: 16-bit operands");
+  static_assert(!BNF || ((DT == DT_BF16 || DT == DT_F16) && !DMA), "DGRAD_BNF: 16-bit, register-staged");
   // DGRAD / WGRAD read the parameters in place in the kernarg segment (constant address space):
   // binding a reference to the by-value argument makes the compiler copy the whole ~1 KB block to
   // scratch once a member array is indexed dynamically (DGRAD tap tables), and costs WGRAD spills.
@@ -276,6 +291,7 @@ __global__ __launch_bounds__(conv_nt<STAGES>(), (PASS_T == WGRAD_BNA ? (BN >= 25
     cls_pw = split & 1;
     ntap = p.ntaps[split];
     kend = ntap * p.Cout;
+    if (BNF && ntap > 0) kend += p.xa_c;   // the Gram operand's k-tiles (landing classes only)
   }
   const int nk = (kend - kbeg + BKE - 1) / BKE;
 
@@ -287,6 +303,7 @@ __global__ __launch_bounds__(conv_nt<STAGES>(), (PASS_T == WGRAD_BNA ? (BN >= 25
   // A (ROW: FWD gather from X, DGRAD gather from dY): rows tid/8 + 32*i, chunk tid&7
   constexpr uint32_t OOB = 0x80000000u;
   int a_base[AR];           // byte offset of the row's tap-(0,0) pixel (FWD/DGRAD), may be < 0
+  uint32_t xa_base[BNF ? AR : 1];   // DGRAD_BNF: byte offset of the row's dX pixel in xa
   uint64_t a_mask[AR];      // bit t: tap t (FWD, R*S <= 64) / class tap t (DGRAD) is inside the image
   uint32_t a_off[AR];       // WGRAD: byte offset of (krow, col) at k0 = kbeg
   int a_krow[AR];
@@ -315,6 +332,10 @@ __global__ __launch_bounds__(conv_nt<STAGES>(), (PASS_T == WGRAD_BNA ? (BN >= 25
           if ((unsigned)((int)yi + p.tdy[split][t]) < (unsigned)p.Ho &&
               (unsigned)((int)xi + p.tdx[split][t]) < (unsigned)p.Wo)
             msk |= 1ull << t;
+        }
+        if constexpr (BNF) {
+          const uint32_t h = yi * p.stride + cls_ph, w = xi * p.stride + cls_pw;
+          xa_base[i] = ((img * p.H + h) * p.W + w) * (uint32_t)p.xa_c * (uint32_t)ES;
         }
       }
       a_mask[i] = okm ? msk : 0ull;
@@ -378,7 +399,7 @@ __global__ __launch_bounds__(conv_nt<STAGES>(), (PASS_T == WGRAD_BNA ? (BN >= 25
     b_bytes = (uint32_t)p.N * p.Kpad * (uint32_t)ES;
   } else if constexpr (PASS == DGRAD) {
     a_bytes = (uint32_t)p.Nb * p.Ho * p.Wo * p.Cout * (uint32_t)ES;
-    b_bytes = (uint32_t)p.Cout * p.R * p.S * p.Cin * (uint32_t)ES;
+    b_bytes = (uint32_t)(p.Cout + (BNF ? p.xa_c : 0)) * p.R * p.S * p.Cin * (uint32_t)ES;
   } else {
     a_bytes = (uint32_t)p.K * p.Cout * (uint32_t)ES;
     b_bytes = (uint32_t)p.Nb * p.H * p.W * p.Cin * (uint32_t)ES;
@@ -396,6 +417,11 @@ __global__ __launch_bounds__(conv_nt<STAGES>(), (PASS_T == WGRAD_BNA ? (BN >= 25
       const_cast<void*>(ABN ? p.a2 : p.a), (short)0, (int)a_bytes, 0x00020000);
   i32x4 ray[ABN ? AR : 1];
   bool av[ABN ? AR : 1];
+  // DGRAD_BNF: the Gram operand (the dX-resolution tensor, xa_c channels)
+  const __amdgpu_buffer_rsrc_t rsx = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<void*>(BNF ? p.xa : p.a), (short)0,
+      BNF ? (int)((uint32_t)p.Nb * p.H * p.W * p.xa_c * (uint32_t)ES) : (int)a_bytes, 0x00020000);
+  bool xt = false;   // DGRAD_BNF: the tile in the staging registers is a Gram-operand tile
 
   i32x4 ra[AR], rb[BR];
   i32x4 ra2[SPLIT ? AR : 1], rb2[SPLIT ? BR : 1];   // DT_F32S: elements 4..7 of each chunk
@@ -409,15 +435,17 @@ __global__ __launch_bounds__(conv_nt<STAGES>(), (PASS_T == WGRAD_BNA ? (BN >= 25
   };
   // prologue state: per-chunk validity (padding must stay 0) and the chunk's 8 channel coeffs
   const bool pro = (PASS == FWD || PASS == WGRAD) && p.pro_sc != nullptr;
-  bool pv[PASS == FWD ? AR : BR];
+  const bool xpro = BNF && p.xa_sc != nullptr;   // DGRAD_BNF: BN+ReLU on the Gram operand
+  bool pv[PASS == WGRAD ? BR : AR];
   f32x2 psc[4], psh[4];
-  auto pro_coeffs = [&](int c) __attribute__((always_inline)) {
+  auto pro_coeffs_of = [&](const float* sc, const float* sh, int c) __attribute__((always_inline)) {
 #pragma unroll
     for (int k = 0; k < EPC / 2; ++k) {
-      psc[k] = *reinterpret_cast<const f32x2*>(p.pro_sc + c + 2 * k);
-      psh[k] = *reinterpret_cast<const f32x2*>(p.pro_sh + c + 2 * k);
+      psc[k] = *reinterpret_cast<const f32x2*>(sc + c + 2 * k);
+      psh[k] = *reinterpret_cast<const f32x2*>(sh + c + 2 * k);
     }
   };
+  auto pro_coeffs = [&](int c) __attribute__((always_inline)) { pro_coeffs_of(p.pro_sc, p.pro_sh, c); };
   if (PASS == WGRAD && pro) pro_coeffs(wb_colok ? wb_c : 0);
   // relu on the packed 16-bit result: bf16/f16 are sign-magnitude, so a signed 16-bit max with 0
   // zeroes exactly the negative values (and -0) -- one v_pk_max_i16 per pair
@@ -501,15 +529,28 @@ __global__ __launch_bounds__(conv_nt<STAGES>(), (PASS_T == WGRAD_BNA ? (BN >= 25
         if (pro) pro_coeffs(c);
       }
     } else if constexpr (PASS == DGRAD) {
-      // tile lies in one tap (Cout % 64 == 0); scalar shift instead of a scalar division
-      const int ti = p.log2Cout >= 0 ? k0 >> p.log2Cout : k0 / p.Cout;
-      const int c = k0 - ti * p.Cout + (tid & 7) * EPC;
-      const int tsel = ti < 9 ? ti : 0;
-      const int toff = ((p.tdy[split][tsel] * p.Wo + p.tdx[split][tsel]) * p.Cout + c) * ES;
+      if (BNF && k0 >= ntap * p.Cout) {   // Gram-operand tile: xa at the dX pixel
+        const int c = k0 - ntap * p.Cout + (tid & 7) * EPC;
 #pragma unroll
-      for (int i = 0; i < AR; ++i) {
-        const bool ok = ((uint32_t)a_mask[i] >> ti) & 1u;
-        lda(i, ok ? (uint32_t)(a_base[i] + toff) : OOB);
+        for (int i = 0; i < AR; ++i) {
+          const bool ok = ((uint32_t)a_mask[i]) & 1u;   // valid row (1x1: its tap lands)
+          ra[i] = bld(rsx, ok ? xa_base[i] + (uint32_t)(c * ES) : OOB);
+          pv[i] = ok;
+        }
+        if (xpro) pro_coeffs_of(p.xa_sc, p.xa_sh, c);
+        xt = true;
+      } else {
+        // tile lies in one tap (Cout % 64 == 0); scalar shift instead of a scalar division
+        const int ti = p.log2Cout >= 0 ? k0 >> p.log2Cout : k0 / p.Cout;
+        const int c = k0 - ti * p.Cout + (tid & 7) * EPC;
+        const int tsel = ti < 9 ? ti : 0;
+        const int toff = ((p.tdy[split][tsel] * p.Wo + p.tdx[split][tsel]) * p.Cout + c) * ES;
+#pragma unroll
+        for (int i = 0; i < AR; ++i) {
+          const bool ok = ((uint32_t)a_mask[i] >> ti) & 1u;
+          lda(i, ok ? (uint32_t)(a_base[i] + toff) : OOB);
+        }
+        if constexpr (BNF) xt = false;
       }
     } else {  // WGRAD A: dY rows m (k), cols n1 (COL tile [64][BM])
       const uint32_t koff = (uint32_t)(kt * BKE * p.Cout) * (uint32_t)ES;
@@ -530,7 +571,8 @@ __global__ __launch_bounds__(conv_nt<STAGES>(), (PASS_T == WGRAD_BNA ? (BN >= 25
     } else if constexpr (PASS == DGRAD) {
       const int ti = p.log2Cout >= 0 ? k0 >> p.log2Cout : k0 / p.Cout;
       const int tap = p.taps[split][ti < 9 ? ti : 0];
-      const uint32_t uoff = (uint32_t)(((k0 - ti * p.Cout) * p.R * p.S + tap) * p.Cin) * (uint32_t)ES;
+      uint32_t uoff = (uint32_t)(((k0 - ti * p.Cout) * p.R * p.S + tap) * p.Cin) * (uint32_t)ES;
+      if (BNF && k0 >= ntap * p.Cout) uoff = (uint32_t)(k0 * p.Cin) * (uint32_t)ES;   // rows of G (1x1)
 #pragma unroll
       for (int i = 0; i < BR; ++i) ldb(i, b_off[i] + uoff);
     } else if (wb_direct) {  // WGRAD B, 1x1 stride-1 conv: X rows ARE the GEMM rows
@@ -573,6 +615,9 @@ __global__ __launch_bounds__(conv_nt<STAGES>(), (PASS_T == WGRAD_BNA ? (BN >= 25
           } else {
             if (pro && pv[i]) pro_apply(ra[i]);
           }
+        }
+        if constexpr (BNF) {
+          if (xt && xpro && pv[i]) pro_apply(ra[i]);
         }
         const int addr = row_addr((tid >> 3) + 32 * i, tid & 7);
         if constexpr (SPLIT) split_put(sa, addr, ra[i], ra2[i]);
@@ -1116,6 +1161,9 @@ __global__ __launch_bounds__(conv_nt<STAGES>(), (PASS_T == WGRAD_BNA ? (BN >= 25
       for_items([&](int rl, int cl, f32x4 v) {
         const int col = wc * (BN / WN) + cl;
         const int row = wr * (BM / WM) + rl;
+        if constexpr (BNF) {   // b = W^T k3 where the class has a tap (a 1x1 conv's landing pixels)
+          if (ntap > 0 && n0 + col < p.N) v += *reinterpret_cast<const f32x4*>(p.dbias + n0 + col);
+        }
         if (relu) v = __builtin_elementwise_max(v, (f32x4){0.f, 0.f, 0.f, 0.f});
         // row & (CPR-1) == lr & (CPR-1) for CPR <= 16 (folded); BN = 256 needs the full row
         const int cbyte = (((col >> 3) ^ (row & (CPR - 1))) << 4) + ((col & 4) << 1);
@@ -1404,6 +1452,109 @@ __global__ __launch_bounds__(256) void wgrad_reduce4_kernel(const float* __restr
   }
 }
 
+
+// Consumer-side BatchNorm-backward fold (DGRAD_BNF operands) in ONE launch. W: the conv's 16-bit
+// weights [Cout][Cin] (1x1, OHWI); k: [k1; k2; k3] (3 x Cout f32, the BN-backward apply
+// coefficients of the BN after the conv). Writes Wf = [k1 o W ; G] ([Cout + Cin][Cin] 16-bit),
+// G = W^T diag(k2) W, and b = W^T k3 (f32 [Cin]).
+// Block (ti, tj) computes the 64x64 tile G[ti*64.., tj*64..] over K = Cout on MFMA 16x16x32: the
+// k-tiles of W's column panels ti (A) and tj (B, scaled by k2 per row while staging) go to LDS in
+// the conv kernel's COL layout and are read back by the same transposed fragment loads. The blocks
+// with ti == 0 also write the k1-scaled rows of their column panel and its bias (per-thread f32
+// partials over fixed row sets, combined in a fixed order: deterministic).
+template <int DT>
+__global__ __launch_bounds__(256) void bn_fold_kernel(const u16* __restrict__ W, const float* __restrict__ k,
+                                                      int Cout, int Cin, u16* __restrict__ Wf,
+                                                      float* __restrict__ bias) {
+  __shared__ __attribute__((aligned(16))) char smem[2 * 64 * 64 * 2];
+  __shared__ float bred[32][64];
+  const int nT = Cin >> 6;
+  const int ti = blockIdx.x / nT, tj = blockIdx.x - ti * nT;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wr = wid >> 1, wc = wid & 1;
+  const float* k1 = k;
+  const float* k2 = k + Cout;
+  const float* k3 = k + 2 * Cout;
+  const bool side = ti == 0;   // this block also writes the k1 rows and the bias of panel tj
+  char* sa = smem;
+  char* sb = smem + 64 * 64 * 2;
+  f32x4 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float bs[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) bs[e] = 0.f;
+  const int cc = tid & 7;   // the thread's 16-B chunk (8 columns) of a 64-column panel row
+  for (int k0 = 0; k0 < Cout; k0 += 64) {
+#pragma unroll
+    for (int r = 0; r < 2; ++r) {
+      const int krow = (tid >> 3) + 32 * r;
+      const int kk = k0 + krow;
+      const i32x4 va = *reinterpret_cast<const i32x4*>(W + (size_t)kk * Cin + ti * 64 + cc * 8);
+      const i32x4 vb = *reinterpret_cast<const i32x4*>(W + (size_t)kk * Cin + tj * 64 + cc * 8);
+      const float s2 = k2[kk];
+      i32x4 wb;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const f32x2 f = unpack2<DT>((uint32_t)vb[q]);
+        wb[q] = (int)pack2<DT>(f32x2{f.x * s2, f.y * s2});
+      }
+      *reinterpret_cast<i32x4*>(sa + col_addr<64>(krow, cc)) = va;
+      *reinterpret_cast<i32x4*>(sb + col_addr<64>(krow, cc)) = wb;
+      if (side) {   // k1 o W rows and the bias partials of panel tj
+        const float s1 = k1[kk], s3 = k3[kk];
+        i32x4 w1;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const f32x2 f = unpack2<DT>((uint32_t)vb[q]);
+          w1[q] = (int)pack2<DT>(f32x2{f.x * s1, f.y * s1});
+          bs[2 * q] = __builtin_fmaf(s3, f.x, bs[2 * q]);
+          bs[2 * q + 1] = __builtin_fmaf(s3, f.y, bs[2 * q + 1]);
+        }
+        *reinterpret_cast<i32x4*>(Wf + (size_t)kk * Cin + tj * 64 + cc * 8) = w1;
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      s16x8 fa[2], fb[2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) fa[i] = frag_col<64>(sa, wr * 32 + i * 16, s, lane);
+#pragma unroll
+      for (int j = 0; j < 2; ++j) fb[j] = frag_col<64>(sb, wc * 32 + j * 16, s, lane);
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j] = mfma16<DT>(fb[j], fa[i], acc[i][j]);
+    }
+    __syncthreads();
+  }
+  // acc[i][j][e] = G[ti*64 + wr*32 + i*16 + (lane&15)][tj*64 + wc*32 + j*16 + 4*(lane>>4) + e]
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int row = ti * 64 + wr * 32 + i * 16 + (lane & 15);
+      const int col = tj * 64 + wc * 32 + j * 16 + 4 * (lane >> 4);
+      uint2 pk;
+      pk.x = pack2<DT>(f32x2{acc[i][j][0], acc[i][j][1]});
+      pk.y = pack2<DT>(f32x2{acc[i][j][2], acc[i][j][3]});
+      *reinterpret_cast<uint2*>(Wf + (size_t)(Cout + row) * Cin + col) = pk;
+    }
+  if (!side) return;
+  // bias: thread (row set tid>>3, chunk cc) holds 8 column partials; fixed-order combine
+#pragma unroll
+  for (int e = 0; e < 8; ++e) bred[tid >> 3][cc * 8 + e] = bs[e];
+  __syncthreads();
+  if (tid < 64) {
+    float b = 0.f;
+    for (int g = 0; g < 32; ++g) b += bred[g][tid];
+    bias[tj * 64 + tid] = b;
+  }
+}
+
 }  // namespace
 
 // ================================================================= host launchers (C ABI)
@@ -1423,7 +1574,7 @@ struct ConvDesc {  // mirrors pytorch_distributed_amd/ops/ext.py ConvDesc
 
 template <int PASS, int DT, int BM, int BN, int ST>
 static int launch(const ConvParams& p, dim3 grid, hipStream_t st) {
-  if constexpr (PASS == WGRAD_BNA && DT != DT_BF16 && DT != DT_F16) {
+  if constexpr ((PASS == WGRAD_BNA || PASS == DGRAD_BNF) && DT != DT_BF16 && DT != DT_F16) {
     return -1;
   } else {
     hipLaunchKernelGGL((conv_gemm_kernel<PASS, DT, BM, BN, ST>), grid, dim3(conv_nt<ST>()), 0, st, p);
@@ -1548,12 +1699,8 @@ struct BnEpi {  // mirrors ops/ext.py BnEpi
   const void* mask;
 };
 
-int pda_conv_dgrad(const ConvDesc* d, const void* dy, const void* w, void* dx, const BnEpi* epi,
-                   int dt, int bm, int bn, hipStream_t st) {
-  if (!fits32((long long)d->Nb * d->Ho * d->Wo * d->Cout, (long long)d->Cout * d->R * d->S * d->Cin,
-              (long long)d->Nb * d->H * d->W * d->Cin, dt))
-    return -4;
-  ConvParams p{};
+static int dgrad_params(ConvParams& p, const ConvDesc* d, const void* dy, const void* w, void* dx,
+                        const BnEpi* epi) {
   fill_geom(p, *d);
   p.a = dy; p.b = w; p.out = dx;
   p.emode = -1;
@@ -1590,9 +1737,67 @@ int pda_conv_dgrad(const ConvDesc* d, const void* dy, const void* w, void* dx, c
     }
   }
   p.K = 0;
+  return 0;
+}
+
+int pda_conv_dgrad(const ConvDesc* d, const void* dy, const void* w, void* dx, const BnEpi* epi,
+                   int dt, int bm, int bn, hipStream_t st) {
+  if (!fits32((long long)d->Nb * d->Ho * d->Wo * d->Cout, (long long)d->Cout * d->R * d->S * d->Cin,
+              (long long)d->Nb * d->H * d->W * d->Cin, dt))
+    return -4;
+  ConvParams p{};
+  const int rc = dgrad_params(p, d, dy, w, dx, epi);
+  if (rc) return rc;
   const int abm = tile_bm(bm);
   const int tiles = ((p.M + abm - 1) / abm) * ((p.N + bn - 1) / bn);
-  return dispatch<DGRAD>(dt, bm, bn, p, dim3(tiles, ncls), st);
+  return dispatch<DGRAD>(dt, bm, bn, p, dim3(tiles, d->stride * d->stride), st);
+}
+
+// DGRAD of a 1x1 conv whose dY = k1*dz + k2*y + k3 is folded (see DGRAD_BNF): dz [Nb,Ho,Wo,Cout];
+// wf = [k1 o W ; G] ([Cout + Cin][Cin], pda_bn_fold); xa [Nb,H,W,Cin] the Gram operand (the conv's
+// forward input; xa_sc / xa_sh: its BN+ReLU prologue, or null); dbias [Cin] f32. Register-staged
+// tiles (-128, 64), (-128, 128), (64, 64), (64, 128); -1 otherwise.
+int pda_conv_dgrad_bnf(const ConvDesc* d, const void* dz, const void* wf, void* dx, const BnEpi* epi,
+                       const void* xa, const float* xa_sc, const float* xa_sh, const float* dbias,
+                       int dt, int bm, int bn, hipStream_t st) {
+  if (dt != DT_BF16 && dt != DT_F16) return -1;
+  if (d->R != 1 || d->S != 1 || d->pad != 0 || (d->Cin % 64) || !xa || !dbias) return -2;
+  if (!fits32((long long)d->Nb * d->Ho * d->Wo * d->Cout, (long long)(d->Cout + d->Cin) * d->Cin,
+              (long long)d->Nb * d->H * d->W * d->Cin, dt))
+    return -4;
+  ConvParams p{};
+  const int rc = dgrad_params(p, d, dz, wf, dx, epi);
+  if (rc) return rc;
+  p.xa = xa; p.xa_sc = xa_sc; p.xa_sh = xa_sh; p.dbias = dbias; p.xa_c = d->Cin;
+  const int abm = tile_bm(bm);
+  const dim3 grid(((p.M + abm - 1) / abm) * ((p.N + bn - 1) / bn), d->stride * d->stride);
+#define BNF_CASE(D, M_, N_, S_) \
+  if (dt == D && bm == (S_ == 1 ? -M_ : M_) && bn == N_) return launch<DGRAD_BNF, D, M_, N_, S_>(p, grid, st);
+#ifndef CONV_DMA_ONLY
+  BNF_CASE(DT_BF16, 128, 64, 1) BNF_CASE(DT_BF16, 128, 128, 1) BNF_CASE(DT_BF16, 64, 64, 2)
+  BNF_CASE(DT_BF16, 64, 128, 2)
+  BNF_CASE(DT_F16, 128, 64, 1) BNF_CASE(DT_F16, 128, 128, 1) BNF_CASE(DT_F16, 64, 64, 2)
+  BNF_CASE(DT_F16, 64, 128, 2)
+#endif
+#undef BNF_CASE
+  return -1;
+}
+
+// Wf = [k1 o W ; W^T diag(k2) W] and b = W^T k3 of a 1x1 conv (W [Cout][Cin] 16-bit, k = [k1;k2;k3]
+// 3 x Cout f32): the operands of pda_conv_dgrad_bnf. Cout, Cin multiples of 64.
+int pda_bn_fold(const void* w, const float* k, int Cout, int Cin, void* wf, float* bias, int dt,
+                hipStream_t st) {
+  if ((Cout % 64) || (Cin % 64) || Cin > 4096) return -2;
+  const dim3 grid((Cin / 64) * (Cin / 64));
+  if (dt == DT_BF16)
+    hipLaunchKernelGGL(bn_fold_kernel<DT_BF16>, grid, dim3(256), 0, st, (const u16*)w, k, Cout, Cin,
+                       (u16*)wf, bias);
+  else if (dt == DT_F16)
+    hipLaunchKernelGGL(bn_fold_kernel<DT_F16>, grid, dim3(256), 0, st, (const u16*)w, k, Cout, Cin,
+                       (u16*)wf, bias);
+  else
+    return -1;
+  return (int)hipGetLastError();
 }
 
 // As pda_conv_wgrad with dY formed while staging from the BatchNorm backward: dY = k1*dz + k2*y + k3
@@ -1620,6 +1825,9 @@ int pda_conv_wgrad_bna(const ConvDesc* d, const void* dz, const void* y, const f
 #ifndef CONV_DMA_ONLY
   BNA_CASE(DT_BF16, 64, 128, 1) BNA_CASE(DT_BF16, 64, 128, 2) BNA_CASE(DT_BF16, 64, 256, 1)
   BNA_CASE(DT_F16, 64, 128, 1) BNA_CASE(DT_F16, 64, 128, 2) BNA_CASE(DT_F16, 64, 256, 1)
+  // the bottleneck conv3 weight gradients of the consumer-side tail fold (DGRAD_BNF)
+  BNA_CASE(DT_BF16, 128, 128, 1) BNA_CASE(DT_BF16, 128, 128, 2) BNA_CASE(DT_BF16, 128, 64, 1)
+  BNA_CASE(DT_F16, 128, 128, 1) BNA_CASE(DT_F16, 128, 128, 2) BNA_CASE(DT_F16, 128, 64, 1)
 #endif
 #undef BNA_CASE
   return -1;

@@ -139,6 +139,8 @@ class NativeResNet(nn.Module):
         # stem wgrad forms its dY from the BN backward in-kernel (PDA_STEM_BNA=0: apply pass)
         self.stem_bna = os.environ.get("PDA_STEM_BNA", "1") != "0"
         self.tail_mask = True         # tails store the ReLU bitmask the backward reads
+        # consumer-side tail fold of the Bottleneck BN backward (see _block_backward)
+        self.bn_fold = os.environ.get("PDA_BN_FOLD", "0") != "0"
         self.ds_stream = True         # the shortcut conv runs on the second stream
         # weight gradients on a second HIP stream: nothing in the backward chain consumes them, so
         # the (compute-bound) wgrad GEMMs fill the CUs left idle by the (HBM-bound) BN-backward
@@ -814,9 +816,30 @@ class NativeResNet(nn.Module):
                 "bn_bwd_reduce")
         return dz, part, G, nq
 
+    def _tail_fold_ok(self, b: Block, Nb: int) -> bool:
+        """Whether block ``b``'s tail BatchNorm backward is folded into its last conv (the
+        consumer-side fold, PDA_BN_FOLD): 16-bit, a 1x1 last conv (Bottleneck conv3), per-rank
+        statistics (SyncBatchNorm keeps the reduce / all-reduce / finalize path) and a weight-gradient
+        plan the in-kernel BN operand (WGRAD_BNA) is built for."""
+        ul = b.units[-1]
+        if not self.bn_fold or self.f32 or ul.conv.kernel_size != (1, 1):
+            return False
+        sync = getattr(self.ws, "sync_comm", None)
+        if sync is not None and sync.world_size > 1:
+            return False
+        g = ul.geom(Nb)
+        return K.bnf_ok(g, self.dtype) and K.wgrad_bna_ok(g, Nb, self.dtype)
+
     def _block_backward(self, b: Block, rec, tail, prev, acc):
         """Returns (dx_main, shortcut_grad, prev_tail) -- the last is the fused reduction of the
-        previous block's tail, or None for the first block."""
+        previous block's tail, or None for the first block.
+
+        Tail fold (Bottleneck blocks, PDA_BN_FOLD=1): the tail BN-backward output dy3 = k1*dz +
+        k2*y3 + k3 is never materialised. Its two consumers take it from (dz, k): the conv3 weight
+        gradient forms dy3 while staging (WGRAD_BNA), and the conv3 data gradient runs
+        dX = dz . (k1 o W3) + a2 . G + W3^T k3 with G = W3^T diag(k2) W3 (y3 = a2 . W3^T is conv3's
+        own forward; csrc/conv_gemm.hip DGRAD_BNF, bn_fold_kernel) -- the apply pass (read dz and
+        y3, write dy3: three passes over the block's widest tensor) is gone from the chain."""
         ws = self.ws
         x = rec["x"]
         ys, acts, yd = rec["ys"], rec["acts"], rec["yd"]
@@ -825,7 +848,10 @@ class NativeResNet(nn.Module):
         ul = b.units[-1]
         sl = rec[f"s{n - 1}"]
         dz, part, G, nq = tail
-        dy = self._empty(*ys[-1].shape)
+        fold = self._tail_fold_ok(b, Nb)
+        kt = (torch.empty((nq - 1) * 3 * ul.cout, dtype=torch.float32, device=self.device)
+              if fold else None)
+        dy = None if fold else self._empty(*ys[-1].shape)
         sc_ev = None
         if b.ds is not None:
             sd = rec["sd"]
@@ -833,7 +859,7 @@ class NativeResNet(nn.Module):
             K.bn_bwd_finish(ws, part, G, nq, ys[-1], sl[0], sl[1], self.gamma(ul), self.dgamma(ul),
                             self.dbeta(ul), dz, dy, y2=yd, mean2=sd[0], invstd2=sd[1],
                             gamma2=self.gamma(b.ds), dgamma2=self.dgamma(b.ds), dbeta2=self.dbeta(b.ds),
-                            dy2_out=dyd, accumulate=acc)
+                            dy2_out=dyd, accumulate=acc, k_out=kt)
             # shortcut branch first: its dX is the second gradient source of the previous tail.
             # On the second stream its dgrad overlaps the conv3/conv2 chain; an event marks it for
             # the conv1 dgrad epilogue (or the stem) that consumes it
@@ -853,7 +879,7 @@ class NativeResNet(nn.Module):
                                                                     wscale=self.wgrad_scale), dyd, x)
         else:
             K.bn_bwd_finish(ws, part, G, nq, ys[-1], sl[0], sl[1], self.gamma(ul), self.dgamma(ul),
-                            self.dbeta(ul), dz, dy, accumulate=acc)
+                            self.dbeta(ul), dz, dy, accumulate=acc, k_out=kt)
             shortcut_g = dz
         dx_main = None
         prev_tail = None
@@ -862,25 +888,42 @@ class NativeResNet(nn.Module):
             u = b.units[j]
             a_in = acts[j]
             g = u.geom(Nb)
+            pro = None
             if a_in is None:   # fused prologue: recompute relu(bn(y_{j-1})) while staging B
                 sp_ = rec[f"s{j - 1}"]
                 a_in = ys[j - 1]
-                self._wgrad(lambda w, u=u, g=g, dy=dy, a=a_in, pro=(sp_[2], sp_[3]):
-                            K.conv_wgrad(dy, a, g, self.wgrad_view(u), w, accumulate=acc, pro=pro,
-                                         wscale=self.wgrad_scale),
-                            dy, a_in)
+                pro = (sp_[2], sp_[3])
+            bnf = None
+            if fold and j == n - 1:
+                # tail fold: (dz, k) stand for dy3 in both of conv3's gradients
+                k3 = kt[:3 * u.cout]
+                cin = u.conv.in_channels
+                wf = self._empty(u.cout + cin, cin)
+                fb = torch.empty(cin, dtype=torch.float32, device=self.device)
+                K.bn_fold(self.w16(u), k3, wf, fb)
+                bnf = (wf, fb)
+                self._wgrad(lambda w, u=u, g=g, a=a_in, pro=pro, y3=ys[-1], k3=k3:
+                            K.conv_wgrad(dz, a, g, self.wgrad_view(u), w, accumulate=acc, pro=pro,
+                                         bna=(y3, k3), wscale=self.wgrad_scale),
+                            dz, a_in, ys[-1], kt)
             else:
-                self._wgrad(lambda w, u=u, g=g, dy=dy, a=a_in:
-                            K.conv_wgrad(dy, a, g, self.wgrad_view(u), w, accumulate=acc,
+                self._wgrad(lambda w, u=u, g=g, dy=dy, a=a_in, pro=pro:
+                            K.conv_wgrad(dy, a, g, self.wgrad_view(u), w, accumulate=acc, pro=pro,
                                          wscale=self.wgrad_scale), dy, a_in)
+
+            def dgrad(out, epi=None, u=u, g=g, dy=dy, bnf=bnf, a_in=a_in, pro=pro):
+                if bnf is not None:
+                    K.conv_dgrad_bnf(dz, bnf[0], g, out, a_in, bnf[1], xa_pro=pro, epi=epi)
+                else:
+                    K.conv_dgrad(dy, self.w16_ohwi(u), g, out, epi=epi)
             out = self._empty(*a_in.shape)
             if j > 0:
                 up = b.units[j - 1]
                 sp = rec[f"s{j - 1}"]
-                Gp = K.dgrad_slabs(g, Nb, dtype=dy.dtype)
+                Gp = K.dgrad_slabs(g, Nb, dtype=ys[-1].dtype)
                 # the dgrad's epilogue produces dz and the BN-backward partials of bn_{j-1}
                 epi, part_p, nq_p = K.bn_epilogue(ws, Gp, ys[j - 1], sp[2], sp[3])
-                K.conv_dgrad(dy, self.w16_ohwi(u), g, out, epi=epi)      # out = dz of bn_{j-1}
+                dgrad(out, epi)                                      # out = dz of bn_{j-1}
                 dyp = self._empty(*ys[j - 1].shape)
                 K.bn_bwd_finish(ws, part_p, Gp, nq_p, ys[j - 1], sp[0], sp[1], self.gamma(up),
                                 self.dgamma(up), self.dbeta(up), out, dyp, accumulate=acc)
@@ -889,13 +932,13 @@ class NativeResNet(nn.Module):
                 pb, prec = prev
                 if sc_ev is not None:
                     cur.wait_event(sc_ev)
-                Gp = K.dgrad_slabs(g, Nb, dtype=dy.dtype)
+                Gp = K.dgrad_slabs(g, Nb, dtype=ys[-1].dtype)
                 epi, part_p, nq_p = K.bn_epilogue(ws, Gp, g2=shortcut_g,
                                                   **self._tail_args(pb, prec, use_mask=True))
-                K.conv_dgrad(dy, self.w16_ohwi(u), g, out, epi=epi)      # out = dz of prev tail
+                dgrad(out, epi)                                      # out = dz of prev tail
                 prev_tail = (out, part_p, Gp, nq_p)
             else:
-                K.conv_dgrad(dy, self.w16_ohwi(u), g, out)
+                dgrad(out)
                 dx_main = out
         if sc_ev is not None:   # the caller (next tail / stem backward) reads shortcut_g on main
             cur.wait_event(sc_ev)

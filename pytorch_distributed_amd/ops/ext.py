@@ -73,12 +73,15 @@ _V, _I, _F, _L, _U, _D = C.c_void_p, C.c_int, C.c_float, C.c_longlong, C.c_uint,
 _SIGS = {
     "pda_conv_fwd": [C.POINTER(ConvDesc), _V, _V, _I, _V, _I, _I, _V, _V, _I, _V, _V, _I, _I, _I, _V],
     "pda_conv_dgrad": [C.POINTER(ConvDesc), _V, _V, _V, C.POINTER(BnEpi), _I, _I, _I, _V],
+    "pda_conv_dgrad_bnf": [C.POINTER(ConvDesc), _V, _V, _V, C.POINTER(BnEpi), _V, _V, _V, _V, _I, _I,
+                           _I, _V],
+    "pda_bn_fold": [_V, _V, _I, _I, _V, _V, _I, _V],
     "pda_conv_wgrad": [C.POINTER(ConvDesc), _V, _V, _V, _I, _I, _V, _V, _I, _I, _I, _V],
     "pda_conv_wgrad_bna": [C.POINTER(ConvDesc), _V, _V, _V, _V, _V, _V, _V, _I, _I, _V, _V, _I, _I, _I,
                            _V],
     "pda_wgrad_reduce": [_V, _V, _I, _I, _I, _I, _I, _I, _F, _I, _V],
-    "pda_bn_fwd_stats": [_V, _I, _I, _I, _I, _I, _V, _V, C.POINTER(BnFwdOut), _V],
-    "pda_bn_bwd_stats": [_V, _I, _I, _I, _I, _V, _V, C.POINTER(BnBwdOut), _V],
+    "pda_bn_fwd_stats": [_V, _I, _I, _I, _I, _I, _V, _V, C.POINTER(BnFwdOut), _I, _V],
+    "pda_bn_bwd_stats": [_V, _I, _I, _I, _I, _V, _V, C.POINTER(BnBwdOut), _I, _V],
     "pda_bn_finalize_tot": [_V, _I, _D, _V, _V, _F, _F, _V, _V, _V, _V, _V, _V, _V, _I, _V],
     "pda_slab_reduce": [_V, _I, _I, _I, _V, _V],
     "pda_bn_eval_coeffs": [_V, _V, _V, _V, _F, _I, _V, _V, _V],

@@ -247,7 +247,7 @@ def bn_finalize_partials(stats: torch.Tensor, T: int, C_: int, bm: int, M: int, 
     (csrc/bn.hip bn_stats_kernel<0>): S blocks per 256-channel group reduce tile ranges to f64 slabs,
     the group's last arriving block sums them and finalizes. SyncBatchNorm (``ws.sync_comm``): the
     launch stops at f64 totals, which are all-reduced before :func:`bn_finalize_tot`."""
-    G = math.ceil(C_ / min(C_, 256))
+    G = math.ceil(C_ / _stats_cg(C_))
     S = _stats_slabs(T, C_)
     ws = bn.ws
     slabs = ws.get("bn_slabs", S * 2 * C_, torch.float64)
@@ -260,7 +260,7 @@ def bn_finalize_partials(stats: torch.Tensor, T: int, C_: int, bm: int, M: int, 
                      ptr(bn.invstd), ptr(bn.scale), ptr(bn.shift), ptr(bn.rmean), ptr(bn.rvar),
                      ptr(bn.nbt), int(bn.update), ptr(tot))
     check(ext.lib().pda_bn_fwd_stats(ptr(stats), T, C_, bm, M, S, ptr(slabs), ptr(cnt), C.byref(o),
-                                     stream(stats.device)), "bn_fwd_stats")
+                                     _stats_cg(C_), stream(stats.device)), "bn_fwd_stats")
     if sync is not None:   # SyncBatchNorm: global f64 totals, then finalize
         sync.all_reduce(tot)
         bn_finalize_tot(tot, C_, M * sync.world_size, bn)
@@ -330,6 +330,50 @@ def conv_dgrad(dy: torch.Tensor, w: torch.Tensor, g: ConvGeom, dx: torch.Tensor,
                                   C.byref(epi) if epi is not None else None, kdt, kbm, kbn,
                                   stream(dy.device))
     check(rc, "conv_dgrad")
+    return dx
+
+
+def bn_fold(w: torch.Tensor, k: torch.Tensor, wf: torch.Tensor, bias: torch.Tensor) -> None:
+    """Operands of :func:`conv_dgrad_bnf` for a 1x1 conv (``w`` 16-bit [Cout, Cin], ``k`` =
+    [k1; k2; k3] 3 x Cout f32 of the BatchNorm after it): ``wf`` [Cout + Cin, Cin] = [k1 o W ;
+    W^T diag(k2) W], ``bias`` [Cin] = W^T k3 (csrc/conv_gemm.hip bn_fold_kernel, one launch)."""
+    Cout, Cin = w.shape[0], w.shape[-1]
+    if wf.shape[0] != Cout + Cin or wf.shape[-1] != Cin or wf.dtype != w.dtype or k.numel() < 3 * Cout:
+        raise ValueError("bn_fold: wf [Cout + Cin, Cin] of the weights' dtype, k 3 x Cout")
+    check(ext.lib().pda_bn_fold(ptr(w), ptr(k), Cout, Cin, ptr(wf), ptr(bias), dt_of(w),
+                                stream(w.device)), "bn_fold")
+
+
+def bnf_ok(g: ConvGeom, dtype: torch.dtype) -> bool:
+    """Whether the consumer-side BN-backward fold (:func:`conv_dgrad_bnf`) serves this conv: a 1x1
+    conv without padding, 16-bit operands, channel counts in whole 64-column panels."""
+    return (g.R == 1 and g.S == 1 and g.pad == 0 and dtype in (torch.bfloat16, torch.float16)
+            and g.Cin % 64 == 0 and g.Cout % 64 == 0
+            and getattr(ext.lib(), "pda_conv_dgrad_bnf", None) is not None)
+
+
+def conv_dgrad_bnf(dz: torch.Tensor, wf: torch.Tensor, g: ConvGeom, dx: torch.Tensor,
+                   xa: torch.Tensor, bias: torch.Tensor, xa_pro=None,
+                   epi: Optional[ext.BnEpi] = None,
+                   tile: Optional[Tuple[int, int]] = None) -> torch.Tensor:
+    """dX of a 1x1 conv whose dY = k1*dz + k2*y + k3 is never materialised (y = the conv's forward
+    output): dX = dz . (k1 o W) + xa . G + b with (wf, bias) from :func:`bn_fold` and ``xa`` the
+    conv's forward input (``xa_pro`` = (scale, shift): xa is PRE-BatchNorm and the activation
+    relu(xa*scale+shift) is recomputed, as the forward's prologue did). ``epi``: the same fused
+    BN-backward epilogue as :func:`conv_dgrad`."""
+    Nb = dz.shape[0]
+    kdt = _kdt(dz)
+    bm, bn = tile or dgrad_tile(g, Nb)
+    kbm, kbn = _ktile(bm, bn, kdt)
+    if kbm > 1000:    # the fold's Gram operand needs the register-staged loader
+        kbm, kbn = -128, min(kbn, 128)
+    d = g.desc(Nb)
+    rc = ext.lib().pda_conv_dgrad_bnf(C.byref(d), ptr(dz), ptr(wf), ptr(dx),
+                                      C.byref(epi) if epi is not None else None, ptr(xa),
+                                      ptr(xa_pro[0] if xa_pro else None),
+                                      ptr(xa_pro[1] if xa_pro else None), ptr(bias), kdt, kbm, kbn,
+                                      stream(dz.device))
+    check(rc, "conv_dgrad_bnf")
     return dx
 
 
@@ -451,7 +495,12 @@ def wgrad_bna_ok(g: ConvGeom, Nb: int, dtype: torch.dtype) -> bool:
     if getattr(ext.lib(), "pda_conv_wgrad_bna", None) is None:
         return False
     bm, bn, _, _ = wgrad_plan(g, Nb)
-    return abs(bm) == 64 and bn in (128, 256)
+    return (abs(bm), bn) in _BNA_TILES
+
+
+# tiles pda_conv_wgrad_bna is built for (csrc/conv_gemm.hip BNA_CASE): the stem's 64-row tiles and
+# the bottleneck conv3 weight gradients of the consumer-side tail fold
+_BNA_TILES = {(64, 128), (64, 256), (128, 128), (128, 64)}
 
 
 def conv_wgrad(dy: torch.Tensor, x: torch.Tensor, g: ConvGeom, grad: torch.Tensor, ws: Workspace,
@@ -638,21 +687,23 @@ def bn_bwd_finish(ws: "Workspace", part, G: int, nq: int, y, mean, invstd, gamma
     bn_stats_kernel<1>: f64 slabs + last-arriver combine -> gamma/beta gradients and the apply
     coefficients of both branches), then the apply pass(es). SyncBatchNorm takes the separate
     reduce -> all-reduce -> finalize path.
-    ``k_out`` (3 x C f32, single-branch, not SyncBatchNorm): write the apply coefficients
-    [k1; k2; k3] there and skip the apply pass (``dy_out`` unused) -- the consumer forms dy itself
-    (:func:`conv_wgrad` ``bna``)."""
+    ``k_out`` (f32, 3 x C per branch: [k1; k2; k3] of branch 1, then of the shortcut branch; not
+    SyncBatchNorm): the apply coefficients are written there and the apply pass of every branch
+    whose output is None is skipped -- its consumer forms dy itself (:func:`conv_wgrad` ``bna``,
+    :func:`conv_dgrad_bnf`)."""
     N, H, W, C_ = y.shape
     mode = 2 if nq == 3 else 1   # dz is materialised in both cases
     a = BwdArgs(None, None, None, 0, ptr(y), None, None, ptr(y2), None, None, mode, None, ptr(part),
                 nq, N * H * W, C_)
     sync = getattr(ws, "sync_comm", None)
-    if k_out is not None and (nq != 2 or (sync is not None and sync.world_size > 1)):
-        raise ValueError("bn_bwd_finish: k_out needs the single-branch, non-synchronised form")
+    if k_out is not None and ((sync is not None and sync.world_size > 1)
+                              or k_out.numel() < 3 * (nq - 1) * C_):
+        raise ValueError("bn_bwd_finish: k_out needs the non-synchronised form and 3 x C per branch")
     if sync is None or sync.world_size == 1:
         k = ws.get("bn_k", 6 * C_) if k_out is None else k_out
         S = _stats_slabs(G, C_)
         slabs = ws.get("bn_slabs", S * nq * C_, torch.float64)
-        cnt = ws.counters(math.ceil(C_ / min(C_, 256)))
+        cnt = ws.counters(math.ceil(C_ / _stats_cg(C_)))
         o = ext.BnBwdOut(float(N * H * W), float(gscale), int(accumulate))
         o.gamma[0], o.mean[0], o.invstd[0] = ptr(gamma), ptr(mean), ptr(invstd)
         o.dgamma[0], o.dbeta[0] = ptr(dgamma), ptr(dbeta)
@@ -661,16 +712,16 @@ def bn_bwd_finish(ws: "Workspace", part, G: int, nq: int, y, mean, invstd, gamma
             o.dgamma[1], o.dbeta[1] = ptr(dgamma2), ptr(dbeta2)
         o.k = ptr(k)
         L, st, dt = ext.lib(), stream(y.device), dt_of(y)
-        check(L.pda_bn_bwd_stats(ptr(part), G, nq, C_, S, ptr(slabs), ptr(cnt), C.byref(o), st),
-              "bn_bwd_stats")
-        if k_out is not None:
-            return
-        if mode == 2 and _BWD_APPLY2 and L.pda_bn_bwd_apply2(
-                ptr(dz), ptr(y), ptr(y2), ptr(k), ptr(dy_out), ptr(dy2_out), N * H * W, C_, dt, st) == 0:
+        check(L.pda_bn_bwd_stats(ptr(part), G, nq, C_, S, ptr(slabs), ptr(cnt), C.byref(o),
+                                 _stats_cg(C_), st), "bn_bwd_stats")
+        if mode == 2 and dy_out is not None and dy2_out is not None and _BWD_APPLY2 and \
+                L.pda_bn_bwd_apply2(ptr(dz), ptr(y), ptr(y2), ptr(k), ptr(dy_out), ptr(dy2_out),
+                                    N * H * W, C_, dt, st) == 0:
             return   # both branches in one pass over dz
-        check(L.pda_bn_bwd_apply(C.byref(a), ptr(dz), ptr(y), ptr(k[0:C_]), ptr(k[C_:2 * C_]),
-                                 ptr(k[2 * C_:3 * C_]), ptr(dy_out), dt, st), "bn_bwd_apply")
-        if mode == 2:
+        if dy_out is not None:
+            check(L.pda_bn_bwd_apply(C.byref(a), ptr(dz), ptr(y), ptr(k[0:C_]), ptr(k[C_:2 * C_]),
+                                     ptr(k[2 * C_:3 * C_]), ptr(dy_out), dt, st), "bn_bwd_apply")
+        if mode == 2 and dy2_out is not None:
             check(L.pda_bn_bwd_apply(C.byref(a), ptr(dz), ptr(y2), ptr(k[3 * C_:4 * C_]),
                                      ptr(k[4 * C_:5 * C_]), ptr(k[5 * C_:6 * C_]), ptr(dy2_out), dt,
                                      st), "bn_bwd_apply2")
@@ -679,11 +730,21 @@ def bn_bwd_finish(ws: "Workspace", part, G: int, nq: int, y, mean, invstd, gamma
                  y2, mean2, invstd2, gamma2, dgamma2, dbeta2, dy2_out, dz, gscale, accumulate)
 
 
+# channels per block group of the statistics kernel (csrc/bn.hip stats_cg): a quad of channels gets
+# 1024 / cg lanes, so narrower groups shorten both levels' serial load chains
+_BN_CG = int(os.environ.get("PDA_BN_CG", "256"))
+_BN_SK = float(os.environ.get("PDA_BN_SK", "0.75"))
+
+
+def _stats_cg(C_: int) -> int:
+    return min(C_, _BN_CG)
+
+
 def _stats_slabs(T: int, C_: int) -> int:
     """Blocks per channel group of the one-launch statistics kernel: level 1 reads T/S tiles per
     block, the group's last arriver S slabs -- S ~ sqrt(T) balances the two (both run at one CU's
     bandwidth), at least 8 when T allows so the level-1 reads spread over CUs."""
-    return max(1, min(T, max(8, int(math.sqrt(0.75 * T)))))
+    return max(1, min(T, max(8, int(math.sqrt(_BN_SK * T)))))
 
 
 def _bn_bwd_tail(ws, part, G, nq, mode, a, y, mean, invstd, gamma, dgamma, dbeta, dy_out,

@@ -780,3 +780,112 @@ def test_bn_stats_handoff_under_uneven_load():
                 bad.append((rep, C, T, err))
     assert not bad, bad
     assert int(ws.counters(64).abs().sum().item()) == 0
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("Cout,Cin", [(256, 64), (512, 128), (2048, 512)])
+def test_bn_fold_operands(Cout, Cin, dtype):
+    """bn_fold_kernel: Wf = [k1 o W ; W^T diag(k2) W] and b = W^T k3 against fp32 torch on the same
+    16-bit weights (G and the k1 rows are rounded to the 16-bit dtype once)."""
+    K = _k()
+    torch.manual_seed(Cout + Cin)
+    w = (torch.randn(Cout, Cin, device=DEV) * 0.05).to(dtype)
+    k = torch.randn(3 * Cout, device=DEV)
+    wf = torch.empty(Cout + Cin, Cin, device=DEV, dtype=dtype)
+    b = torch.empty(Cin, device=DEV)
+    K.bn_fold(w, k, wf, b)
+    torch.cuda.synchronize()
+    wd = w.double()
+    k1, k2, k3 = k[:Cout].double(), k[Cout:2 * Cout].double(), k[2 * Cout:].double()
+    # the kernel scales the 16-bit W by k2 and rounds that product once before the MFMA
+    wk2 = (w.float() * k2.float()[:, None]).to(dtype).double()
+    g_ref = wd.t() @ wk2
+    assert rel_err(wf[:Cout], (wd * k1[:, None])) < 5e-3
+    assert rel_err(wf[Cout:], g_ref) < 5e-3
+    assert rel_err(wf[Cout:], wd.t() @ (k2[:, None] * wd)) < 1e-2
+    assert rel_err(b, wd.t() @ k3) < 1e-5
+
+
+@pytest.mark.parametrize("pro", [True, False])
+@pytest.mark.parametrize("geo", [(2, 8, 64, 256), (3, 7, 128, 512), (1, 7, 512, 2048)])
+def test_conv_dgrad_bnf_matches_applied_dgrad(geo, pro):
+    """DGRAD_BNF (the consumer-side tail fold) == apply dy3 = k1*dz + k2*y3 + k3, then the plain 1x1
+    data gradient -- with y3 = conv(a2) the conv's own forward, a2 = relu(bn2(y2)) recomputed by the
+    prologue (pro) or a materialised input; ragged rows (H = 7); the fused BN-backward epilogue of
+    the preceding BN gives the same dz and partial sums."""
+    K = _k()
+    dtype = torch.bfloat16
+    Nb, H, Cin, Cout = geo
+    torch.manual_seed(Cin)
+    g = K.ConvGeom(Nb, H, H, Cin, Cout, 1, 1, 1, 0)
+    w = (torch.randn(Cout, 1, 1, Cin, device=DEV) * 0.05).to(dtype)
+    y2 = torch.randn(Nb, H, H, Cin, device=DEV).to(dtype)
+    sc2, sh2 = torch.rand(Cin, device=DEV) + 0.5, torch.randn(Cin, device=DEV) * 0.1
+    if pro:
+        xa, xpro = y2, (sc2, sh2)
+        a2 = torch.relu(y2.float() * sc2 + sh2).to(dtype)
+    else:
+        xa, xpro = torch.relu(y2.float()).to(dtype), None
+        a2 = xa
+    y3 = torch.empty(Nb, H, H, Cout, device=DEV, dtype=dtype)
+    K.conv_fwd(a2, w.view(Cout, Cin), g, y3)
+    dz = torch.randn(Nb, H, H, Cout, device=DEV).to(dtype)
+    k = torch.cat([torch.rand(Cout, device=DEV) + 0.5, torch.randn(Cout, device=DEV) * 0.3,
+                   torch.randn(Cout, device=DEV) * 0.2])
+    dy3 = (k[:Cout] * dz.float() + k[Cout:2 * Cout] * y3.float() + k[2 * Cout:]).to(dtype)
+    ws = K.Workspace(DEV)
+    mean, inv = torch.randn(Cin, device=DEV) * 0.1, torch.rand(Cin, device=DEV) + 0.5
+    gamma = torch.rand(Cin, device=DEV) + 0.5
+    res = {}
+    for name in ("ref", "bnf"):
+        G = K.dgrad_slabs(g, Nb, dtype=dtype)
+        epi, part, nq = K.bn_epilogue(ws, G, y2, sc2, sh2)
+        dz2 = torch.empty(Nb, H, H, Cin, device=DEV, dtype=dtype)
+        if name == "ref":
+            K.conv_dgrad(dy3, w, g, dz2, epi=epi)
+        else:
+            wf = torch.empty(Cout + Cin, Cin, device=DEV, dtype=dtype)
+            b = torch.empty(Cin, device=DEV)
+            K.bn_fold(w.view(Cout, Cin), k, wf, b)
+            K.conv_dgrad_bnf(dz, wf, g, dz2, xa, b, xa_pro=xpro, epi=epi)
+        dg, db = torch.zeros(Cin, device=DEV), torch.zeros(Cin, device=DEV)
+        dy2 = torch.empty_like(dz2)
+        K.bn_bwd_finish(ws, part, G, nq, y2, mean, inv, gamma, dg, db, dz2, dy2)
+        torch.cuda.synchronize()
+        res[name] = (dz2.float(), dg.clone(), db.clone())
+    # exact-math reference of the data gradient (fp32): dA2 = dY3 . W  (dY3 unrounded)
+    dy3f = k[:Cout] * dz.float() + k[Cout:2 * Cout] * y3.float() + k[2 * Cout:]
+    da_ref = dy3f.view(-1, Cout) @ w.view(Cout, Cin).float()
+    mask = (y2.float() * sc2 + sh2 > 0).view(-1, Cin)
+    dz2_ref = (da_ref * mask).view(Nb, H, H, Cin)
+    e_bnf, e_ref = rel_err(res["bnf"][0], dz2_ref), rel_err(res["ref"][0], dz2_ref)
+    print(f"dz2 vs fp32: fold {e_bnf:.2e}, apply+dgrad {e_ref:.2e}")
+    assert e_bnf < 2 * e_ref + 5e-3, (e_bnf, e_ref)
+    for a, b in zip(res["bnf"][1:], res["ref"][1:]):
+        assert rel_err(a, b) < 1.5e-2
+
+
+@pytest.mark.parametrize("Cout,Cin,H,tile", [(256, 64, 14, (-128, 128)), (512, 128, 12, (128, 128)),
+                                              (1024, 256, 7, (-128, 64)), (2048, 512, 7, (-128, 128))])
+def test_conv_wgrad_bna_conv3_tiles(Cout, Cin, H, tile):
+    """WGRAD_BNA on the Bottleneck conv3 tiles of the tail fold, with the forward's BN+ReLU
+    prologue on the activation operand: against the apply-then-wgrad path."""
+    K = _k()
+    dtype = torch.bfloat16
+    Nb = 4
+    torch.manual_seed(Cout)
+    g = K.ConvGeom(Nb, H, H, Cin, Cout, 1, 1, 1, 0)
+    y2 = torch.randn(Nb, H, H, Cin, device=DEV).to(dtype)
+    sc, sh = torch.rand(Cin, device=DEV) + 0.5, torch.randn(Cin, device=DEV) * 0.1
+    dz = torch.randn(Nb, H, H, Cout, device=DEV).to(dtype)
+    y3 = (torch.randn(Nb, H, H, Cout, device=DEV) * 2 + 1).to(dtype)
+    kk = torch.randn(3 * Cout, device=DEV)
+    ws = K.Workspace(DEV)
+    dw_f = torch.zeros(Cout * Cin, device=DEV)
+    K.conv_wgrad(dz, y2, g, dw_f, ws, pro=(sc, sh), bna=(y3, kk), tile=tile)
+    dy = (kk[:Cout].double() * dz.double() + (kk[Cout:2 * Cout].double() * y3.double()
+                                              + kk[2 * Cout:].double()).float().double()).float().to(dtype)
+    dw_u = torch.zeros_like(dw_f)
+    K.conv_wgrad(dy, y2, g, dw_u, ws, pro=(sc, sh), tile=tile)
+    torch.cuda.synchronize()
+    assert rel_err(dw_f, dw_u) < 2e-3

@@ -354,3 +354,32 @@ def test_probe_and_segment_hooks_fire_per_block_and_change_nothing():
     sb = nm.stage_bounds()
     assert len(sb) == 3 and all(b in bounds for b in sb) and sb == sorted(sb)
     assert torch.equal(nm.flat_grad, g0)
+
+
+def test_tail_fold_matches_apply_path():
+    """The consumer-side tail fold (PDA_BN_FOLD, default on: the Bottleneck tail BN backward is
+    never applied; conv3's gradients take (dz, k) -- csrc/conv_gemm.hip DGRAD_BNF / WGRAD_BNA)
+    against the apply-pass path on the same forward state: gradients agree to bf16 rounding, and
+    each is as close to the fp32 reference as torch's bf16 autocast is."""
+    tm, nm = _pair("resnet50", image=64)
+    torch.manual_seed(7)
+    x = torch.randn(16, 3, 64, 64, device=DEV).to(torch.bfloat16).float()
+    y = torch.randint(0, 1000, (16,), device=DEV)
+    nm.train()
+    tm.train()
+    F.cross_entropy(tm(x), y).backward()
+    crit = nm.make_criterion()
+    grads = {}
+    for fold in (False, True):
+        nm.bn_fold = fold
+        nm.zero_grad_flat()
+        crit(nm(x), y).backward()
+        torch.cuda.synchronize()
+        grads[fold] = dict((n, p.grad.detach().float().clone()) for n, p in nm.named_parameters())
+    tp = dict(tm.named_parameters())
+    bad = []
+    for n in grads[True]:
+        e_fold, e_apply = rel_err(grads[True][n], tp[n].grad), rel_err(grads[False][n], tp[n].grad)
+        if e_fold > 1.3 * e_apply + 0.01:
+            bad.append((n, e_fold, e_apply))
+    assert not bad, bad

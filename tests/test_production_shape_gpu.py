@@ -1,0 +1,104 @@
+"""Correctness at the reference's own configuration: ResNet-50, batch 400, 224 px
+(``/root/reference/resnet_single_gpu.py:72,83`` -- batch_size 400, ``models.resnet50()``; the step
+at ``:27-31``), through exactly the plan ``bench.py`` times: the per-layer tile tables, the HALO
+forward tiles at 28/14/7 px, the 256x256 LDS-DMA weight-gradient tiles with their split-K targets,
+the >= 50 MiB streaming BatchNorm passes, the 64 MiB slab cap and the 224-px space-to-depth stem
+are all selected by shape, so only this batch and image size compose them as the bench does.
+
+* one training step (forward, loss, backward) of the native bf16 engine against the same weights
+  in PyTorch fp32 (the reference's precision), with PyTorch's own bf16 autocast as the precision
+  yardstick -- logits, loss, every parameter gradient, the running statistics;
+* two identical full training steps (``NativeTrainer.step``: on-device batch, forward, loss,
+  backward on two streams, fused SGD) are bit-identical: gradients, weights, momentum, buffers.
+"""
+import copy
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+DEV = torch.device("cuda", 0)
+B, S = 400, 224
+
+
+def rel_err(a, b):
+    a, b = a.float(), b.float()
+    return ((a - b).norm() / (b.norm() + 1e-12)).item()
+
+
+def _grads(model):
+    return {n: p.grad.detach().float().clone() for n, p in model.named_parameters()}
+
+
+def test_production_step_matches_fp32_reference():
+    from pytorch_distributed_amd.data.synthetic import synthetic_images
+    from pytorch_distributed_amd.models import build_model
+    from pytorch_distributed_amd.models.native import NativeResNet
+    torch.manual_seed(0)
+    ref = build_model("resnet50")
+    # bench step 0's synthetic batch, rounded to bf16 (the native engine's input precision) so all
+    # three models see the same pixels
+    x, y = synthetic_images(torch.arange(B), 0, "train", 1000, S, device=DEV)
+    x = x.to(torch.bfloat16).float()
+    res = {}
+    for mode in ("fp32", "bf16"):
+        tm = copy.deepcopy(ref).to(DEV).train()
+        with torch.autocast("cuda", dtype=torch.bfloat16, enabled=mode == "bf16"):
+            logits = tm(x)
+        loss = F.cross_entropy(logits.float(), y)
+        loss.backward()
+        torch.cuda.synchronize()
+        res[mode] = (logits.detach().float(), loss.item(), _grads(tm),
+                     {n: b.detach().clone() for n, b in tm.named_buffers()})
+        del tm, logits, loss
+        torch.cuda.empty_cache()
+    nm = NativeResNet(ref, device=DEV, dtype=torch.bfloat16, image_size=S).train()
+    crit = nm.make_criterion()
+    ln = nm(x)
+    loss_n = crit(ln, y)
+    loss_n.backward()
+    torch.cuda.synchronize()
+    lt, loss_t, gt, bt = res["fp32"]
+    lb, loss_b, gb, _ = res["bf16"]
+    e_nat, e_bf = rel_err(ln, lt), rel_err(lb, lt)
+    print(f"logits vs fp32: native {e_nat:.2e}, torch bf16 autocast {e_bf:.2e}; loss native "
+          f"{loss_n.item():.5f} fp32 {loss_t:.5f} bf16 {loss_b:.5f}")
+    assert e_nat < 1.3 * e_bf + 0.01, (e_nat, e_bf)
+    assert abs(loss_n.item() - loss_t) < 2 * abs(loss_b - loss_t) + 0.01
+    worse, worst = [], (0.0, "")
+    for name, p in nm.named_parameters():
+        e, eb = rel_err(p.grad, gt[name]), rel_err(gb[name], gt[name])
+        worst = max(worst, (e / (eb + 1e-3), name))
+        if e > 1.5 * eb + 0.02:
+            worse.append((name, e, eb))
+    print(f"worst gradient error ratio native / torch-bf16: {worst[0]:.2f} ({worst[1]})")
+    assert not worse, worse
+    for name, b in nm.named_buffers():
+        if "num_batches" in name:
+            assert int(b.item()) == int(bt[name].item()) == 1, name
+        else:
+            # one momentum-0.1 update from (0, 1): the batch statistics of 400 x HxW values
+            assert rel_err(b, bt[name]) < 2e-2, (name, rel_err(b, bt[name]))
+
+
+def test_production_steps_are_bitwise_reproducible():
+    from pytorch_distributed_amd.models.native import NativeTrainer
+    tr = NativeTrainer("resnet50", B, torch.bfloat16, DEV, image_size=S)
+    m = tr.model
+    p0, b0 = m.flat_params.clone(), m.flat_bufstore.clone()
+    out = []
+    for run in range(2):
+        with torch.no_grad():
+            m.flat_params.copy_(p0)
+            m.flat_bufstore.copy_(b0)
+            tr.opt.flat_mom.zero_()
+        m.refresh_shadow()
+        tr.opt._initialized = False
+        for i in range(2):
+            tr.step(i)
+        torch.cuda.synchronize()
+        out.append([t.clone() for t in (m.flat_grad, m.flat_params, tr.opt.flat_mom, m.flat_bufstore)])
+        assert tr.last_loss() == tr.last_loss() and tr.last_loss() < 10.0
+    for name, a, b in zip(("grad", "params", "momentum", "buffers"), out[0], out[1]):
+        assert torch.equal(a, b), name

@@ -58,7 +58,7 @@ def main():
         dg, db = torch.zeros(C_, device=dev), torch.zeros(C_, device=dev)
         S = K._stats_slabs(T, C_)
         slabs = ws.get("bn_slabs", S * 2 * C_, torch.float64)
-        cnt = ws.counters(math.ceil(C_ / min(C_, 256)))
+        cnt = ws.counters(math.ceil(C_ / K._stats_cg(C_)))
         kk = ws.get("bn_k", 6 * C_)
         o = ext.BnBwdOut(float(M), 1.0, 0)
         o.gamma[0], o.mean[0], o.invstd[0] = K.ptr(gamma), K.ptr(st[0]), K.ptr(st[1])
@@ -67,7 +67,7 @@ def main():
 
         def bwd():
             K.check(L.pda_bn_bwd_stats(K.ptr(partb), T, 2, C_, S, K.ptr(slabs), K.ptr(cnt),
-                                       ext.C.byref(o), K.stream(dev)), "bn_bwd_stats")
+                                       ext.C.byref(o), K._stats_cg(C_), K.stream(dev)), "bn_bwd_stats")
         tb = timeit(bwd)
         tot_f += n * tf
         tot_b += n * tb
