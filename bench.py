@@ -440,7 +440,8 @@ def _dp_pass(ctx: Ctx, args, dtype) -> dict:
                        "dp_loss": rec.get("loss"), "dp_max_mem_gb": rec.get("max_mem_gb"),
                        "dp_gpu_util_pct": rec.get("gpu_util_pct"), "dp_vs_baseline": rec.get("vs_baseline"),
                        "dp_exposed_comm_ms": rec.get("exposed_comm_ms"),
-                       "dp_segments": rec.get("dp_segments")}
+                       "dp_segments": rec.get("dp_segments"),
+                       "dp_side_graphs": rec.get("dp_side_graphs")}
         except subprocess.TimeoutExpired:
             res = {"dp_error": f"timeout after {limit:.0f} s"}
         finally:
@@ -506,7 +507,9 @@ def main():
         tr.dp.timing = False
         ex = tr.dp.exposed_comm_ms()
         diag["exposed_comm_ms"] = None if ex is None else round(ex, 4)
-        diag["dp_segments"] = len(tr.dp._graphs[0].graphs)
+        rg = tr.dp._graphs[0]
+        diag["dp_segments"] = len(rg.graphs)
+        diag["dp_side_graphs"] = sum(g is not None for g in getattr(rg, "sides", []))
         nxt += 1
     if args.dp:   # every replica must hold bit-identical weights (the replicated fused SGD)
         try:

@@ -161,6 +161,10 @@ class NativeResNet(nn.Module):
         # called on the main stream with the flat-gradient offset below which every gradient is
         # final, after each residual block's backward (DataParallel splits its replica graphs there)
         self.segment_hook: Optional[Callable[[int], None]] = None
+        # graph capture with the weight gradients in graphs of their own (parallel/dp.py
+        # _ReplicaGraph side_split): the backward leaves the batched weight-gradient kernels queued
+        # (no flush, no end-of-backward join) for the capture driver to record on the second stream
+        self.defer_side = False
         # diagnostics (tools/layer_times.py): called on the main stream as probe(phase, name) after
         # the stem and after each residual block, forward and backward
         self.probe: Optional[Callable[[str, str], None]] = None
@@ -727,7 +731,7 @@ class NativeResNet(nn.Module):
             rec = sv["blocks"][bi]
             prev = (self.blocks[bi - 1], sv["blocks"][bi - 1]) if bi > 0 else None
             dx_main, shortcut_g, tail = self._block_backward(b, rec, tail, prev, acc)
-            if self._wbatch_mode == "block" or b.ds is not None:
+            if not self.defer_side and (self._wbatch_mode == "block" or b.ds is not None):
                 self._flush_wgrad()
             if red is not None:
                 self._grads_ready(red, self.block_bounds[nblk - bi])
@@ -775,10 +779,11 @@ class NativeResNet(nn.Module):
                 K.conv_wgrad(dy0, x0, g0, self.stem_wgrad, w, wscale=self.wgrad_scale)
                 K.stem_s2d_grad(self.stem_wgrad, self.wgrad_view(u), accumulate=acc)
             self._wgrad(stem_wgrad, dy0, x0)
-        self._flush_wgrad()
-        if self._side is not None:   # join: the optimizer step reads every gradient
-            torch.cuda.current_stream(self.device).wait_stream(self._side)
-            self._keep.clear()
+        if not self.defer_side:
+            self._flush_wgrad()
+            if self._side is not None:   # join: the optimizer step reads every gradient
+                torch.cuda.current_stream(self.device).wait_stream(self._side)
+                self._keep.clear()
         if red is not None:
             red.grads_ready(self.block_bounds[-1])
             red.finish()

@@ -368,15 +368,20 @@ class DataParallel(nn.Module):
         return self._cstreams
 
     def _replay_overlapped(self, jobs, streams) -> None:
-        """Replay segment s of every replica, then all-reduce the gradient slice it completed on
-        per-device comm streams while segment s+1 replays; the replicas' streams join the comm
-        streams before the optimizer step. ``self.timing``: HIP events at the end of backward and
-        after the last all-reduce (``exposed_comm_ms``)."""
+        """Replay segment s of every replica (its main-chain graph on the replica's stream and, in
+        side-split captures, its weight-gradient graph on the replica's second stream), and after
+        each segment that completes a gradient slice all-reduce that slice on per-device comm
+        streams -- ordered after both streams of every replica -- while the next segments replay;
+        the replicas' streams join the comm and second streams before the optimizer step.
+        ``self.timing``: HIP events at the end of backward and after the last all-reduce
+        (``exposed_comm_ms``)."""
         cs = self._comm_streams()
-        nseg = len(jobs[0][0].graphs)
-        bounds = [0] + jobs[0][0].splits + [self.module.numel]
+        rg0 = jobs[0][0]
+        nseg = len(rg0.graphs)
+        ends = rg0.seg_reduce
         threaded = len(jobs) > 1 and os.environ.get("PDA_DP_THREADS", "1") != "0"
         timing = self.timing
+        lo = 0
         for s in range(nseg):
             if threaded:
                 # one host thread per device: hipGraphLaunch of a ~150-node segment costs ~0.5 ms
@@ -389,16 +394,24 @@ class DataParallel(nn.Module):
                     rg.replay(s, x, y, st)
             if timing and s == nseg - 1:
                 self._ev_bwd = [torch.cuda.Event(enable_timing=True) for _ in streams]
-                for e, st in zip(self._ev_bwd, streams):
+                for e, st, (rg, _, _) in zip(self._ev_bwd, streams, jobs):
+                    rg.join_side(st)
                     e.record(st)
-            for c, st in zip(cs, streams):
+            hi = ends[s]
+            if hi is None:
+                continue
+            for c, st, (rg, _, _) in zip(cs, streams, jobs):
                 c.wait_stream(st)
-            self._reduce_slice(bounds[s], bounds[s + 1], streams=cs)
+                if rg.side_split:
+                    c.wait_stream(rg.m._side)
+            self._reduce_slice(lo, hi, streams=cs)
+            lo = hi
         if timing:
             self._ev_comm = [torch.cuda.Event(enable_timing=True) for _ in cs]
             for e, c in zip(self._ev_comm, cs):
                 e.record(c)
-        for c, st in zip(cs, streams):
+        for c, st, (rg, _, _) in zip(cs, streams, jobs):
+            rg.join_side(st)
             st.wait_stream(c)
         for m in self.all_modules:
             m._grads_zero = False
@@ -428,39 +441,77 @@ class _ReplicaGraph:
     """forward + CE loss/gradient + backward of one native replica, captured as HIP graphs on the
     replica's device; inputs are copied into static buffers before each replay.
 
-    ``splits`` (flat-gradient offsets, ``NativeResNet.stage_bounds``): the capture ends and a new
-    graph (same memory pool, replayed in capture order) begins when the backward has finished the
-    gradient below each offset -- after joining the weight-gradient stream, so every kernel
-    writing that slice is inside the ended segment. Between segment replays DataParallel
-    all-reduces the completed slice on a comm stream."""
+    ``splits`` (flat-gradient offsets, ``NativeResNet.stage_bounds``): where DataParallel
+    all-reduces a completed gradient slice between segment replays.
+
+    ``side_split`` (``PDA_DP_SIDE=1``): the weight-gradient kernels are recorded in graphs
+    of their own. The HIP runtime replays one captured graph's fork/join DAG almost serially
+    (``profiles/rocprof_r3_graph_replay.md``: 368 of ~410 kernels on one queue), which loses the
+    two-stream overlap of the eager step; so the capture ends a main-chain graph after every
+    residual block's backward and records the weight gradients queued during that block as a
+    second graph, replayed on the replica's second stream after the main segment -- it runs beside
+    the next block's data-gradient chain, as the eager schedule's "block" fork granularity does.
+    Without it, a segment ends only at the split offsets, after joining the weight-gradient stream."""
 
     def __init__(self, m, shape, global_batch: int, splits: Sequence[int] = ()) -> None:
         self.m = m
         self.dev = m.device
         self.gscale = 1.0 / global_batch
         self.splits = list(splits)
+        self.side_split = (getattr(m, "_side", None) is not None
+                           and os.environ.get("PDA_DP_SIDE", "0") != "0")
         with torch.cuda.device(self.dev):
             self.x = torch.empty(shape, dtype=m.dtype, device=self.dev)
             self.y = torch.empty(shape[0], dtype=torch.int64, device=self.dev)
-        self.graphs: List[torch.cuda.CUDAGraph] = []
+        self.graphs: List[torch.cuda.CUDAGraph] = []     # main-chain segments
+        self.sides: List[Optional[torch.cuda.CUDAGraph]] = []   # weight-gradient graph per segment
+        self.seg_reduce: List[Optional[int]] = []        # slice end all-reducible after segment s
         self.loss = None
         self._capturing = False
+        self._pool_h = None
 
     @property
     def graph(self):
         return self.graphs[0] if self.graphs else None
 
+    def _capture_side(self):
+        """Record the queued weight-gradient kernels as one graph on the second stream."""
+        m = self.m
+        if not m._wbatch:
+            return None
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.stream(m._side):
+            g.capture_begin(pool=self._pool_h)
+            try:
+                for fn in m._wbatch:
+                    fn(m.ws_w)
+            finally:
+                g.capture_end()
+        m._wbatch.clear()
+        return g
+
+    def _end_segment(self, upto: Optional[int]) -> None:
+        self.graphs[-1].capture_end()
+        self.sides.append(self._capture_side() if self.side_split else None)
+        self.seg_reduce.append(upto)
+
     def _split(self, upto: int) -> None:
-        """NativeResNet.segment_hook: at a split offset join the weight-gradient stream (eager and
-        captured schedules alike) and, while capturing, start the next segment's graph."""
+        """NativeResNet.segment_hook, after each residual block's backward."""
+        if self.side_split and self._capturing:
+            self._end_segment(upto if upto in self.splits else None)
+            g = torch.cuda.CUDAGraph()
+            g.capture_begin(pool=self._pool_h)
+            self.graphs.append(g)
+            return
         if upto not in self.splits:
             return
+        # at a split offset join the weight-gradient stream (eager and captured schedules alike)
+        # and, while capturing, start the next segment's graph
         self.m.join_side()
         if self._capturing:
-            g0 = self.graphs[-1]
-            g0.capture_end()
+            self._end_segment(upto)
             g = torch.cuda.CUDAGraph()
-            g.capture_begin(pool=self.graphs[0].pool())
+            g.capture_begin(pool=self._pool_h)
             self.graphs.append(g)
 
     def _body(self) -> None:
@@ -473,23 +524,37 @@ class _ReplicaGraph:
         dlog16 = torch.empty(B, m.fc_rows, dtype=m.dtype, device=self.dev)
         K.xent(logits, self.y, rows, loss, dlog=dlog16, gscale=self.gscale)
         m._grads_zero = True          # every step overwrites the flat gradient
-        m.segment_hook = self._split if self.splits else None
+        m.segment_hook = self._split if (self.splits or self.side_split) else None
+        m.defer_side = self.side_split and self._capturing
         try:
             m.native_backward(dlog16)
         finally:
             m.segment_hook = None
+            m.defer_side = False
         self.loss = loss
+
+    def join_side(self, stream: torch.cuda.Stream) -> None:
+        """Make ``stream`` wait for the replica's weight-gradient graphs replayed so far."""
+        if self.side_split:
+            stream.wait_stream(self.m._side)
 
     def replay(self, s: int, x: torch.Tensor, y: torch.Tensor,
                stream: Optional[torch.cuda.Stream] = None) -> None:
         """Replay segment ``s`` on ``stream`` (the caller's current stream on this device: a
-        worker thread's own current stream is the default stream); segment 0 first takes the
-        inputs."""
-        with torch.cuda.device(self.dev), torch.cuda.stream(stream or torch.cuda.current_stream(self.dev)):
-            if s == 0:
-                self.x.copy_(x, non_blocking=True)
-                self.y.copy_(y, non_blocking=True)
-            self.graphs[s].replay()
+        worker thread's own current stream is the default stream), then its weight-gradient graph
+        on the second stream after it; segment 0 first takes the inputs."""
+        with torch.cuda.device(self.dev):
+            st = stream or torch.cuda.current_stream(self.dev)
+            with torch.cuda.stream(st):
+                if s == 0:
+                    self.x.copy_(x, non_blocking=True)
+                    self.y.copy_(y, non_blocking=True)
+                self.graphs[s].replay()
+            side = self.sides[s] if s < len(self.sides) else None
+            if side is not None:
+                self.m._side.wait_stream(st)
+                with torch.cuda.stream(self.m._side):
+                    side.replay()
             self.loss = self._graph_loss
 
     def run(self, x: torch.Tensor, y: torch.Tensor, graph: bool = True,
@@ -497,8 +562,10 @@ class _ReplicaGraph:
         """The whole step: eagerly (``graph=False``), by replaying every segment, or -- the first
         time -- eagerly for this batch and then captured for the next replays."""
         if graph and self.graphs:
+            st = stream or torch.cuda.current_stream(self.dev)
             for s in range(len(self.graphs)):
-                self.replay(s, x, y, stream)
+                self.replay(s, x, y, st)
+            self.join_side(st)
             return
         with torch.cuda.device(self.dev), torch.cuda.stream(stream or torch.cuda.current_stream(self.dev)):
             self.x.copy_(x, non_blocking=True)
@@ -522,30 +589,42 @@ class _ReplicaGraph:
                 torch.cuda.empty_cache()
                 cap = torch.cuda.Stream(self.dev)
                 cap.wait_stream(cur)
+                if self.m._side is not None:
+                    self.m._side.wait_stream(cur)
                 with torch.cuda.stream(cap):
                     g = torch.cuda.CUDAGraph()
-                    self.graphs = [g]
+                    self.graphs, self.sides, self.seg_reduce = [g], [], []
                     self._capturing = True
                     ended = False
                     try:
                         g.capture_begin()
+                        self._pool_h = g.pool()
                         self._body()
-                        self.graphs[-1].capture_end()
+                        self._end_segment(self.m.numel)
                         ended = True
-                        if len(self.graphs) != len(self.splits) + 1:
-                            # a split offset the backward never reported: the gradient past the
-                            # last segment bound would never be all-reduced
-                            raise RuntimeError(f"replica capture produced {len(self.graphs)} "
-                                               f"segments for {len(self.splits)} split points")
+                        if self.side_split:
+                            # tensors the weight-gradient graphs read stay allocated until every
+                            # segment is recorded: a later segment must not reuse their memory
+                            # while a side graph may still be reading it at replay
+                            self.m._keep.clear()
+                        want = sorted(self.splits) + [self.m.numel]
+                        got = [u for u in self.seg_reduce if u is not None]
+                        if got != want or len(self.sides) != len(self.graphs):
+                            # a split offset the backward never reported: the gradient past it
+                            # would never be all-reduced
+                            raise RuntimeError(f"replica capture: all-reduce points {got}, "
+                                               f"expected {want}")
                     except BaseException:
                         if not ended:   # leave no capture open on the stream
                             try:
                                 self.graphs[-1].capture_end()
                             except Exception:   # noqa: BLE001 (already invalidated)
                                 pass
-                        self.graphs = []
+                        self.graphs, self.sides, self.seg_reduce = [], [], []
                         raise
                     finally:
                         self._capturing = False
                 cur.wait_stream(cap)
+                if self.m._side is not None:
+                    cur.wait_stream(self.m._side)
             self._graph_loss, self.loss = self.loss, eager

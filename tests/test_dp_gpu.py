@@ -43,14 +43,18 @@ def test_native_dataparallel_matches_single_model():
     assert torch.equal(dp.module.flat_params, dp.replicas[0].flat_params)
 
 
+@pytest.mark.parametrize("side", ["1", "0"])
 @pytest.mark.parametrize("segments", ["stage", "0"])
-def test_native_dataparallel_graph_step_matches_eager(segments, monkeypatch):
+def test_native_dataparallel_graph_step_matches_eager(segments, side, monkeypatch):
     """train_step replayed from per-replica HIP graphs == the same schedule launched eagerly (bit
     for bit, 4 steps incl. SGD), and its first step == crit(dp(x), y).backward() (autograd DP with
-    ATen's cross-entropy: equal up to the 16-bit rounding of dlogits). ``stage``: each replica's
-    graph is split after layer4 / layer3 / layer2 and the completed gradient slice is reduced on a
-    comm stream while the next segment replays (4 segments, 4 reductions)."""
+    ATen's cross-entropy: equal up to the 16-bit rounding of dlogits). ``stage``: the completed
+    gradient slice after layer4 / layer3 / layer2 is reduced on a comm stream while the next
+    segments replay (4 reductions). ``side`` (PDA_DP_SIDE): the weight gradients are recorded as
+    graphs of their own, one per residual block, replayed on the second stream beside the next
+    block's main chain (one main segment per block + the stem's)."""
     monkeypatch.setenv("PDA_DP_SEGMENTS", segments)
+    monkeypatch.setenv("PDA_DP_SIDE", side)
     from pytorch_distributed_amd.data import SyntheticImageNet
     from pytorch_distributed_amd.models import build_model
     from pytorch_distributed_amd.models.native import NativeResNet
@@ -90,8 +94,13 @@ def test_native_dataparallel_graph_step_matches_eager(segments, monkeypatch):
         assert torch.equal(graphed.module.flat_params, graphed.replicas[0].flat_params)
         assert torch.equal(eager.module.flat_buffers, graphed.module.flat_buffers)
     assert graphed._graphs[0].graph is not None and eager._graphs[0].graph is None
-    assert len(graphed._graphs[0].graphs) == (4 if segments == "stage" else 1)
-    assert len(graphed._graphs[0].splits) == len(graphed._graphs[0].graphs) - 1
+    rg = graphed._graphs[0]
+    nblk = len(graphed.module.blocks)
+    assert len(rg.graphs) == (nblk + 1 if side == "1" else (4 if segments == "stage" else 1))
+    assert len(rg.sides) == len(rg.graphs)
+    assert (sum(g is not None for g in rg.sides) > nblk // 2) == (side == "1")
+    assert [u for u in rg.seg_reduce if u is not None] == rg.splits + [graphed.module.numel]
+    assert len(rg.splits) == (3 if segments == "stage" else 0)
     ex = graphed.exposed_comm_ms()
     assert ex is not None and 0.0 <= ex < 1000.0, ex
 
