@@ -860,6 +860,20 @@ __device__ __forceinline__ i32x4 ldnt(const i32x4* p) {
   else return *p;
 }
 
+// 16-B output store of the streaming kernels by policy NTM: bit 2 = write-through (sc1: the line
+// leaves the XCD's L2 with the store, so the kernel ends with no dirty output bytes to write back
+// at its boundary -- MI355X_MICROARCH.md "stores of each flavour"), else bit 1 = nontemporal, else
+// plain. ``rs``: buffer resource over the output (32-bit byte offsets; outputs < 2 GiB).
+template <int NTM>
+__device__ __forceinline__ void st_out(i32x4* base, __amdgpu_buffer_rsrc_t rs, int j, i32x4 o) {
+  if constexpr (NTM & 4) __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(i32x4, o), rs, j * 16, 0, 16);
+  else if constexpr (NTM & 2) __builtin_nontemporal_store(o, base + j);
+  else base[j] = o;
+}
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t out_rsrc(void* p, int n8) {
+  return __builtin_amdgcn_make_buffer_rsrc(p, (short)0, (int)((unsigned)n8 * 16u), 0x00020000);
+}
+
 template <int DT, int U, int NTM>
 __global__ __launch_bounds__(NT) void bn_bwd_apply_dz_u_kernel(const void* __restrict__ dz_in,
                                                                const void* __restrict__ ysel,
@@ -881,6 +895,7 @@ __global__ __launch_bounds__(NT) void bn_bwd_apply_dz_u_kernel(const void* __res
   const i32x4* dzp = reinterpret_cast<const i32x4*>(dz_in);
   const i32x4* yp = reinterpret_cast<const i32x4*>(ysel);
   i32x4* op = reinterpret_cast<i32x4*>(dy);
+  const __amdgpu_buffer_rsrc_t rs = out_rsrc(dy, n8);
   for (; i + (U - 1) * stride < n8; i += U * stride) {
     i32x4 dz[U], yv[U];
 #pragma unroll
@@ -895,8 +910,7 @@ __global__ __launch_bounds__(NT) void bn_bwd_apply_dz_u_kernel(const void* __res
       for (int k = 0; k < 4; ++k)
         o[k] = (int)pack2<DT>(bnb_affine2(A[k], B[k], K3[k], unpack2<DT>((uint32_t)dz[u][k]),
                                           unpack2<DT>((uint32_t)yv[u][k])));
-      if constexpr (NTM & 2) __builtin_nontemporal_store(o, op + i + u * stride);
-      else op[i + u * stride] = o;
+      st_out<NTM>(op, rs, i + u * stride, o);
     }
   }
   for (; i < n8; i += stride) {
@@ -939,6 +953,7 @@ __global__ __launch_bounds__(NT) void bn_bwd_apply_dz2_u_kernel(const void* __re
   const i32x4* y2p = reinterpret_cast<const i32x4*>(y2sel);
   i32x4* op = reinterpret_cast<i32x4*>(dy);
   i32x4* op2 = reinterpret_cast<i32x4*>(dy2);
+  const __amdgpu_buffer_rsrc_t rs = out_rsrc(dy, n8), rs2 = out_rsrc(dy2, n8);
   auto one = [&](const i32x4& dz, const i32x4& yv, const i32x4& y2v, int j) __attribute__((always_inline)) {
     i32x4 o, o2;
 #pragma unroll
@@ -947,13 +962,8 @@ __global__ __launch_bounds__(NT) void bn_bwd_apply_dz2_u_kernel(const void* __re
       o[q] = (int)pack2<DT>(bnb_affine2(A[q], B[q], K3[q], d, unpack2<DT>((uint32_t)yv[q])));
       o2[q] = (int)pack2<DT>(bnb_affine2(A2[q], B2[q], K32[q], d, unpack2<DT>((uint32_t)y2v[q])));
     }
-    if constexpr (NTM & 2) {
-      __builtin_nontemporal_store(o, op + j);
-      __builtin_nontemporal_store(o2, op2 + j);
-    } else {
-      op[j] = o;
-      op2[j] = o2;
-    }
+    st_out<NTM>(op, rs, j, o);
+    st_out<NTM>(op2, rs2, j, o2);
   };
   for (; i + (U - 1) * stride < n8; i += U * stride) {
     i32x4 dz[U], yv[U], y2v[U];
@@ -992,6 +1002,7 @@ __global__ __launch_bounds__(NT) void bn_apply_u_kernel(
   const i32x4* yp = reinterpret_cast<const i32x4*>(y);
   const i32x4* rp = reinterpret_cast<const i32x4*>(r2);
   i32x4* op = reinterpret_cast<i32x4*>(out);
+  const __amdgpu_buffer_rsrc_t rs = out_rsrc(out, n8);
   auto one = [&](const i32x4& yv, const i32x4& rv, int j) {
     i32x4 o;
     uint32_t bits = 0;
@@ -1008,8 +1019,7 @@ __global__ __launch_bounds__(NT) void bn_apply_u_kernel(
       bits |= (v.x > 0.f ? 1u : 0u) << (2 * k);
       bits |= (v.y > 0.f ? 1u : 0u) << (2 * k + 1);
     }
-    if constexpr (NTM & 2) __builtin_nontemporal_store(o, op + j);
-    else op[j] = o;
+    st_out<NTM>(op, rs, j, o);
     if (mask) mask[j] = (uint8_t)bits;
   };
   for (; i + (U - 1) * stride < n8; i += U * stride) {
@@ -1050,7 +1060,8 @@ inline int grid_for(long long n, int cap = 8192) {
 }
 
 // Streaming-kernel shape for the 16-bit apply passes: chunks per thread per trip (0 = the plain
-// one-chunk kernels), nontemporal policy (bit 0 loads, bit 1 stores), grid cap in blocks.
+// one-chunk kernels), memory policy (bit 0 nontemporal loads, bit 1 nontemporal stores, bit 2
+// write-through stores -- 4-chunk launches: 4..7 run as 5), grid cap in blocks.
 // unroll < 0 (auto): tensors of at least min_mb MiB (the host passes 50: in-step best of
 // 30-200, ext.stream_cfg) take -unroll chunks (-1: 4), nontemporal policy ntm and grid cap
 // (host default: nt loads + stores, 65536); smaller ones the one-chunk kernels
@@ -1073,6 +1084,7 @@ StreamCfg g_stream{0, 0, 8192, 100};
     else if (u_ == 4 && m_ == 0) hipLaunchKernelGGL((KER<DT, 4, 0>), dim3(g), dim3(NT), 0, st, __VA_ARGS__); \
     else if (u_ == 4 && m_ == 1) hipLaunchKernelGGL((KER<DT, 4, 1>), dim3(g), dim3(NT), 0, st, __VA_ARGS__); \
     else if (u_ == 4 && m_ == 2) hipLaunchKernelGGL((KER<DT, 4, 2>), dim3(g), dim3(NT), 0, st, __VA_ARGS__); \
+    else if (u_ == 4 && m_ >= 4) hipLaunchKernelGGL((KER<DT, 4, 5>), dim3(g), dim3(NT), 0, st, __VA_ARGS__); \
     else if (u_ == 4) hipLaunchKernelGGL((KER<DT, 4, 3>), dim3(g), dim3(NT), 0, st, __VA_ARGS__); \
     else if (m_ == 0) hipLaunchKernelGGL((KER<DT, 1, 0>), dim3(g), dim3(NT), 0, st, __VA_ARGS__); \
     else if (m_ == 1) hipLaunchKernelGGL((KER<DT, 1, 1>), dim3(g), dim3(NT), 0, st, __VA_ARGS__); \
@@ -1107,7 +1119,7 @@ int pda_set_stream_cfg(int unroll, int ntm, int cap, int min_mb) {
   const int prev = g_stream.unroll;
   const int a = unroll < 0 ? -unroll : unroll;
   g_stream.unroll = (a == 1 || a == 2 || a == 4) ? unroll : 0;
-  g_stream.ntm = ntm & 3;
+  g_stream.ntm = ntm & 7;
   g_stream.cap = cap > 0 ? cap : 8192;
   g_stream.min_mb = min_mb >= 0 ? min_mb : 100;
   return prev;

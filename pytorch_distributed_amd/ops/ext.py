@@ -117,7 +117,7 @@ def stream_cfg() -> tuple:
     (tools/gpu_ab.sh, one box): 30.02 ms (one-chunk everywhere) vs 29.41 ms (100 MiB threshold);
     threshold 200 / 100 / 50 / 30 MiB: 29.38-29.53 / 29.16 / 29.06-29.11 / 29.02-29.13 ms; grid cap
     8192 / 16384 / 32768 / 65536: 29.53 / 29.15-29.27 / 28.90-29.09 / 28.86-28.97 ms."""
-    return (-1, 3, 65536, 50)
+    return (-1, int(os.environ.get("PDA_STREAM_NTM", "3")), 65536, 50)
 
 
 def load(required: bool = False) -> Optional[C.CDLL]:

@@ -194,12 +194,14 @@ def test_bn_forward_finalize_apply():
 
 
 @pytest.mark.parametrize("cfg", [(0, 0, 8192, 100), (1, 0, 8192, 100), (2, 0, 8192, 100),
-                                 (4, 3, 8192, 100), (2, 3, 7, 100), (4, 1, 3, 100), (-1, 3, 16384, 0)])
+                                 (4, 3, 8192, 100), (2, 3, 7, 100), (4, 1, 3, 100), (-1, 3, 16384, 0),
+                                 (4, 5, 8192, 100), (-1, 5, 7, 0)])
 @pytest.mark.parametrize("C", [64, 256, 2048])
 def test_bn_streaming_apply_configs(cfg, C):
     """bn_apply (modes 0/1/2 + ReLU bitmask) and bn_bwd_apply (dz read back) under every streaming
-    configuration (chunks per thread U, nontemporal policy, grid cap -- small caps force many
-    trips and the remainder loop; -1 = the auto policy with its size threshold at 0) against plain PyTorch fp32 on the same bf16 inputs."""
+    configuration (chunks per thread U, memory policy -- nontemporal / write-through stores --,
+    grid cap -- small caps force many trips and the remainder loop; -1 = the auto policy with its
+    size threshold at 0) against plain PyTorch fp32 on the same bf16 inputs."""
     K = _k()
     from pytorch_distributed_amd.ops import ext
     L = ext.lib()
