@@ -860,7 +860,11 @@ class NativeResNet(nn.Module):
         sc_ev = None
         if b.ds is not None:
             sd = rec["sd"]
-            dyd = self._empty(*yd.shape)
+            g = b.ds.geom(Nb)
+            # the shortcut branch folds too (its conv is 1x1): dyd = k1d*dz + k2d*yd + k3d is formed by
+            # its weight gradient and its data gradient runs dz . (k1d o Wd) + x . Gd + Wd^T k3d
+            ds_fold = fold and K.bnf_ok(g, self.dtype) and K.wgrad_bna_ok(g, Nb, self.dtype)
+            dyd = None if ds_fold else self._empty(*yd.shape)
             K.bn_bwd_finish(ws, part, G, nq, ys[-1], sl[0], sl[1], self.gamma(ul), self.dgamma(ul),
                             self.dbeta(ul), dz, dy, y2=yd, mean2=sd[0], invstd2=sd[1],
                             gamma2=self.gamma(b.ds), dgamma2=self.dgamma(b.ds), dbeta2=self.dbeta(b.ds),
@@ -868,20 +872,38 @@ class NativeResNet(nn.Module):
             # shortcut branch first: its dX is the second gradient source of the previous tail.
             # On the second stream its dgrad overlaps the conv3/conv2 chain; an event marks it for
             # the conv1 dgrad epilogue (or the stem) that consumes it
-            g = b.ds.geom(Nb)
             shortcut_g = self._empty(*x.shape)
+            kd = kt[3 * ul.cout:6 * ul.cout] if ds_fold else None
+
+            def ds_dgrad():
+                if ds_fold:
+                    cin = b.ds.conv.in_channels
+                    wfd = self._empty(b.ds.cout + cin, cin)
+                    fbd = torch.empty(cin, dtype=torch.float32, device=self.device)
+                    K.bn_fold(self.w16(b.ds), kd, wfd, fbd)
+                    K.conv_dgrad_bnf(dz, wfd, g, shortcut_g, x, fbd)
+                    return [wfd, fbd]
+                K.conv_dgrad(dyd, self.w16_ohwi(b.ds), g, shortcut_g)
+                return []
             if self._side is not None and self.ds_stream:
                 self._side.wait_stream(torch.cuda.current_stream(self.device))
                 with torch.cuda.stream(self._side):
-                    K.conv_dgrad(dyd, self.w16_ohwi(b.ds), g, shortcut_g)
+                    extra = ds_dgrad()
                 sc_ev = torch.cuda.Event()
                 sc_ev.record(self._side)
-                self._keep.extend([dyd, shortcut_g])
+                self._keep.extend([dz, x, kt, shortcut_g, *extra] + ([yd] if ds_fold else [dyd]))
             else:
-                K.conv_dgrad(dyd, self.w16_ohwi(b.ds), g, shortcut_g)
-            self._wgrad(lambda w, u=b.ds, g=g, dyd=dyd: K.conv_wgrad(dyd, x, g, self.wgrad_view(u), w,
-                                                                    accumulate=acc,
-                                                                    wscale=self.wgrad_scale), dyd, x)
+                ds_dgrad()
+            if ds_fold:
+                self._wgrad(lambda w, u=b.ds, g=g: K.conv_wgrad(dz, x, g, self.wgrad_view(u), w,
+                                                               accumulate=acc, bna=(yd, kd),
+                                                               wscale=self.wgrad_scale),
+                            dz, x, yd, kt)
+            else:
+                self._wgrad(lambda w, u=b.ds, g=g, dyd=dyd: K.conv_wgrad(dyd, x, g, self.wgrad_view(u),
+                                                                        w, accumulate=acc,
+                                                                        wscale=self.wgrad_scale),
+                            dyd, x)
         else:
             K.bn_bwd_finish(ws, part, G, nq, ys[-1], sl[0], sl[1], self.gamma(ul), self.dgamma(ul),
                             self.dbeta(ul), dz, dy, accumulate=acc, k_out=kt)

@@ -454,7 +454,8 @@ _WGRAD_DMA = {   # tools/wgrad_sweep.py, kernel + slab reduce (profiles/wgrad_sw
 
 def wgrad_plan(g: ConvGeom, Nb: int, tile: Optional[Tuple[int, int]] = None,
                target_blocks: Optional[int] = None, max_slab_bytes: int = 64 << 20,
-               f32: bool = False, dma: bool = False, wscale: Optional[float] = None):
+               f32: bool = False, dma: bool = False, wscale: Optional[float] = None,
+               bna: bool = False):
     """(bm, bn, splits, k_chunk) of a weight gradient; ``dma``: the launch may use an LDS-DMA tile
     (16-bit operands, no operand prologue); ``wscale``: the split-K block-target factor of the
     caller's schedule (None: ``PDA_WGRAD_SCALE``, the concurrent eager step's x0.7)."""
@@ -471,6 +472,8 @@ def wgrad_plan(g: ConvGeom, Nb: int, tile: Optional[Tuple[int, int]] = None,
         (bm, bn), tb = tuned
         target_blocks = target_blocks or tb
         if f32 and (tile_rows(bm) > 128 or bn > 128):   # 256-wide tiles are 16-bit only
+            bm, bn = -128, 128
+        if bna and (abs(bm), bn) not in _BNA_TILES:     # the nearest tile WGRAD_BNA is built for
             bm, bn = -128, 128
     if target_blocks is None:
         target_blocks = _WGRAD_TARGET
@@ -494,7 +497,7 @@ def wgrad_bna_ok(g: ConvGeom, Nb: int, dtype: torch.dtype) -> bool:
         return False
     if getattr(ext.lib(), "pda_conv_wgrad_bna", None) is None:
         return False
-    bm, bn, _, _ = wgrad_plan(g, Nb)
+    bm, bn, _, _ = wgrad_plan(g, Nb, bna=True)
     return (abs(bm), bn) in _BNA_TILES
 
 
@@ -518,7 +521,7 @@ def conv_wgrad(dy: torch.Tensor, x: torch.Tensor, g: ConvGeom, grad: torch.Tenso
     Nb = dy.shape[0]
     bm, bn, splits, k_chunk = wgrad_plan(g, Nb, tile, target_blocks, f32=dy.dtype == torch.float32,
                                          dma=dy.dtype != torch.float32 and pro is None and bna is None,
-                                         wscale=wscale)
+                                         wscale=wscale, bna=bna is not None)
     if bna is None and bm == -64 and bn == 256:
         # 64x256 is a WGRAD_BNA tile: the plain weight gradient of that plan runs 64x128 tiles over
         # the same split-K chunks (same accumulation order per element: bitwise the same result)

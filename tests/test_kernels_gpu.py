@@ -891,3 +891,38 @@ def test_conv_wgrad_bna_conv3_tiles(Cout, Cin, H, tile):
     K.conv_wgrad(dy, y2, g, dw_u, ws, pro=(sc, sh), tile=tile)
     torch.cuda.synchronize()
     assert rel_err(dw_f, dw_u) < 2e-3
+
+
+@pytest.mark.parametrize("geo", [(2, 8, 64, 256), (2, 14, 256, 512), (1, 14, 512, 1024)])
+def test_conv_dgrad_bnf_stride2_shortcut(geo):
+    """DGRAD_BNF on a strided 1x1 shortcut conv (the downsample branch of the tail fold): the Gram
+    operand is the block input x at the landing pixels, the other parity classes are exact zeros
+    (no bias there), against apply-then-plain-dgrad."""
+    K = _k()
+    dtype = torch.bfloat16
+    Nb, H, Cin, Cout = geo
+    torch.manual_seed(Cout)
+    g = K.ConvGeom(Nb, H, H, Cin, Cout, 1, 1, 2, 0)
+    w = (torch.randn(Cout, 1, 1, Cin, device=DEV) * 0.05).to(dtype)
+    x = torch.relu(torch.randn(Nb, H, H, Cin, device=DEV)).to(dtype)
+    yd = torch.empty(Nb, g.Ho, g.Wo, Cout, device=DEV, dtype=dtype)
+    K.conv_fwd(x, w.view(Cout, Cin), g, yd)
+    dz = torch.randn(Nb, g.Ho, g.Wo, Cout, device=DEV).to(dtype)
+    k = torch.cat([torch.rand(Cout, device=DEV) + 0.5, torch.randn(Cout, device=DEV) * 0.3,
+                   torch.randn(Cout, device=DEV) * 0.2])
+    dyd = (k[:Cout] * dz.float() + k[Cout:2 * Cout] * yd.float() + k[2 * Cout:]).to(dtype)
+    ref = torch.empty(Nb, H, H, Cin, device=DEV, dtype=dtype)
+    K.conv_dgrad(dyd, w, g, ref)
+    wf = torch.empty(Cout + Cin, Cin, device=DEV, dtype=dtype)
+    b = torch.empty(Cin, device=DEV)
+    K.bn_fold(w.view(Cout, Cin), k, wf, b)
+    out = torch.full((Nb, H, H, Cin), 7.0, device=DEV, dtype=dtype)
+    K.conv_dgrad_bnf(dz, wf, g, out, x, b)
+    torch.cuda.synchronize()
+    exact = ((k[:Cout] * dz.float() + k[Cout:2 * Cout] * yd.float() + k[2 * Cout:]).view(-1, Cout)
+             @ w.view(Cout, Cin).float()).view(Nb, g.Ho, g.Wo, Cin)
+    land = out[:, ::2, ::2]
+    assert out[:, 1::2].abs().max().item() == 0 and out[:, :, 1::2].abs().max().item() == 0
+    e_bnf, e_ref = rel_err(land, exact), rel_err(ref[:, ::2, ::2], exact)
+    print(f"shortcut dX vs fp32: fold {e_bnf:.2e}, apply+dgrad {e_ref:.2e}")
+    assert e_bnf < 2 * e_ref + 5e-3, (e_bnf, e_ref)
