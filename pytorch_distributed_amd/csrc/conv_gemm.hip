@@ -188,6 +188,7 @@ constexpr int conv_min_blocks() {
   if (DT == DT_F32S) return BM * BN <= 64 * 64 ? 4 : 2;   // hi + lo tiles: twice the LDS
   if (DT != DT_F32 && BM * BN <= 64 * 64) return 5;
   if (DT != DT_F32 && STAGES == 1 && BM * BN <= 128 * 64) return 4;
+  if (BM > 128) return 2;   // 256-row register tiles (8 A chunks per thread): 3 blocks spill
   return (STAGES == 1 && BM * BN <= 128 * 128) ? 3 : 2;
 }
 
@@ -1627,6 +1628,9 @@ static int dispatch(int dt, int bm, int bn, const ConvParams& p, dim3 grid, hipS
     // 256-wide tiles only where they measured faster (profiles/convbench_r1_v6.txt): wgrad 256x128
     // (3x3 layers 3-4; the dgrad 128x256 tile never beat 128x128 in the step and is not built)
     if constexpr (PASS == WGRAD) { TILE_CASE1(DT_BF16, 256, 128) TILE_CASE1(DT_F16, 256, 128) }
+    // 256x64 forward (the N = 64 stem: K = 256 is 4 k-tiles, so a block's life is mostly its load
+    // -> MFMA -> epilogue latency chain; twice the rows per chain)
+    if constexpr (PASS == FWD) { TILE_CASE1(DT_BF16, 256, 64) TILE_CASE1(DT_F16, 256, 64) }
     TILE_CASE1(DT_F16, 128, 128) TILE_CASE1(DT_F16, 128, 64) TILE_CASE1(DT_F16, 64, 128)
     TILE_CASE1(DT_F32, 128, 128) TILE_CASE1(DT_F32, 128, 64) TILE_CASE1(DT_F32, 64, 128)
     // the split-f32 path stages hi + lo tiles: single-stage only (LDS)

@@ -492,6 +492,8 @@ class _ReplicaGraph:
 
     def _end_segment(self, upto: Optional[int]) -> None:
         self.graphs[-1].capture_end()
+        if self._pool_h is None:   # (torch hands out the pool id only after a finished capture)
+            self._pool_h = self.graphs[0].pool()
         self.sides.append(self._capture_side() if self.side_split else None)
         self.seg_reduce.append(upto)
 
@@ -597,8 +599,8 @@ class _ReplicaGraph:
                     self._capturing = True
                     ended = False
                     try:
+                        self._pool_h = None
                         g.capture_begin()
-                        self._pool_h = g.pool()
                         self._body()
                         self._end_segment(self.m.numel)
                         ended = True

@@ -42,13 +42,19 @@ def test_production_step_matches_fp32_reference():
     x, y = synthetic_images(torch.arange(B), 0, "train", 1000, S, device=DEV)
     x = x.to(torch.bfloat16).float()
     res = {}
+    import time
     for mode in ("fp32", "bf16"):
+        t0 = time.time()
         tm = copy.deepcopy(ref).to(DEV).train()
-        with torch.autocast("cuda", dtype=torch.bfloat16, enabled=mode == "bf16"):
+        # ATen's own convolutions (im2col + BLAS GEMM), not MIOpen: no per-shape kernel compile or
+        # find step on a fresh box (MIOpen's fp32 224-px find alone outlasts the test's budget)
+        with torch.backends.cudnn.flags(enabled=False), \
+                torch.autocast("cuda", dtype=torch.bfloat16, enabled=mode == "bf16"):
             logits = tm(x)
-        loss = F.cross_entropy(logits.float(), y)
-        loss.backward()
+            loss = F.cross_entropy(logits.float(), y)
+            loss.backward()
         torch.cuda.synchronize()
+        print(f"torch {mode} reference step: {time.time() - t0:.1f} s", flush=True)
         res[mode] = (logits.detach().float(), loss.item(), _grads(tm),
                      {n: b.detach().clone() for n, b in tm.named_buffers()})
         del tm, logits, loss

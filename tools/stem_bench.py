@@ -23,7 +23,8 @@ def main():
     y = torch.empty(B, g.Ho, g.Wo, 64, device=dev, dtype=torch.bfloat16)
     M = B * g.Ho * g.Wo
     stats = torch.empty(math.ceil(M / 64) * 3 * 64, device=dev)
-    tiles = [(-128, 64), (128, 64), (64, 64), (-64, 64), (-128, 128), (64, 128), (-64, 128)]
+    tiles = [(-128, 64), (-256, 64), (128, 64), (64, 64), (-64, 64), (-128, 128), (64, 128),
+             (-64, 128)]
     ref = None
     times = {t: [] for t in tiles}
     ok = {}
