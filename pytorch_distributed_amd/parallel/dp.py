@@ -197,7 +197,11 @@ class DataParallel(nn.Module):
         if self.group is not None:
             self.group.all_reduce(ts, streams=streams)
             return
-        # replicas sharing a device (tests): plain copies, on replica 0's stream
+        # replicas sharing a device (tests): plain copies, on replica 0's stream, ordered after every
+        # replica's stream (each waited only on its own replica's work) and before all of them
+        if streams is not None:
+            for c in streams[1:]:
+                streams[0].wait_stream(c)
         ctx = torch.cuda.stream(streams[0]) if streams is not None else contextlib.nullcontext()
         with ctx:
             total = ts[0].clone()
@@ -205,6 +209,9 @@ class DataParallel(nn.Module):
                 total.add_(t.to(total.device))
             for t in ts:
                 t.copy_(total, non_blocking=True)
+        if streams is not None:
+            for c in streams[1:]:
+                c.wait_stream(streams[0])
 
     @torch.no_grad()
     def _reduce_grads(self) -> None:
