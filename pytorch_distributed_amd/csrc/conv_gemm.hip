@@ -1458,27 +1458,34 @@ __global__ __launch_bounds__(256) void wgrad_reduce4_kernel(const float* __restr
 // weights [Cout][Cin] (1x1, OHWI); k: [k1; k2; k3] (3 x Cout f32, the BN-backward apply
 // coefficients of the BN after the conv). Writes Wf = [k1 o W ; G] ([Cout + Cin][Cin] 16-bit),
 // G = W^T diag(k2) W, and b = W^T k3 (f32 [Cin]).
-// Block (ti, tj) computes the 64x64 tile G[ti*64.., tj*64..] over K = Cout on MFMA 16x16x32: the
-// k-tiles of W's column panels ti (A) and tj (B, scaled by k2 per row while staging) go to LDS in
-// the conv kernel's COL layout and are read back by the same transposed fragment loads. The blocks
-// with ti == 0 also write the k1-scaled rows of their column panel and its bias (per-thread f32
-// partials over fixed row sets, combined in a fixed order: deterministic).
+// Block (ti, tj) computes the 64x64 tile G[ti*64.., tj*64..] over K = Cout on MFMA 16x16x32 with
+// FOLD_G = 4 groups of 4 waves: group q takes the k-tiles kt = q, q+4, ... (a quarter of the
+// dependent load -> MFMA chain; the next k-tile is loaded into registers while the current one is
+// multiplied), each group's 64x64 f32 partial goes to LDS and group 0 sums them in group order.
+// The k-tiles of W's column panels ti (A) and tj (B, scaled by k2 per row while staging) use the
+// conv kernel's COL layout and transposed fragment reads. Blocks with ti == 0 also write the
+// k1-scaled rows of their column panel and its bias (per-thread f32 partials over fixed row sets,
+// combined in a fixed order): deterministic.
+constexpr int FOLD_G = 4;
 template <int DT>
-__global__ __launch_bounds__(256) void bn_fold_kernel(const u16* __restrict__ W, const float* __restrict__ k,
-                                                      int Cout, int Cin, u16* __restrict__ Wf,
-                                                      float* __restrict__ bias) {
-  __shared__ __attribute__((aligned(16))) char smem[2 * 64 * 64 * 2];
-  __shared__ float bred[32][64];
+__global__ __launch_bounds__(256 * FOLD_G) void bn_fold_kernel(const u16* __restrict__ W,
+                                                               const float* __restrict__ k, int Cout,
+                                                               int Cin, u16* __restrict__ Wf,
+                                                               float* __restrict__ bias) {
+  // per group: A and B COL tiles (8 KB each); reused afterwards for the f32 partials (16 KB each)
+  __shared__ __attribute__((aligned(16))) char smem[FOLD_G * 2 * 64 * 64 * 2];
+  __shared__ float bred[FOLD_G * 32][64];
   const int nT = Cin >> 6;
   const int ti = blockIdx.x / nT, tj = blockIdx.x - ti * nT;
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int tid = threadIdx.x & 255, grp = threadIdx.x >> 8;
+  const int lane = tid & 63, wid = tid >> 6;
   const int wr = wid >> 1, wc = wid & 1;
   const float* k1 = k;
   const float* k2 = k + Cout;
   const float* k3 = k + 2 * Cout;
   const bool side = ti == 0;   // this block also writes the k1 rows and the bias of panel tj
-  char* sa = smem;
-  char* sb = smem + 64 * 64 * 2;
+  char* sa = smem + grp * (2 * 64 * 64 * 2);
+  char* sb = sa + 64 * 64 * 2;
   f32x4 acc[2][2];
 #pragma unroll
   for (int i = 0; i < 2; ++i)
@@ -1488,28 +1495,44 @@ __global__ __launch_bounds__(256) void bn_fold_kernel(const u16* __restrict__ W,
 #pragma unroll
   for (int e = 0; e < 8; ++e) bs[e] = 0.f;
   const int cc = tid & 7;   // the thread's 16-B chunk (8 columns) of a 64-column panel row
-  for (int k0 = 0; k0 < Cout; k0 += 64) {
+  const int nk = Cout >> 6;
+  i32x4 va[2], vb[2];
+  auto load = [&](int kt) __attribute__((always_inline)) {
+#pragma unroll
+    for (int r = 0; r < 2; ++r) {
+      const int kk = kt * 64 + (tid >> 3) + 32 * r;
+      va[r] = *reinterpret_cast<const i32x4*>(W + (size_t)kk * Cin + ti * 64 + cc * 8);
+      vb[r] = *reinterpret_cast<const i32x4*>(W + (size_t)kk * Cin + tj * 64 + cc * 8);
+    }
+  };
+  if (grp < nk) load(grp);
+  // block-uniform trip count (barriers inside); a group past the end stages zeros
+  for (int kb = 0; kb < nk; kb += FOLD_G) {
+    const int kt = kb + grp;
+    const bool live = kt < nk;
+    if (!live) {
+#pragma unroll
+      for (int r = 0; r < 2; ++r) va[r] = vb[r] = i32x4{0, 0, 0, 0};
+    }
 #pragma unroll
     for (int r = 0; r < 2; ++r) {
       const int krow = (tid >> 3) + 32 * r;
-      const int kk = k0 + krow;
-      const i32x4 va = *reinterpret_cast<const i32x4*>(W + (size_t)kk * Cin + ti * 64 + cc * 8);
-      const i32x4 vb = *reinterpret_cast<const i32x4*>(W + (size_t)kk * Cin + tj * 64 + cc * 8);
+      const int kk = live ? kt * 64 + krow : 0;
       const float s2 = k2[kk];
       i32x4 wb;
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
-        const f32x2 f = unpack2<DT>((uint32_t)vb[q]);
+        const f32x2 f = unpack2<DT>((uint32_t)vb[r][q]);
         wb[q] = (int)pack2<DT>(f32x2{f.x * s2, f.y * s2});
       }
-      *reinterpret_cast<i32x4*>(sa + col_addr<64>(krow, cc)) = va;
+      *reinterpret_cast<i32x4*>(sa + col_addr<64>(krow, cc)) = va[r];
       *reinterpret_cast<i32x4*>(sb + col_addr<64>(krow, cc)) = wb;
-      if (side) {   // k1 o W rows and the bias partials of panel tj
+      if (side && live) {   // k1 o W rows and the bias partials of panel tj
         const float s1 = k1[kk], s3 = k3[kk];
         i32x4 w1;
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
-          const f32x2 f = unpack2<DT>((uint32_t)vb[q]);
+          const f32x2 f = unpack2<DT>((uint32_t)vb[r][q]);
           w1[q] = (int)pack2<DT>(f32x2{f.x * s1, f.y * s1});
           bs[2 * q] = __builtin_fmaf(s3, f.x, bs[2 * q]);
           bs[2 * q + 1] = __builtin_fmaf(s3, f.y, bs[2 * q + 1]);
@@ -1518,6 +1541,7 @@ __global__ __launch_bounds__(256) void bn_fold_kernel(const u16* __restrict__ W,
       }
     }
     __syncthreads();
+    if (kt + FOLD_G < nk) load(kt + FOLD_G);   // in flight during this k-tile's MFMAs
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
       s16x8 fa[2], fb[2];
@@ -1532,27 +1556,39 @@ __global__ __launch_bounds__(256) void bn_fold_kernel(const u16* __restrict__ W,
     }
     __syncthreads();
   }
-  // acc[i][j][e] = G[ti*64 + wr*32 + i*16 + (lane&15)][tj*64 + wc*32 + j*16 + 4*(lane>>4) + e]
+  // group partials -> LDS (f32 [64][64] per group), fixed-order sum by group 0
+  __syncthreads();
+  float* part = reinterpret_cast<float*>(smem) + grp * 64 * 64;
 #pragma unroll
   for (int i = 0; i < 2; ++i)
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
-      const int row = ti * 64 + wr * 32 + i * 16 + (lane & 15);
-      const int col = tj * 64 + wc * 32 + j * 16 + 4 * (lane >> 4);
-      uint2 pk;
-      pk.x = pack2<DT>(f32x2{acc[i][j][0], acc[i][j][1]});
-      pk.y = pack2<DT>(f32x2{acc[i][j][2], acc[i][j][3]});
-      *reinterpret_cast<uint2*>(Wf + (size_t)(Cout + row) * Cin + col) = pk;
+      const int row = wr * 32 + i * 16 + (lane & 15);
+      const int col = wc * 32 + j * 16 + 4 * (lane >> 4);
+      *reinterpret_cast<f32x4*>(part + row * 64 + col) = acc[i][j];
     }
-  if (!side) return;
-  // bias: thread (row set tid>>3, chunk cc) holds 8 column partials; fixed-order combine
 #pragma unroll
-  for (int e = 0; e < 8; ++e) bred[tid >> 3][cc * 8 + e] = bs[e];
+  for (int e = 0; e < 8; ++e) bred[grp * 32 + (tid >> 3)][cc * 8 + e] = bs[e];
   __syncthreads();
-  if (tid < 64) {
-    float b = 0.f;
-    for (int g = 0; g < 32; ++g) b += bred[g][tid];
-    bias[tj * 64 + tid] = b;
+  if (grp == 0) {
+    const float* p0 = reinterpret_cast<const float*>(smem);
+    // thread t: row t / 4, 16 columns (t % 4) * 16 ..
+    const int row = tid >> 2, c0 = (tid & 3) * 16;
+#pragma unroll
+    for (int c = 0; c < 16; c += 4) {
+      f32x4 v = *reinterpret_cast<const f32x4*>(p0 + row * 64 + c0 + c);
+#pragma unroll
+      for (int g = 1; g < FOLD_G; ++g) v += *reinterpret_cast<const f32x4*>(p0 + g * 4096 + row * 64 + c0 + c);
+      uint2 pk;
+      pk.x = pack2<DT>(f32x2{v[0], v[1]});
+      pk.y = pack2<DT>(f32x2{v[2], v[3]});
+      *reinterpret_cast<uint2*>(Wf + (size_t)(Cout + ti * 64 + row) * Cin + tj * 64 + c0 + c) = pk;
+    }
+    if (side && tid < 64) {
+      float b = 0.f;
+      for (int g = 0; g < FOLD_G * 32; ++g) b += bred[g][tid];
+      bias[tj * 64 + tid] = b;
+    }
   }
 }
 
@@ -1794,11 +1830,11 @@ int pda_bn_fold(const void* w, const float* k, int Cout, int Cin, void* wf, floa
   if ((Cout % 64) || (Cin % 64) || Cin > 4096) return -2;
   const dim3 grid((Cin / 64) * (Cin / 64));
   if (dt == DT_BF16)
-    hipLaunchKernelGGL(bn_fold_kernel<DT_BF16>, grid, dim3(256), 0, st, (const u16*)w, k, Cout, Cin,
-                       (u16*)wf, bias);
+    hipLaunchKernelGGL(bn_fold_kernel<DT_BF16>, grid, dim3(256 * FOLD_G), 0, st, (const u16*)w, k,
+                       Cout, Cin, (u16*)wf, bias);
   else if (dt == DT_F16)
-    hipLaunchKernelGGL(bn_fold_kernel<DT_F16>, grid, dim3(256), 0, st, (const u16*)w, k, Cout, Cin,
-                       (u16*)wf, bias);
+    hipLaunchKernelGGL(bn_fold_kernel<DT_F16>, grid, dim3(256 * FOLD_G), 0, st, (const u16*)w, k,
+                       Cout, Cin, (u16*)wf, bias);
   else
     return -1;
   return (int)hipGetLastError();

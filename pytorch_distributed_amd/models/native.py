@@ -140,7 +140,16 @@ class NativeResNet(nn.Module):
         self.stem_bna = os.environ.get("PDA_STEM_BNA", "1") != "0"
         self.tail_mask = True         # tails store the ReLU bitmask the backward reads
         # consumer-side tail fold of the Bottleneck BN backward (see _block_backward)
-        self.bn_fold = os.environ.get("PDA_BN_FOLD", "0") != "0"
+        # ("0" off, "1" every stage, or the stages to fold, e.g. "12" = layer1 and layer2). Default
+        # layer1-3: in-step A/B at the bench config (profiles/ab_r4.md) 28.26 ms off, 27.89 all
+        # stages, 27.55 "12", 27.47 "123"; layer4's fold costs more than its apply pass (its G is
+        # 512x512 over K = 2048 and its 7x7 dgrad has few tiles to hide the extra K). The
+        # shortcut branch of a downsampling block folds too only with PDA_BN_FOLD_DS=1 (otherwise it
+        # keeps the apply pass and its LDS-DMA weight-gradient tile)
+        fold = os.environ.get("PDA_BN_FOLD", "123")
+        self.bn_fold = fold != "0"
+        self.bn_fold_stages = None if fold in ("0", "1") else {int(c) for c in fold if c.isdigit()}
+        self.bn_fold_ds = os.environ.get("PDA_BN_FOLD_DS", "0") != "0"
         self.ds_stream = True         # the shortcut conv runs on the second stream
         # weight gradients on a second HIP stream: nothing in the backward chain consumes them, so
         # the (compute-bound) wgrad GEMMs fill the CUs left idle by the (HBM-bound) BN-backward
@@ -829,6 +838,9 @@ class NativeResNet(nn.Module):
         ul = b.units[-1]
         if not self.bn_fold or self.f32 or ul.conv.kernel_size != (1, 1):
             return False
+        if self.bn_fold_stages is not None and not (
+                b.name.startswith("layer") and int(b.name[5]) in self.bn_fold_stages):
+            return False
         sync = getattr(self.ws, "sync_comm", None)
         if sync is not None and sync.world_size > 1:
             return False
@@ -863,7 +875,7 @@ class NativeResNet(nn.Module):
             g = b.ds.geom(Nb)
             # the shortcut branch folds too (its conv is 1x1): dyd = k1d*dz + k2d*yd + k3d is formed by
             # its weight gradient and its data gradient runs dz . (k1d o Wd) + x . Gd + Wd^T k3d
-            ds_fold = fold and K.bnf_ok(g, self.dtype) and K.wgrad_bna_ok(g, Nb, self.dtype)
+            ds_fold = fold and self.bn_fold_ds and K.bnf_ok(g, self.dtype) and K.wgrad_bna_ok(g, Nb, self.dtype)
             dyd = None if ds_fold else self._empty(*yd.shape)
             K.bn_bwd_finish(ws, part, G, nq, ys[-1], sl[0], sl[1], self.gamma(ul), self.dgamma(ul),
                             self.dbeta(ul), dz, dy, y2=yd, mean2=sd[0], invstd2=sd[1],

@@ -357,8 +357,8 @@ def test_probe_and_segment_hooks_fire_per_block_and_change_nothing():
 
 
 def test_tail_fold_matches_apply_path():
-    """The consumer-side tail fold (PDA_BN_FOLD, default on: the Bottleneck tail BN backward is
-    never applied; conv3's gradients take (dz, k) -- csrc/conv_gemm.hip DGRAD_BNF / WGRAD_BNA)
+    """The consumer-side tail fold (PDA_BN_FOLD=1 PDA_BN_FOLD_DS=1: the Bottleneck tail BN backward
+    is never applied; conv3's gradients take (dz, k) -- csrc/conv_gemm.hip DGRAD_BNF / WGRAD_BNA)
     against the apply-pass path on the same forward state: gradients agree to bf16 rounding, and
     each is as close to the fp32 reference as torch's bf16 autocast is."""
     tm, nm = _pair("resnet50", image=64)
@@ -371,7 +371,7 @@ def test_tail_fold_matches_apply_path():
     crit = nm.make_criterion()
     grads = {}
     for fold in (False, True):
-        nm.bn_fold = fold
+        nm.bn_fold, nm.bn_fold_ds, nm.bn_fold_stages = fold, fold, None
         nm.zero_grad_flat()
         crit(nm(x), y).backward()
         torch.cuda.synchronize()
