@@ -150,6 +150,11 @@ class NativeResNet(nn.Module):
         self.bn_fold = fold != "0"
         self.bn_fold_stages = None if fold in ("0", "1") else {int(c) for c in fold if c.isdigit()}
         self.bn_fold_ds = os.environ.get("PDA_BN_FOLD_DS", "0") != "0"
+        # the head BN (bn1, consumer conv1: 1x1, Cin = 4 Cout) folds in the concatenated form
+        # dX = [dz | y1] . [k1 o W1 ; k2 o W1] + W1^T k3 (K = 2 Cout; the Gram form would be Cout + Cin)
+        # and conv1's weight gradient forms dy1 while staging; digits = stages, "0" none
+        f1 = os.environ.get("PDA_BN_FOLD1", "0")
+        self.bn_fold1 = set() if f1 == "0" else {int(c) for c in f1 if c.isdigit()}
         self.ds_stream = True         # the shortcut conv runs on the second stream
         # weight gradients on a second HIP stream: nothing in the backward chain consumes them, so
         # the (compute-bound) wgrad GEMMs fill the CUs left idle by the (HBM-bound) BN-backward
@@ -847,6 +852,19 @@ class NativeResNet(nn.Module):
         g = ul.geom(Nb)
         return K.bnf_ok(g, self.dtype) and K.wgrad_bna_ok(g, Nb, self.dtype)
 
+    def _head_fold_ok(self, b: Block, Nb: int) -> bool:
+        """Whether block ``b``'s head BatchNorm (bn1) backward is folded into conv1's gradients
+        (PDA_BN_FOLD1, the concatenated form): Bottleneck blocks, 16-bit, per-rank statistics, a 1x1
+        stride-1 conv1 and tiles the fold kernels are built for."""
+        if (not self.bn_fold1 or self.f32 or len(b.units) != 3 or not b.name.startswith("layer")
+                or int(b.name[5]) not in self.bn_fold1):
+            return False
+        sync = getattr(self.ws, "sync_comm", None)
+        if sync is not None and sync.world_size > 1:
+            return False
+        g = b.units[0].geom(Nb)
+        return g.stride == 1 and K.bnf_ok(g, self.dtype) and K.wgrad_bna_ok(g, Nb, self.dtype)
+
     def _block_backward(self, b: Block, rec, tail, prev, acc):
         """Returns (dx_main, shortcut_grad, prev_tail) -- the last is the fused reduction of the
         previous block's tail, or None for the first block.
@@ -923,6 +941,8 @@ class NativeResNet(nn.Module):
         dx_main = None
         prev_tail = None
         cur = torch.cuda.current_stream(self.device)
+        head = self._head_fold_ok(b, Nb)
+        hcat = None    # (dz1, k1) of the folded head BN
         for j in range(n - 1, -1, -1):
             u = b.units[j]
             a_in = acts[j]
@@ -933,7 +953,18 @@ class NativeResNet(nn.Module):
                 a_in = ys[j - 1]
                 pro = (sp_[2], sp_[3])
             bnf = None
-            if fold and j == n - 1:
+            if hcat is not None and j == 0:
+                # head fold: (dz1, k) stand for dy1 in both of conv1's gradients
+                dzc, kc = hcat
+                wf = self._empty(2 * u.cout, u.conv.in_channels)
+                fb = torch.empty(u.conv.in_channels, dtype=torch.float32, device=self.device)
+                K.bn_fold_cat(self.w16(u), kc, wf, fb)
+                bnf = (wf, fb, dzc, ys[0])
+                self._wgrad(lambda w, u=u, g=g, a=a_in, pro=pro, y1=ys[0], dzc=dzc, kc=kc:
+                            K.conv_wgrad(dzc, a, g, self.wgrad_view(u), w, accumulate=acc, pro=pro,
+                                         bna=(y1, kc), wscale=self.wgrad_scale),
+                            dzc, a_in, ys[0], kc)
+            elif fold and j == n - 1:
                 # tail fold: (dz, k) stand for dy3 in both of conv3's gradients
                 k3 = kt[:3 * u.cout]
                 cin = u.conv.in_channels
@@ -951,7 +982,9 @@ class NativeResNet(nn.Module):
                                          wscale=self.wgrad_scale), dy, a_in)
 
             def dgrad(out, epi=None, u=u, g=g, dy=dy, bnf=bnf, a_in=a_in, pro=pro):
-                if bnf is not None:
+                if bnf is not None and len(bnf) == 4:
+                    K.conv_dgrad_bnf(bnf[2], bnf[0], g, out, bnf[3], bnf[1], epi=epi, cat=True)
+                elif bnf is not None:
                     K.conv_dgrad_bnf(dz, bnf[0], g, out, a_in, bnf[1], xa_pro=pro, epi=epi)
                 else:
                     K.conv_dgrad(dy, self.w16_ohwi(u), g, out, epi=epi)
@@ -963,10 +996,18 @@ class NativeResNet(nn.Module):
                 # the dgrad's epilogue produces dz and the BN-backward partials of bn_{j-1}
                 epi, part_p, nq_p = K.bn_epilogue(ws, Gp, ys[j - 1], sp[2], sp[3])
                 dgrad(out, epi)                                      # out = dz of bn_{j-1}
-                dyp = self._empty(*ys[j - 1].shape)
-                K.bn_bwd_finish(ws, part_p, Gp, nq_p, ys[j - 1], sp[0], sp[1], self.gamma(up),
-                                self.dgamma(up), self.dbeta(up), out, dyp, accumulate=acc)
-                dy = dyp
+                if head and j == 1:   # bn1 folded: coefficients only, conv1 consumes (dz1, k)
+                    kc = torch.empty(3 * up.cout, dtype=torch.float32, device=self.device)
+                    K.bn_bwd_finish(ws, part_p, Gp, nq_p, ys[0], sp[0], sp[1], self.gamma(up),
+                                    self.dgamma(up), self.dbeta(up), out, None, accumulate=acc,
+                                    k_out=kc)
+                    hcat = (out, kc)
+                    dy = None
+                else:
+                    dyp = self._empty(*ys[j - 1].shape)
+                    K.bn_bwd_finish(ws, part_p, Gp, nq_p, ys[j - 1], sp[0], sp[1], self.gamma(up),
+                                    self.dgamma(up), self.dbeta(up), out, dyp, accumulate=acc)
+                    dy = dyp
             elif prev is not None:
                 pb, prec = prev
                 if sc_ev is not None:

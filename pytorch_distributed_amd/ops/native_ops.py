@@ -344,6 +344,17 @@ def bn_fold(w: torch.Tensor, k: torch.Tensor, wf: torch.Tensor, bias: torch.Tens
                                 stream(w.device)), "bn_fold")
 
 
+def bn_fold_cat(w: torch.Tensor, k: torch.Tensor, wf: torch.Tensor, bias: torch.Tensor) -> None:
+    """Operands of the concatenated form of :func:`conv_dgrad_bnf` (``xa_c`` = Cout) for a 1x1 conv:
+    ``wf`` [2 Cout, Cin] = [k1 o W ; k2 o W], ``bias`` [Cin] = W^T k3 (csrc/conv_gemm.hip
+    bn_fold_cat_kernel)."""
+    Cout, Cin = w.shape[0], w.shape[-1]
+    if wf.shape[0] != 2 * Cout or wf.shape[-1] != Cin or wf.dtype != w.dtype or k.numel() < 3 * Cout:
+        raise ValueError("bn_fold_cat: wf [2 Cout, Cin] of the weights' dtype, k 3 x Cout")
+    check(ext.lib().pda_bn_fold_cat(ptr(w), ptr(k), Cout, Cin, ptr(wf), ptr(bias), dt_of(w),
+                                    stream(w.device)), "bn_fold_cat")
+
+
 def bnf_ok(g: ConvGeom, dtype: torch.dtype) -> bool:
     """Whether the consumer-side BN-backward fold (:func:`conv_dgrad_bnf`) serves this conv: a 1x1
     conv without padding, 16-bit operands, channel counts in whole 64-column panels."""
@@ -355,12 +366,14 @@ def bnf_ok(g: ConvGeom, dtype: torch.dtype) -> bool:
 def conv_dgrad_bnf(dz: torch.Tensor, wf: torch.Tensor, g: ConvGeom, dx: torch.Tensor,
                    xa: torch.Tensor, bias: torch.Tensor, xa_pro=None,
                    epi: Optional[ext.BnEpi] = None,
-                   tile: Optional[Tuple[int, int]] = None) -> torch.Tensor:
+                   tile: Optional[Tuple[int, int]] = None, cat: bool = False) -> torch.Tensor:
     """dX of a 1x1 conv whose dY = k1*dz + k2*y + k3 is never materialised (y = the conv's forward
     output): dX = dz . (k1 o W) + xa . G + b with (wf, bias) from :func:`bn_fold` and ``xa`` the
     conv's forward input (``xa_pro`` = (scale, shift): xa is PRE-BatchNorm and the activation
     relu(xa*scale+shift) is recomputed, as the forward's prologue did). ``epi``: the same fused
-    BN-backward epilogue as :func:`conv_dgrad`."""
+    BN-backward epilogue as :func:`conv_dgrad`.
+    ``cat``: the concatenated form dX = [dz | y] . [k1 o W ; k2 o W] + b (stride 1) with ``xa`` = y
+    and (wf, bias) from :func:`bn_fold_cat` -- K = 2 Cout instead of Cout + Cin."""
     Nb = dz.shape[0]
     kdt = _kdt(dz)
     bm, bn = tile or dgrad_tile(g, Nb)
@@ -371,8 +384,8 @@ def conv_dgrad_bnf(dz: torch.Tensor, wf: torch.Tensor, g: ConvGeom, dx: torch.Te
     rc = ext.lib().pda_conv_dgrad_bnf(C.byref(d), ptr(dz), ptr(wf), ptr(dx),
                                       C.byref(epi) if epi is not None else None, ptr(xa),
                                       ptr(xa_pro[0] if xa_pro else None),
-                                      ptr(xa_pro[1] if xa_pro else None), ptr(bias), kdt, kbm, kbn,
-                                      stream(dz.device))
+                                      ptr(xa_pro[1] if xa_pro else None), ptr(bias),
+                                      g.Cout if cat else 0, kdt, kbm, kbn, stream(dz.device))
     check(rc, "conv_dgrad_bnf")
     return dx
 
@@ -475,6 +488,8 @@ def wgrad_plan(g: ConvGeom, Nb: int, tile: Optional[Tuple[int, int]] = None,
             bm, bn = -128, 128
         if bna and (abs(bm), bn) not in _BNA_TILES:     # the nearest tile WGRAD_BNA is built for
             bm, bn = -128, 128
+        if bna and M <= 64 and tile_rows(bm) > 64:        # Cout 64 (the layer1 conv1): no idle rows
+            bm, bn = -64, 128
     if target_blocks is None:
         target_blocks = _WGRAD_TARGET
     # (the stem's weight gradient runs alone at the end of the backward: its isolated optimum holds)

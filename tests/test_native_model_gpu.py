@@ -383,3 +383,33 @@ def test_tail_fold_matches_apply_path():
         if e_fold > 1.3 * e_apply + 0.01:
             bad.append((n, e_fold, e_apply))
     assert not bad, bad
+
+
+def test_head_fold_matches_apply_path():
+    """The head-BN fold (PDA_BN_FOLD1: bn1's backward never applied; conv1's data gradient runs the
+    concatenated DGRAD_BNF [dz | y1] . [k1 o W1 ; k2 o W1] + W1^T k3 and its weight gradient
+    WGRAD_BNA) against the apply-pass path: each as close to the fp32 reference as torch's bf16
+    autocast is."""
+    tm, nm = _pair("resnet50", image=64)
+    torch.manual_seed(11)
+    x = torch.randn(16, 3, 64, 64, device=DEV).to(torch.bfloat16).float()
+    y = torch.randint(0, 1000, (16,), device=DEV)
+    nm.train()
+    tm.train()
+    F.cross_entropy(tm(x), y).backward()
+    crit = nm.make_criterion()
+    grads = {}
+    for fold in (False, True):
+        nm.bn_fold1 = {1, 2, 3, 4} if fold else set()
+        nm.zero_grad_flat()
+        crit(nm(x), y).backward()
+        torch.cuda.synchronize()
+        grads[fold] = dict((n, p.grad.detach().float().clone()) for n, p in nm.named_parameters())
+    nm.bn_fold1 = set()
+    tp = dict(tm.named_parameters())
+    bad = []
+    for n in grads[True]:
+        e_fold, e_apply = rel_err(grads[True][n], tp[n].grad), rel_err(grads[False][n], tp[n].grad)
+        if e_fold > 1.3 * e_apply + 0.01:
+            bad.append((n, e_fold, e_apply))
+    assert not bad, bad
