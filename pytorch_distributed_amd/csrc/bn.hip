@@ -1155,8 +1155,7 @@ static int stats_cg(int C, int cg) {
 int pda_bn_fwd_stats(const float* part, int T, int C, int bm, int M, int S, double* slabs, int* cnt,
                      const BnFwdOut* o, int cg, hipStream_t st) {
   if ((C & 3) || S <= 0 || S > T || !o || !cnt || !slabs) return -2;
-  const int CG = stats_cg(C, cg);
-  if (C % CG) return -2;
+  const int CG = stats_cg(C, cg);   // (a ragged last group: its lanes past C stay idle)
   hipLaunchKernelGGL((bn_stats_kernel<0, 2, BnFwdOut>), dim3(S, (C + CG - 1) / CG), dim3(256), 0, st,
                      part, T, C, bm, M, CG, slabs, cnt, *o);
   return (int)hipGetLastError();
@@ -1166,8 +1165,7 @@ int pda_bn_bwd_stats(const float* part, int T, int nq, int C, int S, double* sla
                      const BnBwdOut* o, int cg, hipStream_t st) {
   if ((C & 3) || S <= 0 || S > T || !o || !cnt || !slabs || !o->k || (nq != 2 && nq != 3))
     return -2;
-  const int CG = stats_cg(C, cg);
-  if (C % CG) return -2;
+  const int CG = stats_cg(C, cg);   // (a ragged last group: its lanes past C stay idle)
   const dim3 grid(S, (C + CG - 1) / CG);
   if (nq == 2)
     hipLaunchKernelGGL((bn_stats_kernel<1, 2, BnBwdOut>), grid, dim3(256), 0, st, part, T, C, 0, 0, CG,

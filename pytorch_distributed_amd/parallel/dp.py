@@ -386,7 +386,11 @@ class DataParallel(nn.Module):
         rg0 = jobs[0][0]
         nseg = len(rg0.graphs)
         ends = rg0.seg_reduce
-        threaded = len(jobs) > 1 and os.environ.get("PDA_DP_THREADS", "1") != "0"
+        # (replicas that share a device replay from this thread: concurrent hipGraphLaunch calls
+        # onto ONE device from two host threads crashed inside the HIP runtime in a long GPU test
+        # session -- a segfault in CUDAGraph.replay; distinct devices keep one thread each)
+        threaded = (len(jobs) > 1 and os.environ.get("PDA_DP_THREADS", "1") != "0"
+                    and len(set(self.device_ids)) == len(self.device_ids))
         timing = self.timing
         lo = 0
         for s in range(nseg):
