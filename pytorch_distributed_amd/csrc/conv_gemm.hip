@@ -1458,138 +1458,99 @@ __global__ __launch_bounds__(256) void wgrad_reduce4_kernel(const float* __restr
 // weights [Cout][Cin] (1x1, OHWI); k: [k1; k2; k3] (3 x Cout f32, the BN-backward apply
 // coefficients of the BN after the conv). Writes Wf = [k1 o W ; G] ([Cout + Cin][Cin] 16-bit),
 // G = W^T diag(k2) W, and b = W^T k3 (f32 [Cin]).
-// Block (ti, tj) computes the 64x64 tile G[ti*64.., tj*64..] over K = Cout on MFMA 16x16x32 with
-// FOLD_G = 4 groups of 4 waves: group q takes the k-tiles kt = q, q+4, ... (a quarter of the
-// dependent load -> MFMA chain; the next k-tile is loaded into registers while the current one is
-// multiplied), each group's 64x64 f32 partial goes to LDS and group 0 sums them in group order.
-// The k-tiles of W's column panels ti (A) and tj (B, scaled by k2 per row while staging) use the
-// conv kernel's COL layout and transposed fragment reads. Blocks with ti == 0 also write the
-// k1-scaled rows of their column panel and its bias (per-thread f32 partials over fixed row sets,
-// combined in a fixed order): deterministic.
-constexpr int FOLD_G = 4;
+// Three block roles in one grid:
+//   G    : one 16x16 tile of G per block; its 4 waves take every 4th 32-deep k-step of K = Cout and
+//          load their MFMA 16x16x32 fragments straight from W (lane: column l&15 of the panel, rows
+//          8(l>>4)..+7 of the k-step -- W is a few hundred KiB, L2-resident), the B operand scaled
+//          by k2 and rounded to 16 bits once; the 4 partials are summed in wave order through LDS;
+//   bias : one wave per column i, lanes strided over K, a fixed xor-butterfly combine;
+//   rows : k1 o W, one 16-B chunk per thread.
+// No LDS tile images (4 KiB of LDS): the launch runs on the main stream beside the weight-gradient
+// LDS-DMA tiles (144 KiB of a CU's 160 KiB). The tiled 96 KiB form took 11-17 us per launch with a
+// 188 us outlier when it had to wait for a CU without one. Deterministic.
 template <int DT>
-__global__ __launch_bounds__(256 * FOLD_G) void bn_fold_kernel(const u16* __restrict__ W,
-                                                               const float* __restrict__ k, int Cout,
-                                                               int Cin, u16* __restrict__ Wf,
-                                                               float* __restrict__ bias) {
-  // per group: A and B COL tiles (8 KB each); reused afterwards for the f32 partials (16 KB each)
-  __shared__ __attribute__((aligned(16))) char smem[FOLD_G * 2 * 64 * 64 * 2];
-  __shared__ float bred[FOLD_G * 32][64];
-  const int nT = Cin >> 6;
-  const int ti = blockIdx.x / nT, tj = blockIdx.x - ti * nT;
-  const int tid = threadIdx.x & 255, grp = threadIdx.x >> 8;
-  const int lane = tid & 63, wid = tid >> 6;
-  const int wr = wid >> 1, wc = wid & 1;
+__global__ __launch_bounds__(256) void bn_fold_kernel(const u16* __restrict__ W,
+                                                      const float* __restrict__ k, int Cout, int Cin,
+                                                      u16* __restrict__ Wf, float* __restrict__ bias,
+                                                      int nG, int nB) {
+  __shared__ __attribute__((aligned(16))) f32x4 red[4][64];
   const float* k1 = k;
   const float* k2 = k + Cout;
   const float* k3 = k + 2 * Cout;
-  const bool side = ti == 0;   // this block also writes the k1 rows and the bias of panel tj
-  char* sa = smem + grp * (2 * 64 * 64 * 2);
-  char* sb = sa + 64 * 64 * 2;
-  f32x4 acc[2][2];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  int b = blockIdx.x;
+  if (b < nG) {   // ---- G tile (ti, tj)
+    const int n16 = Cin >> 4;
+    const int ti = b / n16, tj = b - ti * n16;
+    const int r = lane & 15, g = lane >> 4;
+    const u16* pa = W + ti * 16 + r;
+    const u16* pb = W + tj * 16 + r;
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    const int nks = Cout >> 5;
+#pragma unroll 2
+    for (int s = wid; s < nks; s += 4) {
+      const int k0 = s * 32 + 8 * g;
+      const f32x4 q0 = *reinterpret_cast<const f32x4*>(k2 + k0);
+      const f32x4 q1 = *reinterpret_cast<const f32x4*>(k2 + k0 + 4);
+      uint32_t ua[8], ub[8];
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
-#pragma unroll
-    for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  float bs[8];
-#pragma unroll
-  for (int e = 0; e < 8; ++e) bs[e] = 0.f;
-  const int cc = tid & 7;   // the thread's 16-B chunk (8 columns) of a 64-column panel row
-  const int nk = Cout >> 6;
-  i32x4 va[2], vb[2];
-  auto load = [&](int kt) __attribute__((always_inline)) {
-#pragma unroll
-    for (int r = 0; r < 2; ++r) {
-      const int kk = kt * 64 + (tid >> 3) + 32 * r;
-      va[r] = *reinterpret_cast<const i32x4*>(W + (size_t)kk * Cin + ti * 64 + cc * 8);
-      vb[r] = *reinterpret_cast<const i32x4*>(W + (size_t)kk * Cin + tj * 64 + cc * 8);
-    }
-  };
-  if (grp < nk) load(grp);
-  // block-uniform trip count (barriers inside); a group past the end stages zeros
-  for (int kb = 0; kb < nk; kb += FOLD_G) {
-    const int kt = kb + grp;
-    const bool live = kt < nk;
-    if (!live) {
-#pragma unroll
-      for (int r = 0; r < 2; ++r) va[r] = vb[r] = i32x4{0, 0, 0, 0};
-    }
-#pragma unroll
-    for (int r = 0; r < 2; ++r) {
-      const int krow = (tid >> 3) + 32 * r;
-      const int kk = live ? kt * 64 + krow : 0;
-      const float s2 = k2[kk];
-      i32x4 wb;
+      for (int e = 0; e < 8; ++e) {
+        ua[e] = pa[(size_t)(k0 + e) * Cin];
+        ub[e] = pb[(size_t)(k0 + e) * Cin];
+      }
+      s16x8 fa, fb;
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
-        const f32x2 f = unpack2<DT>((uint32_t)vb[r][q]);
-        wb[q] = (int)pack2<DT>(f32x2{f.x * s2, f.y * s2});
+        const uint32_t pa2 = ua[2 * q] | (ua[2 * q + 1] << 16);
+        const f32x2 f = unpack2<DT>(ub[2 * q] | (ub[2 * q + 1] << 16));
+        const float s0 = q < 2 ? q0[2 * q] : q1[2 * q - 4];
+        const float s1 = q < 2 ? q0[2 * q + 1] : q1[2 * q - 3];
+        const uint32_t pb2 = pack2<DT>(f32x2{f.x * s0, f.y * s1});
+        fa[2 * q] = (short)(pa2 & 0xffff); fa[2 * q + 1] = (short)(pa2 >> 16);
+        fb[2 * q] = (short)(pb2 & 0xffff); fb[2 * q + 1] = (short)(pb2 >> 16);
       }
-      *reinterpret_cast<i32x4*>(sa + col_addr<64>(krow, cc)) = va[r];
-      *reinterpret_cast<i32x4*>(sb + col_addr<64>(krow, cc)) = wb;
-      if (side && live) {   // k1 o W rows and the bias partials of panel tj
-        const float s1 = k1[kk], s3 = k3[kk];
-        i32x4 w1;
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const f32x2 f = unpack2<DT>((uint32_t)vb[r][q]);
-          w1[q] = (int)pack2<DT>(f32x2{f.x * s1, f.y * s1});
-          bs[2 * q] = __builtin_fmaf(s3, f.x, bs[2 * q]);
-          bs[2 * q + 1] = __builtin_fmaf(s3, f.y, bs[2 * q + 1]);
-        }
-        *reinterpret_cast<i32x4*>(Wf + (size_t)kk * Cin + tj * 64 + cc * 8) = w1;
-      }
+      acc = mfma16<DT>(fb, fa, acc);
     }
+    // acc[e] = partial G[ti*16 + r][tj*16 + 4g + e]; waves 1-3 hand theirs to wave 0
+    red[wid][lane] = acc;
     __syncthreads();
-    if (kt + FOLD_G < nk) load(kt + FOLD_G);   // in flight during this k-tile's MFMAs
-#pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      s16x8 fa[2], fb[2];
-#pragma unroll
-      for (int i = 0; i < 2; ++i) fa[i] = frag_col<64>(sa, wr * 32 + i * 16, s, lane);
-#pragma unroll
-      for (int j = 0; j < 2; ++j) fb[j] = frag_col<64>(sb, wc * 32 + j * 16, s, lane);
-#pragma unroll
-      for (int i = 0; i < 2; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j) acc[i][j] = mfma16<DT>(fb[j], fa[i], acc[i][j]);
-    }
-    __syncthreads();
-  }
-  // group partials -> LDS (f32 [64][64] per group), fixed-order sum by group 0
-  __syncthreads();
-  float* part = reinterpret_cast<float*>(smem) + grp * 64 * 64;
-#pragma unroll
-  for (int i = 0; i < 2; ++i)
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const int row = wr * 32 + i * 16 + (lane & 15);
-      const int col = wc * 32 + j * 16 + 4 * (lane >> 4);
-      *reinterpret_cast<f32x4*>(part + row * 64 + col) = acc[i][j];
-    }
-#pragma unroll
-  for (int e = 0; e < 8; ++e) bred[grp * 32 + (tid >> 3)][cc * 8 + e] = bs[e];
-  __syncthreads();
-  if (grp == 0) {
-    const float* p0 = reinterpret_cast<const float*>(smem);
-    // thread t: row t / 4, 16 columns (t % 4) * 16 ..
-    const int row = tid >> 2, c0 = (tid & 3) * 16;
-#pragma unroll
-    for (int c = 0; c < 16; c += 4) {
-      f32x4 v = *reinterpret_cast<const f32x4*>(p0 + row * 64 + c0 + c);
-#pragma unroll
-      for (int g = 1; g < FOLD_G; ++g) v += *reinterpret_cast<const f32x4*>(p0 + g * 4096 + row * 64 + c0 + c);
+    if (wid == 0) {
+      const f32x4 v = ((red[0][lane] + red[1][lane]) + red[2][lane]) + red[3][lane];
       uint2 pk;
       pk.x = pack2<DT>(f32x2{v[0], v[1]});
       pk.y = pack2<DT>(f32x2{v[2], v[3]});
-      *reinterpret_cast<uint2*>(Wf + (size_t)(Cout + ti * 64 + row) * Cin + tj * 64 + c0 + c) = pk;
+      *reinterpret_cast<uint2*>(Wf + (size_t)(Cout + ti * 16 + r) * Cin + tj * 16 + 4 * g) = pk;
     }
-    if (side && tid < 64) {
-      float b = 0.f;
-      for (int g = 0; g < FOLD_G * 32; ++g) b += bred[g][tid];
-      bias[tj * 64 + tid] = b;
-    }
+    return;
   }
+  b -= nG;
+  if (b < nB) {   // ---- bias b[i] = sum_k k3[k] W[k][i], one wave per i
+    const int i = b * 4 + wid;
+    if (i >= Cin) return;
+    float acc = 0.f;
+    for (int kk = lane; kk < Cout; kk += 64) {
+      const uint32_t u = W[(size_t)kk * Cin + i];
+      acc = __builtin_fmaf(k3[kk], unpack2<DT>(u).x, acc);
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) acc += __shfl_xor(acc, off);
+    if (lane == 0) bias[i] = acc;
+    return;
+  }
+  b -= nB;   // ---- rows [0, Cout): k1 o W, one 16-B chunk per thread
+  const int c = b * 256 + tid;
+  const int cpr = Cin >> 3;
+  if (c >= Cout * cpr) return;
+  const int row = c / cpr;
+  const float s1 = k1[row];
+  const i32x4 v = *reinterpret_cast<const i32x4*>(W + (size_t)c * 8);
+  i32x4 o;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const f32x2 f = unpack2<DT>((uint32_t)v[q]);
+    o[q] = (int)pack2<DT>(f32x2{f.x * s1, f.y * s1});
+  }
+  *reinterpret_cast<i32x4*>(Wf + (size_t)c * 8) = o;
 }
 
 // Operands of the concatenated BatchNorm-backward fold (pda_conv_dgrad_bnf with xa_c = Cout):
@@ -1893,13 +1854,14 @@ int pda_bn_fold_cat(const void* w, const float* k, int Cout, int Cin, void* wf, 
 int pda_bn_fold(const void* w, const float* k, int Cout, int Cin, void* wf, float* bias, int dt,
                 hipStream_t st) {
   if ((Cout % 64) || (Cin % 64) || Cin > 4096) return -2;
-  const dim3 grid((Cin / 64) * (Cin / 64));
+  const int nG = (Cin / 16) * (Cin / 16), nB = Cin / 4, nR = (Cout * (Cin / 8) + 255) / 256;
+  const dim3 grid(nG + nB + nR);
   if (dt == DT_BF16)
-    hipLaunchKernelGGL(bn_fold_kernel<DT_BF16>, grid, dim3(256 * FOLD_G), 0, st, (const u16*)w, k,
-                       Cout, Cin, (u16*)wf, bias);
+    hipLaunchKernelGGL(bn_fold_kernel<DT_BF16>, grid, dim3(256), 0, st, (const u16*)w, k, Cout, Cin,
+                       (u16*)wf, bias, nG, nB);
   else if (dt == DT_F16)
-    hipLaunchKernelGGL(bn_fold_kernel<DT_F16>, grid, dim3(256 * FOLD_G), 0, st, (const u16*)w, k,
-                       Cout, Cin, (u16*)wf, bias);
+    hipLaunchKernelGGL(bn_fold_kernel<DT_F16>, grid, dim3(256), 0, st, (const u16*)w, k, Cout, Cin,
+                       (u16*)wf, bias, nG, nB);
   else
     return -1;
   return (int)hipGetLastError();

@@ -910,7 +910,7 @@ class NativeResNet(nn.Module):
                     cin = b.ds.conv.in_channels
                     wfd = self._empty(b.ds.cout + cin, cin)
                     fbd = torch.empty(cin, dtype=torch.float32, device=self.device)
-                    K.bn_fold(self.w16(b.ds), kd, wfd, fbd)
+                    K.bn_fold(self.w16(b.ds), kd, wfd, fbd, self.ws_w)
                     K.conv_dgrad_bnf(dz, wfd, g, shortcut_g, x, fbd)
                     return [wfd, fbd]
                 K.conv_dgrad(dyd, self.w16_ohwi(b.ds), g, shortcut_g)
@@ -970,7 +970,7 @@ class NativeResNet(nn.Module):
                 cin = u.conv.in_channels
                 wf = self._empty(u.cout + cin, cin)
                 fb = torch.empty(cin, dtype=torch.float32, device=self.device)
-                K.bn_fold(self.w16(u), k3, wf, fb)
+                K.bn_fold(self.w16(u), k3, wf, fb, ws)
                 bnf = (wf, fb)
                 self._wgrad(lambda w, u=u, g=g, a=a_in, pro=pro, y3=ys[-1], k3=k3:
                             K.conv_wgrad(dz, a, g, self.wgrad_view(u), w, accumulate=acc, pro=pro,

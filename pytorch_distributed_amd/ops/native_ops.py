@@ -84,15 +84,16 @@ class Workspace:
             self._bufs[name] = b
         return b[:numel]
 
-    def counters(self, numel: int) -> torch.Tensor:
-        """int32 arrival counters of the one-launch statistics kernels: zero when allocated, and
-        every kernel that uses them leaves them zero again (its last arrivers reset them)."""
-        b = self._bufs.get("_counters")
+    def counters(self, numel: int, name: str = "_counters") -> torch.Tensor:
+        """int32 arrival counters of the one-launch reduction kernels: zero when allocated, and
+        every kernel that uses them leaves them zero again (its last arrivers reset them). One
+        ``name`` per kernel family that may run concurrently with another on the stream."""
+        b = self._bufs.get(name)
         if b is None or b.numel() < numel:
             if b is not None:
                 self._retired.append(b)
             b = torch.zeros(max(numel, 64), dtype=torch.int32, device=self.device)
-            self._bufs["_counters"] = b
+            self._bufs[name] = b
         return b[:numel]
 
 
@@ -333,10 +334,12 @@ def conv_dgrad(dy: torch.Tensor, w: torch.Tensor, g: ConvGeom, dx: torch.Tensor,
     return dx
 
 
-def bn_fold(w: torch.Tensor, k: torch.Tensor, wf: torch.Tensor, bias: torch.Tensor) -> None:
+def bn_fold(w: torch.Tensor, k: torch.Tensor, wf: torch.Tensor, bias: torch.Tensor,
+            ws: Optional["Workspace"] = None) -> None:
     """Operands of :func:`conv_dgrad_bnf` for a 1x1 conv (``w`` 16-bit [Cout, Cin], ``k`` =
     [k1; k2; k3] 3 x Cout f32 of the BatchNorm after it): ``wf`` [Cout + Cin, Cin] = [k1 o W ;
-    W^T diag(k2) W], ``bias`` [Cin] = W^T k3 (csrc/conv_gemm.hip bn_fold_kernel, one launch)."""
+    W^T diag(k2) W], ``bias`` [Cin] = W^T k3 (csrc/conv_gemm.hip bn_fold_kernel, one launch;
+    ``ws`` is accepted for call-site symmetry and unused)."""
     Cout, Cin = w.shape[0], w.shape[-1]
     if wf.shape[0] != Cout + Cin or wf.shape[-1] != Cin or wf.dtype != w.dtype or k.numel() < 3 * Cout:
         raise ValueError("bn_fold: wf [Cout + Cin, Cin] of the weights' dtype, k 3 x Cout")

@@ -455,7 +455,7 @@ class _ReplicaGraph:
     ``splits`` (flat-gradient offsets, ``NativeResNet.stage_bounds``): where DataParallel
     all-reduces a completed gradient slice between segment replays.
 
-    ``side_split`` (``PDA_DP_SIDE=1``): the weight-gradient kernels are recorded in graphs
+    ``side_split`` (``PDA_DP_SIDE=1``, default): the weight-gradient kernels are recorded in graphs
     of their own. The HIP runtime replays one captured graph's fork/join DAG almost serially
     (``profiles/rocprof_r3_graph_replay.md``: 368 of ~410 kernels on one queue), which loses the
     two-stream overlap of the eager step; so the capture ends a main-chain graph after every
@@ -470,7 +470,7 @@ class _ReplicaGraph:
         self.gscale = 1.0 / global_batch
         self.splits = list(splits)
         self.side_split = (getattr(m, "_side", None) is not None
-                           and os.environ.get("PDA_DP_SIDE", "0") != "0")
+                           and os.environ.get("PDA_DP_SIDE", "1") != "0")
         with torch.cuda.device(self.dev):
             self.x = torch.empty(shape, dtype=m.dtype, device=self.dev)
             self.y = torch.empty(shape[0], dtype=torch.int64, device=self.dev)
