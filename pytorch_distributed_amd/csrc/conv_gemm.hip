@@ -257,7 +257,16 @@ __global__ __launch_bounds__(conv_nt<STAGES>(), (PASS_T == WGRAD_BNA ? (BN >= 25
   constexpr int SLAB_ROWS = BM + 128, SLAB_BYTES = SLAB_ROWS * 128;
   constexpr int ZOFF = 2 * SLAB_BYTES + 3 * B_BYTES;
   // LDS-DMA ring slots: 4 when they fit in 144 KiB (three tiles in flight), else 3
-  constexpr int NSLOT = DMA && !HALO ? (4 * STAGE <= 144 * 1024 ? 4 : 3) : STAGES;
+  // (CONV_WGRAD_DMA_SLOTS, a build-time A/B knob: ring depth of the weight-gradient DMA tiles,
+  // whose LDS footprint decides whether a main-stream block fits beside one on its CU)
+#ifndef CONV_WGRAD_DMA_SLOTS
+#define CONV_WGRAD_DMA_SLOTS 0
+#endif
+  constexpr int NSLOT = DMA && !HALO
+      ? (PASS == WGRAD && CONV_WGRAD_DMA_SLOTS > 0 ? CONV_WGRAD_DMA_SLOTS
+                                                   : (4 * STAGE <= 144 * 1024 ? 4 : 3))
+      : STAGES;
+  static_assert(!DMA || HALO || NSLOT >= 2, "DMA ring");
   constexpr int RING = HALO ? ZOFF + 128 : NSLOT * STAGE;
   constexpr int LDS_0 = RING > RED_BYTES ? RING : RED_BYTES;
   constexpr int LDS_BYTES = LDS_0 > C_BYTES ? LDS_0 : C_BYTES;
@@ -1027,8 +1036,10 @@ __global__ __launch_bounds__(conv_nt<STAGES>(), (PASS_T == WGRAD_BNA ? (BN >= 25
       // tile kt must have landed: the younger tiles kt+1 .. kt+NSLOT-2 may stay in flight
       if constexpr (NSLOT == 4) {
         if (kt + 2 < nk) vm_wait<2 * GP>(); else if (kt + 1 < nk) vm_wait<GP>(); else vm_wait<0>();
-      } else {
+      } else if constexpr (NSLOT == 3) {
         if (kt + 1 < nk) vm_wait<GP>(); else vm_wait<0>();
+      } else {   // two slots: only tile kt is in flight here
+        vm_wait<0>();
       }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();

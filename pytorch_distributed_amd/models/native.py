@@ -138,6 +138,8 @@ class NativeResNet(nn.Module):
         self.fused_stem_bwd = True    # maxpool gather + ReLU mask + BN partials in one pass
         # stem wgrad forms its dY from the BN backward in-kernel (PDA_STEM_BNA=0: apply pass)
         self.stem_bna = os.environ.get("PDA_STEM_BNA", "1") != "0"
+        # the stem's weight gradient on the main stream (beside layer1's on the second stream)
+        self.stem_wgrad_main = os.environ.get("PDA_STEM_WGRAD_MAIN", "1") != "0"
         self.tail_mask = True         # tails store the ReLU bitmask the backward reads
         # consumer-side tail fold of the Bottleneck BN backward (see _block_backward)
         # ("0" off, "1" every stage, or the stages to fold, e.g. "12" = layer1 and layer2). Default
@@ -787,7 +789,12 @@ class NativeResNet(nn.Module):
             def stem_wgrad(w):
                 K.conv_wgrad(dz0, x0, g0, self.stem_wgrad, w, bna=(y0, k0), wscale=self.wgrad_scale)
                 K.stem_s2d_grad(self.stem_wgrad, self.wgrad_view(u), accumulate=acc)
-            self._wgrad(stem_wgrad, dz0, y0, x0, k0)
+            if self.stem_wgrad_main and self._side is not None and not self.defer_side:
+                # the main stream is idle after the stem's BN backward while the second stream still
+                # drains layer1's weight gradients: the stem's runs beside them instead of after
+                stem_wgrad(ws)
+            else:
+                self._wgrad(stem_wgrad, dz0, y0, x0, k0)
         else:
             def stem_wgrad(w):
                 K.conv_wgrad(dy0, x0, g0, self.stem_wgrad, w, wscale=self.wgrad_scale)
