@@ -54,7 +54,14 @@ template <int N> __device__ __forceinline__ void vm_wait() {
 // the K loop runs over dz's Cout channels against rows [0, Cout) of B = [k1 o W ; G] and then over
 // xa_c channels of the Gram operand xa (a2, formed by the BN+ReLU prologue of the forward when
 // xa_sc is set) read at the dX pixel against rows [Cout, Cout + xa_c); the epilogue adds b.
-enum Pass : int { FWD = 0, DGRAD = 1, WGRAD = 2, WGRAD_BNA = 3, DGRAD_BNF = 4 };
+//
+// WGRAD_GRAM: WGRAD of a tensor against itself through its BN+ReLU, Gram = a^T a with
+// a = relu(sc*y + sh) formed while staging BOTH operands (A: ak1 = sc, ak3 = sh; B: the usual
+// prologue), plus the column sums s = sum_p a_p (blocks of the first N-tile accumulate their A
+// chunks; per-split partials behind the slab). With them the tail fold's conv3 weight gradient
+// needs no y3 read (decomposed form, see pda_wgrad_reduce):
+//   dW3 = diag(k1) (dz^T a2) + diag(k2) W3 Gram(a2) + k3 s^T,   y3 = a2 W3^T.
+enum Pass : int { FWD = 0, DGRAD = 1, WGRAD = 2, WGRAD_BNA = 3, DGRAD_BNF = 4, WGRAD_GRAM = 5 };
 
 template <int V> struct IC { static constexpr int value = V; };
 
@@ -197,9 +204,11 @@ template <int PASS_T, int DT, int BM, int BN, int STAGES>
 // (the 16-bit WGRAD budget of 4 spilled 15 VGPRs); its 256-column tile (the stem's whole N: dz and
 // y staged and transformed once instead of once per 128-column tile) needs 246: 2 blocks per CU
 // (the 128x128 WGRAD_BNA tile of the bottleneck conv3 fold: 2 blocks, 3 spilled 89 VGPRs)
-__global__ __launch_bounds__(conv_nt<STAGES>(), (PASS_T == WGRAD_BNA ? (BN >= 256 || BM * BN >= 128 * 128 ? 2 : 3) : conv_min_blocks<DT, BM, BN, STAGES>())) void conv_gemm_kernel(ConvParams p_arg) {
-  constexpr int PASS = PASS_T == WGRAD_BNA ? WGRAD : PASS_T == DGRAD_BNF ? DGRAD : PASS_T;
-  constexpr bool ABN = PASS_T == WGRAD_BNA;
+__global__ __launch_bounds__(conv_nt<STAGES>(), (PASS_T == WGRAD_BNA || PASS_T == WGRAD_GRAM ? (BN >= 256 || BM * BN >= 128 * 128 ? 2 : 3) : conv_min_blocks<DT, BM, BN, STAGES>())) void conv_gemm_kernel(ConvParams p_arg) {
+  constexpr int PASS = PASS_T == WGRAD_BNA || PASS_T == WGRAD_GRAM ? WGRAD
+                       : PASS_T == DGRAD_BNF ? DGRAD : PASS_T;
+  constexpr bool GRAM = PASS_T == WGRAD_GRAM;   // A = relu(ak1*a + ak3); no second tensor
+  constexpr bool ABN = PASS_T == WGRAD_BNA || GRAM;
   constexpr bool BNF = PASS_T == DGRAD_BNF;
   constexpr bool DMA = STAGES >= 3;
   // STAGES == 4 (HALO): tap reuse for 3x3 stride-1 FWD / DGRAD -- see the HALO main loop
@@ -368,10 +377,15 @@ __global__ __launch_bounds__(conv_nt<STAGES>(), (PASS_T == WGRAD_BNA ? (BN >= 25
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
       bk1[k] = *reinterpret_cast<const f32x2*>(p.ak1 + cs + 2 * k);
-      bk2[k] = *reinterpret_cast<const f32x2*>(p.ak2 + cs + 2 * k);
+      if constexpr (!GRAM) bk2[k] = *reinterpret_cast<const f32x2*>(p.ak2 + cs + 2 * k);
       bk3[k] = *reinterpret_cast<const f32x2*>(p.ak3 + cs + 2 * k);
     }
   }
+  // WGRAD_GRAM: column sums of the thread's A chunk (the 8 channels of its column), first N-tile
+  f32x2 gsum[GRAM ? 4 : 1];
+#pragma unroll
+  for (int k = 0; k < (GRAM ? 4 : 1); ++k) gsum[k] = f32x2{0.f, 0.f};
+  const bool gcol = GRAM && tn == 0;
   // B
   uint32_t b_off[BR];
   if constexpr (PASS == FWD) {
@@ -569,7 +583,7 @@ __global__ __launch_bounds__(conv_nt<STAGES>(), (PASS_T == WGRAD_BNA ? (BN >= 25
         const bool ok = k0 + a_krow[i] < kend;
         lda(i, ok ? a_off[i] + koff : OOB);
         if constexpr (ABN) {
-          ray[i] = bld(rsa2, ok ? a_off[i] + koff : OOB);
+          if constexpr (!GRAM) ray[i] = bld(rsa2, ok ? a_off[i] + koff : OOB);
           av[i] = ok && a_off[i] != OOB;
         }
       }
@@ -637,7 +651,17 @@ __global__ __launch_bounds__(conv_nt<STAGES>(), (PASS_T == WGRAD_BNA ? (BN >= 25
       constexpr int CPR = BM / EPC, RPI = NT / CPR;
 #pragma unroll
       for (int i = 0; i < AR; ++i) {
-        if constexpr (ABN) {   // dY = k1*dz + k2*y + k3 on the valid chunks (padding stays 0)
+        if constexpr (GRAM) {   // a = relu(sc*y + sh) on the valid chunks (padding stays 0)
+          if (av[i]) {
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+              const f32x2 u = unpack2<DT>((uint32_t)ra[i][k]);
+              const s16x2 h = __builtin_bit_cast(s16x2, pack2<DT>(fma2(u, bk1[k], bk3[k])));
+              ra[i][k] = __builtin_bit_cast(int, __builtin_elementwise_max(h, (s16x2){0, 0}));
+              if (gcol) gsum[k] += unpack2<DT>((uint32_t)ra[i][k]);   // the rounded operand
+            }
+          }
+        } else if constexpr (ABN) {   // dY = k1*dz + k2*y + k3 on the valid chunks (padding stays 0)
           if (av[i]) {
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
@@ -1139,6 +1163,22 @@ __global__ __launch_bounds__(conv_nt<STAGES>(), (PASS_T == WGRAD_BNA ? (BN >= 25
           if (col + e < p.N) d[e] = v[e];
       }
     });
+    if constexpr (GRAM) {   // column-sum partials of this split: [splits][M] behind the slabs
+      if (gcol) {
+        constexpr int CPR = BM / EPC, RPI = NT / CPR;
+        float* red = reinterpret_cast<float*>(smem);   // [RPI][BM] (the main loop is done with LDS)
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+          *reinterpret_cast<f32x2*>(red + (tid / CPR) * BM + (tid % CPR) * EPC + 2 * k) = gsum[k];
+        __syncthreads();
+        if (tid < BM && m0 + tid < p.M) {
+          float a = 0.f;
+          for (int g = 0; g < RPI; ++g) a += red[g * BM + tid];
+          reinterpret_cast<float*>(p.out)[(size_t)gridDim.y * p.M * p.N + (size_t)split * p.M + m0 + tid] = a;
+        }
+      }
+    }
     return;
   } else {
     if (p.out_f32) {  // fc logits: f32 + bias, direct stores
@@ -1410,14 +1450,25 @@ __global__ __launch_bounds__(conv_nt<STAGES>(), (PASS_T == WGRAD_BNA ? (BN >= 25
 // split-K slab reduction for WGRAD, with layout remap + scale, into the f32 gradient buffer:
 // grad[n1 * dst_pitch + (n2 / cin_pad) * cin_real + n2 % cin_pad] = scale * sum_s slab[s][n1][n2]
 // for n2 % cin_pad < cin_real (stem: Cin padded 3 -> 8).
+// Optional combine (ck != null, the decomposed tail-fold weight gradient): the summed value s of
+// (row n1, column n2) becomes ck[n1] * s + ck[M + n1] * cB[n1 * N + n2] + ck[2M + n1] * cs[n2].
+__device__ __forceinline__ float wg_combine(float s, const float* ck, const float* cB, const float* cs,
+                                            int M, int N, int n1, int n2) {
+  if (!ck) return s;
+  return ck[n1] * s + ck[M + n1] * cB[(size_t)n1 * N + n2] + ck[2 * M + n1] * cs[n2];
+}
+
 __global__ void wgrad_reduce_kernel(const float* __restrict__ slab, float* __restrict__ grad,
                                     int splits, int M, int N, int cin_pad_log2, int cin_real,
-                                    int dst_pitch, float scale, int accumulate) {
+                                    int dst_pitch, float scale, int accumulate,
+                                    const float* __restrict__ ck, const float* __restrict__ cB,
+                                    const float* __restrict__ cs) {
   const int total = M * N;
   for (int idx = blockIdx.x * blockDim.x + threadIdx.x; idx < total; idx += gridDim.x * blockDim.x) {
     float s = 0.f;
     for (int k = 0; k < splits; ++k) s += slab[(size_t)k * total + idx];
     const int n1 = idx / N, n2 = idx - n1 * N;
+    s = wg_combine(s, ck, cB, cs, M, N, n1, n2);
     const int tap = n2 >> cin_pad_log2, c = n2 & ((1 << cin_pad_log2) - 1);
     if (c < cin_real) {
       float* d = grad + (size_t)n1 * dst_pitch + tap * cin_real + c;
@@ -1435,7 +1486,9 @@ __global__ __launch_bounds__(256) void wgrad_reduce4_kernel(const float* __restr
                                                             float* __restrict__ grad, int splits,
                                                             int M, int N, int cin_pad_log2,
                                                             int cin_real, int dst_pitch, float scale,
-                                                            int accumulate) {
+                                                            int accumulate, const float* __restrict__ ck,
+                                                            const float* __restrict__ cB,
+                                                            const float* __restrict__ cs) {
   constexpr int TPE = EPB / 4, SG = 256 / TPE;
   __shared__ f32x4 red[256];
   const int total = M * N;
@@ -1458,8 +1511,9 @@ __global__ __launch_bounds__(256) void wgrad_reduce4_kernel(const float* __restr
     const int n1 = idx / N, n2 = idx - n1 * N;
     const int tap = n2 >> cin_pad_log2, c = n2 & ((1 << cin_pad_log2) - 1);
     if (c < cin_real) {
+      const float v = wg_combine(s[q], ck, cB, cs, M, N, n1, n2);
       float* d = grad + (size_t)n1 * dst_pitch + tap * cin_real + c;
-      *d = accumulate ? *d + scale * s[q] : scale * s[q];
+      *d = accumulate ? *d + scale * v : scale * v;
     }
   }
 }
@@ -1564,6 +1618,26 @@ __global__ __launch_bounds__(256) void bn_fold_kernel(const u16* __restrict__ W,
   *reinterpret_cast<i32x4*>(Wf + (size_t)c * 8) = o;
 }
 
+// B = W Gram (f32 [Cout][C]) for the decomposed tail-fold weight gradient: W 16-bit [Cout][C] (the
+// weights the forward used), Gram f32 [C][C]. Thread: one row, 4 consecutive columns, j in order.
+template <int DT>
+__global__ __launch_bounds__(256) void fold_bgemm_kernel(const u16* __restrict__ W,
+                                                         const float* __restrict__ gram, int Cout,
+                                                         int C, float* __restrict__ B) {
+  const int t = blockIdx.x * 256 + threadIdx.x;
+  const int c4 = C >> 2;
+  if (t >= Cout * c4) return;
+  const int row = t / c4, n = (t - row * c4) * 4;
+  const u16* w = W + (size_t)row * C;
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  for (int j = 0; j < C; j += 2) {
+    const f32x2 wv = unpack2<DT>(*reinterpret_cast<const uint32_t*>(w + j));
+    acc += wv.x * *reinterpret_cast<const f32x4*>(gram + (size_t)j * C + n);
+    acc += wv.y * *reinterpret_cast<const f32x4*>(gram + (size_t)(j + 1) * C + n);
+  }
+  *reinterpret_cast<f32x4*>(B + (size_t)row * C + n) = acc;
+}
+
 // Operands of the concatenated BatchNorm-backward fold (pda_conv_dgrad_bnf with xa_c = Cout):
 // wf = [k1 o W ; k2 o W] ([2 Cout][Cin] 16-bit) and b = W^T k3 (f32 [Cin]). Block = one 64-column
 // panel of W, 256 threads = 8 column chunks x 32 row sets; bias partials per thread over fixed row
@@ -1623,7 +1697,8 @@ struct ConvDesc {  // mirrors pytorch_distributed_amd/ops/ext.py ConvDesc
 
 template <int PASS, int DT, int BM, int BN, int ST>
 static int launch(const ConvParams& p, dim3 grid, hipStream_t st) {
-  if constexpr ((PASS == WGRAD_BNA || PASS == DGRAD_BNF) && DT != DT_BF16 && DT != DT_F16) {
+  if constexpr ((PASS == WGRAD_BNA || PASS == DGRAD_BNF || PASS == WGRAD_GRAM) && DT != DT_BF16 &&
+                DT != DT_F16) {
     return -1;
   } else {
     hipLaunchKernelGGL((conv_gemm_kernel<PASS, DT, BM, BN, ST>), grid, dim3(conv_nt<ST>()), 0, st, p);
@@ -1911,6 +1986,49 @@ int pda_conv_wgrad_bna(const ConvDesc* d, const void* dz, const void* y, const f
   return -1;
 }
 
+// Gram = a^T a and s = sum_p a_p of a = relu(sc*y + sh) (y [Nb,H,W,C] 16-bit; WGRAD_GRAM): slab
+// [splits][C][C] partial Grams, then [splits][C] partial column sums. Tiles (64, 64) two-stage,
+// (-128, 128), (-128, 64); -1 otherwise.
+int pda_conv_wgrad_gram(const ConvDesc* d, const void* y, const float* sc, const float* sh,
+                        float* slab, int splits, int k_chunk, int dt, int bm, int bn, hipStream_t st) {
+  if (dt != DT_BF16 && dt != DT_F16) return -1;
+  if (d->R != 1 || d->S != 1 || d->stride != 1 || d->pad != 0 || d->Cin != d->Cout || (d->Cin % 8))
+    return -2;
+  if (!fits32((long long)d->Nb * d->H * d->W * d->Cin, 1, (long long)splits * d->Cin * (d->Cin + 1), dt))
+    return -4;
+  ConvParams p{};
+  fill_geom(p, *d);
+  p.pro_sc = sc; p.pro_sh = sh;
+  p.a = y; p.ak1 = sc; p.ak3 = sh;
+  p.b = y; p.out = slab;
+  p.M = d->Cout; p.N = d->Cin;
+  p.K = d->Nb * d->Ho * d->Wo;
+  p.k_chunk = k_chunk;
+  const int abm = bm < 0 ? -bm : bm;
+  const dim3 grid(((p.M + abm - 1) / abm) * ((p.N + bn - 1) / bn), splits);
+#define GRAM_CASE(D, M_, N_, S_) \
+  if (dt == D && bm == (S_ == 1 ? -M_ : M_) && bn == N_) return launch<WGRAD_GRAM, D, M_, N_, S_>(p, grid, st);
+#ifndef CONV_DMA_ONLY
+  GRAM_CASE(DT_BF16, 64, 64, 2) GRAM_CASE(DT_BF16, 128, 128, 1) GRAM_CASE(DT_BF16, 128, 64, 1)
+  GRAM_CASE(DT_F16, 64, 64, 2) GRAM_CASE(DT_F16, 128, 128, 1) GRAM_CASE(DT_F16, 128, 64, 1)
+#endif
+#undef GRAM_CASE
+  return -1;
+}
+
+// B = W Gram (f32 [Cout][C]); W 16-bit [Cout][C], Gram f32 [C][C]. C a multiple of 4.
+int pda_fold_bgemm(const void* w, const float* gram, int Cout, int C, float* b, int dt, hipStream_t st) {
+  if (C % 4) return -2;
+  const dim3 grid((Cout * (C / 4) + 255) / 256);
+  if (dt == DT_BF16)
+    hipLaunchKernelGGL(fold_bgemm_kernel<DT_BF16>, grid, dim3(256), 0, st, (const u16*)w, gram, Cout, C, b);
+  else if (dt == DT_F16)
+    hipLaunchKernelGGL(fold_bgemm_kernel<DT_F16>, grid, dim3(256), 0, st, (const u16*)w, gram, Cout, C, b);
+  else
+    return -1;
+  return (int)hipGetLastError();
+}
+
 // slab[splits][Cout][R*S*Cin] partial weight gradients (f32). k_chunk must be a multiple of 64.
 int pda_conv_wgrad(const ConvDesc* d, const void* dy, const void* x, float* slab, int splits,
                    int k_chunk, const float* pro_sc, const float* pro_sh, int dt, int bm, int bn,
@@ -1931,7 +2049,8 @@ int pda_conv_wgrad(const ConvDesc* d, const void* dy, const void* x, float* slab
 }
 
 int pda_wgrad_reduce(const float* slab, float* grad, int splits, int M, int N, int cin_pad_log2,
-                     int cin_real, int dst_pitch, float scale, int accumulate, hipStream_t st) {
+                     int cin_real, int dst_pitch, float scale, int accumulate, const float* ck,
+                     const float* cB, const float* cs, hipStream_t st) {
   const int total = M * N;
   if ((N & 3) == 0) {
     int epb = 256;
@@ -1940,7 +2059,7 @@ int pda_wgrad_reduce(const float* slab, float* grad, int splits, int M, int N, i
 #define RED_CASE(E)                                                                              \
   if (epb == E) {                                                                               \
     hipLaunchKernelGGL(wgrad_reduce4_kernel<E>, grid, dim3(256), 0, st, slab, grad, splits, M, N, \
-                       cin_pad_log2, cin_real, dst_pitch, scale, accumulate);                   \
+                       cin_pad_log2, cin_real, dst_pitch, scale, accumulate, ck, cB, cs);       \
     return (int)hipGetLastError();                                                              \
   }
     RED_CASE(256) RED_CASE(128) RED_CASE(64) RED_CASE(32) RED_CASE(16)
@@ -1949,7 +2068,7 @@ int pda_wgrad_reduce(const float* slab, float* grad, int splits, int M, int N, i
   int blocks = (total + 255) / 256;
   if (blocks > 4096) blocks = 4096;
   hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(blocks), dim3(256), 0, st, slab, grad, splits, M, N,
-                     cin_pad_log2, cin_real, dst_pitch, scale, accumulate);
+                     cin_pad_log2, cin_real, dst_pitch, scale, accumulate, ck, cB, cs);
   return (int)hipGetLastError();
 }
 

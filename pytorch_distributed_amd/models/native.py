@@ -152,6 +152,10 @@ class NativeResNet(nn.Module):
         self.bn_fold = fold != "0"
         self.bn_fold_stages = None if fold in ("0", "1") else {int(c) for c in fold if c.isdigit()}
         self.bn_fold_ds = os.environ.get("PDA_BN_FOLD_DS", "0") != "0"
+        # folded tails take conv3's weight gradient in the decomposed form diag(k1) dz^T a2 +
+        # diag(k2) W3 Gram(a2) + k3 s^T: the Gram and column sums of a2 run in the forward on the
+        # second stream, so the backward's GEMM is a plain dz^T a2 (no y3 read, no VALU transform)
+        self.bn_fold_wg = os.environ.get("PDA_BN_FOLD_WG", "0") != "0"
         # the head BN (bn1, consumer conv1: 1x1, Cin = 4 Cout) folds in the concatenated form
         # dX = [dz | y1] . [k1 o W1 ; k2 o W1] + W1^T k3 (K = 2 Cout; the Gram form would be Cout + Cin)
         # and conv1's weight gradient forms dy1 while staging; digits = stages, "0" none
@@ -603,6 +607,8 @@ class NativeResNet(nn.Module):
                 self._side.wait_stream(cur)
                 with torch.cuda.stream(self._side):
                     yd = self._conv_bn(b.ds, h, train, ws=self.ws_w)
+            gram_side = (save and train and self.bn_fold_wg and self._side is not None
+                         and len(b.units) == 3 and self._tail_fold_ok(b, Nb))
             for j, u in enumerate(b.units):
                 y = self._conv_bn(u, a, train, pro)
                 ys.append(y)
@@ -610,6 +616,8 @@ class NativeResNet(nn.Module):
                     rec[f"s{j}"] = u.state
                 if j < len(b.units) - 1:
                     sc, sh = self._coeffs(u, train)
+                    if gram_side and j == len(b.units) - 2:
+                        rec["gram"] = self._fold_gram(b.units[-1], y, sc, sh)
                     if self._fuse_into(b.units[j + 1]):
                         # the next conv applies BN+ReLU while staging its tiles
                         a, pro = y, (sc, sh)
@@ -649,6 +657,8 @@ class NativeResNet(nn.Module):
             if save:
                 rec["ys"], rec["acts"], rec["yd"] = ys, acts, yd
                 saved["blocks"].append(rec)
+                if "gram" in rec:   # join the second stream's Gram work (graph captures need it)
+                    torch.cuda.current_stream(self.device).wait_stream(self._side)
             h = out
             if self.probe is not None:
                 self.probe("fwd", b.name)
@@ -859,6 +869,20 @@ class NativeResNet(nn.Module):
         g = ul.geom(Nb)
         return K.bnf_ok(g, self.dtype) and K.wgrad_bna_ok(g, Nb, self.dtype)
 
+    def _fold_gram(self, ul: ConvBN, y2, sc, sh):
+        """Forward-time half of the decomposed conv3 weight gradient, on the second stream beside
+        conv3's forward: Gram(a2), the column sums s of a2 = relu(bn2(y2)), and B = W3 Gram(a2)."""
+        C_ = y2.shape[-1]
+        cur = torch.cuda.current_stream(self.device)
+        self._side.wait_stream(cur)
+        with torch.cuda.stream(self._side):
+            gram = torch.empty(C_, C_, dtype=torch.float32, device=self.device)
+            colsum = torch.empty(C_, dtype=torch.float32, device=self.device)
+            K.conv_wgrad_gram(y2, sc, sh, gram, colsum, self.ws_w)
+            B = torch.empty(ul.cout, C_, dtype=torch.float32, device=self.device)
+            K.fold_bgemm(self.w16(ul), gram, B)
+        return B, colsum
+
     def _head_fold_ok(self, b: Block, Nb: int) -> bool:
         """Whether block ``b``'s head BatchNorm (bn1) backward is folded into conv1's gradients
         (PDA_BN_FOLD1, the concatenated form): Bottleneck blocks, 16-bit, per-rank statistics, a 1x1
@@ -979,10 +1003,17 @@ class NativeResNet(nn.Module):
                 fb = torch.empty(cin, dtype=torch.float32, device=self.device)
                 K.bn_fold(self.w16(u), k3, wf, fb, ws)
                 bnf = (wf, fb)
-                self._wgrad(lambda w, u=u, g=g, a=a_in, pro=pro, y3=ys[-1], k3=k3:
-                            K.conv_wgrad(dz, a, g, self.wgrad_view(u), w, accumulate=acc, pro=pro,
-                                         bna=(y3, k3), wscale=self.wgrad_scale),
-                            dz, a_in, ys[-1], kt)
+                if "gram" in rec:   # decomposed form: plain dz^T a2, combined in the split-K reduce
+                    gB, gs = rec["gram"]
+                    self._wgrad(lambda w, u=u, g=g, a=a_in, pro=pro, k3=k3, gB=gB, gs=gs:
+                                K.conv_wgrad(dz, a, g, self.wgrad_view(u), w, accumulate=acc, pro=pro,
+                                             combine=(k3, gB, gs), wscale=self.wgrad_scale),
+                                dz, a_in, kt, gB, gs)
+                else:
+                    self._wgrad(lambda w, u=u, g=g, a=a_in, pro=pro, y3=ys[-1], k3=k3:
+                                K.conv_wgrad(dz, a, g, self.wgrad_view(u), w, accumulate=acc, pro=pro,
+                                             bna=(y3, k3), wscale=self.wgrad_scale),
+                                dz, a_in, ys[-1], kt)
             else:
                 self._wgrad(lambda w, u=u, g=g, dy=dy, a=a_in, pro=pro:
                             K.conv_wgrad(dy, a, g, self.wgrad_view(u), w, accumulate=acc, pro=pro,

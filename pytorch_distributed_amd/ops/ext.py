@@ -80,7 +80,9 @@ _SIGS = {
     "pda_conv_wgrad": [C.POINTER(ConvDesc), _V, _V, _V, _I, _I, _V, _V, _I, _I, _I, _V],
     "pda_conv_wgrad_bna": [C.POINTER(ConvDesc), _V, _V, _V, _V, _V, _V, _V, _I, _I, _V, _V, _I, _I, _I,
                            _V],
-    "pda_wgrad_reduce": [_V, _V, _I, _I, _I, _I, _I, _I, _F, _I, _V],
+    "pda_wgrad_reduce": [_V, _V, _I, _I, _I, _I, _I, _I, _F, _I, _V, _V, _V, _V],
+    "pda_conv_wgrad_gram": [C.POINTER(ConvDesc), _V, _V, _V, _V, _I, _I, _I, _I, _I, _V],
+    "pda_fold_bgemm": [_V, _V, _I, _I, _V, _I, _V],
     "pda_bn_fwd_stats": [_V, _I, _I, _I, _I, _I, _V, _V, C.POINTER(BnFwdOut), _I, _V],
     "pda_bn_bwd_stats": [_V, _I, _I, _I, _I, _V, _V, C.POINTER(BnBwdOut), _I, _V],
     "pda_bn_finalize_tot": [_V, _I, _D, _V, _V, _F, _F, _V, _V, _V, _V, _V, _V, _V, _I, _V],

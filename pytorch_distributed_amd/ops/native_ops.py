@@ -530,12 +530,16 @@ def conv_wgrad(dy: torch.Tensor, x: torch.Tensor, g: ConvGeom, grad: torch.Tenso
                pro: Optional[Tuple[torch.Tensor, torch.Tensor]] = None,
                target_blocks: Optional[int] = None,
                bna: Optional[Tuple[torch.Tensor, torch.Tensor]] = None,
-               wscale: Optional[float] = None) -> torch.Tensor:
+               wscale: Optional[float] = None,
+               combine: Optional[Tuple[torch.Tensor, torch.Tensor, torch.Tensor]] = None) -> torch.Tensor:
     """grad (f32, OHWI with cin_real channels, rows of pitch R*S*cin_real) = scale * dW.
     pro = (scale, shift): x is PRE-BatchNorm; the activation relu(x*scale+shift) is recomputed.
     bna = (y, k) with k = [k1; k2; k3] (3 x Cout f32): ``dy`` is the BN-backward's masked gradient
     dz and the kernel stages dY = k1*dz + k2*y + k3 itself (csrc/conv_gemm.hip WGRAD_BNA; see
-    :func:`wgrad_bna_ok`)."""
+    :func:`wgrad_bna_ok`).
+    combine = (k, B, s): the decomposed form of that weight gradient -- ``dy`` is dz, the GEMM is
+    the plain dz^T x, and the split-K reduce writes k1*(dz^T x) + k2*B + k3*s^T per row, with
+    B = W Gram(x) and s the column sums of x (:func:`conv_wgrad_gram`, :func:`fold_bgemm`)."""
     Nb = dy.shape[0]
     bm, bn, splits, k_chunk = wgrad_plan(g, Nb, tile, target_blocks, f32=dy.dtype == torch.float32,
                                          dma=dy.dtype != torch.float32 and pro is None and bna is None,
@@ -564,10 +568,47 @@ def conv_wgrad(dy: torch.Tensor, x: torch.Tensor, g: ConvGeom, grad: torch.Tenso
                                       kdt, kbm, kbn, st)
         check(rc, "conv_wgrad")
     cr = g.Cin if cin_real is None else cin_real
+    ck, cB, cs = combine if combine is not None else (None, None, None)
     rc = ext.lib().pda_wgrad_reduce(ptr(slab), ptr(grad), splits, M, N, int(math.log2(g.Cin)), cr,
-                                    g.R * g.S * cr, float(scale), int(accumulate), st)
+                                    g.R * g.S * cr, float(scale), int(accumulate), ptr(ck), ptr(cB),
+                                    ptr(cs), st)
     check(rc, "wgrad_reduce")
     return grad
+
+
+def conv_wgrad_gram(y: torch.Tensor, sc: torch.Tensor, sh: torch.Tensor, gram: torch.Tensor,
+                    colsum: torch.Tensor, ws: "Workspace") -> None:
+    """gram [C][C] = a^T a and colsum [C] = sum over pixels of a = relu(y*sc + sh) (y 16-bit NHWC,
+    C channels; csrc/conv_gemm.hip WGRAD_GRAM: both operands staged through the BN+ReLU, split-K
+    slabs reduced in fixed order). The forward-time half of the decomposed tail-fold weight
+    gradient (:func:`conv_wgrad` ``combine``)."""
+    Nb, H, W, C_ = y.shape
+    P = Nb * H * W
+    bm, bn = (64, 64) if C_ <= 64 else (-128, 128)
+    tiles = math.ceil(C_ / tile_rows(bm)) * math.ceil(C_ / bn)
+    splits = max(1, min(math.ceil(2 * _NUM_CU / tiles), math.ceil(P / 256),
+                        max(1, (64 << 20) // (C_ * (C_ + 1) * 4))))
+    k_chunk = math.ceil(P / splits / 64) * 64
+    splits = math.ceil(P / k_chunk)
+    slab = ws.get("gram_slab", splits * C_ * (C_ + 1))
+    d = ConvGeom(Nb, H, W, C_, C_, 1, 1, 1, 0).desc(Nb)
+    st = stream(y.device)
+    kdt = _kdt(y)
+    check(ext.lib().pda_conv_wgrad_gram(C.byref(d), ptr(y), ptr(sc), ptr(sh), ptr(slab), splits,
+                                        k_chunk, kdt, bm, bn, st), "conv_wgrad_gram")
+    lc = int(math.log2(C_)) if C_ & (C_ - 1) == 0 else 0
+    L = ext.lib()
+    check(L.pda_wgrad_reduce(ptr(slab), ptr(gram), splits, C_, C_, int(math.log2(C_)), C_, C_, 1.0, 0,
+                             None, None, None, st), "gram_reduce")
+    check(L.pda_wgrad_reduce(ptr(slab[splits * C_ * C_:]), ptr(colsum), splits, 1, C_,
+                             int(math.log2(C_)), C_, C_, 1.0, 0, None, None, None, st), "colsum_reduce")
+
+
+def fold_bgemm(w: torch.Tensor, gram: torch.Tensor, out: torch.Tensor) -> None:
+    """out [Cout][C] f32 = W Gram (W 16-bit [Cout][C], the forward's weights)."""
+    Cout, C_ = w.shape[0], w.shape[-1]
+    check(ext.lib().pda_fold_bgemm(ptr(w), ptr(gram), Cout, C_, ptr(out), dt_of(w), stream(w.device)),
+          "fold_bgemm")
 
 
 # ------------------------------------------------------------------ batchnorm
@@ -755,6 +796,7 @@ def bn_bwd_finish(ws: "Workspace", part, G: int, nq: int, y, mean, invstd, gamma
 # 1024 / cg lanes, so narrower groups shorten both levels' serial load chains
 _BN_CG = int(os.environ.get("PDA_BN_CG", "256"))
 _BN_SK = float(os.environ.get("PDA_BN_SK", "0.75"))
+_BN_SMIN = int(os.environ.get("PDA_BN_SMIN", "8"))
 
 
 def _stats_cg(C_: int) -> int:
@@ -765,7 +807,7 @@ def _stats_slabs(T: int, C_: int) -> int:
     """Blocks per channel group of the one-launch statistics kernel: level 1 reads T/S tiles per
     block, the group's last arriver S slabs -- S ~ sqrt(T) balances the two (both run at one CU's
     bandwidth), at least 8 when T allows so the level-1 reads spread over CUs."""
-    return max(1, min(T, max(8, int(math.sqrt(_BN_SK * T)))))
+    return max(1, min(T, max(_BN_SMIN, int(math.sqrt(_BN_SK * T)))))
 
 
 def _bn_bwd_tail(ws, part, G, nq, mode, a, y, mean, invstd, gamma, dgamma, dbeta, dy_out,

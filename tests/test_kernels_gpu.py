@@ -1022,3 +1022,66 @@ def test_conv_wgrad_bna_conv1_tiles(Cout, Cin, H):
     K.conv_wgrad(dy, x, g, dw_u, ws, tile=(bm, bn))
     torch.cuda.synchronize()
     assert rel_err(dw_f, dw_u) < 2e-3
+
+
+@pytest.mark.parametrize("C,H", [(64, 14), (128, 12), (256, 7), (512, 7)])
+def test_conv_wgrad_gram_and_bgemm(C, H):
+    """WGRAD_GRAM: Gram(a) = a^T a and the column sums of a = relu(y*sc + sh) (both operands
+    staged through the BN+ReLU, rounded to bf16 as the forward's prologue does) against fp64 torch;
+    fold_bgemm: W Gram."""
+    K = _k()
+    dtype = torch.bfloat16
+    Nb = 3
+    torch.manual_seed(C)
+    y = torch.randn(Nb, H, H, C, device=DEV).to(dtype)
+    sc, sh = torch.rand(C, device=DEV) + 0.5, torch.randn(C, device=DEV) * 0.3
+    ws = K.Workspace(DEV)
+    gram = torch.empty(C, C, device=DEV)
+    colsum = torch.empty(C, device=DEV)
+    K.conv_wgrad_gram(y, sc, sh, gram, colsum, ws)
+    w = (torch.randn(4 * C, C, device=DEV) * 0.05).to(dtype)
+    B = torch.empty(4 * C, C, device=DEV)
+    K.fold_bgemm(w, gram, B)
+    torch.cuda.synchronize()
+    a = torch.relu(y.float() * sc + sh).to(dtype).double().view(-1, C)
+    assert rel_err(gram, a.t() @ a) < 1e-5
+    assert rel_err(colsum, a.sum(0)) < 1e-5
+    assert rel_err(B, w.double() @ gram.double()) < 1e-5
+
+
+@pytest.mark.parametrize("Cout,Cin,H", [(256, 64, 14), (512, 128, 12), (1024, 256, 7)])
+def test_conv_wgrad_decomposed_fold(Cout, Cin, H):
+    """The decomposed tail-fold weight gradient (plain dz^T a2 + the k-combine in the split-K
+    reduce with B = W3 Gram(a2), s = colsum(a2)) against the fp64 dY^T a2 with dY = k1*dz + k2*y3
+    + k3 and y3 = conv3(a2) -- and no worse than the WGRAD_BNA path."""
+    K = _k()
+    dtype = torch.bfloat16
+    Nb = 4
+    torch.manual_seed(Cout + 1)
+    g = K.ConvGeom(Nb, H, H, Cin, Cout, 1, 1, 1, 0)
+    y2 = torch.randn(Nb, H, H, Cin, device=DEV).to(dtype)
+    sc, sh = torch.rand(Cin, device=DEV) + 0.5, torch.randn(Cin, device=DEV) * 0.1
+    a2 = torch.relu(y2.float() * sc + sh).to(dtype)
+    w = (torch.randn(Cout, Cin, device=DEV) * 0.05).to(dtype)
+    y3 = torch.empty(Nb, H, H, Cout, device=DEV, dtype=dtype)
+    K.conv_fwd(a2, w, g, y3)
+    dz = torch.randn(Nb, H, H, Cout, device=DEV).to(dtype)
+    kk = torch.cat([torch.rand(Cout, device=DEV) + 0.5, torch.randn(Cout, device=DEV) * 0.3,
+                    torch.randn(Cout, device=DEV) * 0.2])
+    ws = K.Workspace(DEV)
+    gram = torch.empty(Cin, Cin, device=DEV)
+    colsum = torch.empty(Cin, device=DEV)
+    K.conv_wgrad_gram(y2, sc, sh, gram, colsum, ws)
+    B = torch.empty(Cout, Cin, device=DEV)
+    K.fold_bgemm(w, gram, B)
+    dw_dec = torch.zeros(Cout * Cin, device=DEV)
+    K.conv_wgrad(dz, y2, g, dw_dec, ws, pro=(sc, sh), combine=(kk, B, colsum))
+    dw_bna = torch.zeros(Cout * Cin, device=DEV)
+    K.conv_wgrad(dz, y2, g, dw_bna, ws, pro=(sc, sh), bna=(y3, kk))
+    torch.cuda.synchronize()
+    k1, k2, k3 = (kk[:Cout].double(), kk[Cout:2 * Cout].double(), kk[2 * Cout:].double())
+    dy = k1 * dz.double() + k2 * y3.double() + k3
+    ref = (dy.view(-1, Cout).t() @ a2.double().view(-1, Cin)).reshape(-1)
+    e_dec, e_bna = rel_err(dw_dec, ref), rel_err(dw_bna, ref)
+    print(f"dW3 vs fp64: decomposed {e_dec:.2e}, BNA {e_bna:.2e}")
+    assert e_dec < e_bna + 2e-3, (e_dec, e_bna)

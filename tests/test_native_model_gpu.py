@@ -413,3 +413,32 @@ def test_head_fold_matches_apply_path():
         if e_fold > 1.3 * e_apply + 0.01:
             bad.append((n, e_fold, e_apply))
     assert not bad, bad
+
+
+def test_decomposed_fold_wgrad_matches_apply_path():
+    """PDA_BN_FOLD_WG: the folded tails' conv3 weight gradient in the decomposed form (forward-time
+    Gram and column sums of a2 on the second stream, plain dz^T a2 combined in the split-K reduce)
+    -- every gradient as close to the fp32 reference as the apply path's."""
+    tm, nm = _pair("resnet50", image=64)
+    torch.manual_seed(13)
+    x = torch.randn(16, 3, 64, 64, device=DEV).to(torch.bfloat16).float()
+    y = torch.randint(0, 1000, (16,), device=DEV)
+    nm.train()
+    tm.train()
+    F.cross_entropy(tm(x), y).backward()
+    crit = nm.make_criterion()
+    grads = {}
+    for mode in ("apply", "wg"):
+        nm.bn_fold, nm.bn_fold_stages, nm.bn_fold_wg = mode == "wg", None, mode == "wg"
+        nm.zero_grad_flat()
+        crit(nm(x), y).backward()
+        torch.cuda.synchronize()
+        grads[mode] = dict((n, p.grad.detach().float().clone()) for n, p in nm.named_parameters())
+    nm.bn_fold_wg = False
+    tp = dict(tm.named_parameters())
+    bad = []
+    for n in grads["wg"]:
+        e_wg, e_apply = rel_err(grads["wg"][n], tp[n].grad), rel_err(grads["apply"][n], tp[n].grad)
+        if e_wg > 1.3 * e_apply + 0.01:
+            bad.append((n, e_wg, e_apply))
+    assert not bad, bad
