@@ -155,7 +155,8 @@ class NativeResNet(nn.Module):
         # folded tails take conv3's weight gradient in the decomposed form diag(k1) dz^T a2 +
         # diag(k2) W3 Gram(a2) + k3 s^T: the Gram and column sums of a2 run in the forward on the
         # second stream, so the backward's GEMM is a plain dz^T a2 (no y3 read, no VALU transform)
-        self.bn_fold_wg = os.environ.get("PDA_BN_FOLD_WG", "0") != "0"
+        # (in-step A/B: 27.07 / 27.13 vs 27.22 / 27.20 ms/step, profiles/ab_r4.md section 8)
+        self.bn_fold_wg = os.environ.get("PDA_BN_FOLD_WG", "1") != "0"
         # the head BN (bn1, consumer conv1: 1x1, Cin = 4 Cout) folds in the concatenated form
         # dX = [dz | y1] . [k1 o W1 ; k2 o W1] + W1^T k3 (K = 2 Cout; the Gram form would be Cout + Cin)
         # and conv1's weight gradient forms dy1 while staging; digits = stages, "0" none
