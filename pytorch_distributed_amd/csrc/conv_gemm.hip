@@ -956,6 +956,14 @@ __global__ __launch_bounds__(conv_nt<STAGES>(), (PASS_T == WGRAD_BNA || PASS_T =
 #pragma unroll
           for (int j = 0; j < NI; ++j) acc[i][j] = mfma16<MDT>(fb[j], fl[i], acc[i][j]);
       } else {
+      // data gradients: every fragment read of the k-step issued before its MFMAs, so the
+      // compiler overlaps the next step's reads with this step's MFMAs instead of re-using one
+      // A-fragment register (a read + wait per 4 MFMAs): -1..-6 % per kernel in isolation
+      // (profiles/ab_r4.md section 9; the forward tiles would spill)
+      if constexpr (!SPLIT && !F32 && PASS_T == DGRAD) {
+        __builtin_amdgcn_sched_group_barrier(0x100, MI + (B_ROW ? NI : 2 * NI) + (A_ROW ? 0 : MI), 0);
+        __builtin_amdgcn_sched_group_barrier(0x008, MI * NI, 0);
+      }
 #pragma unroll
       for (int i = 0; i < MI; ++i)
 #pragma unroll
@@ -1081,30 +1089,39 @@ __global__ __launch_bounds__(conv_nt<STAGES>(), (PASS_T == WGRAD_BNA || PASS_T =
       for (int i = 0; i < GP; ++i) voff[i] = pre ? voff[i] : OOB;
       constexpr int NMF = MI * NI;
       constexpr int NKS = BKE / 32;   // MFMA k-steps per tile
-#pragma unroll
-      for (int s = 0; s < NKS; ++s) {
-        s16x8 fa[MI], fb[NI];
+      // the fragments of k-step s+1 are read while the MFMAs of step s run (register double
+      // buffer), and the MFMA bursts of 64-deep tiles run at raised wave priority: -3..-11 % on the
+      // 128x256 / 256x128 weight-gradient tiles in isolation (profiles/ab_r4.md section 9)
+      s16x8 fa[2][MI], fb[2][NI];
+      auto ldf = [&](int s, int b) __attribute__((always_inline)) {
 #pragma unroll
         for (int i = 0; i < MI; ++i) {
           const int rbase = wr * (BM / WM) + i * 16;
-          if constexpr (A_ROW) fa[i] = frag_row(sa, rbase, s, lane);
-          else fa[i] = frag_col<BM>(sa, rbase, s, lane);
+          if constexpr (A_ROW) fa[b][i] = frag_row(sa, rbase, s, lane);
+          else fa[b][i] = frag_col<BM>(sa, rbase, s, lane);
         }
 #pragma unroll
         for (int j = 0; j < NI; ++j) {
           const int cbase = wc * (BN / WN) + j * 16;
-          if constexpr (B_ROW) fb[j] = frag_row(sb, cbase, s, lane);
-          else fb[j] = frag_col<BN>(sb, cbase, s, lane);
+          if constexpr (B_ROW) fb[b][j] = frag_row(sb, cbase, s, lane);
+          else fb[b][j] = frag_col<BN>(sb, cbase, s, lane);
         }
+      };
+      ldf(0, 0);
+#pragma unroll
+      for (int s = 0; s < NKS; ++s) {
+        if (s + 1 < NKS) ldf(s + 1, (s + 1) & 1);
+        if constexpr (NKS > 1) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
         for (int idx = 0; idx < NMF; ++idx) {
           const int i = idx / NI, j = idx % NI;
-          acc[i][j] = mfma16<MDT>(fb[j], fa[i], acc[i][j]);
+          acc[i][j] = mfma16<MDT>(fb[s & 1][j], fa[s & 1][i], acc[i][j]);
           const int g = s * NMF + idx;   // piece pc goes after MFMA (pc * NKS * NMF) / GP
 #pragma unroll
           for (int pc = 0; pc < GP; ++pc)
             if (g == (pc * NKS * NMF) / GP) dma_piece(pc, nslot, voff);
         }
+        if constexpr (NKS > 1) __builtin_amdgcn_s_setprio(0);
       }
       slot = slot == NSLOT - 1 ? 0 : slot + 1;
     }
