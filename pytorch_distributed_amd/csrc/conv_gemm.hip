@@ -386,6 +386,9 @@ __global__ __launch_bounds__(conv_nt<STAGES>(), (PASS_T == WGRAD_BNA || PASS_T =
 #pragma unroll
   for (int k = 0; k < (GRAM ? 4 : 1); ++k) gsum[k] = f32x2{0.f, 0.f};
   const bool gcol = GRAM && tn == 0;
+  // WGRAD_GRAM diagonal tile (tm == tn, square tile): the B image IS the A image (same tensor, same
+  // rows, same channels, same BN+ReLU) -- loaded, transformed and stored once, read twice
+  const bool gsame = GRAM && BM == BN && tm == tn;
   // B
   uint32_t b_off[BR];
   if constexpr (PASS == FWD) {
@@ -601,6 +604,7 @@ __global__ __launch_bounds__(conv_nt<STAGES>(), (PASS_T == WGRAD_BNA || PASS_T =
       for (int i = 0; i < BR; ++i) ldb(i, b_off[i] + uoff);
     } else if (wb_direct) {  // WGRAD B, 1x1 stride-1 conv: X rows ARE the GEMM rows
       constexpr int CPR = BN / EPC, RPI = NT / CPR;
+      if (gsame) return;
 #pragma unroll
       for (int i = 0; i < BR; ++i) {
         const int m = k0 + tid / CPR + RPI * i;
@@ -686,6 +690,7 @@ __global__ __launch_bounds__(conv_nt<STAGES>(), (PASS_T == WGRAD_BNA || PASS_T =
       }
     } else {
       constexpr int CPR = BN / EPC, RPI = NT / CPR;
+      if (gsame) return;
 #pragma unroll
       for (int i = 0; i < BR; ++i) {
         if constexpr (PASS == WGRAD) {
@@ -956,11 +961,13 @@ __global__ __launch_bounds__(conv_nt<STAGES>(), (PASS_T == WGRAD_BNA || PASS_T =
 #pragma unroll
           for (int j = 0; j < NI; ++j) acc[i][j] = mfma16<MDT>(fb[j], fl[i], acc[i][j]);
       } else {
-      // data gradients: every fragment read of the k-step issued before its MFMAs, so the
-      // compiler overlaps the next step's reads with this step's MFMAs instead of re-using one
-      // A-fragment register (a read + wait per 4 MFMAs): -1..-6 % per kernel in isolation
-      // (profiles/ab_r4.md section 9; the forward tiles would spill)
-      if constexpr (!SPLIT && !F32 && PASS_T == DGRAD) {
+      // data gradients (and the forward / folded-dgrad tiles up to 128x64): every fragment read
+      // of the k-step issued before its MFMAs, so the compiler overlaps the next step's reads
+      // with this step's MFMAs instead of re-using one A-fragment register (a read + wait per 4
+      // MFMAs): -1..-6 % per data-gradient kernel in isolation, -0.08 ms/step more with the small
+      // forward tiles (profiles/ab_r4.md sections 9-10; the 128x128 forward tiles would spill)
+      if constexpr (!SPLIT && !F32 && (PASS_T == DGRAD || ((PASS_T == FWD || PASS_T == DGRAD_BNF) &&
+                                                           BM * BN <= 128 * 64))) {
         __builtin_amdgcn_sched_group_barrier(0x100, MI + (B_ROW ? NI : 2 * NI) + (A_ROW ? 0 : MI), 0);
         __builtin_amdgcn_sched_group_barrier(0x008, MI * NI, 0);
       }
@@ -1145,7 +1152,7 @@ __global__ __launch_bounds__(conv_nt<STAGES>(), (PASS_T == WGRAD_BNA || PASS_T =
       }
       if (kt + 1 < nk) load_tile(kt + 1);
       const char* sa = smem + cur * STAGE;
-      mma_tile(sa, sa + A_BYTES);
+      mma_tile(sa, gsame ? sa : sa + A_BYTES);
       if constexpr (STAGES == 2) {
         if (kt + 1 < nk) store_tile(cur ^ 1);
       }
