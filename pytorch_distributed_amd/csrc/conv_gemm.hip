@@ -1048,6 +1048,9 @@ __global__ __launch_bounds__(conv_nt<STAGES>(), (PASS_T == WGRAD_BNA || PASS_T =
             if constexpr (B_ROW) fb[j] = frag_row(sb, cbase, s2, lane);
             else fb[j] = frag_col<BN>(sb, cbase, s2, lane);
           }
+          // data gradients: the MFMA bursts at raised wave priority (-10..-12 % on the C10 / C16
+          // tap-reuse dgrad in isolation; the forward lost 3-8 %: profiles/ab_r4.md section 11)
+          if constexpr (PASS == DGRAD) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
           for (int idx = 0; idx < NMF; ++idx) {
             const int i = idx / NI, j = idx % NI;
@@ -1060,6 +1063,7 @@ __global__ __launch_bounds__(conv_nt<STAGES>(), (PASS_T == WGRAD_BNA || PASS_T =
               else if (t < HA) a_piece(cc + 1, t);
             }
           }
+          if constexpr (PASS == DGRAD) __builtin_amdgcn_s_setprio(0);
         }
       }
     }
@@ -1172,7 +1176,8 @@ __global__ __launch_bounds__(conv_nt<STAGES>(), (PASS_T == WGRAD_BNA || PASS_T =
   };
 
   if constexpr (PASS == WGRAD) {
-    float* slab = reinterpret_cast<float*>(p.out) + (size_t)split * p.M * p.N;
+    // (WGRAD_GRAM: per split an [M + 1][N] block -- the partial Gram, then the column sums)
+    float* slab = reinterpret_cast<float*>(p.out) + (size_t)split * (GRAM ? p.M + 1 : p.M) * p.N;
     const bool vec = (p.N & 3) == 0;
     for_items([&](int rl, int cl, const f32x4& v) {
       const int row = m0 + wr * (BM / WM) + rl;
@@ -1187,7 +1192,7 @@ __global__ __launch_bounds__(conv_nt<STAGES>(), (PASS_T == WGRAD_BNA || PASS_T =
           if (col + e < p.N) d[e] = v[e];
       }
     });
-    if constexpr (GRAM) {   // column-sum partials of this split: [splits][M] behind the slabs
+    if constexpr (GRAM) {   // column-sum partials of this split: row M of its block
       if (gcol) {
         constexpr int CPR = BM / EPC, RPI = NT / CPR;
         float* red = reinterpret_cast<float*>(smem);   // [RPI][BM] (the main loop is done with LDS)
@@ -1199,7 +1204,7 @@ __global__ __launch_bounds__(conv_nt<STAGES>(), (PASS_T == WGRAD_BNA || PASS_T =
         if (tid < BM && m0 + tid < p.M) {
           float a = 0.f;
           for (int g = 0; g < RPI; ++g) a += red[g * BM + tid];
-          reinterpret_cast<float*>(p.out)[(size_t)gridDim.y * p.M * p.N + (size_t)split * p.M + m0 + tid] = a;
+          slab[(size_t)p.M * p.N + m0 + tid] = a;
         }
       }
     }
@@ -2011,8 +2016,8 @@ int pda_conv_wgrad_bna(const ConvDesc* d, const void* dz, const void* y, const f
 }
 
 // Gram = a^T a and s = sum_p a_p of a = relu(sc*y + sh) (y [Nb,H,W,C] 16-bit; WGRAD_GRAM): slab
-// [splits][C][C] partial Grams, then [splits][C] partial column sums. Tiles (64, 64) two-stage,
-// (-128, 128), (-128, 64); -1 otherwise.
+// [splits][C + 1][C] -- per split the partial Gram, then the partial column sums as row C (one
+// split-K reduce gives both). Tiles (64, 64) two-stage, (-128, 128), (-128, 64); -1 otherwise.
 int pda_conv_wgrad_gram(const ConvDesc* d, const void* y, const float* sc, const float* sh,
                         float* slab, int splits, int k_chunk, int dt, int bm, int bn, hipStream_t st) {
   if (dt != DT_BF16 && dt != DT_F16) return -1;

@@ -134,6 +134,8 @@ class NativeResNet(nn.Module):
         # "1" every consumer, "1x1" only 1x1 consumers (a 3x3 consumer gathers each element 9x per
         # N-tile, so it re-applies the prologue 9-36x: there one materialising pass is cheaper),
         # "1x1:H" also 3x3 consumers of input size >= H, "0" none
+        # (round 4 re-check, "1x1" vs "1x1:56": within +-0.05 ms/step over two boxes -- kept,
+        # profiles/ab_r4.md section 11)
         self.fuse_prologue = os.environ.get("PDA_FUSE_PROLOGUE", "1x1:56")
         self.fused_stem_bwd = True    # maxpool gather + ReLU mask + BN partials in one pass
         # stem wgrad forms its dY from the BN backward in-kernel (PDA_STEM_BNA=0: apply pass)
@@ -877,12 +879,11 @@ class NativeResNet(nn.Module):
         cur = torch.cuda.current_stream(self.device)
         self._side.wait_stream(cur)
         with torch.cuda.stream(self._side):
-            gram = torch.empty(C_, C_, dtype=torch.float32, device=self.device)
-            colsum = torch.empty(C_, dtype=torch.float32, device=self.device)
-            K.conv_wgrad_gram(y2, sc, sh, gram, colsum, self.ws_w)
+            gram = torch.empty(C_ + 1, C_, dtype=torch.float32, device=self.device)
+            K.conv_wgrad_gram(y2, sc, sh, gram, self.ws_w)   # Gram rows, then the column sums
             B = torch.empty(ul.cout, C_, dtype=torch.float32, device=self.device)
-            K.fold_bgemm(self.w16(ul), gram, B)
-        return B, colsum
+            K.fold_bgemm(self.w16(ul), gram[:C_], B)
+        return B, gram[C_]
 
     def _head_fold_ok(self, b: Block, Nb: int) -> bool:
         """Whether block ``b``'s head BatchNorm (bn1) backward is folded into conv1's gradients

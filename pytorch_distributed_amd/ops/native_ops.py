@@ -577,12 +577,15 @@ def conv_wgrad(dy: torch.Tensor, x: torch.Tensor, g: ConvGeom, grad: torch.Tenso
 
 
 def conv_wgrad_gram(y: torch.Tensor, sc: torch.Tensor, sh: torch.Tensor, gram: torch.Tensor,
-                    colsum: torch.Tensor, ws: "Workspace") -> None:
-    """gram [C][C] = a^T a and colsum [C] = sum over pixels of a = relu(y*sc + sh) (y 16-bit NHWC,
-    C channels; csrc/conv_gemm.hip WGRAD_GRAM: both operands staged through the BN+ReLU, split-K
-    slabs reduced in fixed order). The forward-time half of the decomposed tail-fold weight
-    gradient (:func:`conv_wgrad` ``combine``)."""
+                    ws: "Workspace") -> None:
+    """gram [C + 1][C]: rows 0..C-1 = a^T a, row C = the column sums of a = relu(y*sc + sh) (y
+    16-bit NHWC, C channels; csrc/conv_gemm.hip WGRAD_GRAM: both operands staged through the
+    BN+ReLU, the diagonal tiles stage one image for both; split-K slabs reduced in fixed order by
+    one launch). The forward-time half of the decomposed tail-fold weight gradient
+    (:func:`conv_wgrad` ``combine``)."""
     Nb, H, W, C_ = y.shape
+    if gram.numel() < (C_ + 1) * C_ or gram.dtype != torch.float32:
+        raise ValueError("conv_wgrad_gram: gram f32 [C + 1][C]")
     P = Nb * H * W
     bm, bn = (64, 64) if C_ <= 64 else (-128, 128)
     tiles = math.ceil(C_ / tile_rows(bm)) * math.ceil(C_ / bn)
@@ -593,15 +596,11 @@ def conv_wgrad_gram(y: torch.Tensor, sc: torch.Tensor, sh: torch.Tensor, gram: t
     slab = ws.get("gram_slab", splits * C_ * (C_ + 1))
     d = ConvGeom(Nb, H, W, C_, C_, 1, 1, 1, 0).desc(Nb)
     st = stream(y.device)
-    kdt = _kdt(y)
-    check(ext.lib().pda_conv_wgrad_gram(C.byref(d), ptr(y), ptr(sc), ptr(sh), ptr(slab), splits,
-                                        k_chunk, kdt, bm, bn, st), "conv_wgrad_gram")
-    lc = int(math.log2(C_)) if C_ & (C_ - 1) == 0 else 0
     L = ext.lib()
-    check(L.pda_wgrad_reduce(ptr(slab), ptr(gram), splits, C_, C_, int(math.log2(C_)), C_, C_, 1.0, 0,
-                             None, None, None, st), "gram_reduce")
-    check(L.pda_wgrad_reduce(ptr(slab[splits * C_ * C_:]), ptr(colsum), splits, 1, C_,
-                             int(math.log2(C_)), C_, C_, 1.0, 0, None, None, None, st), "colsum_reduce")
+    check(L.pda_conv_wgrad_gram(C.byref(d), ptr(y), ptr(sc), ptr(sh), ptr(slab), splits, k_chunk,
+                                _kdt(y), bm, bn, st), "conv_wgrad_gram")
+    check(L.pda_wgrad_reduce(ptr(slab), ptr(gram), splits, C_ + 1, C_, int(math.log2(C_)), C_, C_,
+                             1.0, 0, None, None, None, st), "gram_reduce")
 
 
 def fold_bgemm(w: torch.Tensor, gram: torch.Tensor, out: torch.Tensor) -> None:

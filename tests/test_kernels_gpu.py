@@ -1036,9 +1036,9 @@ def test_conv_wgrad_gram_and_bgemm(C, H):
     y = torch.randn(Nb, H, H, C, device=DEV).to(dtype)
     sc, sh = torch.rand(C, device=DEV) + 0.5, torch.randn(C, device=DEV) * 0.3
     ws = K.Workspace(DEV)
-    gram = torch.empty(C, C, device=DEV)
-    colsum = torch.empty(C, device=DEV)
-    K.conv_wgrad_gram(y, sc, sh, gram, colsum, ws)
+    ge = torch.empty(C + 1, C, device=DEV)
+    K.conv_wgrad_gram(y, sc, sh, ge, ws)
+    gram, colsum = ge[:C], ge[C]
     w = (torch.randn(4 * C, C, device=DEV) * 0.05).to(dtype)
     B = torch.empty(4 * C, C, device=DEV)
     K.fold_bgemm(w, gram, B)
@@ -1069,9 +1069,9 @@ def test_conv_wgrad_decomposed_fold(Cout, Cin, H):
     kk = torch.cat([torch.rand(Cout, device=DEV) + 0.5, torch.randn(Cout, device=DEV) * 0.3,
                     torch.randn(Cout, device=DEV) * 0.2])
     ws = K.Workspace(DEV)
-    gram = torch.empty(Cin, Cin, device=DEV)
-    colsum = torch.empty(Cin, device=DEV)
-    K.conv_wgrad_gram(y2, sc, sh, gram, colsum, ws)
+    ge = torch.empty(Cin + 1, Cin, device=DEV)
+    K.conv_wgrad_gram(y2, sc, sh, ge, ws)
+    gram, colsum = ge[:Cin], ge[Cin]
     B = torch.empty(Cout, Cin, device=DEV)
     K.fold_bgemm(w, gram, B)
     dw_dec = torch.zeros(Cout * Cin, device=DEV)
