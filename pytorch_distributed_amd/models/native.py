@@ -159,6 +159,8 @@ class NativeResNet(nn.Module):
         # second stream, so the backward's GEMM is a plain dz^T a2 (no y3 read, no VALU transform)
         # (in-step A/B: 27.07 / 27.13 vs 27.22 / 27.20 ms/step, profiles/ab_r4.md section 8)
         self.bn_fold_wg = os.environ.get("PDA_BN_FOLD_WG", "1") != "0"
+        # where the main stream joins the Grams: "end" of the forward, or after every "block"
+        self.gram_join_block = os.environ.get("PDA_GRAM_JOIN", "end") == "block"
         # the head BN (bn1, consumer conv1: 1x1, Cin = 4 Cout) folds in the concatenated form
         # dX = [dz | y1] . [k1 o W1 ; k2 o W1] + W1^T k3 (K = 2 Cout; the Gram form would be Cout + Cin)
         # and conv1's weight gradient forms dy1 while staging; digits = stages, "0" none
@@ -593,6 +595,7 @@ class NativeResNet(nn.Module):
         h = p
         feat = None
         nblk = len(self.blocks)
+        gram_pending = False
         for bi, b in enumerate(self.blocks):
             last = bi == nblk - 1
             rec = {"x": h} if save else None
@@ -660,11 +663,19 @@ class NativeResNet(nn.Module):
             if save:
                 rec["ys"], rec["acts"], rec["yd"] = ys, acts, yd
                 saved["blocks"].append(rec)
-                if "gram" in rec:   # join the second stream's Gram work (graph captures need it)
+                gram_pending = gram_pending or "gram" in rec
+                if gram_pending and self.gram_join_block:
                     torch.cuda.current_stream(self.device).wait_stream(self._side)
+                    gram_pending = False
             h = out
             if self.probe is not None:
                 self.probe("fwd", b.name)
+        if gram_pending:
+            # ONE join of the second stream's forward-time Gram work, after the last block: a join
+            # per block stalled the main chain 20-55 us whenever a Gram was still running
+            # (graph captures need every fork joined; the backward's weight gradients follow the
+            # Grams on that stream anyway)
+            torch.cuda.current_stream(self.device).wait_stream(self._side)
         logits = torch.empty(Nb, self.num_classes, dtype=torch.float32, device=self.device)
         g = ConvGeom(Nb, 1, 1, self.feat_dim, self.num_classes, 1, 1, 1, 0)
         K.conv_fwd(feat, self.fc_w16, g, logits,
