@@ -190,6 +190,8 @@ class NativeResNet(nn.Module):
         # _ReplicaGraph side_split): the backward leaves the batched weight-gradient kernels queued
         # (no flush, no end-of-backward join) for the capture driver to record on the second stream
         self.defer_side = False
+        self._early_opt = None        # NativeSGD.arm_overlap: SGD of the final gradients mid-backward
+        self._early_bound = 0
         # diagnostics (tools/layer_times.py): called on the main stream as probe(phase, name) after
         # the stem and after each residual block, forward and backward
         self.probe: Optional[Callable[[str, str], None]] = None
@@ -771,6 +773,18 @@ class NativeResNet(nn.Module):
             rec = sv["blocks"][bi]
             prev = (self.blocks[bi - 1], sv["blocks"][bi - 1]) if bi > 0 else None
             dx_main, shortcut_g, tail = self._block_backward(b, rec, tail, prev, acc)
+            opt = self._early_opt
+            if opt is not None and b.name == "layer2.0" and red is None and not self.defer_side:
+                # every gradient in [0, bound) is final (the flat buffer is in gradient order:
+                # fc, layer4 .. layer2): their fused SGD runs on the second stream now, behind
+                # their weight gradients and after the main stream's BN gradients so far, instead
+                # of in the step's exposed tail (opt.step() then updates layer1 + stem only)
+                bound = self.block_bounds[nblk - bi]
+                self._side.wait_stream(torch.cuda.current_stream(self.device))
+                with torch.cuda.stream(self._side):
+                    opt._launch_range(0, bound)
+                self._early_bound = bound
+                self._early_opt = None
             if not self.defer_side and (self._wbatch_mode == "block" or b.ds is not None):
                 self._flush_wgrad()
             if red is not None:
@@ -1198,17 +1212,34 @@ class NativeSGD(torch.optim.Optimizer):
     def zero_grad(self, set_to_none: bool = True) -> None:
         self.model.zero_grad_flat()
 
+    def arm_overlap(self) -> None:
+        """Let the next backward run the fused SGD of the gradients that are final before layer1's
+        backward on the second stream (single process, eager, no loss scaling: the caller's
+        responsibility -- NativeTrainer arms it only there); step() then covers the rest."""
+        m = self.model
+        if m._side is not None and not m.f32:
+            m._early_opt = self
+
+    def _launch_range(self, lo: int, hi: int, inv_scale=None, found_inf=None) -> None:
+        g = self.param_groups[0]
+        m = self.model
+        K.sgd_flat(m.flat_params[lo:hi], m.flat_grad[lo:hi], self.flat_mom[lo:hi],
+                   None if m.f32 else m.flat_shadow[lo:hi], g["lr"], g["momentum"],
+                   g["weight_decay"], self._initialized, inv_scale=inv_scale, found_inf=found_inf)
+
     def _launch(self, inv_scale=None, found_inf=None) -> None:
         g = self.param_groups[0]
         m = self.model
+        m._early_opt = None
+        lo, m._early_bound = m._early_bound, 0
         if m._grads_zero:
             # zero_grad() and no backward since: torch 2.x's set_to_none leaves every .grad None,
             # and SGD skips parameters without a gradient -- the flat gradient still holds the
             # previous step's values (no memset), so applying it would be a stale update
             return
-        K.sgd_flat(m.flat_params, m.flat_grad, self.flat_mom, None if m.f32 else m.flat_shadow,
-                   g["lr"], g["momentum"], g["weight_decay"], self._initialized, inv_scale=inv_scale,
-                   found_inf=found_inf)
+        if lo:   # the backward already updated [0, lo) on the second stream
+            torch.cuda.current_stream(m.device).wait_stream(m._side)
+        self._launch_range(lo, m.numel, inv_scale, found_inf)
         m._pack_stem()
         # (an overflow-skipped first step leaves the momentum buffer unset on the device but the
         # flag set: the next step then reads the zero-initialised buffer, m*0 + d == d)
@@ -1281,6 +1312,8 @@ class NativeTrainer:
             self.scaler = LossScaler()
         self._loss = None
         self.graphed = None
+        # fused SGD of layer2..fc on the second stream during layer1's backward (eager, 1 process)
+        self.overlap_sgd = os.environ.get("PDA_OVERLAP_SGD", "0") != "0"
         if graph:
             if world > 1:
                 raise ValueError("graph capture of the distributed step is not enabled (RCCL "
@@ -1303,6 +1336,8 @@ class NativeTrainer:
             self.scaler.step(self.opt)
             self.scaler.update()
         else:
+            if self.net is self.model and self.overlap_sgd:
+                self.opt.arm_overlap()
             loss.backward()
             self.opt.step()
         self.opt.zero_grad()
