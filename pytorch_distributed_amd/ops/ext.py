@@ -76,6 +76,7 @@ _SIGS = {
     "pda_conv_dgrad_bnf": [C.POINTER(ConvDesc), _V, _V, _V, C.POINTER(BnEpi), _V, _V, _V, _V, _I, _I,
                            _I, _I, _V],
     "pda_bn_fold": [_V, _V, _I, _I, _V, _V, _I, _V],
+    "pda_stem_fwd": [_V, _V, _V, _V, _I, _I, _I, _I, _I, _V],
     "pda_bn_fold_cat": [_V, _V, _I, _I, _V, _V, _I, _V],
     "pda_conv_wgrad": [C.POINTER(ConvDesc), _V, _V, _V, _I, _I, _V, _V, _I, _I, _I, _V],
     "pda_conv_wgrad_bna": [C.POINTER(ConvDesc), _V, _V, _V, _V, _V, _V, _V, _I, _I, _V, _V, _I, _I, _I,

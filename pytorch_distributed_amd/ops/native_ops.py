@@ -211,6 +211,9 @@ def conv_fwd(x: torch.Tensor, w: torch.Tensor, g: ConvGeom, out: torch.Tensor,
     Nb = x.shape[0]
     M = Nb * g.Ho * g.Wo
     Kpad = w.shape[-1] if w.dim() == 2 else w[0].numel()
+    if (tile is None and pro is None and bias is None and not relu and out.dtype == x.dtype
+            and Kpad == 256 and stem_fwd_ok(g, x.dtype)):
+        return stem_fwd(x, w, g, out, stats, bn, before_finalize)
     bm, bn_ = tile or fwd_tile(g, Nb, x.dtype, pro is not None, Kpad)
     d = g.desc(Nb)
     # direct (unstaged) f32 store + bias: the fc head (16-bit features -> f32 logits, or any conv
@@ -231,6 +234,45 @@ def conv_fwd(x: torch.Tensor, w: torch.Tensor, g: ConvGeom, out: torch.Tensor,
     if bn is not None:
         bn_finalize_partials(stats, T, g.Cout, tile_rows(kbm), M, bn)
     return out
+
+
+_STEM_FWD = os.environ.get("PDA_STEM_FWD", "1") != "0"
+
+
+def stem_fwd_ok(g: ConvGeom, dtype: torch.dtype) -> bool:
+    """Whether the space-to-depth stem conv (4x4/1, pad 2 top/left, 16 -> 64 channels) runs on the
+    dedicated tap-reuse kernel (csrc/stem.hip): 16-bit, H % 4 == 0, W % 16 == 0, W <= 128."""
+    return (_STEM_FWD and dtype in (torch.bfloat16, torch.float16) and g.R == 4 and g.S == 4
+            and g.Cin == 16 and g.Cout == 64 and g.stride == 1 and g.pad == 2 and g.Ho == g.H
+            and g.Wo == g.W and g.H % 4 == 0 and g.W % 16 == 0 and 16 <= g.W <= 128
+            and getattr(ext.lib(), "pda_stem_fwd", None) is not None)
+
+
+def stem_fwd(x: torch.Tensor, w: torch.Tensor, g: ConvGeom, out: torch.Tensor,
+             stats: Optional[torch.Tensor] = None, bn: Optional[BnStats] = None,
+             before_finalize=None) -> torch.Tensor:
+    """The stem conv on csrc/stem.hip (input slab staged once per 4-row tile in LDS, taps read
+    from it; persistent blocks keep the 64 x 256 weights in LDS). Statistics: shifted partials over
+    tiles of 4 * W rows, the format :func:`bn_finalize_partials` / :func:`stats_totals` take
+    (pass ``bm = stem_stats_rows(g)``)."""
+    Nb = x.shape[0]
+    M = Nb * g.Ho * g.Wo
+    rows = stem_stats_rows(g)
+    T = M // rows
+    if bn is not None:
+        stats = bn.ws.get("fwd_stats", T * 3 * g.Cout)
+    check(ext.lib().pda_stem_fwd(ptr(x), ptr(w), ptr(out), ptr(stats), Nb, g.H, g.W, _kdt(x), 0,
+                                 stream(x.device)), "stem_fwd")
+    if before_finalize is not None:
+        before_finalize()
+    if bn is not None:
+        bn_finalize_partials(stats, T, g.Cout, rows, M, bn)
+    return out
+
+
+def stem_stats_rows(g: ConvGeom) -> int:
+    """Rows of M per statistics tile of :func:`stem_fwd` (4 output rows of one image)."""
+    return 4 * g.Wo
 
 
 def stats_totals(stats: torch.Tensor, M: int, C_: int, bm: int) -> torch.Tensor:

@@ -1,5 +1,5 @@
 """Stem (4x4/1 space-to-depth conv, M = B*112*112, N = 64, K = 256) forward with every register
-tile, with the BN-statistics epilogue as in the step; median of 5 interleaved rounds x 5 reps (us).
+tile and the dedicated csrc/stem.hip kernel, with the BN-statistics epilogue as in the step; median of 5 interleaved rounds x 5 reps (us).
 Usage (GPU box): python tools/stem_bench.py"""
 import math
 import os
@@ -47,7 +47,21 @@ def main():
             en.record()
             en.synchronize()
             times[t].append(st.elapsed_time(en) / 5 * 1e3)
+    # the dedicated tap-reuse kernel (csrc/stem.hip), statistics over 4-row tiles
+    ys = torch.empty_like(y)
+    K.stem_fwd(x, w, g, ys, stats)
+    torch.cuda.synchronize()
+    err = (ys.float() - ref.float()).abs().max().item() if ref is not None else float("nan")
+    sk = []
+    for _ in range(5):
+        st.record()
+        for _ in range(5):
+            K.stem_fwd(x, w, g, ys, stats)
+        en.record()
+        en.synchronize()
+        sk.append(st.elapsed_time(en) / 5 * 1e3)
     print(f"stem fwd M={M} N=64 K=256 default tile {K.fwd_tile(g, B, torch.bfloat16, False, 256)}")
+    print(f"  csrc/stem.hip: {statistics.median(sk):8.1f} us (max |diff| vs first tile {err:.3g})")
     for t in tiles:
         print(f"  tile {t}: {statistics.median(times[t]):8.1f} us")
     for t, v in ok.items():
