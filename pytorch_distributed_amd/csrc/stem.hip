@@ -16,10 +16,11 @@
 // MFMA 16x16x32: A = weights (rows = output channel), B = pixels (cols = pixel), so each lane
 // holds 4 consecutive channels of one pixel: 8-byte stores, and one store instruction writes
 // 16 pixels x 32 contiguous bytes.
-// Statistics: shifted per-tile partials (sum(y - s), sum((y - s)^2), s) of the stored (rounded)
-// values with s = the tile's first pixel, the format conv_gemm.hip's FWD epilogue writes and
-// bn.hip bn_stats_kernel<0> finalizes (tile = 4W consecutive rows of M). Fixed reduction order:
-// deterministic.
+// Statistics: shifted partials (sum(y - s), sum((y - s)^2), s) of the stored (rounded) values per
+// output ROW (W consecutive rows of M; s = the row's first pixel), the format conv_gemm.hip's FWD
+// epilogue writes and bn.hip bn_stats_kernel<0> finalizes. Each wave reduces its own row (a
+// halving butterfly over its lanes), so the tile loop has no barrier besides the slab's.
+// Fixed reduction order: deterministic.
 #include "common.h"
 
 #include <type_traits>
@@ -49,8 +50,6 @@ __global__ __launch_bounds__(ST_NT, 2) void stem_fwd_kernel(
   extern __shared__ __attribute__((aligned(16))) char smem[];
   char* sw = smem;                                // weights, 32 KiB
   char* ss = smem + ST_C * 512;                   // input slab
-  float* red = reinterpret_cast<float*>(ss + SLAB);   // [4 waves][2][64]
-  float* shv = red + 4 * 2 * ST_C;                    // [64] shift of the tile
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int l16 = lane & 15, q = lane >> 4;
@@ -85,7 +84,7 @@ __global__ __launch_bounds__(ST_NT, 2) void stem_fwd_kernel(
   load_slab(t0);
 
   for (int t = t0; t < t1; ++t) {
-    __syncthreads();   // previous tile's slab / reduction reads are done (and the weights landed)
+    __syncthreads();   // every wave is done reading the previous tile's slab (and the weights landed)
 #pragma unroll
     for (int i = 0; i < PT; ++i) {
       const int ch = tid + i * ST_NT;
@@ -128,21 +127,14 @@ __global__ __launch_bounds__(ST_NT, 2) void stem_fwd_kernel(
       // ---- epilogue: rounded stores + shifted statistics (shift = the tile's first pixel
       // (oy0, 0), published by wave 0 in the first pass before any wave folds its pixels in)
       typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
-      if constexpr (STATS && P0 == 0) {
-        if (wave == 0 && l16 == 0) {
-#pragma unroll
-          for (int f = 0; f < 4; ++f) {
-            const f32x2 lo = unpack2<DT>(pack2<DT>(f32x2{acc[0][f][0], acc[0][f][1]}));
-            const f32x2 hi = unpack2<DT>(pack2<DT>(f32x2{acc[0][f][2], acc[0][f][3]}));
-            *reinterpret_cast<f32x4*>(shv + 16 * f + 4 * q) = f32x4{lo.x, lo.y, hi.x, hi.y};
-          }
-        }
-        __syncthreads();
+      if constexpr (STATS && P0 == 0) {   // shift = the wave's first pixel (its row's x = 0)
 #pragma unroll
         for (int f = 0; f < 4; ++f) {
-          const f32x4 s4 = *reinterpret_cast<const f32x4*>(shv + 16 * f + 4 * q);
+          const f32x2 lo = unpack2<DT>(pack2<DT>(f32x2{acc[0][f][0], acc[0][f][1]}));
+          const f32x2 hi = unpack2<DT>(pack2<DT>(f32x2{acc[0][f][2], acc[0][f][3]}));
+          const float e[4] = {lo.x, lo.y, hi.x, hi.y};
 #pragma unroll
-          for (int i = 0; i < 4; ++i) sh[f][i] = s4[i];
+          for (int i = 0; i < 4; ++i) sh[f][i] = __shfl(e[i], lane & 48, 64);
         }
       }
 #pragma unroll
@@ -186,23 +178,17 @@ __global__ __launch_bounds__(ST_NT, 2) void stem_fwd_kernel(
       }
     }
     {
+      float* base = stats + ((size_t)t * ST_TH + wave) * 3 * ST_C;
       const int qs = l16 >> 3, f = (l16 >> 1) & 3, i0 = (l16 & 1) * 2;
-      float* dst = red + (wave * 2 + qs) * ST_C + 16 * f + 4 * q + i0;
+      float* dst = base + qs * ST_C + 16 * f + 4 * q + i0;
       dst[0] = v[0];
       dst[1] = v[1];
-    }
-    __syncthreads();
-    if (tid < ST_C) {
-      float a = 0.f, b = 0.f;
+      if (l16 == 0) {
 #pragma unroll
-      for (int wv = 0; wv < 4; ++wv) {
-        a += red[(wv * 2 + 0) * ST_C + tid];
-        b += red[(wv * 2 + 1) * ST_C + tid];
+        for (int f2 = 0; f2 < 4; ++f2)
+          *reinterpret_cast<f32x4*>(base + 2 * ST_C + 16 * f2 + 4 * q) =
+              f32x4{sh[f2][0], sh[f2][1], sh[f2][2], sh[f2][3]};
       }
-      float* dst = stats + (size_t)t * 3 * ST_C + tid;
-      dst[0] = a;
-      dst[ST_C] = b;
-      dst[2 * ST_C] = shv[tid];
     }
   }
 }
@@ -211,9 +197,9 @@ template <int DT, int PF>
 int launch_stem(const void* x, const void* w, void* y, float* stats, int Nb, int H, int grid_cap,
                 hipStream_t st) {
   constexpr int W = PF * 16;
-  const size_t lds = ST_C * 512 + (size_t)(ST_TH + 3) * (W + 3) * 32 + (4 * 2 * ST_C + ST_C) * 4;
+  const size_t lds = ST_C * 512 + (size_t)(ST_TH + 3) * (W + 3) * 32;
   const int tiles = Nb * (H / ST_TH);
-  const int cap = grid_cap > 0 ? grid_cap : 512;
+  const int cap = grid_cap > 0 ? grid_cap : 1024;   // tools/stem_bench.py: 512-1024 best
   const int tpb = (tiles + cap - 1) / cap;
   const int grid = (tiles + tpb - 1) / tpb;
   if (stats)
@@ -228,8 +214,8 @@ int launch_stem(const void* x, const void* w, void* y, float* stats, int Nb, int
 }  // namespace
 
 // y [Nb][H][W][64] = conv4x4/1 (pad 2 top/left) of x [Nb][H][W][16] with w [64][256] (K order
-// tap-major, channel-minor), 16-bit; stats (nullable) [Nb*H/4][3][64] shifted per-tile partials
-// over tiles of 4W rows. Requires H % 4 == 0, W % 16 == 0, W <= 128; returns -1 otherwise.
+// tap-major, channel-minor), 16-bit; stats (nullable) [Nb*H][3][64] shifted partials per output
+// row (W rows of M). Requires H % 4 == 0, W % 16 == 0, W <= 128; returns -1 otherwise.
 extern "C" int pda_stem_fwd(const void* x, const void* w, void* y, float* stats, int Nb, int H, int W,
                             int dt, int grid_cap, hipStream_t st) {
   if (Nb <= 0 || H <= 0 || H % ST_TH || W % 16 || W < 16 || W > 128 || (dt != DT_BF16 && dt != DT_F16))

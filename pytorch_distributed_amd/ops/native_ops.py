@@ -237,6 +237,7 @@ def conv_fwd(x: torch.Tensor, w: torch.Tensor, g: ConvGeom, out: torch.Tensor,
 
 
 _STEM_FWD = os.environ.get("PDA_STEM_FWD", "1") != "0"
+_STEM_GRID = int(os.environ.get("PDA_STEM_GRID", "0"))   # persistent blocks (0: 1024)
 
 
 def stem_fwd_ok(g: ConvGeom, dtype: torch.dtype) -> bool:
@@ -253,7 +254,7 @@ def stem_fwd(x: torch.Tensor, w: torch.Tensor, g: ConvGeom, out: torch.Tensor,
              before_finalize=None) -> torch.Tensor:
     """The stem conv on csrc/stem.hip (input slab staged once per 4-row tile in LDS, taps read
     from it; persistent blocks keep the 64 x 256 weights in LDS). Statistics: shifted partials over
-    tiles of 4 * W rows, the format :func:`bn_finalize_partials` / :func:`stats_totals` take
+    output rows, the format :func:`bn_finalize_partials` / :func:`stats_totals` take
     (pass ``bm = stem_stats_rows(g)``)."""
     Nb = x.shape[0]
     M = Nb * g.Ho * g.Wo
@@ -261,8 +262,8 @@ def stem_fwd(x: torch.Tensor, w: torch.Tensor, g: ConvGeom, out: torch.Tensor,
     T = M // rows
     if bn is not None:
         stats = bn.ws.get("fwd_stats", T * 3 * g.Cout)
-    check(ext.lib().pda_stem_fwd(ptr(x), ptr(w), ptr(out), ptr(stats), Nb, g.H, g.W, _kdt(x), 0,
-                                 stream(x.device)), "stem_fwd")
+    check(ext.lib().pda_stem_fwd(ptr(x), ptr(w), ptr(out), ptr(stats), Nb, g.H, g.W, _kdt(x),
+                                 _STEM_GRID, stream(x.device)), "stem_fwd")
     if before_finalize is not None:
         before_finalize()
     if bn is not None:
@@ -271,8 +272,8 @@ def stem_fwd(x: torch.Tensor, w: torch.Tensor, g: ConvGeom, out: torch.Tensor,
 
 
 def stem_stats_rows(g: ConvGeom) -> int:
-    """Rows of M per statistics tile of :func:`stem_fwd` (4 output rows of one image)."""
-    return 4 * g.Wo
+    """Rows of M per statistics tile of :func:`stem_fwd` (one output row)."""
+    return g.Wo
 
 
 def stats_totals(stats: torch.Tensor, M: int, C_: int, bm: int) -> torch.Tensor:

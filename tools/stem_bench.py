@@ -61,6 +61,20 @@ def main():
         en.synchronize()
         sk.append(st.elapsed_time(en) / 5 * 1e3)
     print(f"stem fwd M={M} N=64 K=256 default tile {K.fwd_tile(g, B, torch.bfloat16, False, 256)}")
+    for cap in (256, 384, 512, 768, 1024, 2048):   # persistent-block count sweep
+        def run(c=cap):
+            K.check(ext.lib().pda_stem_fwd(K.ptr(x), K.ptr(w), K.ptr(ys), K.ptr(stats), B, g.H, g.W,
+                                           1, c, K.stream(dev)), "stem_fwd")
+        run()
+        ts = []
+        for _ in range(5):
+            st.record()
+            for _ in range(5):
+                run()
+            en.record()
+            en.synchronize()
+            ts.append(st.elapsed_time(en) / 5 * 1e3)
+        print(f"  csrc/stem.hip grid cap {cap}: {statistics.median(ts):8.1f} us")
     print(f"  csrc/stem.hip: {statistics.median(sk):8.1f} us (max |diff| vs first tile {err:.3g})")
     for t in tiles:
         print(f"  tile {t}: {statistics.median(times[t]):8.1f} us")
