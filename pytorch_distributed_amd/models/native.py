@@ -192,6 +192,7 @@ class NativeResNet(nn.Module):
         self.defer_side = False
         self._early_opt = None        # NativeSGD.arm_overlap: SGD of the final gradients mid-backward
         self._early_bound = 0
+        self._early_at = "layer2.0"   # "layer2.0": during layer1's backward; "stem": beside the stem's
         # diagnostics (tools/layer_times.py): called on the main stream as probe(phase, name) after
         # the stem and after each residual block, forward and backward
         self.probe: Optional[Callable[[str, str], None]] = None
@@ -774,7 +775,8 @@ class NativeResNet(nn.Module):
             prev = (self.blocks[bi - 1], sv["blocks"][bi - 1]) if bi > 0 else None
             dx_main, shortcut_g, tail = self._block_backward(b, rec, tail, prev, acc)
             opt = self._early_opt
-            if opt is not None and b.name == "layer2.0" and red is None and not self.defer_side:
+            if (opt is not None and b.name == self._early_at and red is None
+                    and not self.defer_side):
                 # every gradient in [0, bound) is final (the flat buffer is in gradient order:
                 # fc, layer4 .. layer2): their fused SGD runs on the second stream now, behind
                 # their weight gradients and after the main stream's BN gradients so far, instead
@@ -823,6 +825,17 @@ class NativeResNet(nn.Module):
             K.bn_bwd(ws, y0, st0[0], st0[1], self.gamma(u), st0[2], st0[3], self.dgamma(u),
                      self.dbeta(u), dy0, g1=dA0, accumulate=acc)
 
+        opt = self._early_opt
+        if opt is not None and self._early_at == "stem" and red is None and not self.defer_side:
+            # every gradient but the stem's is final (its BN gradients were just written on this
+            # stream; layer1's weight gradients are queued ahead on the second stream): their fused
+            # SGD runs there, beside the stem's weight gradient, instead of in the step's tail
+            bound = self.block_bounds[nblk]
+            self._side.wait_stream(torch.cuda.current_stream(self.device))
+            with torch.cuda.stream(self._side):
+                opt._launch_range(0, bound)
+            self._early_bound = bound
+            self._early_opt = None
         if bna:
             def stem_wgrad(w):
                 K.conv_wgrad(dz0, x0, g0, self.stem_wgrad, w, bna=(y0, k0), wscale=self.wgrad_scale)
@@ -1212,13 +1225,16 @@ class NativeSGD(torch.optim.Optimizer):
     def zero_grad(self, set_to_none: bool = True) -> None:
         self.model.zero_grad_flat()
 
-    def arm_overlap(self) -> None:
-        """Let the next backward run the fused SGD of the gradients that are final before layer1's
-        backward on the second stream (single process, eager, no loss scaling: the caller's
-        responsibility -- NativeTrainer arms it only there); step() then covers the rest."""
+    def arm_overlap(self, at: str = "layer2.0") -> None:
+        """Let the next backward run the fused SGD of the gradients that are final at point ``at``
+        on the second stream (single process, eager, no loss scaling: the caller's responsibility --
+        NativeTrainer arms it only there); step() then covers the rest. ``at``: "layer2.0" (after
+        that block's backward: layers 2-4 + fc during layer1's) or "stem" (all but the stem, beside
+        the stem's weight gradient)."""
         m = self.model
         if m._side is not None and not m.f32:
             m._early_opt = self
+            m._early_at = at
 
     def _launch_range(self, lo: int, hi: int, inv_scale=None, found_inf=None) -> None:
         g = self.param_groups[0]
@@ -1312,8 +1328,11 @@ class NativeTrainer:
             self.scaler = LossScaler()
         self._loss = None
         self.graphed = None
-        # fused SGD of layer2..fc on the second stream during layer1's backward (eager, 1 process)
-        self.overlap_sgd = os.environ.get("PDA_OVERLAP_SGD", "0") != "0"
+        # fused SGD of the gradients final before the end of the backward on the second stream
+        # (eager, 1 process): "1" = layers 2-4 + fc during layer1's backward, "stem" = all but the
+        # stem beside the stem's weight gradient
+        ov = os.environ.get("PDA_OVERLAP_SGD", "0")
+        self.overlap_sgd = {"0": None, "1": "layer2.0", "stem": "stem"}.get(ov, None)
         if graph:
             if world > 1:
                 raise ValueError("graph capture of the distributed step is not enabled (RCCL "
@@ -1337,7 +1356,7 @@ class NativeTrainer:
             self.scaler.update()
         else:
             if self.net is self.model and self.overlap_sgd:
-                self.opt.arm_overlap()
+                self.opt.arm_overlap(self.overlap_sgd)
             loss.backward()
             self.opt.step()
         self.opt.zero_grad()
