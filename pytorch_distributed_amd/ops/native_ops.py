@@ -211,9 +211,13 @@ def conv_fwd(x: torch.Tensor, w: torch.Tensor, g: ConvGeom, out: torch.Tensor,
     Nb = x.shape[0]
     M = Nb * g.Ho * g.Wo
     Kpad = w.shape[-1] if w.dim() == 2 else w[0].numel()
-    if (tile is None and pro is None and bias is None and not relu and out.dtype == x.dtype
-            and Kpad == 256 and stem_fwd_ok(g, x.dtype)):
+    dense = (tile is None and bias is None and not relu and out.dtype == x.dtype
+             and x.is_contiguous() and out.is_contiguous() and w.is_contiguous()
+             and x.numel() == Nb * g.H * g.W * g.Cin and out.numel() == M * g.Cout)
+    if dense and pro is None and Kpad == 256 and stem_fwd_ok(g, x.dtype):
         return stem_fwd(x, w, g, out, stats, bn, before_finalize)
+    if dense and Kpad == 576 and tapconv_ok(g, x.dtype):
+        return tapconv_fwd(x, w, g, out, stats, bn, before_finalize, pro)
     bm, bn_ = tile or fwd_tile(g, Nb, x.dtype, pro is not None, Kpad)
     d = g.desc(Nb)
     # direct (unstaged) f32 store + bias: the fc head (16-bit features -> f32 logits, or any conv
@@ -274,6 +278,57 @@ def stem_fwd(x: torch.Tensor, w: torch.Tensor, g: ConvGeom, out: torch.Tensor,
 def stem_stats_rows(g: ConvGeom) -> int:
     """Rows of M per statistics tile of :func:`stem_fwd` (one output row)."""
     return g.Wo
+
+
+# off by default: 170 vs 234 us isolated, but 0.1 ms/step slower in the step with one persistent
+# block per CU beside the second stream (profiles/ab_r4.md section 16)
+_TAPCONV = os.environ.get("PDA_TAPCONV", "0") != "0"
+_TAPCONV_GRID = int(os.environ.get("PDA_TAPCONV_GRID", "0"))   # persistent blocks (0: 256)
+
+
+def tapconv_ok(g: ConvGeom, dtype: torch.dtype) -> bool:
+    """Whether conv_fwd routes this conv to the tap-reuse kernel (``PDA_TAPCONV`` and
+    :func:`tapconv_supported`)."""
+    return _TAPCONV and tapconv_supported(g, dtype)
+
+
+def tapconv_supported(g: ConvGeom, dtype: torch.dtype) -> bool:
+    """Whether the tap-reuse kernel (csrc/tapconv.hip; the layer1 conv2) handles the conv: 3x3 /
+    stride 1 / pad 1, 64 -> 64 channels, 16-bit, H % 8 == 0, W % 8 == 0, 8 <= W <= 64."""
+    return (dtype in (torch.bfloat16, torch.float16) and g.R == 3 and g.S == 3
+            and g.Cin == 64 and g.Cout == 64 and g.stride == 1 and g.pad == 1 and g.Ho == g.H
+            and g.Wo == g.W and g.H % 8 == 0 and g.W % 8 == 0 and 8 <= g.W <= 64
+            and getattr(ext.lib(), "pda_tapconv_fwd", None) is not None)
+
+
+def tapconv_fwd(x: torch.Tensor, w: torch.Tensor, g: ConvGeom, out: torch.Tensor,
+                stats: Optional[torch.Tensor] = None, bn: Optional[BnStats] = None,
+                before_finalize=None,
+                pro: Optional[Tuple[torch.Tensor, torch.Tensor]] = None) -> torch.Tensor:
+    """3x3/1/1 64 -> 64 conv on csrc/tapconv.hip: the input slab of an 8-row tile staged once in
+    LDS (``pro`` = (scale, shift): BN+ReLU applied once while staging), the MFMA pixel operand read
+    from it for all 9 taps, weights resident in LDS. Statistics: shifted partials per output-row
+    pair (``bm = tapconv_stats_rows(g)`` for :func:`stats_totals`)."""
+    Nb = x.shape[0]
+    M = Nb * g.Ho * g.Wo
+    rows = tapconv_stats_rows(g)
+    T = M // rows
+    if bn is not None:
+        stats = bn.ws.get("fwd_stats", T * 3 * g.Cout)
+    check(ext.lib().pda_tapconv_fwd(ptr(x), ptr(w), ptr(out), ptr(stats),
+                                    ptr(pro[0] if pro else None), ptr(pro[1] if pro else None),
+                                    Nb, g.H, g.W, _kdt(x), _TAPCONV_GRID, stream(x.device)),
+          "tapconv_fwd")
+    if before_finalize is not None:
+        before_finalize()
+    if bn is not None:
+        bn_finalize_partials(stats, T, g.Cout, rows, M, bn)
+    return out
+
+
+def tapconv_stats_rows(g: ConvGeom) -> int:
+    """Rows of M per statistics tile of :func:`tapconv_fwd` (two output rows)."""
+    return 2 * g.Wo
 
 
 def stats_totals(stats: torch.Tensor, M: int, C_: int, bm: int) -> torch.Tensor:
