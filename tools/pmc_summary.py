@@ -1,8 +1,10 @@
-"""Summarise rocprofv3 --pmc CSVs of tools/gpu_pmc.sh: mean counter values per conv case."""
+"""Summarise rocprofv3 --pmc CSVs of tools/gpu_pmc.sh: mean counter values per conv case
+(kernels whose name matches the regex PMC_KERNEL, default conv_gemm)."""
 import collections
 import csv
 import glob
 import os
+import re
 import sys
 
 
@@ -13,7 +15,7 @@ def main():
         case = os.path.basename(os.path.dirname(f)).rsplit("_g", 1)[0]
         agg = collections.defaultdict(list)
         for r in csv.DictReader(open(f)):
-            if "conv_gemm" in r["Kernel_Name"]:
+            if re.search(os.environ.get("PMC_KERNEL", "conv_gemm"), r["Kernel_Name"]):
                 agg[r["Counter_Name"]].append(float(r["Counter_Value"]))
         for k, v in agg.items():
             cases[case][k] = sum(v) / len(v)
