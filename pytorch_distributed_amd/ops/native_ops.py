@@ -391,8 +391,15 @@ def dgrad_tile(g: ConvGeom, Nb: int, dma: bool = True) -> Tuple[int, int]:
     the step's critical path: 28.03 -> 27.88 ms/step without it, profiles/ab_r3_dma.md section 11.
     ``dma`` is kept for callers that pass the operand dtype; pass tile=(2256, 128) explicitly to
     run the HALO kernel.)"""
+    if dma and _DMA and _DGRAD_HALO and _halo_geom(g) and g.Cin >= 128:
+        return 2256, 128
     M = Nb * (g.H // g.stride) * (g.W // g.stride)
     return pick_tile(M * g.stride * g.stride, g.Cin, g.Cout * _max_class_taps(g))
+
+
+# re-check knob: the HALO data-gradient tile in the step (round 3: slower; the kernel has since
+# gained raised-priority MFMA bursts, profiles/ab_r4.md section 11)
+_DGRAD_HALO = os.environ.get("PDA_DGRAD_HALO", "0") != "0"
 
 
 def _max_class_taps(g: ConvGeom) -> int:
