@@ -385,21 +385,20 @@ def _halo_geom(g: ConvGeom) -> bool:
 
 
 def dgrad_tile(g: ConvGeom, Nb: int, dma: bool = True) -> Tuple[int, int]:
-    """Data-gradient tile: the register-staged tiles. (The tap-reuse (HALO) 256x128 LDS-DMA tile is
-    faster in isolation on C10 / C16 -- 121 -> 112, 115 -> 112 us -- but slower in the step: its
-    block takes a whole CU beside the weight-gradient stream's tiles, and the data gradients are
-    the step's critical path: 28.03 -> 27.88 ms/step without it, profiles/ab_r3_dma.md section 11.
-    ``dma`` is kept for callers that pass the operand dtype; pass tile=(2256, 128) explicitly to
-    run the HALO kernel.)"""
+    """Data-gradient tile: the tap-reuse (HALO) 256x128 LDS-DMA tile for 3x3 stride-1 layers with
+    >= 128 channels (``PDA_DGRAD_HALO``; round 3 measured it slower in the step, 28.03 -> 27.88
+    ms/step without it, profiles/ab_r3_dma.md section 11; with the round-4 MFMA-burst priority it
+    wins, profiles/ab_r4.md section 17), the register-staged tiles otherwise. ``dma``: 16-bit
+    operands (the DMA tiles need them)."""
     if dma and _DMA and _DGRAD_HALO and _halo_geom(g) and g.Cin >= 128:
         return 2256, 128
     M = Nb * (g.H // g.stride) * (g.W // g.stride)
     return pick_tile(M * g.stride * g.stride, g.Cin, g.Cout * _max_class_taps(g))
 
 
-# re-check knob: the HALO data-gradient tile in the step (round 3: slower; the kernel has since
-# gained raised-priority MFMA bursts, profiles/ab_r4.md section 11)
-_DGRAD_HALO = os.environ.get("PDA_DGRAD_HALO", "0") != "0"
+# the HALO data-gradient tile in the step: slower in round 3; with this round's raised-priority
+# MFMA bursts (profiles/ab_r4.md section 11) -0.03 ms/step over 7 in-step pairs (section 17)
+_DGRAD_HALO = os.environ.get("PDA_DGRAD_HALO", "1") != "0"
 
 
 def _max_class_taps(g: ConvGeom) -> int:

@@ -245,8 +245,11 @@ def test_lds_dma_tile_codes_and_fallback():
     assert K.fwd_tile(g, 400, torch.bfloat16) == (2256, 128)
     assert K.fwd_tile(g, 400, torch.bfloat16, pro=True)[0] < 1000
     assert K.fwd_tile(g, 400, torch.float32)[0] < 1000
-    # data gradients: register-staged in the step (the HALO dgrad tile is explicit-only)
-    assert K.dgrad_tile(g, 400)[0] < 1000 and K.dgrad_tile(g, 400, dma=False)[0] < 1000
+    # data gradients: the HALO tile for 3x3 stride-1 (PDA_DGRAD_HALO), register-staged otherwise
+    assert K.dgrad_tile(g, 400) == ((2256, 128) if K._DGRAD_HALO else K.dgrad_tile(g, 400, dma=False))
+    assert K.dgrad_tile(g, 400, dma=False)[0] < 1000
+    g1 = K.ConvGeom(400, 14, 14, 256, 1024, 1, 1, 1, 0)
+    assert K.dgrad_tile(g1, 400)[0] < 1000
     assert K.dgrad_slabs(g, 400, dtype=torch.float32) == math.ceil(400 * 196 / K.tile_rows(
         K.dgrad_tile(g, 400, dma=False)[0]))
 
