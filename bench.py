@@ -24,12 +24,13 @@ Self-validation for N > 1 (everything below runs AFTER the timed region):
 * finite rendezvous / RCCL-init timeouts (``PDA_DIST_TIMEOUT_S``), so a missing rank is
   an error, not a hang.
 
-``fp32_images_per_sec``: a short pass of the same step in exact fp32 (the reference
-scripts' precision) so the like-for-like number is measured in the same run; and
-``fp32_split_images_per_sec``: the same f32 step with the convolutions on the bf16 MFMA as a
-hi/lo three-term split (~16 significant bits per product -- the reference's fp32 runs use TF32
-convolutions, 10 bits). For N > 1 each rank runs them without gradient all-reduce (per-GPU fp32
-compute, aggregated).
+``fp32_images_per_sec``: a short pass of the same step in fp32 (the reference scripts'
+precision) on the fp32 default -- f32 tensors with the convolutions on the bf16 MFMA as a hi/lo
+three-term split (~16 significant bits per product; every conv pass at or below the error of the
+TF32 convolutions the reference's fp32 runs use, tests/test_f32_precision_gpu.py) -- so the
+like-for-like number is measured in the same run; and ``fp32_exact_images_per_sec``: the same f32
+step on the exact f32 MFMA. For N > 1 each rank runs them without gradient all-reduce (per-GPU
+fp32 compute, aggregated).
 
 Reference metric: images/sec whole node at bs 400/GPU; published
 (derived) 717.0 img/s on 1 GPU (fp32/TF32) and 5,546.7 img/s on 8 GPUs (AMP-DDP "Apex").
@@ -90,7 +91,7 @@ def parse():
                     help="N>1: measure all-reduce latency / bus bandwidth of the gradient "
                          "communicator after the timed region (xgmi_probe in the JSON; 0: skip)")
     ap.add_argument("--fp32-steps", type=int, default=5,
-                    help="timed steps of the exact-fp32 pass (0: skip)")
+                    help="timed steps of each fp32 pass (default split convs, exact; 0: skip)")
     ap.add_argument("--amp-steps", type=int, default=10,
                     help="timed steps of the fp16 AMP-DDP pass (resnet_ddp_apex.py config; 0: skip)")
     ap.add_argument("--dp-steps", type=int, default=10,
@@ -300,11 +301,12 @@ def _verify_consistent(ctx: Ctx, tr) -> dict:
     return {"weights_consistent": ok, "checksum": [int(v) for v in cs.tolist()]}
 
 
-def _fp32_pass(ctx: Ctx, args, mode: str = "exact") -> dict:
+def _fp32_pass(ctx: Ctx, args, mode: str = "split") -> dict:
     """Short fp32 pass (reference precision), each rank locally (no all-reduce). ``mode``: the f32
-    convolution math of the native engine -- "exact" (MFMA 16x16x4 f32) or "split" (bf16 MFMA on a
-    hi/lo three-term split, ~16 significant bits per product: above the TF32 convolutions the
-    reference's fp32 runs use by default)."""
+    convolution math of the native engine -- "split" (the fp32 default: bf16 MFMA on a hi/lo
+    three-term split, ~16 significant bits per product, at or below the error of the TF32
+    convolutions the reference's fp32 runs use by default on A100 -- tests/test_f32_precision_gpu.py)
+    keyed ``fp32_*``, or "exact" (MFMA 16x16x4 f32, f32 rounding only) keyed ``fp32_exact_*``."""
     from pytorch_distributed_amd.bench_step import make_trainer
     from pytorch_distributed_amd.ops import native_ops as K
     old, K._F32_CONV = K._F32_CONV, mode
@@ -315,15 +317,15 @@ def _fp32_pass(ctx: Ctx, args, mode: str = "exact") -> dict:
             return {}
         for i in range(2):
             tr.step(i)
-        el = _timed(ctx, tr, 2, args.fp32_steps, "fp32" if mode == "exact" else "fp32_split")
+        key = "fp32" if mode == "split" else "fp32_exact"
+        el = _timed(ctx, tr, 2, args.fp32_steps, key)
     finally:
         K._F32_CONV = old
     world = ctx.world if ctx.multi else 1
-    key = "fp32" if mode == "exact" else "fp32_split"
     res = {f"{key}_images_per_sec": round(args.batch * world * args.fp32_steps / el, 2),
            f"{key}_ms_per_step": round(1000.0 * el / args.fp32_steps, 3)}
-    if mode == "exact":
-        res.update({"fp32_engine": tr.engine,
+    if mode == "split":
+        res.update({"fp32_engine": tr.engine, "fp32_conv": "split (bf16 MFMA hi/lo, >= TF32)",
                     "fp32_mode": "single" if world == 1 else "per-rank local steps, no all-reduce"})
     del tr
     if ctx.cuda:
@@ -548,7 +550,7 @@ def main():
             torch.cuda.empty_cache()
         if args.fp32_steps > 0 and args.dtype != "fp32":
             extra.update(_fp32_pass(ctx, args))
-            extra.update(_fp32_pass(ctx, args, "split"))
+            extra.update(_fp32_pass(ctx, args, "exact"))
         if args.amp_steps > 0 and args.dtype != "fp16":
             extra.update(_guarded(ctx, "amp_fp16", _amp_pass, ctx, args))
         if args.dp_steps > 0 and ctx.cuda:

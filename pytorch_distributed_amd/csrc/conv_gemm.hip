@@ -1667,46 +1667,6 @@ __global__ __launch_bounds__(256) void fold_bgemm_kernel(const u16* __restrict__
   *reinterpret_cast<f32x4*>(B + (size_t)row * C + n) = acc;
 }
 
-// Operands of the concatenated BatchNorm-backward fold (pda_conv_dgrad_bnf with xa_c = Cout):
-// wf = [k1 o W ; k2 o W] ([2 Cout][Cin] 16-bit) and b = W^T k3 (f32 [Cin]). Block = one 64-column
-// panel of W, 256 threads = 8 column chunks x 32 row sets; bias partials per thread over fixed row
-// sets, combined in a fixed order: deterministic.
-template <int DT>
-__global__ __launch_bounds__(256) void bn_fold_cat_kernel(const u16* __restrict__ W,
-                                                          const float* __restrict__ k, int Cout,
-                                                          int Cin, u16* __restrict__ Wf,
-                                                          float* __restrict__ bias) {
-  __shared__ float bred[32][64];
-  const int tid = threadIdx.x, cc = tid & 7, rs = tid >> 3;
-  const int col = blockIdx.x * 64 + cc * 8;
-  float bs[8];
-#pragma unroll
-  for (int e = 0; e < 8; ++e) bs[e] = 0.f;
-  for (int row = rs; row < Cout; row += 32) {
-    const i32x4 v = *reinterpret_cast<const i32x4*>(W + (size_t)row * Cin + col);
-    const float s1 = k[row], s2 = k[Cout + row], s3 = k[2 * Cout + row];
-    i32x4 w1, w2;
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const f32x2 f = unpack2<DT>((uint32_t)v[q]);
-      w1[q] = (int)pack2<DT>(f32x2{f.x * s1, f.y * s1});
-      w2[q] = (int)pack2<DT>(f32x2{f.x * s2, f.y * s2});
-      bs[2 * q] = __builtin_fmaf(s3, f.x, bs[2 * q]);
-      bs[2 * q + 1] = __builtin_fmaf(s3, f.y, bs[2 * q + 1]);
-    }
-    *reinterpret_cast<i32x4*>(Wf + (size_t)row * Cin + col) = w1;
-    *reinterpret_cast<i32x4*>(Wf + (size_t)(Cout + row) * Cin + col) = w2;
-  }
-#pragma unroll
-  for (int e = 0; e < 8; ++e) bred[rs][cc * 8 + e] = bs[e];
-  __syncthreads();
-  if (tid < 64) {
-    float b = 0.f;
-    for (int g = 0; g < 32; ++g) b += bred[g][tid];
-    bias[blockIdx.x * 64 + tid] = b;
-  }
-}
-
 }  // namespace
 
 // ================================================================= host launchers (C ABI)
@@ -1913,19 +1873,12 @@ int pda_conv_dgrad(const ConvDesc* d, const void* dy, const void* w, void* dx, c
 // wf = [k1 o W ; G] ([Cout + Cin][Cin], pda_bn_fold); xa [Nb,H,W,Cin] the Gram operand (the conv's
 // forward input; xa_sc / xa_sh: its BN+ReLU prologue, or null); dbias [Cin] f32. Register-staged
 // tiles (-128, 64), (-128, 128), (64, 64), (64, 128); -1 otherwise.
-// xa_c = Cout (stride 1): the concatenated form dX = [dz | y] . [k1 o W ; k2 o W] + b, with xa = y
-// (the conv's forward output) and wf from pda_bn_fold_cat -- for convs whose Cin > Cout, where the
-// Gram operand would make K longer than the conv's own.
 int pda_conv_dgrad_bnf(const ConvDesc* d, const void* dz, const void* wf, void* dx, const BnEpi* epi,
                        const void* xa, const float* xa_sc, const float* xa_sh, const float* dbias,
-                       int xa_c, int dt, int bm, int bn, hipStream_t st) {
+                       int dt, int bm, int bn, hipStream_t st) {
   if (dt != DT_BF16 && dt != DT_F16) return -1;
-  if (xa_c <= 0) xa_c = d->Cin;
-  if (d->R != 1 || d->S != 1 || d->pad != 0 || (d->Cin % 64) || (xa_c % 64) || !xa || !dbias)
-    return -2;
-  // the second operand is read at the dX pixel: with xa_c != Cin it is the conv's own output y
-  // (the concatenated [dz | y] form), which needs stride 1
-  if (xa_c != d->Cin && d->stride != 1) return -2;
+  const int xa_c = d->Cin;
+  if (d->R != 1 || d->S != 1 || d->pad != 0 || (d->Cin % 64) || !xa || !dbias) return -2;
   if (!fits32((long long)d->Nb * d->Ho * d->Wo * d->Cout, (long long)(d->Cout + d->Cin) * d->Cin,
               (long long)d->Nb * d->H * d->W * d->Cin, dt))
     return -4;
@@ -1945,23 +1898,6 @@ int pda_conv_dgrad_bnf(const ConvDesc* d, const void* dz, const void* wf, void* 
 #endif
 #undef BNF_CASE
   return -1;
-}
-
-// Wf = [k1 o W ; k2 o W] and b = W^T k3 of a 1x1 conv (W [Cout][Cin] 16-bit, k = [k1;k2;k3]): the
-// operands of the concatenated form of pda_conv_dgrad_bnf (xa_c = Cout). Cin a multiple of 64.
-int pda_bn_fold_cat(const void* w, const float* k, int Cout, int Cin, void* wf, float* bias, int dt,
-                    hipStream_t st) {
-  if ((Cin % 64) || Cout <= 0) return -2;
-  const dim3 grid(Cin / 64);
-  if (dt == DT_BF16)
-    hipLaunchKernelGGL(bn_fold_cat_kernel<DT_BF16>, grid, dim3(256), 0, st, (const u16*)w, k, Cout,
-                       Cin, (u16*)wf, bias);
-  else if (dt == DT_F16)
-    hipLaunchKernelGGL(bn_fold_cat_kernel<DT_F16>, grid, dim3(256), 0, st, (const u16*)w, k, Cout,
-                       Cin, (u16*)wf, bias);
-  else
-    return -1;
-  return (int)hipGetLastError();
 }
 
 // Wf = [k1 o W ; W^T diag(k2) W] and b = W^T k3 of a 1x1 conv (W [Cout][Cin] 16-bit, k = [k1;k2;k3]

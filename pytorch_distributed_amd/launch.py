@@ -27,49 +27,75 @@ __all__ = ["DistEnv", "dist_env", "spawn", "free_port", "bind_numa", "init_distr
 
 # KFD topology (sysfs): the GPU list in HSA agent order, readable without initialising HIP
 _KFD_ROOT = "/sys/class/kfd/kfd/topology/nodes"
+_DRI_ROOT = "/dev/dri"
+_UNPARSED = object()   # a *_VISIBLE_DEVICES selector that is not a list of indices (UUIDs)
 
 
 def _kfd_gpus():
-    """Property dicts of the GPU nodes of the KFD topology (simd_count > 0), in HSA agent order;
-    None when the topology is not readable."""
+    """Property dicts of the GPU nodes of the KFD topology (simd_count > 0) that this process may
+    open, in HSA agent order; None when the topology is not readable. sysfs is not namespaced: a
+    container given only some render nodes still lists every GPU of the host, so a node counts only
+    when its ``/dev/dri/renderD<drm_render_minor>`` is accessible (when /dev/dri exists at all)."""
     try:
         gpus = []
+        dri = os.path.isdir(_DRI_ROOT)
         for n in sorted((d for d in os.listdir(_KFD_ROOT) if d.isdigit()), key=int):
             with open(f"{_KFD_ROOT}/{n}/properties") as f:
                 kv = dict(l.split(" ", 1) for l in f.read().split("\n") if " " in l)
-            if int(kv.get("simd_count", "0")) > 0:
-                gpus.append(kv)
+            if int(kv.get("simd_count", "0")) <= 0:
+                continue
+            minor = kv.get("drm_render_minor")
+            if dri and minor is not None and int(minor) > 0 and not os.access(
+                    f"{_DRI_ROOT}/renderD{int(minor)}", os.R_OK | os.W_OK):
+                continue
+            gpus.append(kv)
         return gpus
     except (OSError, ValueError):
         return None
 
 
-def _visible_list() -> Optional[list]:
-    """Physical GPU indices selected by ROCR_/HIP_/CUDA_VISIBLE_DEVICES (applied in that order, each
-    one indexing the devices the previous left), or None when none is set. Non-integer entries
-    (UUIDs) make the mapping unknown: None."""
+def _visible_list():
+    """Indices (into the KFD GPU list) of the GPUs the *_VISIBLE_DEVICES variables select, or None
+    when none is set. ROCR_VISIBLE_DEVICES applies first (ROCr); HIP then applies
+    HIP_VISIBLE_DEVICES, or CUDA_VISIBLE_DEVICES only when HIP_VISIBLE_DEVICES is unset (HIP reads
+    one of the two, not both). ``_UNPARSED`` when a selector is not a list of integers (UUIDs)."""
     sel = None
-    for var in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+    hip = "HIP_VISIBLE_DEVICES" if "HIP_VISIBLE_DEVICES" in os.environ else "CUDA_VISIBLE_DEVICES"
+    for var in ("ROCR_VISIBLE_DEVICES", hip):
         v = os.environ.get(var)
         if v is None:
             continue
         try:
             ids = [int(x) for x in v.split(",") if x.strip() != ""]
         except ValueError:
-            return None
+            return _UNPARSED
         sel = ids if sel is None else [sel[i] for i in ids if 0 <= i < len(sel)]
     return sel
+
+
+def _child_device_count() -> int:
+    """torch's device count, taken in a short-lived child process so that THIS process starts no
+    HIP runtime (and its threads) before the launcher binds its NUMA node."""
+    import subprocess
+    import sys
+    try:
+        r = subprocess.run([sys.executable, "-c", "import torch; print(torch.cuda.device_count())"],
+                           capture_output=True, text=True, timeout=300)
+        return int(r.stdout.strip().splitlines()[-1])
+    except (OSError, ValueError, IndexError, subprocess.SubprocessError):
+        return 0
 
 
 def visible_gpu_count() -> int:
     """GPUs this process will see, counted from the KFD topology and the *_VISIBLE_DEVICES
     variables -- no HIP call, so the launcher can bind a rank's NUMA node BEFORE the HIP runtime
-    starts its threads (they inherit the affinity the process has then). Falls back to
-    ``torch.cuda.device_count()`` only where the topology is not readable (no ROCm driver)."""
+    starts its threads (they inherit the affinity the process has then). Where the topology is
+    not readable (no ROCm driver) or a selector names devices by UUID, the count comes from torch
+    in a child process instead of a guess."""
     gpus = _kfd_gpus()
-    if gpus is None:
-        return torch.cuda.device_count()
-    sel = _visible_list()
+    sel = _visible_list() if gpus is not None else None
+    if gpus is None or sel is _UNPARSED:
+        return _child_device_count()
     if sel is None:
         return len(gpus)
     return sum(1 for i in sel if 0 <= i < len(gpus))
@@ -119,6 +145,8 @@ def gpu_pci_bdf(index: int) -> Optional[str]:
     if not gpus:
         return None
     sel = _visible_list()
+    if sel is _UNPARSED:
+        return None
     if sel is not None:
         if not 0 <= index < len(sel):
             return None

@@ -138,34 +138,26 @@ class NativeResNet(nn.Module):
         # profiles/ab_r4.md section 11)
         self.fuse_prologue = os.environ.get("PDA_FUSE_PROLOGUE", "1x1:56")
         self.fused_stem_bwd = True    # maxpool gather + ReLU mask + BN partials in one pass
-        # stem wgrad forms its dY from the BN backward in-kernel (PDA_STEM_BNA=0: apply pass)
-        self.stem_bna = os.environ.get("PDA_STEM_BNA", "1") != "0"
-        # the stem's weight gradient on the main stream (beside layer1's on the second stream)
-        self.stem_wgrad_main = os.environ.get("PDA_STEM_WGRAD_MAIN", "1") != "0"
+        # the stem wgrad forms its dY from the BN backward in-kernel (WGRAD_BNA: no apply pass;
+        # stem_bna = False keeps the apply-pass form for tests) and runs on the main stream, beside
+        # layer1's weight gradients on the second stream (profiles/ab_r4.md section 8)
+        self.stem_bna = True
         self.tail_mask = True         # tails store the ReLU bitmask the backward reads
         # consumer-side tail fold of the Bottleneck BN backward (see _block_backward)
         # ("0" off, "1" every stage, or the stages to fold, e.g. "12" = layer1 and layer2). Default
         # layer1-3: in-step A/B at the bench config (profiles/ab_r4.md) 28.26 ms off, 27.89 all
         # stages, 27.55 "12", 27.47 "123"; layer4's fold costs more than its apply pass (its G is
         # 512x512 over K = 2048 and its 7x7 dgrad has few tiles to hide the extra K). The
-        # shortcut branch of a downsampling block folds too only with PDA_BN_FOLD_DS=1 (otherwise it
-        # keeps the apply pass and its LDS-DMA weight-gradient tile)
+        # shortcut branch of a downsampling block keeps its apply pass and LDS-DMA weight-gradient
+        # tile (folding it lost at every stage set, profiles/ab_r4.md section 5)
         fold = os.environ.get("PDA_BN_FOLD", "123")
         self.bn_fold = fold != "0"
         self.bn_fold_stages = None if fold in ("0", "1") else {int(c) for c in fold if c.isdigit()}
-        self.bn_fold_ds = os.environ.get("PDA_BN_FOLD_DS", "0") != "0"
         # folded tails take conv3's weight gradient in the decomposed form diag(k1) dz^T a2 +
         # diag(k2) W3 Gram(a2) + k3 s^T: the Gram and column sums of a2 run in the forward on the
         # second stream, so the backward's GEMM is a plain dz^T a2 (no y3 read, no VALU transform)
         # (in-step A/B: 27.07 / 27.13 vs 27.22 / 27.20 ms/step, profiles/ab_r4.md section 8)
         self.bn_fold_wg = os.environ.get("PDA_BN_FOLD_WG", "1") != "0"
-        # where the main stream joins the Grams: "end" of the forward, or after every "block"
-        self.gram_join_block = os.environ.get("PDA_GRAM_JOIN", "end") == "block"
-        # the head BN (bn1, consumer conv1: 1x1, Cin = 4 Cout) folds in the concatenated form
-        # dX = [dz | y1] . [k1 o W1 ; k2 o W1] + W1^T k3 (K = 2 Cout; the Gram form would be Cout + Cin)
-        # and conv1's weight gradient forms dy1 while staging; digits = stages, "0" none
-        f1 = os.environ.get("PDA_BN_FOLD1", "0")
-        self.bn_fold1 = set() if f1 == "0" else {int(c) for c in f1 if c.isdigit()}
         self.ds_stream = True         # the shortcut conv runs on the second stream
         # weight gradients on a second HIP stream: nothing in the backward chain consumes them, so
         # the (compute-bound) wgrad GEMMs fill the CUs left idle by the (HBM-bound) BN-backward
@@ -190,9 +182,6 @@ class NativeResNet(nn.Module):
         # _ReplicaGraph side_split): the backward leaves the batched weight-gradient kernels queued
         # (no flush, no end-of-backward join) for the capture driver to record on the second stream
         self.defer_side = False
-        self._early_opt = None        # NativeSGD.arm_overlap: SGD of the final gradients mid-backward
-        self._early_bound = 0
-        self._early_at = "layer2.0"   # "layer2.0": during layer1's backward; "stem": beside the stem's
         # diagnostics (tools/layer_times.py): called on the main stream as probe(phase, name) after
         # the stem and after each residual block, forward and backward
         self.probe: Optional[Callable[[str, str], None]] = None
@@ -667,9 +656,6 @@ class NativeResNet(nn.Module):
                 rec["ys"], rec["acts"], rec["yd"] = ys, acts, yd
                 saved["blocks"].append(rec)
                 gram_pending = gram_pending or "gram" in rec
-                if gram_pending and self.gram_join_block:
-                    torch.cuda.current_stream(self.device).wait_stream(self._side)
-                    gram_pending = False
             h = out
             if self.probe is not None:
                 self.probe("fwd", b.name)
@@ -774,19 +760,6 @@ class NativeResNet(nn.Module):
             rec = sv["blocks"][bi]
             prev = (self.blocks[bi - 1], sv["blocks"][bi - 1]) if bi > 0 else None
             dx_main, shortcut_g, tail = self._block_backward(b, rec, tail, prev, acc)
-            opt = self._early_opt
-            if (opt is not None and b.name == self._early_at and red is None
-                    and not self.defer_side):
-                # every gradient in [0, bound) is final (the flat buffer is in gradient order:
-                # fc, layer4 .. layer2): their fused SGD runs on the second stream now, behind
-                # their weight gradients and after the main stream's BN gradients so far, instead
-                # of in the step's exposed tail (opt.step() then updates layer1 + stem only)
-                bound = self.block_bounds[nblk - bi]
-                self._side.wait_stream(torch.cuda.current_stream(self.device))
-                with torch.cuda.stream(self._side):
-                    opt._launch_range(0, bound)
-                self._early_bound = bound
-                self._early_opt = None
             if not self.defer_side and (self._wbatch_mode == "block" or b.ds is not None):
                 self._flush_wgrad()
             if red is not None:
@@ -824,23 +797,11 @@ class NativeResNet(nn.Module):
             K.maxpool_bwd(dx_main, arg, dA0, dout2=shortcut_g)
             K.bn_bwd(ws, y0, st0[0], st0[1], self.gamma(u), st0[2], st0[3], self.dgamma(u),
                      self.dbeta(u), dy0, g1=dA0, accumulate=acc)
-
-        opt = self._early_opt
-        if opt is not None and self._early_at == "stem" and red is None and not self.defer_side:
-            # every gradient but the stem's is final (its BN gradients were just written on this
-            # stream; layer1's weight gradients are queued ahead on the second stream): their fused
-            # SGD runs there, beside the stem's weight gradient, instead of in the step's tail
-            bound = self.block_bounds[nblk]
-            self._side.wait_stream(torch.cuda.current_stream(self.device))
-            with torch.cuda.stream(self._side):
-                opt._launch_range(0, bound)
-            self._early_bound = bound
-            self._early_opt = None
         if bna:
             def stem_wgrad(w):
                 K.conv_wgrad(dz0, x0, g0, self.stem_wgrad, w, bna=(y0, k0), wscale=self.wgrad_scale)
                 K.stem_s2d_grad(self.stem_wgrad, self.wgrad_view(u), accumulate=acc)
-            if self.stem_wgrad_main and self._side is not None and not self.defer_side:
+            if self._side is not None and not self.defer_side:
                 # the main stream is idle after the stem's BN backward while the second stream still
                 # drains layer1's weight gradients: the stem's runs beside them instead of after
                 stem_wgrad(ws)
@@ -923,19 +884,6 @@ class NativeResNet(nn.Module):
             K.fold_bgemm(self.w16(ul), gram[:C_], B)
         return B, gram[C_]
 
-    def _head_fold_ok(self, b: Block, Nb: int) -> bool:
-        """Whether block ``b``'s head BatchNorm (bn1) backward is folded into conv1's gradients
-        (PDA_BN_FOLD1, the concatenated form): Bottleneck blocks, 16-bit, per-rank statistics, a 1x1
-        stride-1 conv1 and tiles the fold kernels are built for."""
-        if (not self.bn_fold1 or self.f32 or len(b.units) != 3 or not b.name.startswith("layer")
-                or int(b.name[5]) not in self.bn_fold1):
-            return False
-        sync = getattr(self.ws, "sync_comm", None)
-        if sync is not None and sync.world_size > 1:
-            return False
-        g = b.units[0].geom(Nb)
-        return g.stride == 1 and K.bnf_ok(g, self.dtype) and K.wgrad_bna_ok(g, Nb, self.dtype)
-
     def _block_backward(self, b: Block, rec, tail, prev, acc):
         """Returns (dx_main, shortcut_grad, prev_tail) -- the last is the fused reduction of the
         previous block's tail, or None for the first block.
@@ -962,10 +910,7 @@ class NativeResNet(nn.Module):
         if b.ds is not None:
             sd = rec["sd"]
             g = b.ds.geom(Nb)
-            # the shortcut branch folds too (its conv is 1x1): dyd = k1d*dz + k2d*yd + k3d is formed by
-            # its weight gradient and its data gradient runs dz . (k1d o Wd) + x . Gd + Wd^T k3d
-            ds_fold = fold and self.bn_fold_ds and K.bnf_ok(g, self.dtype) and K.wgrad_bna_ok(g, Nb, self.dtype)
-            dyd = None if ds_fold else self._empty(*yd.shape)
+            dyd = self._empty(*yd.shape)
             K.bn_bwd_finish(ws, part, G, nq, ys[-1], sl[0], sl[1], self.gamma(ul), self.dgamma(ul),
                             self.dbeta(ul), dz, dy, y2=yd, mean2=sd[0], invstd2=sd[1],
                             gamma2=self.gamma(b.ds), dgamma2=self.dgamma(b.ds), dbeta2=self.dbeta(b.ds),
@@ -974,37 +919,22 @@ class NativeResNet(nn.Module):
             # On the second stream its dgrad overlaps the conv3/conv2 chain; an event marks it for
             # the conv1 dgrad epilogue (or the stem) that consumes it
             shortcut_g = self._empty(*x.shape)
-            kd = kt[3 * ul.cout:6 * ul.cout] if ds_fold else None
 
             def ds_dgrad():
-                if ds_fold:
-                    cin = b.ds.conv.in_channels
-                    wfd = self._empty(b.ds.cout + cin, cin)
-                    fbd = torch.empty(cin, dtype=torch.float32, device=self.device)
-                    K.bn_fold(self.w16(b.ds), kd, wfd, fbd, self.ws_w)
-                    K.conv_dgrad_bnf(dz, wfd, g, shortcut_g, x, fbd)
-                    return [wfd, fbd]
                 K.conv_dgrad(dyd, self.w16_ohwi(b.ds), g, shortcut_g)
-                return []
             if self._side is not None and self.ds_stream:
                 self._side.wait_stream(torch.cuda.current_stream(self.device))
                 with torch.cuda.stream(self._side):
-                    extra = ds_dgrad()
+                    ds_dgrad()
                 sc_ev = torch.cuda.Event()
                 sc_ev.record(self._side)
-                self._keep.extend([dz, x, kt, shortcut_g, *extra] + ([yd] if ds_fold else [dyd]))
+                self._keep.extend([dz, x, kt, shortcut_g, dyd])
             else:
                 ds_dgrad()
-            if ds_fold:
-                self._wgrad(lambda w, u=b.ds, g=g: K.conv_wgrad(dz, x, g, self.wgrad_view(u), w,
-                                                               accumulate=acc, bna=(yd, kd),
-                                                               wscale=self.wgrad_scale),
-                            dz, x, yd, kt)
-            else:
-                self._wgrad(lambda w, u=b.ds, g=g, dyd=dyd: K.conv_wgrad(dyd, x, g, self.wgrad_view(u),
-                                                                        w, accumulate=acc,
-                                                                        wscale=self.wgrad_scale),
-                            dyd, x)
+            self._wgrad(lambda w, u=b.ds, g=g, dyd=dyd: K.conv_wgrad(dyd, x, g, self.wgrad_view(u),
+                                                                    w, accumulate=acc,
+                                                                    wscale=self.wgrad_scale),
+                        dyd, x)
         else:
             K.bn_bwd_finish(ws, part, G, nq, ys[-1], sl[0], sl[1], self.gamma(ul), self.dgamma(ul),
                             self.dbeta(ul), dz, dy, accumulate=acc, k_out=kt)
@@ -1012,8 +942,6 @@ class NativeResNet(nn.Module):
         dx_main = None
         prev_tail = None
         cur = torch.cuda.current_stream(self.device)
-        head = self._head_fold_ok(b, Nb)
-        hcat = None    # (dz1, k1) of the folded head BN
         for j in range(n - 1, -1, -1):
             u = b.units[j]
             a_in = acts[j]
@@ -1024,18 +952,7 @@ class NativeResNet(nn.Module):
                 a_in = ys[j - 1]
                 pro = (sp_[2], sp_[3])
             bnf = None
-            if hcat is not None and j == 0:
-                # head fold: (dz1, k) stand for dy1 in both of conv1's gradients
-                dzc, kc = hcat
-                wf = self._empty(2 * u.cout, u.conv.in_channels)
-                fb = torch.empty(u.conv.in_channels, dtype=torch.float32, device=self.device)
-                K.bn_fold_cat(self.w16(u), kc, wf, fb)
-                bnf = (wf, fb, dzc, ys[0])
-                self._wgrad(lambda w, u=u, g=g, a=a_in, pro=pro, y1=ys[0], dzc=dzc, kc=kc:
-                            K.conv_wgrad(dzc, a, g, self.wgrad_view(u), w, accumulate=acc, pro=pro,
-                                         bna=(y1, kc), wscale=self.wgrad_scale),
-                            dzc, a_in, ys[0], kc)
-            elif fold and j == n - 1:
+            if fold and j == n - 1:
                 # tail fold: (dz, k) stand for dy3 in both of conv3's gradients
                 k3 = kt[:3 * u.cout]
                 cin = u.conv.in_channels
@@ -1060,9 +977,7 @@ class NativeResNet(nn.Module):
                                          wscale=self.wgrad_scale), dy, a_in)
 
             def dgrad(out, epi=None, u=u, g=g, dy=dy, bnf=bnf, a_in=a_in, pro=pro):
-                if bnf is not None and len(bnf) == 4:
-                    K.conv_dgrad_bnf(bnf[2], bnf[0], g, out, bnf[3], bnf[1], epi=epi, cat=True)
-                elif bnf is not None:
+                if bnf is not None:
                     K.conv_dgrad_bnf(dz, bnf[0], g, out, a_in, bnf[1], xa_pro=pro, epi=epi)
                 else:
                     K.conv_dgrad(dy, self.w16_ohwi(u), g, out, epi=epi)
@@ -1074,18 +989,10 @@ class NativeResNet(nn.Module):
                 # the dgrad's epilogue produces dz and the BN-backward partials of bn_{j-1}
                 epi, part_p, nq_p = K.bn_epilogue(ws, Gp, ys[j - 1], sp[2], sp[3])
                 dgrad(out, epi)                                      # out = dz of bn_{j-1}
-                if head and j == 1:   # bn1 folded: coefficients only, conv1 consumes (dz1, k)
-                    kc = torch.empty(3 * up.cout, dtype=torch.float32, device=self.device)
-                    K.bn_bwd_finish(ws, part_p, Gp, nq_p, ys[0], sp[0], sp[1], self.gamma(up),
-                                    self.dgamma(up), self.dbeta(up), out, None, accumulate=acc,
-                                    k_out=kc)
-                    hcat = (out, kc)
-                    dy = None
-                else:
-                    dyp = self._empty(*ys[j - 1].shape)
-                    K.bn_bwd_finish(ws, part_p, Gp, nq_p, ys[j - 1], sp[0], sp[1], self.gamma(up),
-                                    self.dgamma(up), self.dbeta(up), out, dyp, accumulate=acc)
-                    dy = dyp
+                dyp = self._empty(*ys[j - 1].shape)
+                K.bn_bwd_finish(ws, part_p, Gp, nq_p, ys[j - 1], sp[0], sp[1], self.gamma(up),
+                                self.dgamma(up), self.dbeta(up), out, dyp, accumulate=acc)
+                dy = dyp
             elif prev is not None:
                 pb, prec = prev
                 if sc_ev is not None:
@@ -1225,17 +1132,6 @@ class NativeSGD(torch.optim.Optimizer):
     def zero_grad(self, set_to_none: bool = True) -> None:
         self.model.zero_grad_flat()
 
-    def arm_overlap(self, at: str = "layer2.0") -> None:
-        """Let the next backward run the fused SGD of the gradients that are final at point ``at``
-        on the second stream (single process, eager, no loss scaling: the caller's responsibility --
-        NativeTrainer arms it only there); step() then covers the rest. ``at``: "layer2.0" (after
-        that block's backward: layers 2-4 + fc during layer1's) or "stem" (all but the stem, beside
-        the stem's weight gradient)."""
-        m = self.model
-        if m._side is not None and not m.f32:
-            m._early_opt = self
-            m._early_at = at
-
     def _launch_range(self, lo: int, hi: int, inv_scale=None, found_inf=None) -> None:
         g = self.param_groups[0]
         m = self.model
@@ -1246,16 +1142,12 @@ class NativeSGD(torch.optim.Optimizer):
     def _launch(self, inv_scale=None, found_inf=None) -> None:
         g = self.param_groups[0]
         m = self.model
-        m._early_opt = None
-        lo, m._early_bound = m._early_bound, 0
         if m._grads_zero:
             # zero_grad() and no backward since: torch 2.x's set_to_none leaves every .grad None,
             # and SGD skips parameters without a gradient -- the flat gradient still holds the
             # previous step's values (no memset), so applying it would be a stale update
             return
-        if lo:   # the backward already updated [0, lo) on the second stream
-            torch.cuda.current_stream(m.device).wait_stream(m._side)
-        self._launch_range(lo, m.numel, inv_scale, found_inf)
+        self._launch_range(0, m.numel, inv_scale, found_inf)
         m._pack_stem()
         # (an overflow-skipped first step leaves the momentum buffer unset on the device but the
         # flag set: the next step then reads the zero-initialised buffer, m*0 + d == d)
@@ -1328,11 +1220,6 @@ class NativeTrainer:
             self.scaler = LossScaler()
         self._loss = None
         self.graphed = None
-        # fused SGD of the gradients final before the end of the backward on the second stream
-        # (eager, 1 process): "1" = layers 2-4 + fc during layer1's backward, "stem" = all but the
-        # stem beside the stem's weight gradient
-        ov = os.environ.get("PDA_OVERLAP_SGD", "0")
-        self.overlap_sgd = {"0": None, "1": "layer2.0", "stem": "stem"}.get(ov, None)
         if graph:
             if world > 1:
                 raise ValueError("graph capture of the distributed step is not enabled (RCCL "
@@ -1355,8 +1242,6 @@ class NativeTrainer:
             self.scaler.step(self.opt)
             self.scaler.update()
         else:
-            if self.net is self.model and self.overlap_sgd:
-                self.opt.arm_overlap(self.overlap_sgd)
             loss.backward()
             self.opt.step()
         self.opt.zero_grad()

@@ -74,11 +74,9 @@ _SIGS = {
     "pda_conv_fwd": [C.POINTER(ConvDesc), _V, _V, _I, _V, _I, _I, _V, _V, _I, _V, _V, _I, _I, _I, _V],
     "pda_conv_dgrad": [C.POINTER(ConvDesc), _V, _V, _V, C.POINTER(BnEpi), _I, _I, _I, _V],
     "pda_conv_dgrad_bnf": [C.POINTER(ConvDesc), _V, _V, _V, C.POINTER(BnEpi), _V, _V, _V, _V, _I, _I,
-                           _I, _I, _V],
+                           _I, _V],
     "pda_bn_fold": [_V, _V, _I, _I, _V, _V, _I, _V],
     "pda_stem_fwd": [_V, _V, _V, _V, _I, _I, _I, _I, _I, _V],
-    "pda_tapconv_fwd": [_V, _V, _V, _V, _V, _V, _I, _I, _I, _I, _I, _V],
-    "pda_bn_fold_cat": [_V, _V, _I, _I, _V, _V, _I, _V],
     "pda_conv_wgrad": [C.POINTER(ConvDesc), _V, _V, _V, _I, _I, _V, _V, _I, _I, _I, _V],
     "pda_conv_wgrad_bna": [C.POINTER(ConvDesc), _V, _V, _V, _V, _V, _V, _V, _I, _I, _V, _V, _I, _I, _I,
                            _V],
@@ -122,7 +120,9 @@ def stream_cfg() -> tuple:
     (tools/gpu_ab.sh, one box): 30.02 ms (one-chunk everywhere) vs 29.41 ms (100 MiB threshold);
     threshold 200 / 100 / 50 / 30 MiB: 29.38-29.53 / 29.16 / 29.06-29.11 / 29.02-29.13 ms; grid cap
     8192 / 16384 / 32768 / 65536: 29.53 / 29.15-29.27 / 28.90-29.09 / 28.86-28.97 ms."""
-    return (-1, int(os.environ.get("PDA_STREAM_NTM", "3")), 65536, 50)
+    # memory policy bits: 1 nontemporal loads, 2 nontemporal stores (write-through sc1 stores, bit
+    # 4, measured +0.27 ms/step: profiles/ab_r4.md section 1)
+    return (-1, 3, 65536, 50)
 
 
 def load(required: bool = False) -> Optional[C.CDLL]:

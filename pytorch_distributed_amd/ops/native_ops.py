@@ -106,10 +106,12 @@ _WGRAD_TARGET = 2 * _NUM_CU   # default split-K block target of the weight gradi
 _WGRAD_SCALE = float(os.environ.get("PDA_WGRAD_SCALE", "0.7"))
 
 
-# f32 convolutions: "exact" = MFMA 16x16x4 f32 (DT_F32); "split" = f32 tensors with the products on
-# the bf16 MFMA as a three-term hi/lo split (DT_F32S, ~16 significant bits per product -- above
-# the TF32 convolutions of the reference's fp32 runs; csrc/common.h DType)
-_F32_CONV = os.environ.get("PDA_F32_CONV", os.environ.get("MX_F32_CONV", "exact"))
+# f32 convolutions: "split" (default) = f32 tensors with the products on the bf16 MFMA as a
+# three-term hi/lo split (DT_F32S, ~16 significant bits per product: every ResNet-50 conv pass at
+# or below the error of TF32 convolutions -- the reference's fp32 runs on A100 -- against float64,
+# tests/test_f32_precision_gpu.py; 1.6x the exact path); "exact" = MFMA 16x16x4 f32 (DT_F32, f32
+# rounding only; csrc/common.h DType)
+_F32_CONV = os.environ.get("PDA_F32_CONV", os.environ.get("MX_F32_CONV", "split"))
 if _F32_CONV not in ("exact", "split"):
     raise ValueError(f"MX_F32_CONV / PDA_F32_CONV must be exact|split, got {_F32_CONV!r}")
 _SPLIT_BN = 128      # widest N tile of the split kernels
@@ -186,16 +188,14 @@ def fwd_tile(g: ConvGeom, Nb: int, dtype: torch.dtype, pro: bool = False,
     """Default tile of a forward conv. The LDS-DMA tiles take 16-bit operands without the BN
     prologue (their bytes never pass through registers): tap reuse (HALO) on the 3x3 stride-1
     layers with >= 128 output channels (C10 118 -> 105 us, C16 114 -> 98, C22 127 -> 109); other
-    launches keep the register-staged choice (PDA_FWD_DMA256=1: the 128x256 DMA tile on deep-K
-    layers, :func:`pick_tile`)."""
+    launches keep the register-staged choice."""
     dma = _kdt(torch.empty(0, dtype=dtype)) in (1, 2) and not pro and g.Cin >= 64
     if dma and _DMA and _halo_geom(g) and g.Cout >= 128:
         return 2256, 128
     M = Nb * g.Ho * g.Wo
     # (the 128x256 LDS-DMA tile wins 4-9 % per kernel on the deep-K layers but loses in the step:
     # 28.65 -> 28.52 ms/step without it, profiles/ab_r3_dma.md section 12; explicit tile only)
-    return pick_tile(M, g.Cout, Kpad if Kpad is not None else g.R * g.S * g.Cin,
-                     dma=dma and os.environ.get("PDA_FWD_DMA256", "0") != "0")
+    return pick_tile(M, g.Cout, Kpad if Kpad is not None else g.R * g.S * g.Cin)
 
 
 def conv_fwd(x: torch.Tensor, w: torch.Tensor, g: ConvGeom, out: torch.Tensor,
@@ -214,10 +214,11 @@ def conv_fwd(x: torch.Tensor, w: torch.Tensor, g: ConvGeom, out: torch.Tensor,
     dense = (tile is None and bias is None and not relu and out.dtype == x.dtype
              and x.is_contiguous() and out.is_contiguous() and w.is_contiguous()
              and x.numel() == Nb * g.H * g.W * g.Cin and out.numel() == M * g.Cout)
-    if dense and pro is None and Kpad == 256 and stem_fwd_ok(g, x.dtype):
+    # (the stem kernel writes one statistics partial per output ROW, not per fwd_tile M-tile: a
+    # caller-sized ``stats`` buffer without ``bn`` keeps the generic tile's layout)
+    if dense and pro is None and Kpad == 256 and (stats is None or bn is not None) \
+            and stem_fwd_ok(g, x.dtype):
         return stem_fwd(x, w, g, out, stats, bn, before_finalize)
-    if dense and Kpad == 576 and tapconv_ok(g, x.dtype):
-        return tapconv_fwd(x, w, g, out, stats, bn, before_finalize, pro)
     bm, bn_ = tile or fwd_tile(g, Nb, x.dtype, pro is not None, Kpad)
     d = g.desc(Nb)
     # direct (unstaged) f32 store + bias: the fc head (16-bit features -> f32 logits, or any conv
@@ -241,7 +242,9 @@ def conv_fwd(x: torch.Tensor, w: torch.Tensor, g: ConvGeom, out: torch.Tensor,
 
 
 _STEM_FWD = os.environ.get("PDA_STEM_FWD", "1") != "0"
-_STEM_GRID = int(os.environ.get("PDA_STEM_GRID", "0"))   # persistent blocks (0: 1024)
+# persistent blocks of the stem kernel: 256 / 512 / 1024 / 2048 measured 305 / 267 / 258 / 278 us
+# (profiles/ab_r4.md section 15); 0 = the kernel's default, 1024
+_STEM_GRID = 0
 
 
 def stem_fwd_ok(g: ConvGeom, dtype: torch.dtype) -> bool:
@@ -266,6 +269,9 @@ def stem_fwd(x: torch.Tensor, w: torch.Tensor, g: ConvGeom, out: torch.Tensor,
     T = M // rows
     if bn is not None:
         stats = bn.ws.get("fwd_stats", T * 3 * g.Cout)
+    if stats is not None and stats.numel() < T * 3 * g.Cout:
+        raise ValueError(f"stem_fwd: stats needs {T * 3 * g.Cout} floats (one partial per output "
+                         f"row, stem_stats_rows), got {stats.numel()}")
     check(ext.lib().pda_stem_fwd(ptr(x), ptr(w), ptr(out), ptr(stats), Nb, g.H, g.W, _kdt(x),
                                  _STEM_GRID, stream(x.device)), "stem_fwd")
     if before_finalize is not None:
@@ -278,57 +284,6 @@ def stem_fwd(x: torch.Tensor, w: torch.Tensor, g: ConvGeom, out: torch.Tensor,
 def stem_stats_rows(g: ConvGeom) -> int:
     """Rows of M per statistics tile of :func:`stem_fwd` (one output row)."""
     return g.Wo
-
-
-# off by default: 170 vs 234 us isolated, but 0.1 ms/step slower in the step with one persistent
-# block per CU beside the second stream (profiles/ab_r4.md section 16)
-_TAPCONV = os.environ.get("PDA_TAPCONV", "0") != "0"
-_TAPCONV_GRID = int(os.environ.get("PDA_TAPCONV_GRID", "0"))   # persistent blocks (0: 256)
-
-
-def tapconv_ok(g: ConvGeom, dtype: torch.dtype) -> bool:
-    """Whether conv_fwd routes this conv to the tap-reuse kernel (``PDA_TAPCONV`` and
-    :func:`tapconv_supported`)."""
-    return _TAPCONV and tapconv_supported(g, dtype)
-
-
-def tapconv_supported(g: ConvGeom, dtype: torch.dtype) -> bool:
-    """Whether the tap-reuse kernel (csrc/tapconv.hip; the layer1 conv2) handles the conv: 3x3 /
-    stride 1 / pad 1, 64 -> 64 channels, 16-bit, H % 8 == 0, W % 8 == 0, 8 <= W <= 64."""
-    return (dtype in (torch.bfloat16, torch.float16) and g.R == 3 and g.S == 3
-            and g.Cin == 64 and g.Cout == 64 and g.stride == 1 and g.pad == 1 and g.Ho == g.H
-            and g.Wo == g.W and g.H % 8 == 0 and g.W % 8 == 0 and 8 <= g.W <= 64
-            and getattr(ext.lib(), "pda_tapconv_fwd", None) is not None)
-
-
-def tapconv_fwd(x: torch.Tensor, w: torch.Tensor, g: ConvGeom, out: torch.Tensor,
-                stats: Optional[torch.Tensor] = None, bn: Optional[BnStats] = None,
-                before_finalize=None,
-                pro: Optional[Tuple[torch.Tensor, torch.Tensor]] = None) -> torch.Tensor:
-    """3x3/1/1 64 -> 64 conv on csrc/tapconv.hip: the input slab of an 8-row tile staged once in
-    LDS (``pro`` = (scale, shift): BN+ReLU applied once while staging), the MFMA pixel operand read
-    from it for all 9 taps, weights resident in LDS. Statistics: shifted partials per output-row
-    pair (``bm = tapconv_stats_rows(g)`` for :func:`stats_totals`)."""
-    Nb = x.shape[0]
-    M = Nb * g.Ho * g.Wo
-    rows = tapconv_stats_rows(g)
-    T = M // rows
-    if bn is not None:
-        stats = bn.ws.get("fwd_stats", T * 3 * g.Cout)
-    check(ext.lib().pda_tapconv_fwd(ptr(x), ptr(w), ptr(out), ptr(stats),
-                                    ptr(pro[0] if pro else None), ptr(pro[1] if pro else None),
-                                    Nb, g.H, g.W, _kdt(x), _TAPCONV_GRID, stream(x.device)),
-          "tapconv_fwd")
-    if before_finalize is not None:
-        before_finalize()
-    if bn is not None:
-        bn_finalize_partials(stats, T, g.Cout, rows, M, bn)
-    return out
-
-
-def tapconv_stats_rows(g: ConvGeom) -> int:
-    """Rows of M per statistics tile of :func:`tapconv_fwd` (two output rows)."""
-    return 2 * g.Wo
 
 
 def stats_totals(stats: torch.Tensor, M: int, C_: int, bm: int) -> torch.Tensor:
@@ -451,17 +406,6 @@ def bn_fold(w: torch.Tensor, k: torch.Tensor, wf: torch.Tensor, bias: torch.Tens
                                 stream(w.device)), "bn_fold")
 
 
-def bn_fold_cat(w: torch.Tensor, k: torch.Tensor, wf: torch.Tensor, bias: torch.Tensor) -> None:
-    """Operands of the concatenated form of :func:`conv_dgrad_bnf` (``xa_c`` = Cout) for a 1x1 conv:
-    ``wf`` [2 Cout, Cin] = [k1 o W ; k2 o W], ``bias`` [Cin] = W^T k3 (csrc/conv_gemm.hip
-    bn_fold_cat_kernel)."""
-    Cout, Cin = w.shape[0], w.shape[-1]
-    if wf.shape[0] != 2 * Cout or wf.shape[-1] != Cin or wf.dtype != w.dtype or k.numel() < 3 * Cout:
-        raise ValueError("bn_fold_cat: wf [2 Cout, Cin] of the weights' dtype, k 3 x Cout")
-    check(ext.lib().pda_bn_fold_cat(ptr(w), ptr(k), Cout, Cin, ptr(wf), ptr(bias), dt_of(w),
-                                    stream(w.device)), "bn_fold_cat")
-
-
 def bnf_ok(g: ConvGeom, dtype: torch.dtype) -> bool:
     """Whether the consumer-side BN-backward fold (:func:`conv_dgrad_bnf`) serves this conv: a 1x1
     conv without padding, 16-bit operands, channel counts in whole 64-column panels."""
@@ -473,14 +417,12 @@ def bnf_ok(g: ConvGeom, dtype: torch.dtype) -> bool:
 def conv_dgrad_bnf(dz: torch.Tensor, wf: torch.Tensor, g: ConvGeom, dx: torch.Tensor,
                    xa: torch.Tensor, bias: torch.Tensor, xa_pro=None,
                    epi: Optional[ext.BnEpi] = None,
-                   tile: Optional[Tuple[int, int]] = None, cat: bool = False) -> torch.Tensor:
+                   tile: Optional[Tuple[int, int]] = None) -> torch.Tensor:
     """dX of a 1x1 conv whose dY = k1*dz + k2*y + k3 is never materialised (y = the conv's forward
     output): dX = dz . (k1 o W) + xa . G + b with (wf, bias) from :func:`bn_fold` and ``xa`` the
     conv's forward input (``xa_pro`` = (scale, shift): xa is PRE-BatchNorm and the activation
     relu(xa*scale+shift) is recomputed, as the forward's prologue did). ``epi``: the same fused
-    BN-backward epilogue as :func:`conv_dgrad`.
-    ``cat``: the concatenated form dX = [dz | y] . [k1 o W ; k2 o W] + b (stride 1) with ``xa`` = y
-    and (wf, bias) from :func:`bn_fold_cat` -- K = 2 Cout instead of Cout + Cin."""
+    BN-backward epilogue as :func:`conv_dgrad`."""
     Nb = dz.shape[0]
     kdt = _kdt(dz)
     bm, bn = tile or dgrad_tile(g, Nb)
@@ -492,7 +434,7 @@ def conv_dgrad_bnf(dz: torch.Tensor, wf: torch.Tensor, g: ConvGeom, dx: torch.Te
                                       C.byref(epi) if epi is not None else None, ptr(xa),
                                       ptr(xa_pro[0] if xa_pro else None),
                                       ptr(xa_pro[1] if xa_pro else None), ptr(bias),
-                                      g.Cout if cat else 0, kdt, kbm, kbn, stream(dz.device))
+                                      kdt, kbm, kbn, stream(dz.device))
     check(rc, "conv_dgrad_bnf")
     return dx
 
@@ -897,9 +839,11 @@ def bn_bwd_finish(ws: "Workspace", part, G: int, nq: int, y, mean, invstd, gamma
 
 # channels per block group of the statistics kernel (csrc/bn.hip stats_cg): a quad of channels gets
 # 1024 / cg lanes, so narrower groups shorten both levels' serial load chains
-_BN_CG = int(os.environ.get("PDA_BN_CG", "256"))
-_BN_SK = float(os.environ.get("PDA_BN_SK", "0.75"))
-_BN_SMIN = int(os.environ.get("PDA_BN_SMIN", "8"))
+# statistics-kernel geometry, measured (profiles/ab_r4.md sections 4, 8, 13): 256-channel block
+# groups (64: +0.03 ms/step), S = sqrt(0.75 T) slabs with at least 8 (1 / 4: within noise)
+_BN_CG = 256
+_BN_SK = 0.75
+_BN_SMIN = 8
 
 
 def _stats_cg(C_: int) -> int:

@@ -303,7 +303,10 @@ class DataParallel(nn.Module):
             self._replay_overlapped(jobs, streams)
             if len(jobs[0][0].graphs) > 1 and not getattr(self, "_segments_verified", False):
                 self._verify_segmented_reduce(optimizer)
-                return self._step_loss(xs, B)
+                loss = self._step_loss(xs, B)   # this step's graphs hold its losses
+                if getattr(self, "_force_single_segment", False):
+                    self._graphs = None         # re-captured without split points next step
+                return loss
         else:
             for rg, x, y in jobs:
                 rg.run(x, y, graph)
@@ -342,8 +345,7 @@ class DataParallel(nn.Module):
         warnings.warn("DataParallel: the per-stage gradient all-reduce left replicas with different "
                       "gradients; falling back to one all-reduce after backward (PDA_DP_SEGMENTS=0) "
                       "and re-syncing every replica from replica 0", RuntimeWarning)
-        self._force_single_segment = True
-        self._graphs = None      # re-captured without split points at the next step
+        self._force_single_segment = True   # (train_step_chunks drops the graphs after the loss)
         m0 = self.module
         opt0 = optimizer.opts[0] if hasattr(optimizer, "opts") else None
         for i, r in enumerate(self.replicas):

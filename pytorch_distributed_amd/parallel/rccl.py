@@ -118,8 +118,7 @@ class RcclCommunicator(Communicator):
         # slower at the image's GPU_MAX_HW_QUEUES=4 (28.8 -> 43.3 ms/step, ResNet-50 bs 400; fine
         # at 3, 6 or 8 queues, 32.0 at 5): the HIP runtime's queue mapping for a second priority
         # level, not the collectives, cost it (tools/ddp_sync_diag.py, profiles/ddp_overhead_r3.md).
-        # PDA_COMM_PRIO=-1 restores the high-priority stream for A/B runs.
-        self.stream = torch.cuda.Stream(self.device, priority=int(os.environ.get("PDA_COMM_PRIO", "0")))
+        self.stream = torch.cuda.Stream(self.device, priority=0)
         self._watchdog_error = None
         self._watchdog = None
         self._watchdog_stop = None

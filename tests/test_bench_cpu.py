@@ -132,6 +132,41 @@ def test_numa_binding_precedes_any_hip_call(monkeypatch, tmp_path):
     assert launch.gpu_pci_bdf(0) == "0000:03:00.0"     # visible 0 = physical GPU 1 (node 2)
 
 
+def test_visible_gpu_count_render_nodes_and_selectors(monkeypatch, tmp_path):
+    """The launcher's GPU count (no HIP call): a KFD node counts only when its render node is
+    accessible (sysfs lists every GPU of the host inside a container given only some); HIP applies
+    HIP_VISIBLE_DEVICES, or CUDA_VISIBLE_DEVICES only without it; a UUID selector is counted by torch
+    in a child process, never taken as 'no filter'."""
+    from pytorch_distributed_amd import launch
+    dri = tmp_path / "dri"
+    dri.mkdir()
+    for i, simd in enumerate((0, 304, 304, 304, 304)):
+        d = tmp_path / "nodes" / str(i)
+        d.mkdir(parents=True)
+        minor = 127 + i if simd else 0
+        (d / "properties").write_text(f"simd_count {simd}\ndomain 0\nlocation_id {256 * (i + 1)}\n"
+                                      f"drm_render_minor {minor}\n")
+    for minor in (128, 130):          # the container may open GPU nodes 1 and 3 only
+        (dri / f"renderD{minor}").write_text("")
+    monkeypatch.setattr(launch, "_KFD_ROOT", str(tmp_path / "nodes"))
+    monkeypatch.setattr(launch, "_DRI_ROOT", str(dri))
+    for var in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        monkeypatch.delenv(var, raising=False)
+    assert launch.visible_gpu_count() == 2
+    assert launch.gpu_pci_bdf(1) == "0000:04:00.0"    # the second accessible GPU = KFD node 3
+    monkeypatch.setenv("CUDA_VISIBLE_DEVICES", "1")
+    assert launch.visible_gpu_count() == 1
+    monkeypatch.setenv("HIP_VISIBLE_DEVICES", "0,1")  # HIP reads this one, not CUDA_VISIBLE_DEVICES
+    assert launch.visible_gpu_count() == 2
+    monkeypatch.setenv("ROCR_VISIBLE_DEVICES", "1")   # applied first: one device left, index 0
+    assert launch.visible_gpu_count() == 1
+    monkeypatch.delenv("ROCR_VISIBLE_DEVICES")
+    monkeypatch.setenv("HIP_VISIBLE_DEVICES", "GPU-0123456789abcdef")
+    monkeypatch.setattr(launch, "_child_device_count", lambda: 7)
+    assert launch.visible_gpu_count() == 7
+    assert launch.gpu_pci_bdf(0) is None
+
+
 def test_bench_cpu_diverged_rank_fails(tmp_path):
     r = _run(2, {"PDA_BENCH_PERTURB_RANK": "1"}, tmp=tmp_path)
     assert r.returncode != 0

@@ -48,9 +48,9 @@ def test_bench_torchrun_two_ranks(tmp_path):
     assert rec["comm"] == "ProcessGroupCommunicator" and rec["rccl_world"] is None   # gloo here
     pr = rec["xgmi_probe"]                    # device tensors through the gradient communicator
     assert len(pr["ms"]) == len(pr["bytes"]) and all(v > 0 for v in pr["ms"])
-    # the like-for-like exact-fp32 pass, and the split-f32 (>= TF32 precision) pass
+    # the default fp32 pass (split convs, >= TF32 precision) and the exact-f32 MFMA pass
     assert rec["fp32_images_per_sec"] > 0 and rec["fp32_engine"] == "native"
-    assert rec["fp32_split_images_per_sec"] > 0
+    assert rec["fp32_conv"].startswith("split") and rec["fp32_exact_images_per_sec"] > 0
     # the other GPU configurations of BASELINE.json, each labelled with its config/dtype:
     # fp16 AMP-DDP (resnet_ddp_apex.py) on both ranks, DataParallel (resnet_dp.py) by rank 0
     # over the visible devices (one here) while rank 1 waits on the store

@@ -255,15 +255,12 @@ def test_lds_dma_tile_codes_and_fallback():
 
 
 def test_dedicated_conv_kernel_routing(monkeypatch):
-    """Which convs conv_fwd hands to the dedicated kernels: the space-to-depth stem geometry to
-    csrc/stem.hip (16-bit, H % 4, W % 16, W <= 128), the 3x3 64 -> 64 stride-1 conv to
-    csrc/tapconv.hip (opt-in PDA_TAPCONV; H % 8, W % 8, W <= 64); statistics tiles of one / two
-    output rows."""
+    """Which convs conv_fwd hands to the dedicated stem kernel: the space-to-depth stem geometry to
+    csrc/stem.hip (16-bit, H % 4, W % 16, W <= 128); statistics tiles of one output row."""
     from pytorch_distributed_amd.ops import native_ops as K
 
     class Lib:
         pda_stem_fwd = object()
-        pda_tapconv_fwd = object()
     monkeypatch.setattr(K.ext, "lib", lambda: Lib)
     g = K.stem_s2d_geom(400, 224)
     assert K.stem_fwd_ok(g, torch.bfloat16) and K.stem_fwd_ok(g, torch.float16)
@@ -271,15 +268,6 @@ def test_dedicated_conv_kernel_routing(monkeypatch):
     assert not K.stem_fwd_ok(K.stem_s2d_geom(2, 40), torch.bfloat16)    # W = 20: not % 16
     assert not K.stem_fwd_ok(K.stem_s2d_geom(2, 288), torch.bfloat16)   # W = 144 > 128
     assert K.stem_stats_rows(g) == 112
-    c2 = K.ConvGeom(400, 56, 56, 64, 64, 3, 3, 1, 1)
-    assert K.tapconv_supported(c2, torch.bfloat16) and K.tapconv_stats_rows(c2) == 112
-    assert not K.tapconv_supported(K.ConvGeom(400, 28, 28, 128, 128, 3, 3, 1, 1), torch.bfloat16)
-    assert not K.tapconv_supported(K.ConvGeom(400, 56, 56, 64, 64, 3, 3, 2, 1), torch.bfloat16)
-    assert not K.tapconv_supported(K.ConvGeom(4, 28, 28, 64, 64, 3, 3, 1, 1), torch.bfloat16)  # H % 8
-    monkeypatch.setattr(K, "_TAPCONV", False)
-    assert not K.tapconv_ok(c2, torch.bfloat16)
-    monkeypatch.setattr(K, "_TAPCONV", True)
-    assert K.tapconv_ok(c2, torch.bfloat16)
 
 
 def test_dataparallel_segment_bounds_and_step_busy(monkeypatch):

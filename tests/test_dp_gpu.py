@@ -105,6 +105,46 @@ def test_native_dataparallel_graph_step_matches_eager(segments, side, monkeypatc
     assert ex is not None and 0.0 <= ex < 1000.0, ex
 
 
+def test_native_dataparallel_segment_mismatch_falls_back(monkeypatch):
+    """The first segmented replay verifies that every replica holds the same summed gradient; a
+    mismatch (forced here: the checksum reports a different value for one replica) must not break
+    the step -- it returns this step's loss, warns, re-syncs the replicas from replica 0, and the
+    next step re-captures ONE graph per replica (one all-reduce after backward) and trains on."""
+    monkeypatch.setenv("PDA_DP_SEGMENTS", "stage")
+    monkeypatch.setenv("PDA_DP_SIDE", "0")
+    from pytorch_distributed_amd import bench_step
+    from pytorch_distributed_amd.data import SyntheticImageNet
+    from pytorch_distributed_amd.models import build_model
+    from pytorch_distributed_amd.models.native import NativeResNet
+    from pytorch_distributed_amd.parallel import DataParallel
+    torch.manual_seed(0)
+    dp = DataParallel(NativeResNet(build_model("resnet18"), device=DEV, image_size=64),
+                      device_ids=[0, 0])
+    opt = dp.make_optimizer(lr=0.05, momentum=0.9, weight_decay=1e-4)
+    gen = dp.module.input_generator(SyntheticImageNet("train", image_size=64))
+    real = bench_step.tensor_checksum
+    calls = []
+
+    def skewed(ts):
+        calls.append(1)
+        c = real(ts)
+        return c + 1 if len(calls) == 2 else c      # the second replica "differs"
+    monkeypatch.setattr(bench_step, "tensor_checksum", skewed)
+    x, y = gen(torch.arange(16))
+    with pytest.warns(RuntimeWarning, match="falling back"):
+        l0 = dp.train_step(x, y, opt)
+    torch.cuda.synchronize()
+    assert torch.isfinite(l0).item()
+    assert dp._graphs is None and dp._force_single_segment
+    assert torch.equal(dp.module.flat_params, dp.replicas[0].flat_params)
+    x, y = gen(torch.arange(16) + 16)
+    l1 = dp.train_step(x, y, opt)
+    torch.cuda.synchronize()
+    assert torch.isfinite(l1).item()
+    assert len(dp._graphs[0].graphs) == 1 and dp._graphs[0].splits == []
+    assert torch.equal(dp.module.flat_params, dp.replicas[0].flat_params)
+
+
 def test_native_dataparallel_resume_reloads_every_replica():
     """Resuming a DataParallel run (trainer.load_model_state, used by run()) must put the
     checkpoint weights into EVERY replica, not only replica 0."""

@@ -928,76 +928,6 @@ def test_conv_dgrad_bnf_stride2_shortcut(geo):
     assert e_bnf < 2 * e_ref + 5e-3, (e_bnf, e_ref)
 
 
-@pytest.mark.parametrize("Cout,Cin", [(64, 256), (128, 512), (512, 2048)])
-def test_bn_fold_cat_operands(Cout, Cin):
-    """bn_fold_cat_kernel: Wf = [k1 o W ; k2 o W] and b = W^T k3 against fp32 torch."""
-    K = _k()
-    dtype = torch.bfloat16
-    torch.manual_seed(Cout)
-    w = (torch.randn(Cout, Cin, device=DEV) * 0.05).to(dtype)
-    k = torch.randn(3 * Cout, device=DEV)
-    wf = torch.empty(2 * Cout, Cin, device=DEV, dtype=dtype)
-    b = torch.empty(Cin, device=DEV)
-    K.bn_fold_cat(w, k, wf, b)
-    torch.cuda.synchronize()
-    wd = w.double()
-    k1, k2, k3 = k[:Cout].double(), k[Cout:2 * Cout].double(), k[2 * Cout:].double()
-    assert rel_err(wf[:Cout], wd * k1[:, None]) < 5e-3
-    assert rel_err(wf[Cout:], wd * k2[:, None]) < 5e-3
-    assert rel_err(b, wd.t() @ k3) < 1e-5
-
-
-@pytest.mark.parametrize("geo", [(2, 8, 256, 64), (3, 7, 512, 128), (1, 7, 2048, 512)])
-def test_conv_dgrad_bnf_concat_matches_applied_dgrad(geo):
-    """The concatenated fold of a head BN (conv1: 1x1, Cin = 4 Cout): dX = [dz | y1] . [k1 o W ;
-    k2 o W] + W^T k3 with y1 = conv1(x) read at the dX pixel, with the fused BN-backward epilogue of
-    the preceding tail -- against apply-then-plain-dgrad and the fp32 math; ragged rows (H = 7)."""
-    K = _k()
-    dtype = torch.bfloat16
-    Nb, H, Cin, Cout = geo
-    torch.manual_seed(Cin)
-    g = K.ConvGeom(Nb, H, H, Cin, Cout, 1, 1, 1, 0)
-    w = (torch.randn(Cout, 1, 1, Cin, device=DEV) * 0.05).to(dtype)
-    x = torch.relu(torch.randn(Nb, H, H, Cin, device=DEV)).to(dtype)
-    y1 = torch.empty(Nb, H, H, Cout, device=DEV, dtype=dtype)
-    K.conv_fwd(x, w.view(Cout, Cin), g, y1)
-    dz = torch.randn(Nb, H, H, Cout, device=DEV).to(dtype)
-    k = torch.cat([torch.rand(Cout, device=DEV) + 0.5, torch.randn(Cout, device=DEV) * 0.3,
-                   torch.randn(Cout, device=DEV) * 0.2])
-    dy1 = (k[:Cout] * dz.float() + k[Cout:2 * Cout] * y1.float() + k[2 * Cout:]).to(dtype)
-    ws = K.Workspace(DEV)
-    yp = torch.randn(Nb, H, H, Cin, device=DEV).to(dtype)     # the previous tail's pre-BN output
-    scp, shp = torch.rand(Cin, device=DEV) + 0.5, torch.randn(Cin, device=DEV) * 0.1
-    mean, inv = torch.randn(Cin, device=DEV) * 0.1, torch.rand(Cin, device=DEV) + 0.5
-    gamma = torch.rand(Cin, device=DEV) + 0.5
-    res = {}
-    for name in ("ref", "cat"):
-        G = K.dgrad_slabs(g, Nb, dtype=dtype)
-        epi, part, nq = K.bn_epilogue(ws, G, yp, scp, shp)
-        dzp = torch.empty(Nb, H, H, Cin, device=DEV, dtype=dtype)
-        if name == "ref":
-            K.conv_dgrad(dy1, w, g, dzp, epi=epi)
-        else:
-            wf = torch.empty(2 * Cout, Cin, device=DEV, dtype=dtype)
-            b = torch.empty(Cin, device=DEV)
-            K.bn_fold_cat(w.view(Cout, Cin), k, wf, b)
-            K.conv_dgrad_bnf(dz, wf, g, dzp, y1, b, epi=epi, cat=True)
-        dg, db = torch.zeros(Cin, device=DEV), torch.zeros(Cin, device=DEV)
-        dyp = torch.empty_like(dzp)
-        K.bn_bwd_finish(ws, part, G, nq, yp, mean, inv, gamma, dg, db, dzp, dyp)
-        torch.cuda.synchronize()
-        res[name] = (dzp.float(), dg.clone(), db.clone())
-    dy1f = k[:Cout] * dz.float() + k[Cout:2 * Cout] * y1.float() + k[2 * Cout:]
-    da_ref = dy1f.view(-1, Cout) @ w.view(Cout, Cin).float()
-    mask = (yp.float() * scp + shp > 0).view(-1, Cin)
-    ref = (da_ref * mask).view(Nb, H, H, Cin)
-    e_cat, e_ref = rel_err(res["cat"][0], ref), rel_err(res["ref"][0], ref)
-    print(f"dX vs fp32: concat fold {e_cat:.2e}, apply+dgrad {e_ref:.2e}")
-    assert e_cat < 2 * e_ref + 5e-3, (e_cat, e_ref)
-    for a, b in zip(res["cat"][1:], res["ref"][1:]):
-        assert rel_err(a, b) < 1.5e-2
-
-
 @pytest.mark.parametrize("Cout,Cin,H", [(64, 256, 14), (128, 512, 12), (256, 1024, 7), (512, 2048, 7)])
 def test_conv_wgrad_bna_conv1_tiles(Cout, Cin, H):
     """WGRAD_BNA on the Bottleneck conv1 shapes of the head fold (M = Cout small, N = Cin = 4 Cout):

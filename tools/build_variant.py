@@ -2,9 +2,9 @@
 
     python tools/build_variant.py NAME REF|DIR [file ...]   (files default to csrc/conv_gemm.hip)
 
-Writes pytorch_distributed_amd/_lib/variants/libpda_kernels_NAME.so: the listed sources are taken
+Writes pytorch_distributed_amd/_lib/ab/libpda_kernels_NAME.so: the listed sources are taken
 from git REF, the rest from the working tree. Select it at run time with
-PDA_KERNEL_LIB=variants/libpda_kernels_NAME.so, so that two variants can be timed back to back on
+PDA_KERNEL_LIB=ab/libpda_kernels_NAME.so, so that two variants can be timed back to back on
 ONE device in one call (cdna_hip_programming.md §5.4 rule 24)."""
 import os
 import subprocess
@@ -19,7 +19,7 @@ from pytorch_distributed_amd import _build  # noqa: E402
 def main():
     name, ref = sys.argv[1], sys.argv[2]
     files = sys.argv[3:] or ["conv_gemm.hip"]
-    out = _build.OUT / "variants"
+    out = _build.OUT / "ab"
     out.mkdir(parents=True, exist_ok=True)
     with tempfile.TemporaryDirectory() as td:
         td = Path(td)

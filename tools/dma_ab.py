@@ -1,7 +1,7 @@
 """A/B of conv kernel variants in ONE process (cdna_hip_programming.md §5.4 rule 24).
 
 Build (CPU):  python tools/dma_ab.py build NAME [-DFLAG=V ...] [--full]
-    -> pytorch_distributed_amd/_lib/variants/libconv_NAME.so (conv_gemm.hip only; without --full
+    -> pytorch_distributed_amd/_lib/ab/libconv_NAME.so (conv_gemm.hip only; without --full
        only the LDS-DMA instantiations: -DCONV_DMA_ONLY, a ~10 s build)
 Run (GPU):    python tools/dma_ab.py run NAME[,NAME...] SHAPE:PASS:BM:BN [...] [--rounds R] [--reps N]
     times every (case, variant) interleaved over R rounds; prints the median and min (us, TF/s).
@@ -19,7 +19,7 @@ sys.path.insert(0, str(ROOT))
 
 def build(name, flags, full):
     from pytorch_distributed_amd import _build
-    out = _build.OUT / "variants"
+    out = _build.OUT / "ab"
     out.mkdir(parents=True, exist_ok=True)
     obj = out / f"conv_{name}.o"
     extra = list(flags) + ([] if full else ["-DCONV_DMA_ONLY"])
@@ -39,7 +39,7 @@ def run(names, cases, rounds, reps):
     for n in names:
         ext._LIB = None
         ext.LIBPATH = (ext.LIBPATH.parent.parent / "_lib" / "libpda_kernels.so" if n == "main" else
-                       ROOT / "pytorch_distributed_amd" / "_lib" / "variants" / f"libconv_{n}.so")
+                       ROOT / "pytorch_distributed_amd" / "_lib" / "ab" / f"libconv_{n}.so")
         libs[n] = ext.load(required=True)
     dev = torch.device("cuda", 0)
     B, dt = 400, torch.bfloat16

@@ -31,8 +31,6 @@ def main():
     for _ in range(reps):
         if which == "stem":
             K.stem_fwd(x, w, g, y, stats)
-        elif which == "tap":
-            K.tapconv_fwd(x, w, g, y, stats, pro=pro)
         else:
             K.conv_fwd(x, w, g, y, stats=stats, tile=(-128, 64), pro=pro)
     torch.cuda.synchronize()
