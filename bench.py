@@ -409,7 +409,7 @@ def _dp_pass(ctx: Ctx, args, dtype) -> dict:
     the other ranks wait on the TCP store -- a host-side wait (an RCCL barrier would occupy their
     GPUs), and a failure or hang of the pass costs its keys, never the headline record."""
     import subprocess
-    n = min(ctx.world if ctx.multi else 1, torch.cuda.device_count())
+    n = min(ctx.world if ctx.multi else 1, torch.cuda.device_count()) if ctx.cuda else 1
     store = None
     if ctx.multi:
         import torch.distributed as dist
@@ -425,7 +425,8 @@ def _dp_pass(ctx: Ctx, args, dtype) -> dict:
             cmd = [sys.executable, os.path.abspath(__file__), "--dp", "--gpus", str(n),
                    "--steps", str(args.dp_steps), "--warmup", "3", "--batch", str(args.batch),
                    "--arch", args.arch, "--image-size", str(args.image_size), "--dtype", args.dtype,
-                   "--fp32-steps", "0", "--amp-steps", "0", "--dp-steps", "0"]
+                   "--fp32-steps", "0", "--amp-steps", "0", "--dp-steps", "0",
+                   "--device", "cuda" if ctx.cuda else "cpu"]
             r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=limit)
             lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
             if r.returncode != 0 or not lines:
@@ -481,7 +482,8 @@ def main():
         if ctx.world > 1:
             raise SystemExit("--dp is one process driving --gpus devices; do not launch it with torchrun")
         from pytorch_distributed_amd.bench_step import make_dp_trainer
-        tr = make_dp_trainer(args.arch, args.batch, dtype, args.gpus, args.image_size)
+        tr = make_dp_trainer(args.arch, args.batch, dtype, args.gpus, args.image_size,
+                             device=args.device)
         world = args.gpus            # images/sec over all devices of the process
     else:
         tr = make_trainer(args.arch, args.batch, dtype, ctx.device, engine=args.engine,
@@ -491,7 +493,7 @@ def main():
     for i in range(args.warmup):
         tr.step(i)
     ctx.sync()
-    util_devs = list(range(args.gpus)) if args.dp else ([ctx.device.index] if ctx.cuda else [])
+    util_devs = (list(range(args.gpus)) if args.dp else [ctx.device.index]) if ctx.cuda else []
     with BusySampler(util_devs) as busy:
         elapsed = _timed(ctx, tr, args.warmup, args.steps)   # barrier + sync on both sides, MAX
     loss = tr.last_loss()
@@ -553,7 +555,7 @@ def main():
             extra.update(_fp32_pass(ctx, args, "exact"))
         if args.amp_steps > 0 and args.dtype != "fp16":
             extra.update(_guarded(ctx, "amp_fp16", _amp_pass, ctx, args))
-        if args.dp_steps > 0 and ctx.cuda:
+        if args.dp_steps > 0:   # (on the CPU: the launch / store hand-off rehearsal)
             extra.update(_guarded(ctx, "dp", _dp_pass, ctx, args, dtype))
     if ctx.rank == 0:
         rec = {

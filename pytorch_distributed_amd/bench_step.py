@@ -121,7 +121,25 @@ class _DPTrainer:
         return sums[0]
 
 
-def make_dp_trainer(arch: str, batch: int, dtype: torch.dtype, ngpus: int, image_size: int = 224):
+class _DPTrainerCPU(_TorchTrainer):
+    """``bench.py --dp --device cpu``: the rehearsal of the DataParallel pass's launch and record
+    contract without a GPU -- the framework's DataParallel around the torch-engine model on the CPU
+    (no replicas), one autograd step per call."""
+
+    engine = "torch-dp-cpu"
+
+    def __init__(self, arch, batch, dtype, image_size):
+        super().__init__(arch, batch, dtype, torch.device("cpu"), 1, 0, 32.0, image_size)
+        from .parallel.dp import DataParallel
+        self.dp = DataParallel(self.model)
+        self.net = self.dp
+        self.graphed = False
+
+
+def make_dp_trainer(arch: str, batch: int, dtype: torch.dtype, ngpus: int, image_size: int = 224,
+                    device: str = "cuda"):
+    if device == "cpu":
+        return _DPTrainerCPU(arch, batch, dtype, image_size)
     return _DPTrainer(arch, batch, dtype, list(range(ngpus)), image_size)
 
 

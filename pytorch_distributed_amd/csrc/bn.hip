@@ -353,12 +353,8 @@ __global__ __launch_bounds__(NT) void bn_apply_kernel(
     uint32_t bits = 0;   // ReLU mask of the output (bit e = element e > 0), for the backward
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
-      f32x2 v = unpack2<DT>((uint32_t)yv[k]) * a[k] + b[k];
-      if (mode) {
-        f32x2 w = unpack2<DT>((uint32_t)rv[k]);
-        if (mode == 2) w = w * a2[k] + b2[k];
-        v += w;
-      }
+      f32x2 v = tail_pre2(unpack2<DT>((uint32_t)yv[k]), a[k], b[k], unpack2<DT>((uint32_t)rv[k]),
+                          a2[k], b2[k], mode);
       if (relu) v = f32x2{fmaxf(v.x, 0.f), fmaxf(v.y, 0.f)};
       o[k] = (int)pack2<DT>(v);
       bits |= (v.x > 0.f ? 1u : 0u) << (2 * k);
@@ -1008,12 +1004,8 @@ __global__ __launch_bounds__(NT) void bn_apply_u_kernel(
     uint32_t bits = 0;
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
-      f32x2 v = unpack2<DT>((uint32_t)yv[k]) * a[k] + b[k];
-      if (mode) {
-        f32x2 w = unpack2<DT>((uint32_t)rv[k]);
-        if (mode == 2) w = w * a2[k] + b2[k];
-        v += w;
-      }
+      f32x2 v = tail_pre2(unpack2<DT>((uint32_t)yv[k]), a[k], b[k], unpack2<DT>((uint32_t)rv[k]),
+                          a2[k], b2[k], mode);
       if (relu) v = f32x2{fmaxf(v.x, 0.f), fmaxf(v.y, 0.f)};
       o[k] = (int)pack2<DT>(v);
       bits |= (v.x > 0.f ? 1u : 0u) << (2 * k);

@@ -63,9 +63,9 @@ void run_ranks(int world, F f) {
   for (auto& t : ts) t.join();
 }
 
-// world 4: buckets launched in rank-specific readiness patterns, averaged exactly; timing
-void multi_rank_average() {
-  const int W = 4;
+// world W (4, and 8 = the driver's one-node scaling run): buckets launched in rank-specific
+// readiness patterns, averaged exactly; timing
+void multi_rank_average(const int W) {
   const long long N = 10000;
   const std::vector<long long> bounds = {0, 1000, 1000, 4000, 4000, 4096, 4096, 10000};
   char id[128];
@@ -91,7 +91,7 @@ void multi_rank_average() {
         CHECK(pda_reducer_ready(red, upto, nullptr) == 0);
       }
       CHECK(pda_reducer_finish(red, nullptr, nullptr) == 0);
-      const float avg_rank = 8.f * (0 + 1 + 2 + 3) / W;
+      const float avg_rank = 8.f * (float)(W * (W - 1) / 2) / W;
       for (long long i = 0; i < N; ++i) CHECK(flat[i] == avg_rank + (float)(i % 97) + step);
       CHECK(pda_reducer_launched(red) == 4LL * (step + 1));
       if (step == 3) {
@@ -104,7 +104,7 @@ void multi_rank_average() {
     CHECK(pda_reducer_destroy(red) == 0);
     CHECK(pda_comm_destroy(h, 0) == 0);
   });
-  std::printf("PASS multi_rank_average\n");
+  std::printf("PASS multi_rank_average world %d\n", W);
 }
 
 // the Python handle closes the communicator while a reducer still references it
@@ -236,12 +236,13 @@ void collectives() {
   std::printf("PASS collectives\n");
 }
 
-// in-process DataParallel group: one thread, ncclCommInitAll, grouped all-reduce
-void dp_group() {
-  const int D = 4;
-  const int devs[D] = {0, 1, 2, 3};
+// in-process DataParallel group: one thread, ncclCommInitAll, grouped all-reduce (D = 4, and 8 =
+// resnet_dp.py's node: the segmented replay reduces each gradient slice this way)
+void dp_group(const int D) {
+  std::vector<int> devs(D);
+  for (int d = 0; d < D; ++d) devs[d] = d;
   void* h = nullptr;
-  CHECK(pda_comm_init_all(devs, D, &h) == 0);
+  CHECK(pda_comm_init_all(devs.data(), D, &h) == 0);
   std::vector<std::vector<float>> bufs(D, std::vector<float>(333));
   std::vector<void*> ptrs(D);
   std::vector<hipStream_t> sts(D, nullptr);
@@ -251,21 +252,33 @@ void dp_group() {
   }
   CHECK(pda_group_allreduce(h, ptrs.data(), 333, kF32, kSum, sts.data()) == 0);
   for (int d = 0; d < D; ++d)
-    for (int i = 0; i < 333; ++i) CHECK(bufs[d][i] == (float)(6 + 4 * i));
+    for (int i = 0; i < 333; ++i) CHECK(bufs[d][i] == (float)(D * (D - 1) / 2 + D * i));
+  // the segmented DataParallel reduce: consecutive slices of the flat gradient, one grouped call
+  // each, in stage order
+  const int cuts[4] = {0, 100, 250, 333};
+  for (int s = 0; s < 3; ++s) {
+    std::vector<void*> sp(D);
+    for (int d = 0; d < D; ++d) sp[d] = bufs[d].data() + cuts[s];
+    CHECK(pda_group_allreduce(h, sp.data(), cuts[s + 1] - cuts[s], kF32, kSum, sts.data()) == 0);
+  }
+  for (int d = 0; d < D; ++d)
+    for (int i = 0; i < 333; ++i) CHECK(bufs[d][i] == (float)D * (float)(D * (D - 1) / 2 + D * i));
   CHECK(pda_comm_destroy(h, 0) == 0);
-  std::printf("PASS dp_group\n");
+  std::printf("PASS dp_group %d devices\n", D);
 }
 
 }  // namespace
 
 int main() {
   alarm(120);   // a deadlock fails the test instead of hanging it
-  multi_rank_average();
+  multi_rank_average(4);
+  multi_rank_average(8);
   destroy_comm_before_reducer();
   abort_while_enqueuing();
   bad_arguments();
   collectives();
-  dp_group();
+  dp_group(4);
+  dp_group(8);
   std::printf("ALL PASS\n");
   return 0;
 }

@@ -51,6 +51,18 @@ __device__ __forceinline__ float bnb_affine(float k1, float k2, float k3, float 
 __device__ __forceinline__ f32x2 bnb_affine2(f32x2 k1, f32x2 k2, f32x2 k3, f32x2 dz, f32x2 y) {
   return f32x2{bnb_affine(k1.x, k2.x, k3.x, dz.x, y.x), bnb_affine(k1.y, k2.y, k3.y, dz.y, y.y)};
 }
+// BatchNorm apply of a residual block's tail, before the ReLU: bn(y) [+ r (mode 1) | + bn2(r)
+// (mode 2)], as explicit fmas shared by the apply kernels (bn.hip) and the FWD_TAIL conv prologue
+// (conv_gemm.hip), so the activation one of them writes is bit-identical to the other's.
+__device__ __forceinline__ f32x2 tail_pre2(f32x2 y, f32x2 a, f32x2 b, f32x2 r, f32x2 a2, f32x2 b2,
+                                           int mode) {
+  f32x2 v = f32x2{__builtin_fmaf(y.x, a.x, b.x), __builtin_fmaf(y.y, a.y, b.y)};
+  if (mode) {
+    if (mode == 2) r = f32x2{__builtin_fmaf(r.x, a2.x, b2.x), __builtin_fmaf(r.y, a2.y, b2.y)};
+    v = f32x2{v.x + r.x, v.y + r.y};
+  }
+  return v;
+}
 template <int DT> __device__ __forceinline__ f32x2 unpack2(uint32_t w);
 template <> __device__ __forceinline__ f32x2 unpack2<DT_BF16>(uint32_t w) {
   return f32x2{__uint_as_float(w << 16), __uint_as_float(w & 0xffff0000u)};

@@ -61,7 +61,14 @@ template <int N> __device__ __forceinline__ void vm_wait() {
 // chunks; per-split partials behind the slab). With them the tail fold's conv3 weight gradient
 // needs no y3 read (decomposed form, see pda_wgrad_reduce):
 //   dW3 = diag(k1) (dz^T a2) + diag(k2) W3 Gram(a2) + k3 s^T,   y3 = a2 W3^T.
-enum Pass : int { FWD = 0, DGRAD = 1, WGRAD = 2, WGRAD_BNA = 3, DGRAD_BNF = 4, WGRAD_GRAM = 5 };
+//
+// FWD_TAIL: FWD of a 1x1 stride-1 conv whose input is the PREVIOUS block's output
+// a = relu(bn3(y3) + r), r = the residual (pro_mode 1) or bn_d(yd) (pro_mode 2, the downsample
+// branch), formed while staging A from y3 (p.a) and r (p.pro_res) -- the tail's BN-apply pass is
+// folded into its consumer: a is written once by the blocks of the first N-tile (p.pro_out, plus the
+// ReLU bitmask p.pro_mask in mode 1) instead of written by an apply pass and read back by the conv.
+enum Pass : int { FWD = 0, DGRAD = 1, WGRAD = 2, WGRAD_BNA = 3, DGRAD_BNF = 4, WGRAD_GRAM = 5,
+                  FWD_TAIL = 6 };
 
 template <int V> struct IC { static constexpr int value = V; };
 
@@ -93,6 +100,11 @@ struct ConvParams {
   // staging the tile (padding stays exactly 0), so the activation is never materialised.
   const float* pro_sc;
   const float* pro_sh;
+  // FWD_TAIL: the residual operand (mode 1: added as is; mode 2: with its own BN pro_sc2 / pro_sh2),
+  // the materialised activation a and its ReLU bitmask (1 byte per 8 elements, mode 1; nullable)
+  const void* pro_res; const float* pro_sc2; const float* pro_sh2;
+  void* pro_out; uint8_t* pro_mask;
+  int pro_mode;
   // DGRAD fused BatchNorm-backward epilogue (emode < 0: plain dX store)
   int emode, enq;                 // 0 relu(bn(y)), 1 relu(bn(y)+ey2), 2 relu(bn(y)+bn2(ey2)),
                                   // 3 as 1 with the ReLU mask read from emask (no residual read)
@@ -204,9 +216,12 @@ template <int PASS_T, int DT, int BM, int BN, int STAGES>
 // (the 16-bit WGRAD budget of 4 spilled 15 VGPRs); its 256-column tile (the stem's whole N: dz and
 // y staged and transformed once instead of once per 128-column tile) needs 246: 2 blocks per CU
 // (the 128x128 WGRAD_BNA tile of the bottleneck conv3 fold: 2 blocks, 3 spilled 89 VGPRs)
-__global__ __launch_bounds__(conv_nt<STAGES>(), (PASS_T == WGRAD_BNA || PASS_T == WGRAD_GRAM ? (BN >= 256 || BM * BN >= 128 * 128 ? 2 : 3) : conv_min_blocks<DT, BM, BN, STAGES>())) void conv_gemm_kernel(ConvParams p_arg) {
+// FWD_TAIL holds the residual chunks and both branches' BN coefficients across the MFMAs: the
+// 128x64 tile at 3 blocks per CU, 128x128 at 2 (the plain FWD budgets spill 43 / 50 VGPRs)
+__global__ __launch_bounds__(conv_nt<STAGES>(), (PASS_T == WGRAD_BNA || PASS_T == WGRAD_GRAM ? (BN >= 256 || BM * BN >= 128 * 128 ? 2 : 3) : PASS_T == FWD_TAIL ? (BM * BN >= 128 * 128 ? 2 : 3) : conv_min_blocks<DT, BM, BN, STAGES>())) void conv_gemm_kernel(ConvParams p_arg) {
   constexpr int PASS = PASS_T == WGRAD_BNA || PASS_T == WGRAD_GRAM ? WGRAD
-                       : PASS_T == DGRAD_BNF ? DGRAD : PASS_T;
+                       : PASS_T == DGRAD_BNF ? DGRAD : PASS_T == FWD_TAIL ? FWD : PASS_T;
+  constexpr bool TAILP = PASS_T == FWD_TAIL;   // tail-apply prologue (a = relu(bn3(y3) + r))
   constexpr bool GRAM = PASS_T == WGRAD_GRAM;   // A = relu(ak1*a + ak3); no second tensor
   constexpr bool ABN = PASS_T == WGRAD_BNA || GRAM;
   constexpr bool BNF = PASS_T == DGRAD_BNF;
@@ -220,6 +235,7 @@ __global__ __launch_bounds__(conv_nt<STAGES>(), (PASS_T == WGRAD_BNA || PASS_T =
   static_assert(!DMA || ((DT == DT_BF16 || DT == DT_F16) && !ABN), "LDS-DMA: 16-bit");
   static_assert(!ABN || DT == DT_BF16 || DT == DT_F16, "WGRAD_BNA: 16-bit operands");
   static_assert(!BNF || ((DT == DT_BF16 || DT == DT_F16) && !DMA), "DGRAD_BNF: 16-bit, register-staged");
+  static_assert(!TAILP || ((DT == DT_BF16 || DT == DT_F16) && STAGES == 1), "FWD_TAIL: 16-bit, single-stage");
   // DGRAD / WGRAD read the parameters in place in the kernarg segment (constant address space):
   // binding a reference to the by-value argument makes the compiler copy the whole ~1 KB block to
   // scratch once a member array is indexed dynamically (DGRAD tap tables), and costs WGRAD spills.
@@ -449,6 +465,13 @@ __global__ __launch_bounds__(conv_nt<STAGES>(), (PASS_T == WGRAD_BNA || PASS_T =
       const_cast<void*>(BNF ? p.xa : p.a), (short)0,
       BNF ? (int)((uint32_t)p.Nb * p.H * p.W * p.xa_c * (uint32_t)ES) : (int)a_bytes, 0x00020000);
   bool xt = false;   // DGRAD_BNF: the tile in the staging registers is a Gram-operand tile
+  // FWD_TAIL: the residual (same geometry as A), its staged chunks, the staged tile's channel base
+  const __amdgpu_buffer_rsrc_t rsr = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<void*>(TAILP ? p.pro_res : p.a), (short)0, (int)a_bytes, 0x00020000);
+  i32x4 rres[TAILP ? AR : 1];
+  int st_c = 0, st_c_w = 0;     // channel base of the loaded / of the staged k-tile
+  uint32_t tail_bits = 0;       // ReLU bits of the staged chunks (byte i: chunk i)
+  const bool tail_wr = TAILP && tn == 0;   // the first N-tile's blocks write a (each A chunk once)
 
   i32x4 ra[AR], rb[BR];
   i32x4 ra2[SPLIT ? AR : 1], rb2[SPLIT ? BR : 1];   // DT_F32S: elements 4..7 of each chunk
@@ -461,15 +484,22 @@ __global__ __launch_bounds__(conv_nt<STAGES>(), (PASS_T == WGRAD_BNA || PASS_T =
     if constexpr (SPLIT) rb2[i] = bld(rsb, off + 16u);
   };
   // prologue state: per-chunk validity (padding must stay 0) and the chunk's 8 channel coeffs
-  const bool pro = (PASS == FWD || PASS == WGRAD) && p.pro_sc != nullptr;
+  const bool pro = (PASS == FWD || PASS == WGRAD) && (TAILP || p.pro_sc != nullptr);
   const bool xpro = BNF && p.xa_sc != nullptr;   // DGRAD_BNF: BN+ReLU on the Gram operand
   bool pv[PASS == WGRAD ? BR : AR];
   f32x2 psc[4], psh[4];
+  f32x2 psc2[TAILP ? 4 : 1], psh2[TAILP ? 4 : 1];
   auto pro_coeffs_of = [&](const float* sc, const float* sh, int c) __attribute__((always_inline)) {
 #pragma unroll
     for (int k = 0; k < EPC / 2; ++k) {
       psc[k] = *reinterpret_cast<const f32x2*>(sc + c + 2 * k);
       psh[k] = *reinterpret_cast<const f32x2*>(sh + c + 2 * k);
+      if constexpr (TAILP) {
+        if (p.pro_mode == 2) {
+          psc2[k] = *reinterpret_cast<const f32x2*>(p.pro_sc2 + c + 2 * k);
+          psh2[k] = *reinterpret_cast<const f32x2*>(p.pro_sh2 + c + 2 * k);
+        }
+      }
     }
   };
   auto pro_coeffs = [&](int c) __attribute__((always_inline)) { pro_coeffs_of(p.pro_sc, p.pro_sh, c); };
@@ -492,6 +522,24 @@ __global__ __launch_bounds__(conv_nt<STAGES>(), (PASS_T == WGRAD_BNA || PASS_T =
         v[k] = __builtin_bit_cast(int, __builtin_elementwise_max(h, (s16x2){0, 0}));
       }
     }
+  };
+
+  // FWD_TAIL: a = relu(bn3(y3) + r) on the chunk (the same fma chain as the apply pass,
+  // common.h tail_act2, so the written activation is bit-identical to it); returns the ReLU bits
+  auto tail_apply = [&](i32x4& v, const i32x4& r) __attribute__((always_inline)) -> uint32_t {
+    uint32_t bits = 0;
+    if constexpr (TAILP) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        f32x2 a = tail_pre2(unpack2<DT>((uint32_t)v[k]), psc[k], psh[k],
+                            unpack2<DT>((uint32_t)r[k]), psc2[k], psh2[k], p.pro_mode);
+        a = f32x2{fmaxf(a.x, 0.f), fmaxf(a.y, 0.f)};
+        v[k] = (int)pack2<DT>(a);
+        bits |= (a.x > 0.f ? 1u : 0u) << (2 * k);
+        bits |= (a.y > 0.f ? 1u : 0u) << (2 * k + 1);
+      }
+    }
+    return bits;
   };
 
   // DT_F32S: BN+ReLU on the chunk's 8 f32 values (v0: channels 0-3, v1: 4-7)
@@ -537,8 +585,10 @@ __global__ __launch_bounds__(conv_nt<STAGES>(), (PASS_T == WGRAD_BNA || PASS_T =
           const uint32_t mw = word ? (uint32_t)(a_mask[i] >> 32) : (uint32_t)a_mask[i];
           const bool ok = (mw >> bit) & 1u;
           lda(i, ok ? (uint32_t)(a_base[i] + toff) : OOB);
+          if constexpr (TAILP) rres[i] = bld(rsr, ok ? (uint32_t)(a_base[i] + toff) : OOB);
           pv[i] = ok;
         }
+        if constexpr (TAILP) st_c = c0;
         if (pro) pro_coeffs(c0 + (tid & 7) * EPC);
       } else {   // Cin < 64 (the space-to-depth stem): taps change inside the k-tile
         const int k = k0 + (tid & 7) * EPC;
@@ -637,7 +687,10 @@ __global__ __launch_bounds__(conv_nt<STAGES>(), (PASS_T == WGRAD_BNA || PASS_T =
     if constexpr (A_ROW) {
 #pragma unroll
       for (int i = 0; i < AR; ++i) {
-        if constexpr (PASS == FWD) {
+        if constexpr (TAILP) {
+          if (i == 0) { st_c_w = st_c; tail_bits = 0; }
+          if (pv[i]) tail_bits |= tail_apply(ra[i], rres[i]) << (8 * i);
+        } else if constexpr (PASS == FWD) {
           if constexpr (SPLIT) {
             if (pro && pv[i]) pro_apply2(ra[i], ra2[i]);
           } else {
@@ -704,6 +757,24 @@ __global__ __launch_bounds__(conv_nt<STAGES>(), (PASS_T == WGRAD_BNA || PASS_T =
                             : col_addr<BN>(tid / CPR + RPI * i, tid % CPR);
         if constexpr (SPLIT) split_put(sb, cb_, rb[i], rb2[i]);
         else *reinterpret_cast<i32x4*>(sb + cb_) = rb[i];
+      }
+    }
+  };
+
+  // FWD_TAIL: write the staged activation chunks (and their ReLU bytes) of the k-tile in LDS,
+  // read back from the tile image -- issued after the MFMAs, i.e. after the NEXT tile's loads: a
+  // global store issued before those loads would hold their vmcnt wait behind its completion (VMEM
+  // counts loads and stores in order), which made the in-staging store 4x slower per launch
+  auto tail_store = [&]() __attribute__((always_inline)) {
+    if constexpr (TAILP) {
+      if (!tail_wr) return;
+#pragma unroll
+      for (int i = 0; i < AR; ++i) {
+        if (!pv[i]) continue;   // 1x1 stride 1: row validity is the same for every k-tile
+        const i32x4 v = *reinterpret_cast<const i32x4*>(smem + row_addr((tid >> 3) + 32 * i, tid & 7));
+        const uint32_t e = (uint32_t)(a_base[i] / ES) + (uint32_t)(st_c_w + (tid & 7) * EPC);
+        *reinterpret_cast<i32x4*>(reinterpret_cast<u16*>(p.pro_out) + e) = v;
+        if (p.pro_mask) p.pro_mask[e >> 3] = (uint8_t)(tail_bits >> (8 * i));
       }
     }
   };
@@ -1160,6 +1231,7 @@ __global__ __launch_bounds__(conv_nt<STAGES>(), (PASS_T == WGRAD_BNA || PASS_T =
       if constexpr (STAGES == 2) {
         if (kt + 1 < nk) store_tile(cur ^ 1);
       }
+      tail_store();
       __syncthreads();
     }
   }
@@ -1686,8 +1758,8 @@ struct ConvDesc {  // mirrors pytorch_distributed_amd/ops/ext.py ConvDesc
 
 template <int PASS, int DT, int BM, int BN, int ST>
 static int launch(const ConvParams& p, dim3 grid, hipStream_t st) {
-  if constexpr ((PASS == WGRAD_BNA || PASS == DGRAD_BNF || PASS == WGRAD_GRAM) && DT != DT_BF16 &&
-                DT != DT_F16) {
+  if constexpr ((PASS == WGRAD_BNA || PASS == DGRAD_BNF || PASS == WGRAD_GRAM || PASS == FWD_TAIL) &&
+                DT != DT_BF16 && DT != DT_F16) {
     return -1;
   } else {
     hipLaunchKernelGGL((conv_gemm_kernel<PASS, DT, BM, BN, ST>), grid, dim3(conv_nt<ST>()), 0, st, p);
@@ -1804,6 +1876,39 @@ int pda_conv_fwd(const ConvDesc* d, const void* x, const void* w, int Kpad, void
   const int abm = tile_bm(bm);
   const int tiles = ((p.M + abm - 1) / abm) * ((p.N + bn - 1) / bn);
   return dispatch<FWD>(dt, bm, bn, p, dim3(tiles, 1), st);
+}
+
+// FWD_TAIL (see the Pass enum): Y = conv(a, W) of a 1x1 stride-1 conv whose input
+// a = relu(y3 * sc + sh + r) (mode 1, r = res) or relu(y3 * sc + sh + res * sc2 + sh2) (mode 2) is
+// formed while staging; a is written to a_out (and its ReLU bitmask to mask, mode 1, nullable) by
+// the first N-tile's blocks. Register-staged single-stage tiles (-128, 64) / (-128, 128).
+int pda_conv_fwd_tail(const ConvDesc* d, const void* y3, const void* w, int Kpad, void* y,
+                      float* stats, const float* sc, const float* sh, const void* res,
+                      const float* sc2, const float* sh2, void* a_out, void* mask, int mode, int dt,
+                      int bm, int bn, hipStream_t st) {
+  if (dt != DT_BF16 && dt != DT_F16) return -1;
+  if (d->R != 1 || d->S != 1 || d->stride != 1 || d->pad != 0 || (d->Cin % 64) || Kpad != d->Cin ||
+      !sc || !sh || !res || !a_out || (mode != 1 && mode != 2) || (mode == 2 && (!sc2 || !sh2)))
+    return -2;
+  if (!fits32((long long)d->Nb * d->H * d->W * d->Cin, (long long)d->Cout * Kpad,
+              (long long)d->Nb * d->Ho * d->Wo * d->Cout, dt))
+    return -4;
+  ConvParams p{};
+  fill_geom(p, *d);
+  p.pro_sc = sc; p.pro_sh = sh;
+  p.pro_res = res; p.pro_sc2 = sc2; p.pro_sh2 = sh2; p.pro_out = a_out;
+  p.pro_mask = (uint8_t*)mask; p.pro_mode = mode;
+  p.a = y3; p.b = w; p.out = y; p.stats = stats; p.bias = nullptr;
+  p.M = d->Nb * d->Ho * d->Wo; p.N = d->Cout; p.Kpad = Kpad; p.K = Kpad;
+  p.out_f32 = 0; p.relu = 0; p.out_pitch = d->Cout;
+  const int tiles = ((p.M + 127) / 128) * ((p.N + bn - 1) / bn);
+#define TAIL_CASE(D, N_) \
+  if (dt == D && bm == -128 && bn == N_) return launch<FWD_TAIL, D, 128, N_, 1>(p, dim3(tiles, 1), st);
+#ifndef CONV_DMA_ONLY
+  TAIL_CASE(DT_BF16, 64) TAIL_CASE(DT_BF16, 128) TAIL_CASE(DT_F16, 64) TAIL_CASE(DT_F16, 128)
+#endif
+#undef TAIL_CASE
+  return -1;
 }
 
 // dX[Nb,H,W,Cin] = conv_transpose(dY, W). Every dX element is written (zeros where no tap lands).

@@ -143,6 +143,10 @@ class NativeResNet(nn.Module):
         # layer1's weight gradients on the second stream (profiles/ab_r4.md section 8)
         self.stem_bna = True
         self.tail_mask = True         # tails store the ReLU bitmask the backward reads
+        # a block's tail BN apply (+ residual + ReLU) runs inside the next block's conv1 forward,
+        # which stages a = relu(bn3(y3) + r) from y3 and r and writes a once (FWD_TAIL); blocks whose
+        # successor has a shortcut conv keep the apply pass (PDA_TAIL_FUSE=0: every tail does)
+        self.tail_fuse = os.environ.get("PDA_TAIL_FUSE", "1") != "0"
         # consumer-side tail fold of the Bottleneck BN backward (see _block_backward)
         # ("0" off, "1" every stage, or the stages to fold, e.g. "12" = layer1 and layer2). Default
         # layer1-3: in-step A/B at the bench config (profiles/ab_r4.md) 28.26 ms off, 27.89 all
@@ -535,9 +539,11 @@ class NativeResNet(nn.Module):
         return ":" in mode and u.H >= int(mode.split(":")[1])
 
     def _conv_bn(self, u: ConvBN, x: torch.Tensor, train: bool, pro=None, ws=None,
-                 before_finalize=None) -> torch.Tensor:
+                 before_finalize=None, tail=None) -> torch.Tensor:
         """y = conv(x) and BN coefficients (batch stats in training, running stats in eval).
         ``pro=(scale, shift)``: x is the previous PRE-BN tensor; the conv applies BN+ReLU on load.
+        ``tail`` (:class:`~..ops.native_ops.TailIn`): x is the previous block's pre-BN tail and the
+        conv forms (and writes) that block's output while staging.
         ``before_finalize``: called between the conv launch and the BN finalize launch."""
         ws = self.ws if ws is None else ws
         Nb = x.shape[0]
@@ -549,9 +555,10 @@ class NativeResNet(nn.Module):
                            u.bn.momentum if u.bn.momentum is not None else 0.1,
                            st[0], st[1], st[2], st[3], self.rmean(u), self.rvar(u),
                            self.flat_nbt[u.nbt_idx:u.nbt_idx + 1], update_running=True)
-            K.conv_fwd(x, self.w16(u), g, y, pro=pro, bn=bn, before_finalize=before_finalize)
+            K.conv_fwd(x, self.w16(u), g, y, pro=pro, bn=bn, before_finalize=before_finalize,
+                       tail=tail)
         else:
-            K.conv_fwd(x, self.w16(u), g, y, pro=pro)
+            K.conv_fwd(x, self.w16(u), g, y, pro=pro, tail=tail)
             if before_finalize is not None:
                 before_finalize()
             K.bn_eval_coeffs(self.gamma(u), self.beta(u), self.rmean(u), self.rvar(u), u.bn.eps,
@@ -588,6 +595,7 @@ class NativeResNet(nn.Module):
         feat = None
         nblk = len(self.blocks)
         gram_pending = False
+        tail_in = None   # (y3, (sc, sh), TailIn): the previous tail, folded into this block's conv1
         for bi, b in enumerate(self.blocks):
             last = bi == nblk - 1
             rec = {"x": h} if save else None
@@ -595,6 +603,8 @@ class NativeResNet(nn.Module):
             ys, acts = [], [h]
             pro = None
             yd = None
+            if tail_in is not None:
+                a, pro = tail_in[0], tail_in[1]
             # (SyncBatchNorm: the shortcut BN's all-reduce must not run on a second stream beside
             # the main chain's -- two streams on one communicator can order its collectives
             # differently on different ranks and deadlock -- so the shortcut stays on the chain)
@@ -608,7 +618,7 @@ class NativeResNet(nn.Module):
             gram_side = (save and train and self.bn_fold_wg and self._side is not None
                          and len(b.units) == 3 and self._tail_fold_ok(b, Nb))
             for j, u in enumerate(b.units):
-                y = self._conv_bn(u, a, train, pro)
+                y = self._conv_bn(u, a, train, pro, tail=tail_in[2] if j == 0 and tail_in else None)
                 ys.append(y)
                 if save:
                     rec[f"s{j}"] = u.state
@@ -633,6 +643,16 @@ class NativeResNet(nn.Module):
                     rec["sd"] = b.ds.state
             ul = b.units[-1]
             sc, sh = self._coeffs(ul, train)
+            tail_in = None
+            nb = self.blocks[bi + 1] if not last else None
+            # the tail's BN apply folds into the next block's conv1 (FWD_TAIL) unless a shortcut conv
+            # on the second stream reads the output first; layers 1-2 only (conv1 of <= 128 channels,
+            # K <= 512): on the deep-K layers 3-4 the fused launch is slower than the apply pass and
+            # the plain conv together (tools/tail_bench.py: layer1 422 vs 482 us, layer2 233 vs 244,
+            # layer3 196 vs 142, layer4 214 vs 105 -- profiles/ab_r5.md section 2)
+            fuse = (nb is not None and self.tail_fuse and nb.ds is None
+                    and nb.units[0].cout <= 128
+                    and K.tail_fuse_ok(nb.units[0].geom(Nb), self.dtype))
             if last:
                 feat = self._empty(Nb, ul.cout)
                 if yd is not None:
@@ -643,13 +663,21 @@ class NativeResNet(nn.Module):
             else:
                 out = self._empty(*ys[-1].shape)
                 if yd is not None:
-                    K.bn_apply(ys[-1], sc, sh, out, y2=yd, scale2=b.ds.state[2], shift2=b.ds.state[3])
+                    if fuse:
+                        tail_in = (ys[-1], (sc, sh), K.TailIn(yd, out, sc2=b.ds.state[2],
+                                                              sh2=b.ds.state[3]))
+                    else:
+                        K.bn_apply(ys[-1], sc, sh, out, y2=yd, scale2=b.ds.state[2],
+                                   shift2=b.ds.state[3])
                 else:
                     # identity tail: keep its ReLU bitmask (1/16 of the tensor) so the backward
                     # rebuilds the mask without re-reading the residual
                     mask = (torch.empty(out.numel() // 8, dtype=torch.uint8, device=self.device)
                             if save and self.tail_mask else None)
-                    K.bn_apply(ys[-1], sc, sh, out, res=h, mask=mask)
+                    if fuse:
+                        tail_in = (ys[-1], (sc, sh), K.TailIn(h, out, mask=mask))
+                    else:
+                        K.bn_apply(ys[-1], sc, sh, out, res=h, mask=mask)
                     if save:
                         rec["mask"] = mask
             if save:

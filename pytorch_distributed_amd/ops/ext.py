@@ -72,6 +72,8 @@ class BnBwdOut(C.Structure):
 _V, _I, _F, _L, _U, _D = C.c_void_p, C.c_int, C.c_float, C.c_longlong, C.c_uint, C.c_double
 _SIGS = {
     "pda_conv_fwd": [C.POINTER(ConvDesc), _V, _V, _I, _V, _I, _I, _V, _V, _I, _V, _V, _I, _I, _I, _V],
+    "pda_conv_fwd_tail": [C.POINTER(ConvDesc), _V, _V, _I, _V, _V, _V, _V, _V, _V, _V, _V, _V, _I, _I,
+                          _I, _I, _V],
     "pda_conv_dgrad": [C.POINTER(ConvDesc), _V, _V, _V, C.POINTER(BnEpi), _I, _I, _I, _V],
     "pda_conv_dgrad_bnf": [C.POINTER(ConvDesc), _V, _V, _V, C.POINTER(BnEpi), _V, _V, _V, _V, _I, _I,
                            _I, _V],

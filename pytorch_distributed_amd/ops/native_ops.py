@@ -202,12 +202,17 @@ def conv_fwd(x: torch.Tensor, w: torch.Tensor, g: ConvGeom, out: torch.Tensor,
              stats: Optional[torch.Tensor] = None, bias: Optional[torch.Tensor] = None,
              relu: bool = False, tile: Optional[Tuple[int, int]] = None,
              pro: Optional[Tuple[torch.Tensor, torch.Tensor]] = None,
-             bn: Optional[BnStats] = None, before_finalize=None) -> torch.Tensor:
+             bn: Optional[BnStats] = None, before_finalize=None,
+             tail: Optional["TailIn"] = None) -> torch.Tensor:
     """out[M, Cout] (16-bit or f32) = conv(x, w). w: [Cout, Kpad] 16-bit, Kpad = w.shape[1].
     stats (f32, >= ceil(M/bm)*3*Cout) receives per-M-tile shifted partials (sum(y-s),
     sum((y-s)^2), s) -- see :func:`stats_totals`; ``bn`` (:class:`BnStats`) also finalizes the
     BatchNorm from them. pro = (scale, shift): x is a PRE-BatchNorm tensor and the conv consumes
-    relu(x*scale+shift)."""
+    relu(x*scale+shift). ``tail`` (:class:`TailIn`, 1x1 stride-1 convs, see :func:`tail_fuse_ok`):
+    x is the previous block's pre-BN tail y3 and the conv consumes a = relu(bn3(y3) + r), writing a
+    (and its ReLU bitmask) on the way -- the tail's BN-apply pass folded into its consumer."""
+    if tail is not None:
+        return _conv_fwd_tail(x, w, g, out, pro, tail, stats, bn, before_finalize)
     Nb = x.shape[0]
     M = Nb * g.Ho * g.Wo
     Kpad = w.shape[-1] if w.dim() == 2 else w[0].numel()
@@ -238,6 +243,55 @@ def conv_fwd(x: torch.Tensor, w: torch.Tensor, g: ConvGeom, out: torch.Tensor,
         before_finalize()
     if bn is not None:
         bn_finalize_partials(stats, T, g.Cout, tile_rows(kbm), M, bn)
+    return out
+
+
+@dataclass
+class TailIn:
+    """Operands of a residual block's tail a = relu(y3 * sc + sh + r) formed by the consumer conv
+    (conv_fwd ``tail``): ``res`` is r itself (identity shortcut) or, with ``sc2`` / ``sh2``, the
+    downsample branch's pre-BN output whose BN is applied too; ``out`` receives a, ``mask`` (uint8,
+    numel / 8, identity tails) its ReLU bitmask -- exactly what :func:`bn_apply` would write."""
+    res: torch.Tensor
+    out: torch.Tensor
+    mask: Optional[torch.Tensor] = None
+    sc2: Optional[torch.Tensor] = None
+    sh2: Optional[torch.Tensor] = None
+
+
+def tail_fuse_ok(g: ConvGeom, dtype: torch.dtype) -> bool:
+    """Whether a tail can be folded into this consumer conv (csrc/conv_gemm.hip FWD_TAIL): a 1x1
+    stride-1 conv without padding on 16-bit operands, Cin a multiple of 64."""
+    return (dtype in (torch.bfloat16, torch.float16) and g.R == 1 and g.S == 1 and g.stride == 1
+            and g.pad == 0 and g.Cin % 64 == 0
+            and getattr(ext.lib(), "pda_conv_fwd_tail", None) is not None)
+
+
+def _conv_fwd_tail(y3, w, g: ConvGeom, out, pro, tail: TailIn, stats, bn, before_finalize):
+    if pro is None or not tail_fuse_ok(g, y3.dtype):
+        raise ValueError("conv_fwd tail: needs pro = (scale, shift) of the tail BN and a 1x1 "
+                         "stride-1 16-bit conv (tail_fuse_ok)")
+    if tail.out.shape != y3.shape or tail.res.shape != y3.shape or tail.out.dtype != y3.dtype:
+        raise ValueError("conv_fwd tail: y3, the residual and the output activation share one shape")
+    if tail.mask is not None and tail.mask.numel() * 8 < y3.numel():
+        raise ValueError("conv_fwd tail: mask needs numel / 8 bytes")
+    Nb = y3.shape[0]
+    M = Nb * g.Ho * g.Wo
+    Kpad = w.shape[-1] if w.dim() == 2 else w[0].numel()
+    bm, bn_ = -128, (64 if g.Cout <= 64 else 128)
+    T = math.ceil(M / 128)
+    if bn is not None:
+        stats = bn.ws.get("fwd_stats", T * 3 * g.Cout)
+    mode = 2 if tail.sc2 is not None else 1
+    d = g.desc(Nb)
+    check(ext.lib().pda_conv_fwd_tail(C.byref(d), ptr(y3), ptr(w), Kpad, ptr(out), ptr(stats),
+                                      ptr(pro[0]), ptr(pro[1]), ptr(tail.res), ptr(tail.sc2),
+                                      ptr(tail.sh2), ptr(tail.out), ptr(tail.mask), mode,
+                                      _kdt(y3), bm, bn_, stream(y3.device)), "conv_fwd_tail")
+    if before_finalize is not None:
+        before_finalize()
+    if bn is not None:
+        bn_finalize_partials(stats, T, g.Cout, 128, M, bn)
     return out
 
 

@@ -10,7 +10,7 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 ARGS = ["--device", "cpu", "--arch", "resnet18", "--batch", "2", "--image-size", "32",
-        "--steps", "2", "--warmup", "1", "--dtype", "fp32", "--fp32-steps", "0"]
+        "--steps", "2", "--warmup", "1", "--dtype", "fp32", "--fp32-steps", "0", "--dp-steps", "0"]
 
 
 def _port():
@@ -90,6 +90,33 @@ def test_bench_cpu_four_ranks(tmp_path):
     assert abs(rec["value"] - 8 * 1000.0 / rec["ms_per_step"]) / rec["value"] < 1e-2
     sp = rec["rank_time_spread"]["headline"]
     assert 0 < sp["min_s"] <= sp["max_s"]
+
+
+def test_bench_cpu_eight_ranks(tmp_path):
+    """World 8 -- the rank count of the driver's one-node scaling run: one record, all eight ranks
+    in the timing spread, weights bit-identical on every rank, and the DataParallel pass's hand-off
+    (rank 0 runs ``bench.py --dp`` as a child process while ranks 1-7 wait on the TCP store for its
+    keys) rehearsed on the CPU."""
+    r = _run(8, tmp=tmp_path, extra_args=("--amp-steps", "0", "--comm-probe", "0", "--dp-steps", "2"))
+    assert r.returncode == 0, r.stderr[-4000:]
+    rec = _record(r)
+    assert rec["n_gpus"] == 8 and rec["config"]["global_batch"] == 16
+    assert rec["config"]["parallelism"] == "dp8"
+    assert rec["weights_consistent"] is True
+    assert abs(rec["value"] - 16 * 1000.0 / rec["ms_per_step"]) / rec["value"] < 1e-2
+    sp = rec["rank_time_spread"]["headline"]
+    assert 0 < sp["min_s"] <= sp["max_s"] and sp["spread_pct"] >= 0
+    assert "dp_error" not in rec, rec.get("dp_error")
+    assert rec["dp_images_per_sec"] > 0 and rec["dp_replicas_consistent"] is True
+    assert rec["dp_config"].startswith("dataparallel1")
+
+
+def test_bench_cpu_eight_ranks_diverged_rank_fails(tmp_path):
+    """At world 8 a single rank whose weights diverge (rank 5) still fails the run."""
+    r = _run(8, {"PDA_BENCH_PERTURB_RANK": "5"}, tmp=tmp_path,
+             extra_args=("--amp-steps", "0", "--comm-probe", "0"))
+    assert r.returncode != 0
+    assert "parameters differ across ranks" in r.stderr
 
 
 def test_numa_binding_precedes_any_hip_call(monkeypatch, tmp_path):

@@ -4,7 +4,8 @@ detection, §5.3 failure detection), on the CPU.
 ``csrc/comm/rccl_comm.cpp`` and ``csrc/comm/reducer.cpp`` -- the exact sources of
 ``libpda_comm.so`` -- are compiled with g++ against a host stub of the HIP/RCCL calls they use
 (``csrc/comm/hoststub/``), whose collectives run across threads, and driven by
-``hoststub/harness.cpp`` with world sizes 2-4: bucket sequencing under rank-specific readiness
+``hoststub/harness.cpp`` with world sizes 2-8 (8 = the driver's one-node scaling run and
+resnet_dp.py's node): bucket sequencing under rank-specific readiness
 patterns, reset, the communicator closed before its reducer, a dead peer with the watchdog
 aborting while another thread is blocked inside a bucket all-reduce, bad arguments, and the
 in-process DataParallel group. Run twice: AddressSanitizer + UBSan (+ LeakSanitizer), and
@@ -36,8 +37,9 @@ def _build_and_run(tmp_path, name, flags, env):
     out = r.stdout + r.stderr
     assert r.returncode == 0, out[-6000:]
     assert "ALL PASS" in r.stdout
-    for s in ("multi_rank_average", "destroy_comm_before_reducer", "abort_while_enqueuing",
-              "bad_arguments", "collectives", "dp_group"):
+    for s in ("multi_rank_average world 4", "multi_rank_average world 8",
+              "destroy_comm_before_reducer", "abort_while_enqueuing", "bad_arguments", "collectives",
+              "dp_group 4 devices", "dp_group 8 devices"):
         assert f"PASS {s}" in r.stdout
     assert "ERROR: AddressSanitizer" not in out and "WARNING: ThreadSanitizer" not in out
     return out

@@ -131,18 +131,21 @@ def test_native_dataparallel_segment_mismatch_falls_back(monkeypatch):
         return c + 1 if len(calls) == 2 else c      # the second replica "differs"
     monkeypatch.setattr(bench_step, "tensor_checksum", skewed)
     x, y = gen(torch.arange(16))
-    with pytest.warns(RuntimeWarning, match="falling back"):
-        l0 = dp.train_step(x, y, opt)
-    torch.cuda.synchronize()
-    assert torch.isfinite(l0).item()
-    assert dp._graphs is None and dp._force_single_segment
-    assert torch.equal(dp.module.flat_params, dp.replicas[0].flat_params)
+    dp.train_step(x, y, opt)             # first step: eager + capture (the replays verify)
     x, y = gen(torch.arange(16) + 16)
-    l1 = dp.train_step(x, y, opt)
+    with pytest.warns(RuntimeWarning, match="falling back"):
+        l1 = dp.train_step(x, y, opt)    # first segmented replay: the forced mismatch
     torch.cuda.synchronize()
     assert torch.isfinite(l1).item()
-    assert len(dp._graphs[0].graphs) == 1 and dp._graphs[0].splits == []
+    assert dp._graphs is None and dp._force_single_segment
     assert torch.equal(dp.module.flat_params, dp.replicas[0].flat_params)
+    for step in (2, 3):                  # re-capture without split points, then replay
+        x, y = gen(torch.arange(16) + 16 * step)
+        ls = dp.train_step(x, y, opt)
+        torch.cuda.synchronize()
+        assert torch.isfinite(ls).item()
+        assert len(dp._graphs[0].graphs) == 1 and dp._graphs[0].splits == []
+        assert torch.equal(dp.module.flat_params, dp.replicas[0].flat_params)
 
 
 def test_native_dataparallel_resume_reloads_every_replica():

@@ -1015,3 +1015,47 @@ def test_conv_wgrad_decomposed_fold(Cout, Cin, H):
     e_dec, e_bna = rel_err(dw_dec, ref), rel_err(dw_bna, ref)
     print(f"dW3 vs fp64: decomposed {e_dec:.2e}, BNA {e_bna:.2e}")
     assert e_dec < e_bna + 2e-3, (e_dec, e_bna)
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("mode", [1, 2])
+@pytest.mark.parametrize("geo", [(2, 9, 256, 64), (3, 7, 512, 128), (2, 5, 1024, 256), (1, 7, 2048, 512)])
+def test_conv_fwd_tail_matches_apply_then_conv(geo, mode, dtype):
+    """FWD_TAIL: conv1 of a block consuming the previous tail a = relu(bn3(y3) + r) (r = the
+    residual, mode 1, or bn_d(yd), mode 2) formed while staging, writing a and its ReLU bitmask --
+    against bn_apply + the plain conv on the same operands: a, the mask, the conv output and its
+    BatchNorm statistics all bit-identical (ragged M: H = 5, 7, 9; 1, 2 and 4 N-tiles)."""
+    K = _k()
+    Nb, H, Cin, Cout = geo
+    torch.manual_seed(Cin + mode)
+    g = K.ConvGeom(Nb, H, H, Cin, Cout, 1, 1, 1, 0)
+    y3 = torch.randn(Nb, H, H, Cin, device=DEV).to(dtype)
+    r = torch.randn(Nb, H, H, Cin, device=DEV).to(dtype)
+    sc, sh = torch.rand(Cin, device=DEV) + 0.5, torch.randn(Cin, device=DEV) * 0.3
+    sc2, sh2 = (torch.rand(Cin, device=DEV) + 0.5, torch.randn(Cin, device=DEV) * 0.3) if mode == 2 \
+        else (None, None)
+    w = (torch.randn(Cout, Cin, device=DEV) / math.sqrt(Cin)).to(dtype)
+    M = Nb * H * H
+    T = math.ceil(M / 128)
+    # reference: the apply pass, then the plain conv on the 128-row tile the fused launch uses
+    a_ref = torch.empty_like(y3)
+    m_ref = torch.zeros(y3.numel() // 8, dtype=torch.uint8, device=DEV)
+    if mode == 1:
+        K.bn_apply(y3, sc, sh, a_ref, res=r, mask=m_ref)
+    else:
+        K.bn_apply(y3, sc, sh, a_ref, y2=r, scale2=sc2, shift2=sh2)
+    y_ref = torch.empty(Nb, H, H, Cout, device=DEV, dtype=dtype)
+    st_ref = torch.zeros(T * 3 * Cout, device=DEV)
+    K.conv_fwd(a_ref, w, g, y_ref, stats=st_ref, tile=(-128, 64 if Cout <= 64 else 128))
+    a = torch.full_like(y3, float("nan"))
+    m = torch.zeros_like(m_ref)
+    y = torch.empty_like(y_ref)
+    st = torch.zeros_like(st_ref)
+    tail = K.TailIn(r, a, mask=m if mode == 1 else None, sc2=sc2, sh2=sh2)
+    K.conv_fwd(y3, w, g, y, stats=st, pro=(sc, sh), tail=tail)
+    torch.cuda.synchronize()
+    assert torch.equal(a, a_ref)
+    if mode == 1:
+        assert torch.equal(m, m_ref)
+    assert torch.equal(y, y_ref)
+    assert torch.equal(st, st_ref)

@@ -14,7 +14,7 @@ def family(name: str) -> str:
         re.search(r"conv_gemm_kernelILi(\d+)ELi(\d+)ELi(\d+)ELi(\d+)E(?:Li(\d+)E)?(?:Li(\d+)E)?", n)
     if m:
         p = {"0": "fwd", "1": "dgrad", "2": "wgrad", "3": "wgrad_bna", "4": "dgrad_bnf",
-             "5": "wgrad_gram"}[m.group(1)]
+             "5": "wgrad_gram", "6": "fwd_tail"}[m.group(1)]
         st = f" st{m.group(5)}" if m.group(5) else ""
         pro = " mf32" if m.group(6) == "32" else ""
         return f"conv_{p} {m.group(3)}x{m.group(4)}{st}{pro}"
