@@ -114,6 +114,11 @@ def _configure_process(args) -> dict:
     RCCL/HSA settings for the JSON record."""
     os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
     os.environ.setdefault("MX_WATCHDOG", "0")   # timed runs: no polling thread beside the step
+    graph = getattr(args, "graph", -1)
+    if getattr(args, "dp", False) or graph == 1 or (graph < 0 and GRAPH_DEFAULT):
+        # graph replay needs the single-queue graph launch, set before HIP starts
+        # (pytorch_distributed_amd/runtime/graphs.py GRAPH_QUEUES_VAR)
+        os.environ.setdefault("DEBUG_HIP_FORCE_GRAPH_QUEUES", "1")
     if args.nccl_channels > 0:
         os.environ["NCCL_MIN_NCHANNELS"] = os.environ["NCCL_MAX_NCHANNELS"] = str(args.nccl_channels)
     if args.nccl_proto:

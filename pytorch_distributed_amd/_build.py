@@ -25,7 +25,7 @@ ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
 HIPCC = os.path.join(ROCM, "bin", "hipcc")
 ARCH = os.environ.get("PDA_ARCH", "gfx950")
 
-KERNEL_SRCS = ["conv_gemm.hip", "bn.hip", "misc.hip", "stem.hip"]
+KERNEL_SRCS = ["conv_gemm.hip", "bn.hip", "misc.hip", "stem.hip", "wgrad_tap.hip"]
 COMM_SRCS = ["comm/rccl_comm.cpp", "comm/reducer.cpp"]
 CFLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wno-unused-result"]
 

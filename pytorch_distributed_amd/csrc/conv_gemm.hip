@@ -1620,6 +1620,66 @@ __global__ __launch_bounds__(256) void wgrad_reduce4_kernel(const float* __restr
 }
 
 
+// Several split-K reductions in ONE launch (the weight gradients of a whole stage, queued by
+// native_ops.ReduceBatch): block b serves descriptor k with blk0[k] <= b < blk0[k+1], then runs
+// wgrad_reduce4_kernel<64>'s fixed-order sum (16 split groups x 16 float4 columns, LDS combine in
+// group order: deterministic) with that descriptor's remap / scale / combine.
+constexpr int RB_MAX = 24;
+struct RedDesc {
+  const float* slab; float* grad; const float* ck; const float* cB; const float* cs;
+  int splits, M, N, cin_log2, cin_real, pitch, accumulate, blk0;
+  float scale;
+};
+struct RedBatch {
+  int n;
+  RedDesc d[RB_MAX];
+};
+__global__ __launch_bounds__(256) void wgrad_reduce_batch_kernel(RedBatch b_arg) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  typedef const __attribute__((address_space(4))) RedBatch KB;
+  KB& b = *(KB*)__builtin_amdgcn_kernarg_segment_ptr();
+#else
+  const RedBatch& b = b_arg;
+#endif
+  const int bid = blockIdx.x;
+  int k = 0;
+  while (k + 1 < b.n && bid >= b.d[k + 1].blk0) ++k;
+  const float* slab = b.d[k].slab;
+  const int M = b.d[k].M, N = b.d[k].N, splits = b.d[k].splits;
+  constexpr int EPB = 64, TPE = EPB / 4, SG = 256 / TPE;
+  __shared__ f32x4 red[256];
+  const int total = M * N;
+  const int t = threadIdx.x, sg = t / TPE, e4 = t - sg * TPE;
+  const int base = (bid - b.d[k].blk0) * EPB + e4 * 4;
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  if (base < total) {
+    const float* src = slab + base;
+#pragma unroll 4
+    for (int s = sg; s < splits; s += SG) acc += *reinterpret_cast<const f32x4*>(src + (size_t)s * total);
+  }
+  red[t] = acc;
+  __syncthreads();
+  if (sg != 0 || base >= total) return;
+  f32x4 sum = red[e4];
+  for (int g = 1; g < SG; ++g) sum += red[g * TPE + e4];
+  const int cl = b.d[k].cin_log2, cr = b.d[k].cin_real, pitch = b.d[k].pitch;
+  const float scale = b.d[k].scale;
+  const bool accumulate = b.d[k].accumulate != 0;
+  float* grad = b.d[k].grad;
+  const float *ck = b.d[k].ck, *cB = b.d[k].cB, *cs = b.d[k].cs;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int idx = base + q;
+    const int n1 = idx / N, n2 = idx - n1 * N;
+    const int tap = n2 >> cl, c = n2 & ((1 << cl) - 1);
+    if (c < cr) {
+      const float v = wg_combine(sum[q], ck, cB, cs, M, N, n1, n2);
+      float* d = grad + (size_t)n1 * pitch + tap * cr + c;
+      *d = accumulate ? *d + scale * v : scale * v;
+    }
+  }
+}
+
 // Consumer-side BatchNorm-backward fold (DGRAD_BNF operands) in ONE launch. W: the conv's 16-bit
 // weights [Cout][Cin] (1x1, OHWI); k: [k1; k2; k3] (3 x Cout f32, the BN-backward apply
 // coefficients of the BN after the conv). Writes Wf = [k1 o W ; G] ([Cout + Cin][Cin] 16-bit),
@@ -2116,6 +2176,33 @@ int pda_conv_wgrad(const ConvDesc* d, const void* dy, const void* x, float* slab
   const int abm = tile_bm(bm);
   const int tiles = ((p.M + abm - 1) / abm) * ((p.N + bn - 1) / bn);
   return dispatch<WGRAD>(dt, bm, bn, p, dim3(tiles, splits), st);
+}
+
+// Host-side descriptor of one queued reduction (mirrors ops/ext.py RedDescC).
+struct RedDescC {
+  const float* slab; float* grad; const float* ck; const float* cB; const float* cs;
+  int splits, M, N, cin_log2, cin_real, pitch, accumulate;
+  float scale;
+};
+
+// n (<= 24) split-K reductions of pda_wgrad_reduce's kind, N % 4 == 0 each, in one launch.
+int pda_wgrad_reduce_batch(const RedDescC* ds, int n, hipStream_t st) {
+  if (n <= 0) return 0;
+  if (n > RB_MAX) return -2;
+  RedBatch b{};
+  b.n = n;
+  int blk = 0;
+  for (int i = 0; i < n; ++i) {
+    const RedDescC& c = ds[i];
+    if (c.N % 4 || c.M <= 0 || c.splits <= 0) return -2;
+    RedDesc& d = b.d[i];
+    d.slab = c.slab; d.grad = c.grad; d.ck = c.ck; d.cB = c.cB; d.cs = c.cs;
+    d.splits = c.splits; d.M = c.M; d.N = c.N; d.cin_log2 = c.cin_log2; d.cin_real = c.cin_real;
+    d.pitch = c.pitch; d.accumulate = c.accumulate; d.scale = c.scale; d.blk0 = blk;
+    blk += (c.M * c.N + 63) / 64;
+  }
+  hipLaunchKernelGGL(wgrad_reduce_batch_kernel, dim3(blk), dim3(256), 0, st, b);
+  return (int)hipGetLastError();
 }
 
 int pda_wgrad_reduce(const float* slab, float* grad, int splits, int M, int N, int cin_pad_log2,

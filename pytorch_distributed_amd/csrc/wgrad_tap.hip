@@ -1,0 +1,322 @@
+// Tap-reuse weight gradient of 3x3 stride-1 pad-1 convolutions for gfx950 (MI355X).
+//
+//   dW[co][r][s][ci] = sum over output pixels p of dY[p][co] * X[p + (r-1, s-1)][ci]
+//
+// The generic implicit-GEMM weight gradient (csrc/conv_gemm.hip WGRAD) gathers its B operand per
+// (tap, channel) column tile, so every N-tile re-reads X for its taps and dY for its rows: at the
+// layer1 3x3 (64 -> 64, 56x56, batch 400) a launch reads 1.6 GB for 0.32 GB of operands
+// (profiles/pmc_r5_step.md). Here a block owns a range of pixels and ALL nine taps of a 64 x 64
+// (co, ci) tile: every dY and X byte of the range is loaded once, and the nine taps read the same
+// LDS image of X at nine row offsets.
+//
+// Padded pixel space: pixel rows are indexed as q = (n, y + 1, x + 1) in an image padded by one
+// pixel on every side (Hp = H + 2, Wp = W + 2), with dY and X zero at the padding positions. Tap
+// (r, s) is then a constant row shift d = (r - 1) Wp + (s - 1) of the X image for EVERY q -- no
+// per-element boundary masks -- at (Hp Wp) / (H W) extra MFMA work (1.07x at 56, 1.15x at 28).
+//
+// Block = 512 threads (8 waves, one block per CU), its padded-row range [q0, q0 + KB) in steps of
+// 64 rows. LDS: X in a 512-row ring (64 channels = 128-B rows, chunks XOR-swizzled by row as the
+// COL images of conv_gemm.hip), dY in NS + 1 tile slots [64 rows][64 co]. Operands arrive by
+// LDS-DMA (buffer_load ... lds; padding and out-of-range rows as out-of-bounds offsets, which
+// write zeros), NS = 4 steps ahead, one counted vmcnt + one barrier per step. The BN+ReLU operand
+// prologue of a PRE-BatchNorm X is applied in LDS to the rows the NEXT step adds, between the
+// barrier and this step's MFMAs (no wave of this step reads those rows; the next barrier publishes
+// them), with the 64 channels' coefficients staged in LDS once. MFMA 16x16x32
+// with swapped operands (D = X_frag x dY_frag^T): each lane ends with 4 consecutive (ci) columns of
+// one co row, stored as f32x4 into the split-K slab [split][Cout][9 Cin] that pda_wgrad_reduce sums.
+// Wave (wr, wc): co rows 32 wr .. +32, columns 144 wc .. +144 of the 576 = 9 taps x 64 ci.
+#include "common.h"
+
+namespace {
+
+constexpr int WT_NT = 512;
+constexpr int WT_NS = 4;            // steps in flight
+constexpr int WT_RING = 512;        // X ring rows (power of two)
+constexpr int WT_SLAB = WT_RING * 128;
+constexpr int WT_ATILE = 64 * 128;  // dY tile [64 rows][64 co]
+constexpr int WT_COEF = 64 * 2 * 4;  // BN scale / shift of the block's 64 input channels (f32)
+constexpr int WT_LDS = WT_SLAB + (WT_NS + 1) * WT_ATILE + WT_COEF;
+
+struct WtParams {
+  const void* dy;      // [Nb, H, W, Cout] 16-bit
+  const void* x;       // [Nb, H, W, Cin] 16-bit (PRE-BatchNorm when pro_sc is set)
+  float* slab;         // [splits][Cout][9 Cin]
+  const float* pro_sc; const float* pro_sh;   // optional BN+ReLU applied to X (channel Cin)
+  int Nb, H, W, Cin, Cout;
+  int Hp, Wp, Kp;      // padded geometry, Kp = Nb Hp Wp
+  int kb;              // padded rows per block (multiple of 64)
+  int nsteps;          // kb / 64
+  int halo;            // Wp + 1
+  int co_tiles, ci_tiles;
+  FastDiv dHpWp, dWp;
+};
+
+__device__ __forceinline__ void wt_dma16(__amdgpu_buffer_rsrc_t r, char* lds, uint32_t voff) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)lds, 16,
+                                           (int)voff, 0, 0, 0);
+}
+template <int N> __device__ __forceinline__ void wt_vm_wait() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+// chunk swizzle of a 64-column (128-B) k-major row, conv_gemm.hip col_swz<64>: conflict-free
+// transposed fragment reads for ANY row offset (rows r .. r+3, r+8 .. r+11 of a read fall on 8
+// distinct (row parity, swizzle) classes for every r)
+__device__ __forceinline__ int wt_swz(int row) { return (((row >> 1) & 1) << 1) | (((row >> 3) & 1) << 2); }
+
+constexpr uint32_t WT_OOB = 0x80000000u;
+
+template <int DT, bool PRO>
+__global__ __launch_bounds__(WT_NT, 1) void wgrad_tap_kernel(WtParams p_arg) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  typedef const __attribute__((address_space(4))) WtParams KP;
+  KP& p = *(KP*)__builtin_amdgcn_kernarg_segment_ptr();
+#else
+  const WtParams& p = p_arg;
+#endif
+  __shared__ __attribute__((aligned(16))) char smem[WT_LDS];
+  char* slab = smem;
+  char* atl = smem + WT_SLAB;
+  float* coef = reinterpret_cast<float*>(smem + WT_SLAB + (WT_NS + 1) * WT_ATILE);   // [2][64]
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = wid & 1, wc = wid >> 1;
+  const int ntile = p.co_tiles * p.ci_tiles;
+  const int lt = (int)xcd_remap(blockIdx.x, gridDim.x);   // the tiles of one split share an XCD
+  const int split = lt / ntile, tile = lt - split * ntile;
+  const int cot = tile / p.ci_tiles, cit = tile - cot * p.ci_tiles;
+  // padded row q -> byte offset of element c_elems of its pixel in an NHWC tensor of C channels, or
+  // OOB for padding / out-of-range rows
+  const FastDiv dHpWp = p.dHpWp, dWp = p.dWp;
+  const int Kp = p.Kp, H = p.H, W = p.W;
+  auto wt_pix = [&](int q, int C, int c_elems) __attribute__((always_inline)) -> uint32_t {
+    if (q < 0 || q >= Kp) return WT_OOB;
+    const uint32_t n = fdiv((uint32_t)q, dHpWp), rem = (uint32_t)q - n * dHpWp.d;
+    const uint32_t yp = fdiv(rem, dWp), xp = rem - yp * dWp.d;
+    if (yp < 1 || yp > (uint32_t)H || xp < 1 || xp > (uint32_t)W) return WT_OOB;
+    return ((((n * H + yp - 1) * W + xp - 1) * (uint32_t)C) + (uint32_t)c_elems) * 2u;
+  };
+  const int q0 = split * p.kb;
+  const int q_end = min(q0 + p.kb, p.Kp);
+  const int ns = p.nsteps;
+  const __amdgpu_buffer_rsrc_t rdy = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<void*>(p.dy), (short)0, (int)((uint32_t)p.Nb * p.H * p.W * p.Cout * 2u), 0x00020000);
+  const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<void*>(p.x), (short)0, (int)((uint32_t)p.Nb * p.H * p.W * p.Cin * 2u), 0x00020000);
+
+  // X rows: step s reads [q0 + 64 s - halo, q0 + 64 s + 64 + halo); rows are issued in 8-row
+  // pieces from the 8-aligned base b0; fr(s) = first row not needed by steps <= s (8-aligned)
+  const int b0 = (q0 - p.halo) & ~7;
+  auto fr = [&](int s) { return (q0 + 64 * (s + 1) + p.halo + 7) & ~7; };
+  const int lrow = lane >> 3, lch = lane & 7;
+  // one 8-row X piece starting at row r (8-aligned): lane -> row r + lrow, physical chunk lch
+  auto x_piece = [&](int r, bool live) __attribute__((always_inline)) {
+    const int row = r + lrow;
+    const int lc = lch ^ wt_swz(row);
+    wt_dma16(rx, slab + (r & (WT_RING - 1)) * 128, live ? wt_pix(row, p.Cin, cit * 64 + lc * 8) : WT_OOB);
+  };
+  // the dY tile of step s, piece w: rows q0 + 64 s + 8 w + lrow (rows past the range: zero)
+  auto a_piece = [&](int s, int w) __attribute__((always_inline)) {
+    const int rl = 8 * w + lrow;
+    const int q = q0 + 64 * s + rl;
+    const int lc = lch ^ wt_swz(rl);
+    const uint32_t off = q < q_end ? wt_pix(q, p.Cout, cot * 64 + lc * 8) : WT_OOB;
+    wt_dma16(rdy, atl + (s % (WT_NS + 1)) * WT_ATILE + 8 * w * 128, off);
+  };
+  // prologue: issue the operands of steps 0 .. NS-1, in step order (step 0 carries the X rows
+  // [b0, fr(0)), every later step the 64 rows [fr(s-1), fr(s)) and its dY tile). The counted
+  // waits below only ever leave YOUNGER groups in flight, so the size of the step-0 group (which
+  // differs between waves) never enters a count.
+  for (int r = b0 + 8 * wid; r < fr(0); r += 64) x_piece(r, true);
+  a_piece(0, wid);
+#pragma unroll
+  for (int s = 1; s < WT_NS; ++s) {
+    x_piece(fr(s - 1) + 8 * wid, s < ns);
+    a_piece(s, wid);
+  }
+  // BN+ReLU in LDS of the X rows [r_lo, r_hi) (padding rows stay 0): one 16-B chunk per thread
+  // per 64 rows; the coefficients of the block's 64 channels come from LDS
+  auto pro_rows = [&](int r_lo, int r_hi) __attribute__((always_inline)) {
+    if constexpr (PRO) {
+      for (int rr = r_lo + (tid >> 3); rr < r_hi; rr += WT_NT / 8) {
+        if (wt_pix(rr, p.Cin, 0) == WT_OOB) continue;
+        const int lc = lch ^ wt_swz(rr);
+        i32x4* cp = reinterpret_cast<i32x4*>(slab + (rr & (WT_RING - 1)) * 128 + lch * 16);
+        i32x4 v = *cp;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const f32x2 sc = *reinterpret_cast<const f32x2*>(coef + lc * 8 + 2 * k);
+          const f32x2 sh = *reinterpret_cast<const f32x2*>(coef + 64 + lc * 8 + 2 * k);
+          const f32x2 u = unpack2<DT>((uint32_t)v[k]);
+          const f32x2 f = f32x2{fmaxf(__builtin_fmaf(u.x, sc.x, sh.x), 0.f),
+                                fmaxf(__builtin_fmaf(u.y, sc.y, sh.y), 0.f)};
+          v[k] = (int)pack2<DT>(f);
+        }
+        *cp = v;
+      }
+    }
+  };
+  if constexpr (PRO) {
+    if (tid < 64) {
+      coef[tid] = p.pro_sc[cit * 64 + tid];
+      coef[64 + tid] = p.pro_sh[cit * 64 + tid];
+    }
+    // step 0's rows: landed (every wave's step-0 group), then transformed before the loop's first
+    // barrier publishes them
+    wt_vm_wait<2 * (WT_NS - 1)>();
+    __syncthreads();
+    pro_rows(b0, fr(0));
+  }
+
+  f32x4 acc[2][9];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 9; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  // per column tile j of the wave: tap row shift and channel base (wave-uniform)
+  int dsh[9], cb[9];
+#pragma unroll
+  for (int j = 0; j < 9; ++j) {
+    const int col = wc * 144 + 16 * j;
+    const int t = col >> 6;
+    dsh[j] = (t / 3 - 1) * p.Wp + (t % 3 - 1);
+    cb[j] = col & 63;
+  }
+  const int g = lane >> 4, fi = lane & 15, fq = fi >> 2, fp = fi & 3;
+  // Fragment addresses, precomputed per lane (the transposed reads of frag_col, conv_gemm.hip):
+  // lane reads rows L, L + 4 (L = 8g + fq) of a 32-row substep, 8 bytes at column chunk
+  // cbase/8 + fp/2 (+ 8 B for odd fp). X rows of tap shift d at step s, substep s2 are
+  // q0 + 64 s + 32 s2 + d + L: the ring row advances by 32 per substep, and as 32 = 0 mod 16 the
+  // row swizzle (bits 1 and 3) is the same at every step -- so each address is its step-0 value
+  // plus (64 s + 32 s2) * 128 B, wrapped at the 64 KiB ring: one add and one and per address.
+  const int L0 = 8 * g + fq;
+  const int half = (fp & 1) << 3;
+  int xa[9][2];    // X: ring byte offset at s = s2 = 0, rows L0 / L0 + 4
+#pragma unroll
+  for (int j = 0; j < 9; ++j)
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int r = q0 + dsh[j] + L0 + 4 * h;
+      const int chunk = cb[j] / 8 + (fp >> 1);
+      xa[j][h] = (r & (WT_RING - 1)) * 128 + ((chunk ^ wt_swz(r)) << 4) + half;
+    }
+  int aa[2][2][2];   // dY tile: byte offset of substep s2, co tile i, row L0 / L0 + 4
+#pragma unroll
+  for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int k = s2 * 32 + L0 + 4 * h;
+        const int chunk = (wr * 32 + 16 * i) / 8 + (fp >> 1);
+        aa[s2][i][h] = k * 128 + ((chunk ^ wt_swz(k)) << 4) + half;
+      }
+
+  for (int s = 0; s < ns; ++s) {
+    // step s's operands have landed -- with the prologue, step s+1's too (it transforms them now)
+    if constexpr (PRO) wt_vm_wait<2 * (WT_NS - 2)>();
+    else wt_vm_wait<2 * (WT_NS - 1)>();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    // the operands of step s + NS (past the range: out-of-bounds no-ops, so the count per step
+    // stays 2 per wave); their slots were last read in step s - 1
+    x_piece(fr(s + WT_NS - 1) + 8 * wid, s + WT_NS < ns);
+    a_piece(s + WT_NS, wid);
+    // BN+ReLU of the rows step s+1 adds: nothing in step s reads them (rows >= fr(s))
+    if (s + 1 < ns) pro_rows(fr(s), fr(s + 1));
+    const char* sa = atl + (s % (WT_NS + 1)) * WT_ATILE;
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2) {
+      s16x8 fa[2], fb[9];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {   // dY: rows s2*32 + L0 (+4) of the tile, co column
+        const s16x4 v0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(s16x4, sa + aa[s2][i][0]));
+        const s16x4 v1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(s16x4, sa + aa[s2][i][1]));
+        fa[i] = s16x8{v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
+      }
+      const int roff = (64 * s + 32 * s2) * 128;
+#pragma unroll
+      for (int j = 0; j < 9; ++j) {   // X: ring rows of the tap shift, this step and substep
+        const int a0 = (xa[j][0] + roff) & (WT_SLAB - 1);
+        const int a1 = (xa[j][1] + roff) & (WT_SLAB - 1);
+        const s16x4 v0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(s16x4, slab + a0));
+        const s16x4 v1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(s16x4, slab + a1));
+        fb[j] = s16x8{v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
+      }
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 9; ++j) acc[i][j] = mfma16<DT>(fb[j], fa[i], acc[i][j]);
+      __builtin_amdgcn_s_setprio(0);
+    }
+  }
+  wt_vm_wait<0>();   // the trailing no-op DMAs, before the block can exit
+
+  // slab[split][co][t * Cin + ci]: lane = co row (lane & 15) of tile i, 4 consecutive columns
+  const size_t N = 9 * (size_t)p.Cin;
+  float* out = p.slab + (size_t)split * p.Cout * N;
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int co = cot * 64 + wr * 32 + 16 * i + fi;
+#pragma unroll
+    for (int j = 0; j < 9; ++j) {
+      const int col = wc * 144 + 16 * j;
+      const int t = col >> 6;
+      const int ci = cit * 64 + (col & 63) + 4 * g;
+      *reinterpret_cast<f32x4*>(out + (size_t)co * N + (size_t)t * p.Cin + ci) = acc[i][j];
+    }
+  }
+}
+
+FastDiv wt_div(uint32_t d) {
+  FastDiv f;
+  f.d = d;
+  uint32_t s = 0;
+  while ((1ull << s) < d) ++s;
+  f.s = s;
+  f.m = (uint32_t)(((1ull << 32) * ((1ull << s) - d)) / d + 1);
+  return f;
+}
+
+}  // namespace
+
+extern "C" {
+
+// Split-K weight-gradient slabs of a 3x3 / stride-1 / pad-1 convolution, tap-reuse form:
+// slab [splits][Cout][9 Cin] (f32) -- pda_wgrad_reduce sums them like the generic kernel's.
+// dy [Nb,H,W,Cout], x [Nb,H,W,Cin] 16-bit; pro_sc / pro_sh: BN+ReLU of a PRE-BatchNorm x (or null).
+// kb: padded rows per split (multiple of 64); splits = ceil(Nb (H+2)(W+2) / kb). Cin, Cout multiples
+// of 64; W <= 59 (the X ring holds 4 steps + the two halos). Returns -2 on a shape it does not take.
+int pda_wgrad_tap(const void* dy, const void* x, float* slab, const float* pro_sc,
+                  const float* pro_sh, int Nb, int H, int W, int Cin, int Cout, int kb, int splits,
+                  int dt, hipStream_t st) {
+  if ((Cin % 64) || (Cout % 64) || kb <= 0 || (kb % 64) || W > 59 || H <= 0 || W <= 0)
+    return -2;
+  if ((pro_sc == nullptr) != (pro_sh == nullptr)) return -2;
+  WtParams p{};
+  p.dy = dy; p.x = x; p.slab = slab; p.pro_sc = pro_sc; p.pro_sh = pro_sh;
+  p.Nb = Nb; p.H = H; p.W = W; p.Cin = Cin; p.Cout = Cout;
+  p.Hp = H + 2; p.Wp = W + 2;
+  const long long kp = (long long)Nb * p.Hp * p.Wp;
+  if (kp >= (1ll << 30) || (long long)Nb * H * W * (Cin > Cout ? Cin : Cout) * 2 >= 0x7fffffffll) return -4;
+  p.Kp = (int)kp;
+  p.kb = kb; p.nsteps = kb / 64; p.halo = p.Wp + 1;
+  if ((long long)splits * kb < kp || (long long)(splits - 1) * kb >= kp) return -3;
+  p.co_tiles = Cout / 64; p.ci_tiles = Cin / 64;
+  p.dHpWp = wt_div((uint32_t)(p.Hp * p.Wp));
+  p.dWp = wt_div((uint32_t)p.Wp);
+  const dim3 grid(splits * p.co_tiles * p.ci_tiles);
+  const bool pro = pro_sc != nullptr;
+  if (dt == DT_BF16) {
+    if (pro) hipLaunchKernelGGL((wgrad_tap_kernel<DT_BF16, true>), grid, dim3(WT_NT), 0, st, p);
+    else hipLaunchKernelGGL((wgrad_tap_kernel<DT_BF16, false>), grid, dim3(WT_NT), 0, st, p);
+  } else if (dt == DT_F16) {
+    if (pro) hipLaunchKernelGGL((wgrad_tap_kernel<DT_F16, true>), grid, dim3(WT_NT), 0, st, p);
+    else hipLaunchKernelGGL((wgrad_tap_kernel<DT_F16, false>), grid, dim3(WT_NT), 0, st, p);
+  } else {
+    return -1;
+  }
+  return (int)hipGetLastError();
+}
+
+}  // extern "C"

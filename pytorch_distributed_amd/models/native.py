@@ -147,6 +147,9 @@ class NativeResNet(nn.Module):
         # which stages a = relu(bn3(y3) + r) from y3 and r and writes a once (FWD_TAIL); blocks whose
         # successor has a shortcut conv keep the apply pass (PDA_TAIL_FUSE=0: every tail does)
         self.tail_fuse = os.environ.get("PDA_TAIL_FUSE", "1") != "0"
+        # the second stream's split-K weight-gradient reductions batched into one launch per stage
+        # (per block under DDP) instead of one per conv (ops/native_ops.py ReduceBatch)
+        self.reduce_batching = os.environ.get("PDA_REDUCE_BATCH", "1") != "0"
         # consumer-side tail fold of the Bottleneck BN backward (see _block_backward)
         # ("0" off, "1" every stage, or the stages to fold, e.g. "12" = layer1 and layer2). Default
         # layer1-3: in-step A/B at the bench config (profiles/ab_r4.md) 28.26 ms off, 27.89 all
@@ -731,6 +734,13 @@ class NativeResNet(nn.Module):
                 fn(self.ws_w)
         self._wbatch.clear()
 
+    def _flush_reduces(self) -> None:
+        """Run the queued split-K reductions of the second stream's weight gradients (one launch)."""
+        rb = self.ws_w.reduce_batch
+        if rb is not None and rb.items:
+            with torch.cuda.stream(self._side):
+                rb.flush()
+
     def _grads_ready(self, red, upto: int) -> None:
         """DDP bucket readiness: the bucket's BN grads come from the main stream, its conv weight
         grads from the wgrad stream -- launch the all-reduce after both."""
@@ -738,6 +748,7 @@ class NativeResNet(nn.Module):
             red.grads_ready(upto)
             return
         self._flush_wgrad()
+        self._flush_reduces()
         self._side.wait_stream(torch.cuda.current_stream(self.device))
         with torch.cuda.stream(self._side):
             red.grads_ready(upto)
@@ -763,6 +774,12 @@ class NativeResNet(nn.Module):
             red.reset()
         Nb = dlog16.shape[0]
         ws = self.ws
+        # the second stream's split-K reductions are queued and run ONE launch per stage (per block
+        # under DDP, whose buckets need each block's gradients) instead of one per weight gradient
+        # (eager launches only: a graph capture records them where they are issued)
+        self.ws_w.reduce_batch = (K.ReduceBatch(self.ws_w) if self.reduce_batching and
+                                  self._side is not None and self._wbatch is None and
+                                  not self.defer_side else None)
         # ---- fc
         gfc = ConvGeom(Nb, 1, 1, self.feat_dim, self.fc_rows, 1, 1, 1, 0)
 
@@ -790,6 +807,8 @@ class NativeResNet(nn.Module):
             dx_main, shortcut_g, tail = self._block_backward(b, rec, tail, prev, acc)
             if not self.defer_side and (self._wbatch_mode == "block" or b.ds is not None):
                 self._flush_wgrad()
+            if bi == 0 or self.blocks[bi - 1].name[:6] != b.name[:6]:
+                self._flush_reduces()   # (stage boundary; under DDP _grads_ready flushes per block)
             if red is not None:
                 self._grads_ready(red, self.block_bounds[nblk - bi])
             if self.segment_hook is not None:
@@ -827,7 +846,10 @@ class NativeResNet(nn.Module):
                      self.dbeta(u), dy0, g1=dA0, accumulate=acc)
         if bna:
             def stem_wgrad(w):
+                # (stem_s2d_grad reads the reduced gradient at once: its reduce runs unbatched)
+                rb, w.reduce_batch = w.reduce_batch, None
                 K.conv_wgrad(dz0, x0, g0, self.stem_wgrad, w, bna=(y0, k0), wscale=self.wgrad_scale)
+                w.reduce_batch = rb
                 K.stem_s2d_grad(self.stem_wgrad, self.wgrad_view(u), accumulate=acc)
             if self._side is not None and not self.defer_side:
                 # the main stream is idle after the stem's BN backward while the second stream still
@@ -837,11 +859,15 @@ class NativeResNet(nn.Module):
                 self._wgrad(stem_wgrad, dz0, y0, x0, k0)
         else:
             def stem_wgrad(w):
+                rb, w.reduce_batch = w.reduce_batch, None
                 K.conv_wgrad(dy0, x0, g0, self.stem_wgrad, w, wscale=self.wgrad_scale)
+                w.reduce_batch = rb
                 K.stem_s2d_grad(self.stem_wgrad, self.wgrad_view(u), accumulate=acc)
             self._wgrad(stem_wgrad, dy0, x0)
         if not self.defer_side:
             self._flush_wgrad()
+            self._flush_reduces()
+            self.ws_w.reduce_batch = None
             if self._side is not None:   # join: the optimizer step reads every gradient
                 torch.cuda.current_stream(self.device).wait_stream(self._side)
                 self._keep.clear()
@@ -1248,6 +1274,11 @@ class NativeTrainer:
             self.scaler = LossScaler()
         self._loss = None
         self.graphed = None
+        if graph:
+            from ..runtime.graphs import graphs_unsafe_warning, single_queue_graphs
+            if not single_queue_graphs():
+                graphs_unsafe_warning("NativeTrainer(graph=True)")
+                graph = False
         if graph:
             if world > 1:
                 raise ValueError("graph capture of the distributed step is not enabled (RCCL "

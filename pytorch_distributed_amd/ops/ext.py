@@ -69,6 +69,14 @@ class BnBwdOut(C.Structure):
                 ("dgamma", C.c_void_p * 2), ("dbeta", C.c_void_p * 2), ("k", C.c_void_p)]
 
 
+class RedDescC(C.Structure):
+    """One split-K reduction of pda_wgrad_reduce_batch (csrc/conv_gemm.hip RedDescC)."""
+    _fields_ = [("slab", C.c_void_p), ("grad", C.c_void_p), ("ck", C.c_void_p), ("cB", C.c_void_p),
+                ("cs", C.c_void_p)] + [(n, C.c_int) for n in
+                                       ("splits", "M", "N", "cin_log2", "cin_real", "pitch",
+                                        "accumulate")] + [("scale", C.c_float)]
+
+
 _V, _I, _F, _L, _U, _D = C.c_void_p, C.c_int, C.c_float, C.c_longlong, C.c_uint, C.c_double
 _SIGS = {
     "pda_conv_fwd": [C.POINTER(ConvDesc), _V, _V, _I, _V, _I, _I, _V, _V, _I, _V, _V, _I, _I, _I, _V],
@@ -78,11 +86,13 @@ _SIGS = {
     "pda_conv_dgrad_bnf": [C.POINTER(ConvDesc), _V, _V, _V, C.POINTER(BnEpi), _V, _V, _V, _V, _I, _I,
                            _I, _V],
     "pda_bn_fold": [_V, _V, _I, _I, _V, _V, _I, _V],
+    "pda_wgrad_tap": [_V, _V, _V, _V, _V, _I, _I, _I, _I, _I, _I, _I, _I, _V],
     "pda_stem_fwd": [_V, _V, _V, _V, _I, _I, _I, _I, _I, _V],
     "pda_conv_wgrad": [C.POINTER(ConvDesc), _V, _V, _V, _I, _I, _V, _V, _I, _I, _I, _V],
     "pda_conv_wgrad_bna": [C.POINTER(ConvDesc), _V, _V, _V, _V, _V, _V, _V, _I, _I, _V, _V, _I, _I, _I,
                            _V],
     "pda_wgrad_reduce": [_V, _V, _I, _I, _I, _I, _I, _I, _F, _I, _V, _V, _V, _V],
+    "pda_wgrad_reduce_batch": [C.POINTER(RedDescC), _I, _V],
     "pda_conv_wgrad_gram": [C.POINTER(ConvDesc), _V, _V, _V, _V, _I, _I, _I, _I, _I, _V],
     "pda_fold_bgemm": [_V, _V, _I, _I, _V, _I, _V],
     "pda_bn_fwd_stats": [_V, _I, _I, _I, _I, _I, _V, _V, C.POINTER(BnFwdOut), _I, _V],

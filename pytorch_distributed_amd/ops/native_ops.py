@@ -62,6 +62,41 @@ class ConvGeom:
                         self.ho, self.wo)
 
 
+class ReduceBatch:
+    """Split-K reductions queued instead of launched one by one (:func:`conv_wgrad` on a
+    :class:`Workspace` whose ``reduce_batch`` is set): each queued weight gradient gets a slab of its
+    own, and :meth:`flush` reduces all of them in ONE launch (csrc/conv_gemm.hip
+    wgrad_reduce_batch_kernel: the same fixed-order sums, deterministic). The owner flushes on the
+    stream the weight gradients ran on, before anything reads the gradients."""
+
+    MAX = 24
+
+    def __init__(self, ws: "Workspace") -> None:
+        self.ws = ws
+        self.items = []
+        self._keep = []
+
+    def slab(self, numel: int) -> torch.Tensor:
+        if len(self.items) >= self.MAX:
+            self.flush()
+        return self.ws.get(f"wgrad_slab_b{len(self.items)}", numel)
+
+    def add(self, slab, grad, splits, M, N, cin_log2, cin_real, pitch, scale, accumulate,
+            ck=None, cB=None, cs=None) -> None:
+        self.items.append(ext.RedDescC(ptr(slab), ptr(grad), ptr(ck), ptr(cB), ptr(cs), splits, M, N,
+                                       cin_log2, cin_real, pitch, int(accumulate), float(scale)))
+        self._keep.extend(t for t in (ck, cB, cs) if t is not None)
+
+    def flush(self) -> None:
+        if not self.items:
+            return
+        arr = (ext.RedDescC * len(self.items))(*self.items)
+        check(ext.lib().pda_wgrad_reduce_batch(arr, len(self.items), stream(self.ws.device)),
+              "wgrad_reduce_batch")
+        self.items = []
+        self._keep = []
+
+
 class Workspace:
     """Grow-only scratch buffers (split-K slabs, BN partials) reused by every layer on a stream.
 
@@ -74,6 +109,7 @@ class Workspace:
         self._bufs = {}
         self._retired = []   # outgrown buffers stay allocated: a captured HIP graph may use them
         self.sync_comm = None
+        self.reduce_batch: Optional[ReduceBatch] = None   # set: conv_wgrad queues its reduce
 
     def get(self, name: str, numel: int, dtype=torch.float32) -> torch.Tensor:
         b = self._bufs.get(name)
@@ -295,7 +331,7 @@ def _conv_fwd_tail(y3, w, g: ConvGeom, out, pro, tail: TailIn, stats, bn, before
     return out
 
 
-_STEM_FWD = os.environ.get("PDA_STEM_FWD", "1") != "0"
+_STEM_FWD = True   # the stem conv on csrc/stem.hip (False: the generic 128x64 tile, tests)
 # persistent blocks of the stem kernel: 256 / 512 / 1024 / 2048 measured 305 / 267 / 258 / 278 us
 # (profiles/ab_r4.md section 15); 0 = the kernel's default, 1024
 _STEM_GRID = 0
@@ -641,6 +677,9 @@ def conv_wgrad(dy: torch.Tensor, x: torch.Tensor, g: ConvGeom, grad: torch.Tenso
     the plain dz^T x, and the split-K reduce writes k1*(dz^T x) + k2*B + k3*s^T per row, with
     B = W Gram(x) and s the column sums of x (:func:`conv_wgrad_gram`, :func:`fold_bgemm`)."""
     Nb = dy.shape[0]
+    if (tile is None and target_blocks is None and bna is None and combine is None
+            and cin_real is None and wgrad_tap_ok(g, dy.dtype)):
+        return conv_wgrad_tap(dy, x, g, grad, ws, scale, accumulate, pro)
     bm, bn, splits, k_chunk = wgrad_plan(g, Nb, tile, target_blocks, f32=dy.dtype == torch.float32,
                                          dma=dy.dtype != torch.float32 and pro is None and bna is None,
                                          wscale=wscale, bna=bna is not None)
@@ -649,7 +688,8 @@ def conv_wgrad(dy: torch.Tensor, x: torch.Tensor, g: ConvGeom, grad: torch.Tenso
         # the same split-K chunks (same accumulation order per element: bitwise the same result)
         bn = 128
     M, N = g.Cout, g.R * g.S * g.Cin
-    slab = ws.get("wgrad_slab", splits * M * N)
+    rb = ws.reduce_batch if N % 4 == 0 else None
+    slab = rb.slab(splits * M * N) if rb is not None else ws.get("wgrad_slab", splits * M * N)
     d = g.desc(Nb)
     st = stream(dy.device)
     kdt = _kdt(dy)
@@ -669,10 +709,63 @@ def conv_wgrad(dy: torch.Tensor, x: torch.Tensor, g: ConvGeom, grad: torch.Tenso
         check(rc, "conv_wgrad")
     cr = g.Cin if cin_real is None else cin_real
     ck, cB, cs = combine if combine is not None else (None, None, None)
+    if rb is not None:
+        rb.add(slab, grad, splits, M, N, int(math.log2(g.Cin)), cr, g.R * g.S * cr, scale,
+               accumulate, ck, cB, cs)
+        return grad
     rc = ext.lib().pda_wgrad_reduce(ptr(slab), ptr(grad), splits, M, N, int(math.log2(g.Cin)), cr,
                                     g.R * g.S * cr, float(scale), int(accumulate), ptr(ck), ptr(cB),
                                     ptr(cs), st)
     check(rc, "wgrad_reduce")
+    return grad
+
+
+# which 3x3 stride-1 weight gradients run the tap-reuse kernel (csrc/wgrad_tap.hip), by image width
+# ("0": none); the generic tiles re-read X per (tap, channel) column tile and dY per N-tile
+_WGRAD_TAP = {int(v) for v in os.environ.get("PDA_WGRAD_TAP", "56,28").split(",") if v.strip() not in ("", "0")}
+_WGRAD_TAP_BLOCKS = 256   # one 104 KiB block per CU: the split count is the block count
+
+
+def wgrad_tap_ok(g: ConvGeom, dtype: torch.dtype) -> bool:
+    """Whether :func:`conv_wgrad` runs the tap-reuse kernel for this conv: 3x3 / stride 1 / pad 1,
+    16-bit, channel counts in 64-column tiles, image width in the ``PDA_WGRAD_TAP`` set (<= 59)."""
+    return (dtype in (torch.bfloat16, torch.float16) and g.R == 3 and g.S == 3 and g.stride == 1
+            and g.pad == 1 and g.Ho == g.H and g.Wo == g.W and g.W <= 59 and g.W in _WGRAD_TAP
+            and g.Cin % 64 == 0 and g.Cout % 64 == 0
+            and getattr(ext.lib(), "pda_wgrad_tap", None) is not None)
+
+
+def wgrad_tap_plan(g: ConvGeom, Nb: int, blocks: int = _WGRAD_TAP_BLOCKS) -> Tuple[int, int]:
+    """(kb, splits): padded pixel rows per split (a multiple of 64) and the split count of the
+    tap-reuse weight gradient for ~``blocks`` blocks over its (Cout / 64) x (Cin / 64) tiles."""
+    kp = Nb * (g.H + 2) * (g.W + 2)
+    tiles = (g.Cout // 64) * (g.Cin // 64)
+    want = max(1, blocks // tiles)
+    kb = max(64, math.ceil(kp / want / 64) * 64)
+    return kb, math.ceil(kp / kb)
+
+
+def conv_wgrad_tap(dy: torch.Tensor, x: torch.Tensor, g: ConvGeom, grad: torch.Tensor,
+                   ws: "Workspace", scale: float = 1.0, accumulate: bool = False,
+                   pro: Optional[Tuple[torch.Tensor, torch.Tensor]] = None) -> torch.Tensor:
+    """grad (f32 OHWI) = scale * dW of a 3x3 stride-1 conv on the tap-reuse kernel: each block
+    loads its pixel range of dY and X once for all nine taps (csrc/wgrad_tap.hip), split-K slabs
+    reduced by the same fixed-order launch as :func:`conv_wgrad`. ``pro`` as there."""
+    Nb = dy.shape[0]
+    kb, splits = wgrad_tap_plan(g, Nb)
+    M, N = g.Cout, 9 * g.Cin
+    rb = ws.reduce_batch
+    slab = rb.slab(splits * M * N) if rb is not None else ws.get("wgrad_slab", splits * M * N)
+    st = stream(dy.device)
+    L = ext.lib()
+    check(L.pda_wgrad_tap(ptr(dy), ptr(x), ptr(slab), ptr(pro[0] if pro else None),
+                          ptr(pro[1] if pro else None), Nb, g.H, g.W, g.Cin, g.Cout, kb, splits,
+                          _kdt(dy), st), "wgrad_tap")
+    if rb is not None:
+        rb.add(slab, grad, splits, M, N, int(math.log2(g.Cin)), g.Cin, N, scale, accumulate)
+        return grad
+    check(L.pda_wgrad_reduce(ptr(slab), ptr(grad), splits, M, N, int(math.log2(g.Cin)), g.Cin, N,
+                             float(scale), int(accumulate), None, None, None, st), "wgrad_reduce")
     return grad
 
 

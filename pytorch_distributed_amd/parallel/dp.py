@@ -270,8 +270,14 @@ class DataParallel(nn.Module):
         """The HIP-graph step serves the native engine without loss scaling (the DP script's
         configuration). ``MX_GRAPH=0`` forces the eager autograd path."""
         import os
-        return (self._native and bool(self.device_ids) and (scaler is None or not scaler.enabled)
-                and os.environ.get("MX_GRAPH", "1") != "0")
+        ok = (self._native and bool(self.device_ids) and (scaler is None or not scaler.enabled)
+              and os.environ.get("MX_GRAPH", "1") != "0")
+        if ok:
+            from ..runtime.graphs import graphs_unsafe_warning, single_queue_graphs
+            if not single_queue_graphs():   # replica graphs need the single-queue graph launch
+                graphs_unsafe_warning("DataParallel")
+                return False
+        return ok
 
     def train_step(self, samples: torch.Tensor, labels: torch.Tensor, optimizer,
                    graph: bool = True) -> torch.Tensor:
@@ -290,6 +296,11 @@ class DataParallel(nn.Module):
     def train_step_chunks(self, xs, ys, optimizer, graph: bool = True) -> torch.Tensor:
         """:meth:`train_step` on per-replica input chunks (e.g. generated on each GPU directly,
         skipping the scatter from ``device_ids[0]``)."""
+        if graph:
+            from ..runtime.graphs import graphs_unsafe_warning, single_queue_graphs
+            if not single_queue_graphs():   # the replica graphs need the single-queue launch
+                graphs_unsafe_warning("DataParallel")
+                graph = False
         self._broadcast_state()
         B = sum(x.shape[0] for x in xs)
         if getattr(self, "_graphs", None) is None or [x.shape for x in xs] != self._graph_shapes:

@@ -22,13 +22,15 @@ single-GPU entrypoint's training loop (``MX_GRAPH=1``, :mod:`pytorch_distributed
 """
 from __future__ import annotations
 
+import os
 from typing import Callable, Optional
 
 import torch
 
 from ..ops import native_ops as K
 
-__all__ = ["GraphedNativeStep", "native_train_step"]
+__all__ = ["GraphedNativeStep", "native_train_step", "single_queue_graphs",
+           "request_single_queue_graphs"]
 
 
 def native_train_step(model, opt, x: torch.Tensor, y: torch.Tensor, scaler=None) -> torch.Tensor:
@@ -54,6 +56,44 @@ def native_train_step(model, opt, x: torch.Tensor, y: torch.Tensor, scaler=None)
         opt.step()
     opt.zero_grad()
     return loss
+
+
+# The HIP runtime's multi-queue graph launch (a graph's parallel branches spread over internal
+# streams) segfaulted inside hipGraphLaunch -- an out-of-range read of a per-graph stream list in
+# libamdhip64.so -- on this framework's DataParallel replica graphs: at once in `bench.py --dp`, and
+# after ~85 tests of one GPU session (profiles/ab_r4.md section 7; standalone reproducer with the
+# same capture shape: tools/graph_queue_repro.py, profiles/ab_r5.md). With
+# DEBUG_HIP_FORCE_GRAPH_QUEUES=1 graphs launch on one queue and never crashed. The variable is
+# read ONCE, when HIP initialises, so it is set by the entry points that replay graphs before their
+# first HIP call (resnet_dp.py, `bench.py --dp / --graph 1`, the GPU test session), and every graph
+# path checks it and falls back to eager launches (with a warning) when it is not in effect.
+GRAPH_QUEUES_VAR = "DEBUG_HIP_FORCE_GRAPH_QUEUES"
+
+
+def single_queue_graphs() -> bool:
+    """Whether HIP graphs launch on one queue in this process (see GRAPH_QUEUES_VAR)."""
+    return os.environ.get(GRAPH_QUEUES_VAR) == "1"
+
+
+def request_single_queue_graphs() -> bool:
+    """Ask for single-queue graph launch if HIP has not started yet in this process (an explicit
+    setting is kept); returns whether graph replay is safe here (:func:`single_queue_graphs`)."""
+    if os.environ.get(GRAPH_QUEUES_VAR) is None and not torch.cuda.is_initialized():
+        os.environ[GRAPH_QUEUES_VAR] = "1"
+    return single_queue_graphs()
+
+
+_WARNED = set()
+
+
+def graphs_unsafe_warning(what: str) -> None:
+    if what in _WARNED:
+        return
+    _WARNED.add(what)
+    import warnings
+    warnings.warn(f"{what}: HIP graph replay disabled -- {GRAPH_QUEUES_VAR}=1 was not set before "
+                  "HIP started (the runtime's multi-queue graph launch crashes on these graphs); "
+                  "launching eagerly", RuntimeWarning)
 
 
 class GraphedNativeStep:

@@ -120,6 +120,10 @@ def _graphed_step(model, optimizer, ctx: Context):
         return None
     if not hasattr(model, "native_forward") or hasattr(model, "replicas"):
         return None
+    from .runtime.graphs import graphs_unsafe_warning, single_queue_graphs
+    if not single_queue_graphs():
+        graphs_unsafe_warning("MX_GRAPH=1")
+        return None
     g = ctx.extra.get("graphed")
     if g is None:
         from .runtime.graphs import GraphedNativeStep
@@ -303,6 +307,9 @@ def run(cfg: RunConfig, mode: str, local_rank: int = 0, nprocs: Optional[int] = 
     """``main()`` of the reference scripts. Returns the best top-1 accuracy."""
     from .launch import dist_env, init_distributed
     distributed = mode in ("ddp", "ddp_amp")
+    if mode == "dp" or cfg.graph:   # before the first HIP call (resolve_device sets the device)
+        from .runtime.graphs import request_single_queue_graphs
+        request_single_queue_graphs()
     device = resolve_device(cfg, local_rank)
     dtype = resolve_dtype(cfg, device)
     engine = resolve_engine(cfg, device, dtype)

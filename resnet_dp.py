@@ -4,9 +4,14 @@ Global batch 3200 (= 400 per GPU on 8 GPUs), split across devices by
 pytorch_distributed_amd.parallel.DataParallel. No CLI arguments needed; optional flags
 mirror the MX_* env vars (``--help``).
 """
+import os
 import sys
 
-from pytorch_distributed_amd.config import config_for
+# the DataParallel replicas replay HIP graphs: single-queue graph launch, set before HIP starts
+# (pytorch_distributed_amd/runtime/graphs.py GRAPH_QUEUES_VAR)
+os.environ.setdefault("DEBUG_HIP_FORCE_GRAPH_QUEUES", "1")
+
+from pytorch_distributed_amd.config import config_for  # noqa: E402
 from pytorch_distributed_amd.trainer import run
 
 

@@ -3,10 +3,14 @@ import sys
 
 import pytest
 
+# the GPU session replays HIP graphs (DataParallel replicas, whole-step graphs): single-queue graph
+# launch, set before HIP starts (pytorch_distributed_amd/runtime/graphs.py GRAPH_QUEUES_VAR)
+os.environ.setdefault("DEBUG_HIP_FORCE_GRAPH_QUEUES", "1")
+
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 if ROOT not in sys.path:
     sys.path.insert(0, ROOT)
-import pytorch_distributed_amd  # noqa: E402,F401  (HIP runtime settings before the first HIP call)
+import pytorch_distributed_amd  # noqa: E402,F401
 
 
 def pytest_configure(config):

@@ -191,3 +191,50 @@ def test_rccl_group_single_device_collectives():
         assert torch.equal(f, ref)
     finally:
         g.close()
+
+
+def test_dataparallel_without_single_queue_graphs_runs_eagerly():
+    """Under HIP's default multi-queue graph launch (DEBUG_HIP_FORCE_GRAPH_QUEUES unset / 0 -- it
+    crashes inside hipGraphLaunch on the replica graphs, runtime/graphs.py) DataParallel must not
+    replay graphs: graph_step_ok() is False with a warning and train_step launches eagerly, with the
+    same result as the graph-replay-free schedule. In a child process (the variable is read when HIP
+    starts)."""
+    import os
+    import subprocess
+    import sys
+    code = r'''
+import warnings, torch
+from pytorch_distributed_amd.data import SyntheticImageNet
+from pytorch_distributed_amd.models import build_model
+from pytorch_distributed_amd.models.native import NativeResNet
+from pytorch_distributed_amd.parallel import DataParallel
+dev = torch.device("cuda", 0)
+torch.manual_seed(0)
+sd = build_model("resnet18").state_dict()
+dps = []
+for _ in range(2):
+    r = build_model("resnet18"); r.load_state_dict(sd)
+    dps.append(DataParallel(NativeResNet(r, device=dev, image_size=64), device_ids=[0, 0]))
+a, b = dps
+with warnings.catch_warnings(record=True) as w:
+    warnings.simplefilter("always")
+    ok = a.graph_step_ok()
+assert not ok and any("graph replay disabled" in str(x.message) for x in w), [str(x.message) for x in w]
+oa, ob = a.make_optimizer(lr=0.05), b.make_optimizer(lr=0.05)
+gen = a.module.input_generator(SyntheticImageNet("train", image_size=64))
+for step in range(2):
+    x, y = gen(torch.arange(16) + 16 * step)
+    la = a.train_step(x, y, oa)            # graph=True requested, eager because of the setting
+    lb = b.train_step(x, y, ob, graph=False)
+    torch.cuda.synchronize()
+    assert la.item() == lb.item(), (la.item(), lb.item())
+    assert torch.equal(a.module.flat_params, b.module.flat_params)
+assert a._graphs[0].graph is None
+print("EAGER_OK")
+'''
+    env = dict(os.environ)
+    env["DEBUG_HIP_FORCE_GRAPH_QUEUES"] = "0"
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, "-c", code], cwd=root, env=env, capture_output=True,
+                       text=True, timeout=240)
+    assert r.returncode == 0 and "EAGER_OK" in r.stdout, (r.stdout[-2000:] + r.stderr[-3000:])

@@ -1059,3 +1059,93 @@ def test_conv_fwd_tail_matches_apply_then_conv(geo, mode, dtype):
         assert torch.equal(m, m_ref)
     assert torch.equal(y, y_ref)
     assert torch.equal(st, st_ref)
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("geo", [(2, 56, 64, 64, False), (2, 56, 64, 64, True), (3, 28, 128, 128, False),
+                                 (2, 28, 64, 128, True), (3, 14, 256, 256, False), (5, 7, 128, 64, True)])
+def test_wgrad_tap_matches_fp32_and_generic(geo, dtype):
+    """csrc/wgrad_tap.hip: the 3x3 stride-1 weight gradient with all nine taps per block (padded
+    pixel rows, X in an LDS ring, BN+ReLU prologue applied in LDS) against the fp32 reference on the
+    same 16-bit operands and against the generic implicit-GEMM weight gradient; bitwise
+    deterministic run to run; several split counts (last split ragged), Cin != Cout."""
+    K = _k()
+    Nb, H, Cin, Cout, pro = geo
+    torch.manual_seed(H + Cin)
+    g = K.ConvGeom(Nb, H, H, Cin, Cout, 3, 3, 1, 1)
+    x = (torch.randn(Nb, H, H, Cin, device=DEV) + 0.2).to(dtype)
+    dy = (torch.randn(Nb, H, H, Cout, device=DEV) * 0.1).to(dtype)
+    sc = torch.rand(Cin, device=DEV) + 0.5 if pro else None
+    sh = torch.randn(Cin, device=DEV) * 0.3 if pro else None
+    xa = torch.relu(x.float() * sc + sh).to(dtype).float() if pro else x.float()
+    ref = torch.nn.grad.conv2d_weight(xa.permute(0, 3, 1, 2), (Cout, Cin, 3, 3),
+                                      dy.float().permute(0, 3, 1, 2), padding=1)
+    ref = ref.permute(0, 2, 3, 1).contiguous()          # OHWI
+    ws = K.Workspace(torch.device(DEV))
+    p = (sc, sh) if pro else None
+    outs = []
+    for blocks in (7, 64, 256):
+        gw = torch.full((Cout * 9 * Cin,), float("nan"), device=DEV)
+        kb, splits = K.wgrad_tap_plan(g, Nb, blocks)
+        slab = ws.get("wgrad_slab", splits * Cout * 9 * Cin)
+        L = K.ext.lib()
+        K.check(L.pda_wgrad_tap(K.ptr(dy), K.ptr(x), K.ptr(slab), K.ptr(sc), K.ptr(sh), Nb, H, H,
+                                Cin, Cout, kb, splits, K.ext.dt_of(dy), K.stream(torch.device(DEV))), "tap")
+        K.check(L.pda_wgrad_reduce(K.ptr(slab), K.ptr(gw), splits, Cout, 9 * Cin, int(math.log2(Cin)),
+                                   Cin, 9 * Cin, 1.0, 0, None, None, None, K.stream(torch.device(DEV))),
+                "reduce")
+        outs.append(gw.clone())
+    gen = torch.zeros(Cout * 9 * Cin, device=DEV)
+    K.conv_wgrad(dy, x, g, gen, ws, pro=p, tile=(-128, 128))   # the generic kernel
+    again = torch.full_like(outs[-1], float("nan"))
+    K.conv_wgrad_tap(dy, x, g, again, ws, pro=p)
+    torch.cuda.synchronize()
+    e_gen = rel_err(gen.view_as(ref), ref)
+    for o in outs:
+        e = rel_err(o.view_as(ref), ref)
+        assert e < 2 * e_gen + 1e-5, (e, e_gen)
+    k2 = K.conv_wgrad_tap(dy, x, g, torch.empty_like(again), ws, pro=p)
+    torch.cuda.synchronize()
+    assert torch.equal(again, k2)
+
+
+def test_wgrad_reduce_batch_matches_single_reduces():
+    """native_ops.ReduceBatch: several weight gradients (1x1, 3x3 tap-reuse, the decomposed-fold
+    combine, accumulate, the stem's padded-channel remap) with their split-K reductions queued and run
+    in ONE launch, against the same weight gradients reduced one launch each (equal to f32 rounding:
+    the batched kernel sums the splits in its own fixed order) and bitwise run to run."""
+    K = _k()
+    dev = torch.device(DEV)
+    dtype = torch.bfloat16
+    torch.manual_seed(5)
+    cases = [K.ConvGeom(4, 14, 14, 256, 64, 1, 1, 1, 0), K.ConvGeom(2, 28, 28, 128, 128, 3, 3, 1, 1),
+             K.ConvGeom(3, 7, 7, 512, 512, 3, 3, 1, 1), K.ConvGeom(2, 56, 56, 64, 64, 3, 3, 1, 1)]
+    ops = []
+    for g in cases:
+        x = torch.randn(g.Nb, g.H, g.W, g.Cin, device=dev).to(dtype)
+        dy = (torch.randn(g.Nb, g.Ho, g.Wo, g.Cout, device=dev) * 0.1).to(dtype)
+        ops.append((g, dy, x))
+    g1 = cases[0]
+    k = torch.randn(3 * g1.Cout, device=dev)
+    cB = torch.randn(g1.Cout, g1.Cin, device=dev)
+    cs = torch.randn(g1.Cin, device=dev)
+
+    def run(batched):
+        ws = K.Workspace(dev)
+        if batched:
+            ws.reduce_batch = K.ReduceBatch(ws)
+        outs = []
+        for n, (g, dy, x) in enumerate(ops):
+            o = torch.full((g.Cout * g.R * g.S * g.Cin,), 0.5, device=dev)
+            K.conv_wgrad(dy, x, g, o, ws, scale=0.25, accumulate=n == 1,
+                         combine=(k, cB, cs) if n == 0 else None)
+            outs.append(o)
+        if batched:
+            assert len(ws.reduce_batch.items) == len(ops)
+            ws.reduce_batch.flush()
+        torch.cuda.synchronize()
+        return outs
+    single, batch, again = run(False), run(True), run(True)
+    for a, b, c in zip(single, batch, again):
+        assert rel_err(b, a) < 1e-6, rel_err(b, a)
+        assert torch.equal(b, c)
