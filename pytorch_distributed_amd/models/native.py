@@ -147,9 +147,12 @@ class NativeResNet(nn.Module):
         # which stages a = relu(bn3(y3) + r) from y3 and r and writes a once (FWD_TAIL); blocks whose
         # successor has a shortcut conv keep the apply pass (PDA_TAIL_FUSE=0: every tail does)
         self.tail_fuse = os.environ.get("PDA_TAIL_FUSE", "1") != "0"
-        # the second stream's split-K weight-gradient reductions batched into one launch per stage
-        # (per block under DDP) instead of one per conv (ops/native_ops.py ReduceBatch)
-        self.reduce_batching = os.environ.get("PDA_REDUCE_BATCH", "1") != "0"
+        # opt-in (PDA_REDUCE_BATCH=1): the second stream's split-K weight-gradient reductions
+        # batched into one launch per stage (per block under DDP) instead of one per conv
+        # (ops/native_ops.py ReduceBatch). Off by default: fewer launches and -79 us of kernel time,
+        # but each stage's burst of reduce blocks slows the main chain's data-gradient convs beside it
+        # (+0.25..0.4 ms/step in-step, profiles/ab_r5.md section 4)
+        self.reduce_batching = os.environ.get("PDA_REDUCE_BATCH", "0") == "1"
         # consumer-side tail fold of the Bottleneck BN backward (see _block_backward)
         # ("0" off, "1" every stage, or the stages to fold, e.g. "12" = layer1 and layer2). Default
         # layer1-3: in-step A/B at the bench config (profiles/ab_r4.md) 28.26 ms off, 27.89 all

@@ -194,11 +194,10 @@ def test_rccl_group_single_device_collectives():
 
 
 def test_dataparallel_without_single_queue_graphs_runs_eagerly():
-    """Under HIP's default multi-queue graph launch (DEBUG_HIP_FORCE_GRAPH_QUEUES unset / 0 -- it
-    crashes inside hipGraphLaunch on the replica graphs, runtime/graphs.py) DataParallel must not
-    replay graphs: graph_step_ok() is False with a warning and train_step launches eagerly, with the
-    same result as the graph-replay-free schedule. In a child process (the variable is read when HIP
-    starts)."""
+    """Without the single-queue graph launch (DEBUG_HIP_FORCE_GRAPH_QUEUES unset: HIP's multi-queue
+    default, see runtime/graphs.py) DataParallel does not replay graphs: graph_step_ok() is False
+    with a warning and train_step launches eagerly, with the same result as the graph-replay-free
+    schedule. In a child process (the variable is read when HIP starts)."""
     import os
     import subprocess
     import sys
@@ -233,8 +232,56 @@ assert a._graphs[0].graph is None
 print("EAGER_OK")
 '''
     env = dict(os.environ)
-    env["DEBUG_HIP_FORCE_GRAPH_QUEUES"] = "0"
+    env.pop("DEBUG_HIP_FORCE_GRAPH_QUEUES", None)
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     r = subprocess.run([sys.executable, "-c", code], cwd=root, env=env, capture_output=True,
                        text=True, timeout=240)
     assert r.returncode == 0 and "EAGER_OK" in r.stdout, (r.stdout[-2000:] + r.stderr[-3000:])
+
+
+def test_dataparallel_graph_replay_under_default_graph_queues():
+    """The DataParallel replica graphs replayed under HIP's DEFAULT graph launch (the variable
+    unset: a graph's independent branches go to the runtime's internal streams), with the framework's
+    gate bypassed: 40 graphed steps (per-block side graphs + stage segments, two replicas on one
+    device) equal to the eager schedule bit for bit. Evidence for runtime/graphs.py: the replay
+    itself is correct under the default; the single-queue setting is kept for the long-session
+    crash recorded in profiles/ab_r4.md section 7 (profiles/ab_r5.md section 7)."""
+    import os
+    import subprocess
+    import sys
+    code = r'''
+import os, torch
+assert os.environ.get("DEBUG_HIP_FORCE_GRAPH_QUEUES") is None
+import pytorch_distributed_amd.runtime.graphs as G
+G.single_queue_graphs = lambda: True          # bypass the gate: replay under the default
+from pytorch_distributed_amd.data import SyntheticImageNet
+from pytorch_distributed_amd.models import build_model
+from pytorch_distributed_amd.models.native import NativeResNet
+from pytorch_distributed_amd.parallel import DataParallel
+dev = torch.device("cuda", 0)
+torch.manual_seed(0)
+sd = build_model("resnet18").state_dict()
+dps = []
+for _ in range(2):
+    r = build_model("resnet18"); r.load_state_dict(sd)
+    dps.append(DataParallel(NativeResNet(r, device=dev, image_size=64), device_ids=[0, 0]))
+g, e = dps
+assert g.graph_step_ok()
+og, oe = g.make_optimizer(lr=0.05, momentum=0.9), e.make_optimizer(lr=0.05, momentum=0.9)
+gen = g.module.input_generator(SyntheticImageNet("train", image_size=64))
+for step in range(40):
+    x, y = gen(torch.arange(16) + 16 * step)
+    lg = g.train_step(x, y, og)
+    le = e.train_step(x, y, oe, graph=False)
+    torch.cuda.synchronize()
+    assert lg.item() == le.item(), (step, lg.item(), le.item())
+assert torch.equal(g.module.flat_params, e.module.flat_params)
+assert g._graphs[0].graph is not None and len(g._graphs[0].graphs) > 1
+print("DEFAULT_QUEUES_OK", len(g._graphs[0].graphs), "segment graphs per replica")
+'''
+    env = dict(os.environ)
+    env.pop("DEBUG_HIP_FORCE_GRAPH_QUEUES", None)
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, "-c", code], cwd=root, env=env, capture_output=True,
+                       text=True, timeout=300)
+    assert r.returncode == 0 and "DEFAULT_QUEUES_OK" in r.stdout, (r.returncode, r.stdout[-2000:] + r.stderr[-3000:])

@@ -20,6 +20,7 @@ Usage: DEBUG_HIP_FORCE_GRAPH_QUEUES=0 python tools/graph_queue_repro.py [--side]
 import argparse
 import json
 import os
+import sys
 import threading
 import time
 
@@ -41,7 +42,7 @@ def body(x, ws, side, nseg, branches, cut, fork=True):
                     with torch.cuda.stream(side):
                         ws[2 + b].add_(h.t() @ h, alpha=1e-6)   # 'weight gradient' on the 2nd stream
             h = h @ ws[1]
-        if fork:
+        if fork and branches > 0:
             cur.wait_stream(side)
         cut(s)
     return h
@@ -59,12 +60,15 @@ class Replica:
             cur = torch.cuda.current_stream(dev)
             body(self.x, self.ws, self.side, nseg, branches, lambda s: None)   # warm-up, eager
             torch.cuda.synchronize(dev)
+            print("warm-up done", file=sys.stderr, flush=True)
             cap.wait_stream(cur)
             self.side.wait_stream(cur)
             pool = [None]
 
             def cut(s):
+                print(f"segment {s}: capture_end", file=sys.stderr, flush=True)
                 self.graphs[-1].capture_end()
+                print(f"segment {s}: instantiated", file=sys.stderr, flush=True)
                 if pool[0] is None:
                     pool[0] = self.graphs[0].pool()
                 if side_split:
@@ -115,7 +119,10 @@ def main():
     t0 = time.time()
     dev = torch.device("cuda", 0)
     reps = [Replica(dev, a.n, a.segments, a.branches, a.side) for _ in range(max(1, a.threads))]
+    print(f"captured {len(reps)} replica(s)", file=sys.stderr, flush=True)
     for it in range(a.iters):
+        if it < 3:
+            print(f"replay {it}", file=sys.stderr, flush=True)
         if a.threads > 1:
             ts = [threading.Thread(target=r.replay) for r in reps]
             for t in ts:
