@@ -296,6 +296,12 @@ class DataParallel(nn.Module):
     def train_step_chunks(self, xs, ys, optimizer, graph: bool = True) -> torch.Tensor:
         """:meth:`train_step` on per-replica input chunks (e.g. generated on each GPU directly,
         skipping the scatter from ``device_ids[0]``)."""
+        if graph and not self.replicas:
+            # one device: the module's own (eager, two-stream) step, as torch's DataParallel calls
+            # the module directly for a single device; replay only pays where one host thread
+            # drives several GPUs (the per-block segment graphs cost ~5 % on one device,
+            # profiles/ab_r5.md section 7)
+            graph = False
         if graph:
             from ..runtime.graphs import graphs_unsafe_warning, single_queue_graphs
             if not single_queue_graphs():   # the replica graphs need the single-queue launch

@@ -58,15 +58,22 @@ def native_train_step(model, opt, x: torch.Tensor, y: torch.Tensor, scaler=None)
     return loss
 
 
-# The HIP runtime's multi-queue graph launch (a graph's parallel branches spread over internal
-# streams) segfaulted inside hipGraphLaunch -- an out-of-range read of a per-graph stream list in
-# libamdhip64.so -- on this framework's DataParallel replica graphs: at once in `bench.py --dp`, and
-# after ~85 tests of one GPU session (profiles/ab_r4.md section 7; standalone reproducer with the
-# same capture shape: tools/graph_queue_repro.py, profiles/ab_r5.md). With
-# DEBUG_HIP_FORCE_GRAPH_QUEUES=1 graphs launch on one queue and never crashed. The variable is
-# read ONCE, when HIP initialises, so it is set by the entry points that replay graphs before their
-# first HIP call (resnet_dp.py, `bench.py --dp / --graph 1`, the GPU test session), and every graph
-# path checks it and falls back to eager launches (with a warning) when it is not in effect.
+# HIP graph launch queues. By default the HIP runtime spreads a graph's independent branches over
+# internal streams; DEBUG_HIP_FORCE_GRAPH_QUEUES=1 launches every graph on one queue. A full GPU test
+# session once segfaulted inside hipGraphLaunch (an out-of-range read of a per-graph stream list in
+# libamdhip64.so) on the DataParallel replica graphs after ~85 tests, and =1 removed it
+# (profiles/ab_r4.md section 7). Round 5 (profiles/ab_r5.md section 7, tools/graph_queue_repro.py):
+# * the "immediate core dump under =0" of round 4 was the degenerate ZERO-queue setting -- =0
+#   crashes (SIGFPE) inside capture_end for ANY captured graph, even a linear one without a fork;
+#   it is not HIP's default;
+# * under the real default (variable unset) the standalone reproducer (fork/join captures, segment
+#   graphs sharing a pool, side graphs, up to 4 replica threads x 16 graphs x 500 replays) and the
+#   DataParallel replica graphs (tests/test_dp_gpu.py, 40 steps bit-exact vs eager) run clean; the
+#   long-session crash was not reproduced standalone.
+# The variable is read ONCE, when HIP initialises: the entry points that replay graphs request
+# single-queue launch before their first HIP call (resnet_dp.py, `bench.py --dp / --graph 1`, the
+# GPU test session), and the graph paths replay only under it (else eager launches + a warning) --
+# the configuration that ran every long session clean.
 GRAPH_QUEUES_VAR = "DEBUG_HIP_FORCE_GRAPH_QUEUES"
 
 

@@ -12,11 +12,14 @@ native ResNet kernels:
   * replay: segment graphs on the caller's stream, side graphs on the second stream behind them,
     many iterations, optionally from a worker thread per replica (``--threads``).
 
-Run it under DEBUG_HIP_FORCE_GRAPH_QUEUES=0 (HIP's default: a graph's parallel branches launch on
-internal streams) and =1 (one queue). Prints one JSON line; a crash is the HIP runtime's (the
-script uses only public torch APIs).
-Usage: DEBUG_HIP_FORCE_GRAPH_QUEUES=0 python tools/graph_queue_repro.py [--side] [--threads N]
-       [--segments S] [--iters I] [--branches B]"""
+Run it with DEBUG_HIP_FORCE_GRAPH_QUEUES unset (HIP's default: a graph's parallel branches launch
+on internal streams) and =1 (one queue). Prints one JSON line (progress on stderr); a crash is the
+HIP runtime's (the script uses only public torch APIs).
+Round-5 results (profiles/ab_r5.md section 7): unset and =1 run clean in every configuration
+(up to --threads 4 --segments 8 --side, 500 replays); =0 is NOT the default but zero graph queues:
+it dies with SIGFPE inside capture_end (graph instantiation) even with --segments 1 --branches 0.
+Usage: env -u DEBUG_HIP_FORCE_GRAPH_QUEUES python tools/graph_queue_repro.py [--side]
+       [--threads N] [--segments S] [--iters I] [--branches B]"""
 import argparse
 import json
 import os
