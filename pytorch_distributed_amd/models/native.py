@@ -147,6 +147,7 @@ class NativeResNet(nn.Module):
         # which stages a = relu(bn3(y3) + r) from y3 and r and writes a once (FWD_TAIL); blocks whose
         # successor has a shortcut conv keep the apply pass (PDA_TAIL_FUSE=0: every tail does)
         self.tail_fuse = os.environ.get("PDA_TAIL_FUSE", "1") != "0"
+        self.tail_fuse_ds = os.environ.get("PDA_TAIL_FUSE", "1") != "nods"
         # opt-in (PDA_REDUCE_BATCH=1): the second stream's split-K weight-gradient reductions
         # batched into one launch per stage (per block under DDP) instead of one per conv
         # (ops/native_ops.py ReduceBatch). Off by default: fewer launches and -79 us of kernel time,
@@ -616,15 +617,23 @@ class NativeResNet(nn.Module):
             # differently on different ranks and deadlock -- so the shortcut stays on the chain)
             ds_side = (b.ds is not None and self._side is not None and self.ds_stream
                        and self.ws.sync_comm is None)
-            if ds_side:   # the shortcut conv (+BN stats) runs beside conv1..conv3 on the 2nd stream
-                cur = torch.cuda.current_stream(self.device)
+            # with the previous tail folded into conv1, conv1 writes this block's input h: the
+            # shortcut conv forks after it
+            ds_late = ds_side and tail_in is not None
+            cur = torch.cuda.current_stream(self.device)
+
+            def fork_ds():   # the shortcut conv (+BN stats) beside conv1..conv3 on the 2nd stream
                 self._side.wait_stream(cur)
                 with torch.cuda.stream(self._side):
-                    yd = self._conv_bn(b.ds, h, train, ws=self.ws_w)
+                    return self._conv_bn(b.ds, h, train, ws=self.ws_w)
+            if ds_side and not ds_late:
+                yd = fork_ds()
             gram_side = (save and train and self.bn_fold_wg and self._side is not None
                          and len(b.units) == 3 and self._tail_fold_ok(b, Nb))
             for j, u in enumerate(b.units):
                 y = self._conv_bn(u, a, train, pro, tail=tail_in[2] if j == 0 and tail_in else None)
+                if j == 0 and ds_late:
+                    yd = fork_ds()
                 ys.append(y)
                 if save:
                     rec[f"s{j}"] = u.state
@@ -651,12 +660,13 @@ class NativeResNet(nn.Module):
             sc, sh = self._coeffs(ul, train)
             tail_in = None
             nb = self.blocks[bi + 1] if not last else None
-            # the tail's BN apply folds into the next block's conv1 (FWD_TAIL) unless a shortcut conv
-            # on the second stream reads the output first; layers 1-2 only (conv1 of <= 128 channels,
-            # K <= 512): on the deep-K layers 3-4 the fused launch is slower than the apply pass and
-            # the plain conv together (tools/tail_bench.py: layer1 422 vs 482 us, layer2 233 vs 244,
-            # layer3 196 vs 142, layer4 214 vs 105 -- profiles/ab_r5.md section 2)
-            fuse = (nb is not None and self.tail_fuse and nb.ds is None
+            # the tail's BN apply folds into the next block's conv1 (FWD_TAIL; a downsampling next
+            # block forks its shortcut conv after that conv1); layers 1-2 only (conv1 of <= 128
+            # channels, K <= 512): on the deep-K layers 3-4 the fused launch is slower than the
+            # apply pass and the plain conv together (tools/tail_bench.py: layer1 422 vs 482 us,
+            # layer2 233 vs 244, layer3 196 vs 142, layer4 214 vs 105 -- profiles/ab_r5.md
+            # section 2). PDA_TAIL_FUSE=nods: not into downsampling blocks (the round-5 start)
+            fuse = (nb is not None and self.tail_fuse and (nb.ds is None or self.tail_fuse_ds)
                     and nb.units[0].cout <= 128
                     and K.tail_fuse_ok(nb.units[0].geom(Nb), self.dtype))
             if last:

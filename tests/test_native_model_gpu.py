@@ -385,6 +385,50 @@ def test_tail_fold_matches_apply_path():
     assert not bad, bad
 
 
+def test_forward_tail_fold_matches_apply_path():
+    """FWD_TAIL (a block's tail BN apply + residual + ReLU formed inside the next block's conv1,
+    including the downsampling blocks, whose shortcut conv then forks after that conv1; the kernel
+    itself is bit-exact vs apply + conv, test_kernels_gpu.py) at the model level: with the fold, with
+    it off for downsampling blocks and with it off entirely, logits and gradients are as close to
+    the fp32 reference as torch's bf16 autocast is (the unfused conv1 may take another M-tile, so
+    its BN partials group differently and random-init ResNets amplify that rounding ~1 %/block),
+    and the folded step is bitwise deterministic run to run."""
+    tm, nm = _pair("resnet50", image=64)
+    tb = copy.deepcopy(tm)
+    torch.manual_seed(11)
+    x = torch.randn(16, 3, 64, 64, device=DEV).to(torch.bfloat16).float()
+    y = torch.randint(0, 1000, (16,), device=DEV)
+    tm.train()
+    tb.train()
+    nm.train()
+    lt = tm(x)
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        lb = tb(x)
+    F.cross_entropy(lt, y).backward()
+    F.cross_entropy(lb.float(), y).backward()
+    tp, bp = dict(tm.named_parameters()), dict(tb.named_parameters())
+    crit = nm.make_criterion()
+    res = {}
+    for mode in ("warm", "all", "nods", "off", "all2"):   # (a first step grows the workspaces)
+        nm.tail_fuse, nm.tail_fuse_ds = mode != "off", mode != "nods"
+        nm.zero_grad_flat()
+        out = nm(x)
+        crit(out, y).backward()
+        torch.cuda.synchronize()
+        res[mode] = (out.detach().float().clone(), nm.flat_grad.detach().float().clone(),
+                     {n: p.grad.detach().float().clone() for n, p in nm.named_parameters()})
+    for m in ("warm", "all2"):
+        assert torch.equal(res["all"][0], res[m][0]) and torch.equal(res["all"][1], res[m][1]), m
+    e_ref = rel_err(lb, lt)
+    for m in ("all", "nods", "off"):
+        e = rel_err(res[m][0], lt)
+        assert e < 1.3 * e_ref + 0.01, (m, e, e_ref)
+        worse = [(n, rel_err(g, tp[n].grad), rel_err(bp[n].grad, tp[n].grad))
+                 for n, g in res[m][2].items()
+                 if rel_err(g, tp[n].grad) > 1.5 * rel_err(bp[n].grad, tp[n].grad) + 0.02]
+        assert not worse, (m, worse)
+
+
 def test_decomposed_fold_wgrad_matches_apply_path():
     """PDA_BN_FOLD_WG: the folded tails' conv3 weight gradient in the decomposed form (forward-time
     Gram and column sums of a2 on the second stream, plain dz^T a2 combined in the split-K reduce)
