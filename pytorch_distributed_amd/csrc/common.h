@@ -2,6 +2,7 @@
 // Wave64 everywhere; 16-bit element types are moved as raw shorts and bit-cast at the MFMA.
 #pragma once
 #include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
 #include <stdint.h>
 
 typedef short s16x8 __attribute__((ext_vector_type(8)));
@@ -187,3 +188,22 @@ __device__ __forceinline__ uint32_t xcd_remap(uint32_t bid, uint32_t nwg) {
   const uint32_t base = x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q;
   return base + (bid >> 3);
 }
+
+// ---------------------------------------------------------------------------------------------
+// Fork tracking (models/native.py _fork_side, csrc/misc.hip pda_track): while armed for this host
+// thread, every launch on the tracked stream completes g_trk_event through its own dispatch
+// (hipExtLaunchKernel stop event), so a second stream can wait for "the latest launch on the main
+// stream" without an event-record marker between kernels (~4-5 us of main-stream bubble per fork
+// measured by tools/fork_bench.py; the stop event costs ~nothing when nobody waits).
+extern thread_local hipStream_t g_trk_stream;
+extern thread_local hipEvent_t g_trk_event;
+extern thread_local unsigned long long g_trk_count;   // tracked launches so far (this thread)
+#define PDA_LAUNCH(K, G, B, S, ST, ...)                                                        \
+  do {                                                                                         \
+    hipStream_t pda_st_ = (ST);                                                                \
+    if (g_trk_event != nullptr && pda_st_ == g_trk_stream) {                                   \
+      hipExtLaunchKernelGGL(K, G, B, S, pda_st_, nullptr, g_trk_event, 0, __VA_ARGS__);        \
+      ++g_trk_count;                                                                           \
+    } else                                                                                     \
+      hipLaunchKernelGGL(K, G, B, S, pda_st_, __VA_ARGS__);                                    \
+  } while (0)

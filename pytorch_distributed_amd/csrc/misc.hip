@@ -401,26 +401,60 @@ inline int grid_for(long long n, int cap = 4096) {
 
 }  // namespace
 
+// Streaming probe for tools/fork_bench.py: dst = 2 * src over n floats; launched through
+// hipExtLaunchKernelGGL when ``stop`` is given, so the kernel dispatch itself completes that event
+// (no separate marker on the stream) -- the cheapest fork point a second stream can wait on.
+__global__ __launch_bounds__(256) void fork_probe_kernel(float* __restrict__ dst,
+                                                         const float* __restrict__ src, int n) {
+  for (int i = (blockIdx.x * 256 + threadIdx.x) * 4; i < n; i += gridDim.x * 256 * 4)
+    *reinterpret_cast<f32x4*>(dst + i) = 2.f * *reinterpret_cast<const f32x4*>(src + i);
+}
+
+thread_local hipStream_t g_trk_stream = nullptr;
+thread_local hipEvent_t g_trk_event = nullptr;
+thread_local unsigned long long g_trk_count = 0;
+
 extern "C" {
+
+// Arm (ev != null) / disarm fork tracking of this host thread's launches on stream st (common.h).
+int pda_track(hipStream_t st, hipEvent_t ev) {
+  g_trk_stream = st;
+  g_trk_event = ev;
+  return 0;
+}
+unsigned long long pda_track_count() { return g_trk_count; }
+int pda_event_create(hipEvent_t* ev) { return (int)hipEventCreateWithFlags(ev, hipEventDisableTiming); }
+int pda_event_destroy(hipEvent_t ev) { return (int)hipEventDestroy(ev); }
+int pda_stream_wait_event(hipStream_t st, hipEvent_t ev) { return (int)hipStreamWaitEvent(st, ev, 0); }
+
+int pda_fork_probe(float* dst, const float* src, int n, hipEvent_t stop, hipStream_t st) {
+  if (n % 4) return -2;
+  const dim3 grid(2048), block(256);
+  if (stop != nullptr)
+    hipExtLaunchKernelGGL(fork_probe_kernel, grid, block, 0, st, nullptr, stop, 0, dst, src, n);
+  else
+    PDA_LAUNCH(fork_probe_kernel, grid, block, 0, st, dst, src, n);
+  return (int)hipGetLastError();
+}
 
 int pda_xent(const float* logits, int B, int K, int ld_in, const long long* labels, float* loss_rows,
              float* loss, void* dlog, int ld_out, float gscale, const float* gdev, int dt,
              int want_grad, hipStream_t st) {
-  hipLaunchKernelGGL(xent_kernel, dim3((B + 3) / 4), dim3(NT), 0, st, logits, B, K, ld_in, labels,
+  PDA_LAUNCH(xent_kernel, dim3((B + 3) / 4), dim3(NT), 0, st, logits, B, K, ld_in, labels,
                      loss_rows, dlog, ld_out, gscale, gdev, dt, want_grad);
-  if (loss) hipLaunchKernelGGL(mean_kernel, dim3(1), dim3(1024), 0, st, loss_rows, B, loss);
+  if (loss) PDA_LAUNCH(mean_kernel, dim3(1), dim3(1024), 0, st, loss_rows, B, loss);
   return (int)hipGetLastError();
 }
 
 int pda_topk(const float* logits, int B, int K, int ld, const long long* labels, float* hits,
              hipStream_t st) {
-  hipLaunchKernelGGL(topk_kernel, dim3((B + 3) / 4), dim3(NT), 0, st, logits, B, K, ld, labels, hits);
+  PDA_LAUNCH(topk_kernel, dim3((B + 3) / 4), dim3(NT), 0, st, logits, B, K, ld, labels, hits);
   return (int)hipGetLastError();
 }
 
 int pda_col_sum(const void* x, int rows, int C, int ld, float scale, float* out, int dt,
                 int accumulate, hipStream_t st) {
-  hipLaunchKernelGGL(col_sum_kernel, dim3((C + 63) / 64), dim3(1024), 0, st, x, rows, C, ld,
+  PDA_LAUNCH(col_sum_kernel, dim3((C + 63) / 64), dim3(1024), 0, st, x, rows, C, ld,
                      scale, out, dt, accumulate);
   return (int)hipGetLastError();
 }
@@ -428,19 +462,19 @@ int pda_col_sum(const void* x, int rows, int C, int ld, float scale, float* out,
 int pda_sgd_flat(float* p, float* g, float* buf, void* shadow, long long n, float lr, float momentum,
                  float wd, const float* scale, const float* found_inf, int flags, int dt,
                  hipStream_t st) {
-  hipLaunchKernelGGL(sgd_flat_kernel, dim3(grid_for(n / 4 + 1, 8192)), dim3(NT), 0, st, p, g, buf,
+  PDA_LAUNCH(sgd_flat_kernel, dim3(grid_for(n / 4 + 1, 8192)), dim3(NT), 0, st, p, g, buf,
                      (u16*)shadow, n, lr, momentum, wd, scale, found_inf, flags, dt);
   return (int)hipGetLastError();
 }
 
 int pda_cast_flat(const float* p, void* s, long long n, int dt, hipStream_t st) {
-  hipLaunchKernelGGL(cast_flat_kernel, dim3(grid_for(n, 8192)), dim3(NT), 0, st, p, (u16*)s, n, dt);
+  PDA_LAUNCH(cast_flat_kernel, dim3(grid_for(n, 8192)), dim3(NT), 0, st, p, (u16*)s, n, dt);
   return (int)hipGetLastError();
 }
 
 int pda_amp_scan(const float* g, long long n, float* found_inf, float* inv, float* scale,
                  int* tracker, int* ws, float growth, float backoff, int interval, hipStream_t st) {
-  hipLaunchKernelGGL(amp_scan_kernel, dim3(grid_for(n / 4 + 1, 2048)), dim3(NT), 0, st, g, n,
+  PDA_LAUNCH(amp_scan_kernel, dim3(grid_for(n / 4 + 1, 2048)), dim3(NT), 0, st, g, n,
                      found_inf, inv, scale, tracker, ws, growth, backoff, interval);
   return (int)hipGetLastError();
 }
@@ -448,49 +482,49 @@ int pda_amp_scan(const float* g, long long n, float* found_inf, float* inv, floa
 int pda_pack_stem(const float* src, void* dst, int Cout, int RS, int Cin, int Cpad, int Kpad, int dt,
                   hipStream_t st) {
   const int n = Cout * Kpad;
-  hipLaunchKernelGGL(pack_stem_kernel, dim3((n + 255) / 256), dim3(256), 0, st, src, dst, Cout,
+  PDA_LAUNCH(pack_stem_kernel, dim3((n + 255) / 256), dim3(256), 0, st, src, dst, Cout,
                      RS, Cin, Cpad, Kpad, dt);
   return (int)hipGetLastError();
 }
 
 int pda_synth(const long long* ids, int B, unsigned salt, int num_classes, unsigned* keys,
               long long* labels, int S, void* out, int dt, hipStream_t st) {
-  hipLaunchKernelGGL(synth_labels_kernel, dim3((B + 255) / 256), dim3(256), 0, st, ids, B, salt,
+  PDA_LAUNCH(synth_labels_kernel, dim3((B + 255) / 256), dim3(256), 0, st, ids, B, salt,
                      num_classes, keys, labels);
-  hipLaunchKernelGGL(synth_nhwc8_kernel, dim3(grid_for((long long)B * S * S, 8192)), dim3(NT), 0, st,
+  PDA_LAUNCH(synth_nhwc8_kernel, dim3(grid_for((long long)B * S * S, 8192)), dim3(NT), 0, st,
                      keys, labels, B, S, out, dt);
   return (int)hipGetLastError();
 }
 
 int pda_synth_s2d(const long long* ids, int B, unsigned salt, int num_classes, unsigned* keys,
                   long long* labels, int S, void* out, int dt, hipStream_t st) {
-  hipLaunchKernelGGL(synth_labels_kernel, dim3((B + 255) / 256), dim3(256), 0, st, ids, B, salt,
+  PDA_LAUNCH(synth_labels_kernel, dim3((B + 255) / 256), dim3(256), 0, st, ids, B, salt,
                      num_classes, keys, labels);
-  hipLaunchKernelGGL(synth_s2d_kernel, dim3(grid_for((long long)B * (S / 2) * (S / 2), 8192)), dim3(NT),
+  PDA_LAUNCH(synth_s2d_kernel, dim3(grid_for((long long)B * (S / 2) * (S / 2), 8192)), dim3(NT),
                      0, st, keys, labels, B, S, out, dt);
   return (int)hipGetLastError();
 }
 
 int pda_nchw_to_s2d(const float* x, int B, int C, int S, void* out, int dt, hipStream_t st) {
-  hipLaunchKernelGGL(nchw_to_s2d_kernel, dim3(grid_for((long long)B * (S / 2) * (S / 2), 8192)),
+  PDA_LAUNCH(nchw_to_s2d_kernel, dim3(grid_for((long long)B * (S / 2) * (S / 2), 8192)),
                      dim3(NT), 0, st, x, B, C, S, out, dt);
   return (int)hipGetLastError();
 }
 
 int pda_pack_stem_s2d(const float* src, void* dst, int Cout, int dt, hipStream_t st) {
-  hipLaunchKernelGGL(pack_stem_s2d_kernel, dim3((Cout * 256 + 255) / 256), dim3(256), 0, st, src,
+  PDA_LAUNCH(pack_stem_s2d_kernel, dim3((Cout * 256 + 255) / 256), dim3(256), 0, st, src,
                      dst, Cout, dt);
   return (int)hipGetLastError();
 }
 
 int pda_stem_s2d_grad(const float* gp, float* g, int Cout, int accumulate, hipStream_t st) {
-  hipLaunchKernelGGL(stem_s2d_grad_kernel, dim3((Cout * 147 + 255) / 256), dim3(256), 0, st, gp, g,
+  PDA_LAUNCH(stem_s2d_grad_kernel, dim3((Cout * 147 + 255) / 256), dim3(256), 0, st, gp, g,
                      Cout, accumulate);
   return (int)hipGetLastError();
 }
 
 int pda_nchw_to_nhwc8(const float* x, int B, int C, int H, int W, void* out, int dt, hipStream_t st) {
-  hipLaunchKernelGGL(nchw_to_nhwc8_kernel, dim3(grid_for((long long)B * H * W, 8192)), dim3(NT), 0, st,
+  PDA_LAUNCH(nchw_to_nhwc8_kernel, dim3(grid_for((long long)B * H * W, 8192)), dim3(NT), 0, st,
                      x, B, C, H, W, out, dt);
   return (int)hipGetLastError();
 }

@@ -28,6 +28,7 @@ re-points their parameters/buffers into the flat storage.
 from __future__ import annotations
 
 import contextlib
+import ctypes as C
 import math
 import os
 from dataclasses import dataclass
@@ -193,6 +194,15 @@ class NativeResNet(nn.Module):
         # _ReplicaGraph side_split): the backward leaves the batched weight-gradient kernels queued
         # (no flush, no end-of-backward join) for the capture driver to record on the second stream
         self.defer_side = False
+        # fork tracking (csrc/common.h PDA_LAUNCH): while the native forward / backward runs
+        # eagerly, every kernel launch on the main stream completes one event through its own
+        # dispatch, and a fork to the second stream waits on that event instead of recording a
+        # marker between kernels (the marker costs ~4-5 us of main-stream bubble per fork,
+        # tools/fork_bench.py; ~60 forks per step). Off under graph capture, SyncBatchNorm (its
+        # collectives run on the main stream) and PDA_FORK_TRACK=0.
+        self.fork_tracking = os.environ.get("PDA_FORK_TRACK", "1") != "0"
+        self._trk_ev = None
+        self._trk_on = False
         # diagnostics (tools/layer_times.py): called on the main stream as probe(phase, name) after
         # the stem and after each residual block, forward and backward
         self.probe: Optional[Callable[[str, str], None]] = None
@@ -578,6 +588,13 @@ class NativeResNet(nn.Module):
         return u.state[2], u.state[3]
 
     def native_forward(self, x: torch.Tensor, train: bool, save: bool) -> torch.Tensor:
+        self._track(train)
+        try:
+            return self._native_forward(x, train, save)
+        finally:
+            self._track(False)
+
+    def _native_forward(self, x: torch.Tensor, train: bool, save: bool) -> torch.Tensor:
         x = self.prepare_input(x)
         Nb = x.shape[0]
         # per-unit BN state (mean/invstd/scale/shift) is referenced, not copied, by the saved
@@ -623,7 +640,7 @@ class NativeResNet(nn.Module):
             cur = torch.cuda.current_stream(self.device)
 
             def fork_ds():   # the shortcut conv (+BN stats) beside conv1..conv3 on the 2nd stream
-                self._side.wait_stream(cur)
+                self._fork()
                 with torch.cuda.stream(self._side):
                     return self._conv_bn(b.ds, h, train, ws=self.ws_w)
             if ds_side and not ds_late:
@@ -720,6 +737,40 @@ class NativeResNet(nn.Module):
         return logits
 
     # ------------------------------------------------------------------ backward
+    def _track(self, on: bool) -> None:
+        """Arm / disarm fork tracking of this thread's launches on the current (main) stream."""
+        L = ext.lib()
+        if not on:
+            if self._trk_on:
+                L.pda_track(None, None)
+                self._trk_on = False
+            return
+        if (not self.fork_tracking or self._side is None or self.defer_side
+                or getattr(self.ws, "sync_comm", None) is not None
+                or torch.cuda.is_current_stream_capturing()
+                or getattr(L, "pda_track", None) is None):
+            return
+        if self._trk_ev is None:
+            ev = C.c_void_p()
+            K.check(L.pda_event_create(C.byref(ev)), "pda_event_create")
+            self._trk_ev = ev
+        L.pda_track(C.c_void_p(torch.cuda.current_stream(self.device).cuda_stream), self._trk_ev)
+        self._trk_on = True
+        self._trk_c0 = L.pda_track_count()
+
+    def _fork(self) -> None:
+        """The second stream waits for everything queued on the main stream so far: on the tracked
+        event (completed by the latest native launch) when the main stream has issued a native
+        launch since tracking was armed -- the forward / backward issue nothing else on it between
+        forks -- else with a regular event record."""
+        cur = torch.cuda.current_stream(self.device)
+        L = ext.lib()
+        if self._trk_on and L.pda_track_count() != self._trk_c0:
+            K.check(L.pda_stream_wait_event(C.c_void_p(self._side.cuda_stream), self._trk_ev),
+                    "pda_stream_wait_event")
+        else:
+            self._side.wait_stream(cur)
+
     def _wgrad(self, fn: Callable, *keep: torch.Tensor) -> None:
         """Enqueue ``fn(workspace)`` (weight-gradient kernels) on the wgrad stream, ordered after
         everything queued so far on the main stream. Tensors the side stream reads are kept alive
@@ -732,7 +783,7 @@ class NativeResNet(nn.Module):
             self._wbatch.append(fn)
             self._keep.extend(keep)
             return
-        self._side.wait_stream(torch.cuda.current_stream(self.device))
+        self._fork()
         with torch.cuda.stream(self._side):
             fn(self.ws_w)
         self._keep.extend(keep)
@@ -741,7 +792,7 @@ class NativeResNet(nn.Module):
         """Run the queued weight-gradient kernels (PDA_WGRAD_BATCH=block) after one fork."""
         if not self._wbatch:
             return
-        self._side.wait_stream(torch.cuda.current_stream(self.device))
+        self._fork()
         with torch.cuda.stream(self._side):
             for fn in self._wbatch:
                 fn(self.ws_w)
@@ -762,11 +813,18 @@ class NativeResNet(nn.Module):
             return
         self._flush_wgrad()
         self._flush_reduces()
-        self._side.wait_stream(torch.cuda.current_stream(self.device))
+        self._fork()
         with torch.cuda.stream(self._side):
             red.grads_ready(upto)
 
     def native_backward(self, dlog16: torch.Tensor) -> None:
+        self._track(True)
+        try:
+            self._native_backward(dlog16)
+        finally:
+            self._track(False)
+
+    def _native_backward(self, dlog16: torch.Tensor) -> None:
         """dlog16: [B, fc_rows] 16-bit d(loss)/d(logits) (zero padded).
 
         Schedule per bottleneck block (last to first): finish the tail BN backward (its reduction
@@ -942,8 +1000,7 @@ class NativeResNet(nn.Module):
         """Forward-time half of the decomposed conv3 weight gradient, on the second stream beside
         conv3's forward: Gram(a2), the column sums s of a2 = relu(bn2(y2)), and B = W3 Gram(a2)."""
         C_ = y2.shape[-1]
-        cur = torch.cuda.current_stream(self.device)
-        self._side.wait_stream(cur)
+        self._fork()
         with torch.cuda.stream(self._side):
             gram = torch.empty(C_ + 1, C_, dtype=torch.float32, device=self.device)
             K.conv_wgrad_gram(y2, sc, sh, gram, self.ws_w)   # Gram rows, then the column sums
@@ -990,7 +1047,7 @@ class NativeResNet(nn.Module):
             def ds_dgrad():
                 K.conv_dgrad(dyd, self.w16_ohwi(b.ds), g, shortcut_g)
             if self._side is not None and self.ds_stream:
-                self._side.wait_stream(torch.cuda.current_stream(self.device))
+                self._fork()
                 with torch.cuda.stream(self._side):
                     ds_dgrad()
                 sc_ev = torch.cuda.Event()

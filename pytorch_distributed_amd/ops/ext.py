@@ -122,6 +122,12 @@ _SIGS = {
     "pda_pack_stem_s2d": [_V, _V, _I, _I, _V],
     "pda_stem_s2d_grad": [_V, _V, _I, _I, _V],
     "pda_set_stream_cfg": [_I, _I, _I, _I],
+    "pda_fork_probe": [_V, _V, _I, _V, _V],
+    "pda_track": [_V, _V],
+    "pda_track_count": [],
+    "pda_event_create": [_V],
+    "pda_event_destroy": [_V],
+    "pda_stream_wait_event": [_V, _V],
     "pda_bn_bwd_apply2": [_V, _V, _V, _V, _V, _V, _L, _I, _I, _V],
 }
 
