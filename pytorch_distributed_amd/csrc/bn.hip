@@ -1069,19 +1069,19 @@ StreamCfg g_stream{0, 0, 8192, 100};
 #define STREAM_DISPATCH_UM(KER, DT, g, st, U_, M_, ...)                                    \
   do {                                                                                        \
     const int u_ = (U_), m_ = (M_);                                                           \
-    if (u_ == 2 && m_ == 0) PDA_LAUNCH((KER<DT, 2, 0>), dim3(g), dim3(NT), 0, st, __VA_ARGS__); \
-    else if (u_ == 2 && m_ == 1) PDA_LAUNCH((KER<DT, 2, 1>), dim3(g), dim3(NT), 0, st, __VA_ARGS__); \
-    else if (u_ == 2 && m_ == 2) PDA_LAUNCH((KER<DT, 2, 2>), dim3(g), dim3(NT), 0, st, __VA_ARGS__); \
-    else if (u_ == 2) PDA_LAUNCH((KER<DT, 2, 3>), dim3(g), dim3(NT), 0, st, __VA_ARGS__); \
-    else if (u_ == 4 && m_ == 0) PDA_LAUNCH((KER<DT, 4, 0>), dim3(g), dim3(NT), 0, st, __VA_ARGS__); \
-    else if (u_ == 4 && m_ == 1) PDA_LAUNCH((KER<DT, 4, 1>), dim3(g), dim3(NT), 0, st, __VA_ARGS__); \
-    else if (u_ == 4 && m_ == 2) PDA_LAUNCH((KER<DT, 4, 2>), dim3(g), dim3(NT), 0, st, __VA_ARGS__); \
-    else if (u_ == 4 && m_ >= 4) PDA_LAUNCH((KER<DT, 4, 5>), dim3(g), dim3(NT), 0, st, __VA_ARGS__); \
-    else if (u_ == 4) PDA_LAUNCH((KER<DT, 4, 3>), dim3(g), dim3(NT), 0, st, __VA_ARGS__); \
-    else if (m_ == 0) PDA_LAUNCH((KER<DT, 1, 0>), dim3(g), dim3(NT), 0, st, __VA_ARGS__); \
-    else if (m_ == 1) PDA_LAUNCH((KER<DT, 1, 1>), dim3(g), dim3(NT), 0, st, __VA_ARGS__); \
-    else if (m_ == 2) PDA_LAUNCH((KER<DT, 1, 2>), dim3(g), dim3(NT), 0, st, __VA_ARGS__); \
-    else PDA_LAUNCH((KER<DT, 1, 3>), dim3(g), dim3(NT), 0, st, __VA_ARGS__);         \
+    if (u_ == 2 && m_ == 0) TRACKED_LAUNCH((KER<DT, 2, 0>), dim3(g), dim3(NT), 0, st, __VA_ARGS__); \
+    else if (u_ == 2 && m_ == 1) TRACKED_LAUNCH((KER<DT, 2, 1>), dim3(g), dim3(NT), 0, st, __VA_ARGS__); \
+    else if (u_ == 2 && m_ == 2) TRACKED_LAUNCH((KER<DT, 2, 2>), dim3(g), dim3(NT), 0, st, __VA_ARGS__); \
+    else if (u_ == 2) TRACKED_LAUNCH((KER<DT, 2, 3>), dim3(g), dim3(NT), 0, st, __VA_ARGS__); \
+    else if (u_ == 4 && m_ == 0) TRACKED_LAUNCH((KER<DT, 4, 0>), dim3(g), dim3(NT), 0, st, __VA_ARGS__); \
+    else if (u_ == 4 && m_ == 1) TRACKED_LAUNCH((KER<DT, 4, 1>), dim3(g), dim3(NT), 0, st, __VA_ARGS__); \
+    else if (u_ == 4 && m_ == 2) TRACKED_LAUNCH((KER<DT, 4, 2>), dim3(g), dim3(NT), 0, st, __VA_ARGS__); \
+    else if (u_ == 4 && m_ >= 4) TRACKED_LAUNCH((KER<DT, 4, 5>), dim3(g), dim3(NT), 0, st, __VA_ARGS__); \
+    else if (u_ == 4) TRACKED_LAUNCH((KER<DT, 4, 3>), dim3(g), dim3(NT), 0, st, __VA_ARGS__); \
+    else if (m_ == 0) TRACKED_LAUNCH((KER<DT, 1, 0>), dim3(g), dim3(NT), 0, st, __VA_ARGS__); \
+    else if (m_ == 1) TRACKED_LAUNCH((KER<DT, 1, 1>), dim3(g), dim3(NT), 0, st, __VA_ARGS__); \
+    else if (m_ == 2) TRACKED_LAUNCH((KER<DT, 1, 2>), dim3(g), dim3(NT), 0, st, __VA_ARGS__); \
+    else TRACKED_LAUNCH((KER<DT, 1, 3>), dim3(g), dim3(NT), 0, st, __VA_ARGS__);         \
   } while (0)
 
 // chunks per thread per trip: unroll > 0 as given; auto (unroll < 0): -unroll, -1 meaning 4
@@ -1120,7 +1120,7 @@ int pda_set_stream_cfg(int unroll, int ntm, int cap, int min_mb) {
 int pda_slab_reduce(const float* in, int G, int QC, int S, float* out, hipStream_t st) {
   const int rows_per = (G + S - 1) / S;
   const int s = (G + rows_per - 1) / rows_per;
-  PDA_LAUNCH(slab_reduce_kernel, dim3((QC + 255) / 256, s), dim3(256), 0, st, in, G, QC, rows_per,
+  TRACKED_LAUNCH(slab_reduce_kernel, dim3((QC + 255) / 256, s), dim3(256), 0, st, in, G, QC, rows_per,
                      out);
   return (int)hipGetLastError() ? -1 : s;
 }
@@ -1129,7 +1129,7 @@ int pda_bn_finalize_tot(const double* tot, int C, double count, const float* gam
                         const float* beta, float eps, float momentum, float* mean, float* invstd,
                         float* scale, float* shift, float* rmean, float* rvar, long long* nbt,
                         int update_running, hipStream_t st) {
-  PDA_LAUNCH(bn_finalize_tot_kernel, dim3((C + 255) / 256), dim3(256), 0, st, tot, C, count,
+  TRACKED_LAUNCH(bn_finalize_tot_kernel, dim3((C + 255) / 256), dim3(256), 0, st, tot, C, count,
                      gamma, beta, eps, momentum, mean, invstd, scale, shift, rmean, rvar, nbt,
                      update_running);
   return (int)hipGetLastError();
@@ -1148,7 +1148,7 @@ int pda_bn_fwd_stats(const float* part, int T, int C, int bm, int M, int S, doub
                      const BnFwdOut* o, int cg, hipStream_t st) {
   if ((C & 3) || S <= 0 || S > T || !o || !cnt || !slabs) return -2;
   const int CG = stats_cg(C, cg);   // (a ragged last group: its lanes past C stay idle)
-  PDA_LAUNCH((bn_stats_kernel<0, 2, BnFwdOut>), dim3(S, (C + CG - 1) / CG), dim3(256), 0, st,
+  TRACKED_LAUNCH((bn_stats_kernel<0, 2, BnFwdOut>), dim3(S, (C + CG - 1) / CG), dim3(256), 0, st,
                      part, T, C, bm, M, CG, slabs, cnt, *o);
   return (int)hipGetLastError();
 }
@@ -1160,17 +1160,17 @@ int pda_bn_bwd_stats(const float* part, int T, int nq, int C, int S, double* sla
   const int CG = stats_cg(C, cg);   // (a ragged last group: its lanes past C stay idle)
   const dim3 grid(S, (C + CG - 1) / CG);
   if (nq == 2)
-    PDA_LAUNCH((bn_stats_kernel<1, 2, BnBwdOut>), grid, dim3(256), 0, st, part, T, C, 0, 0, CG,
+    TRACKED_LAUNCH((bn_stats_kernel<1, 2, BnBwdOut>), grid, dim3(256), 0, st, part, T, C, 0, 0, CG,
                        slabs, cnt, *o);
   else
-    PDA_LAUNCH((bn_stats_kernel<1, 3, BnBwdOut>), grid, dim3(256), 0, st, part, T, C, 0, 0, CG,
+    TRACKED_LAUNCH((bn_stats_kernel<1, 3, BnBwdOut>), grid, dim3(256), 0, st, part, T, C, 0, 0, CG,
                        slabs, cnt, *o);
   return (int)hipGetLastError();
 }
 
 int pda_bn_eval_coeffs(const float* gamma, const float* beta, const float* rm, const float* rv,
                        float eps, int C, float* scale, float* shift, hipStream_t st) {
-  PDA_LAUNCH(bn_eval_coeffs_kernel, dim3((C + 255) / 256), dim3(256), 0, st, gamma, beta, rm,
+  TRACKED_LAUNCH(bn_eval_coeffs_kernel, dim3((C + 255) / 256), dim3(256), 0, st, gamma, beta, rm,
                      rv, eps, C, scale, shift);
   return (int)hipGetLastError();
 }
@@ -1203,9 +1203,9 @@ int pda_bn_apply(const void* y, const float* sc, const float* sh, const void* r2
       return (int)hipGetLastError();
     }
   }
-  if (dt == DT_BF16) PDA_LAUNCH(bn_apply_kernel<DT_BF16>, dim3(g), dim3(NT), 0, st, ARGS);
-  else if (dt == DT_F32) PDA_LAUNCH(bn_apply_kernel<DT_F32>, dim3(g), dim3(NT), 0, st, ARGS);
-  else PDA_LAUNCH(bn_apply_kernel<DT_F16>, dim3(g), dim3(NT), 0, st, ARGS);
+  if (dt == DT_BF16) TRACKED_LAUNCH(bn_apply_kernel<DT_BF16>, dim3(g), dim3(NT), 0, st, ARGS);
+  else if (dt == DT_F32) TRACKED_LAUNCH(bn_apply_kernel<DT_F32>, dim3(g), dim3(NT), 0, st, ARGS);
+  else TRACKED_LAUNCH(bn_apply_kernel<DT_F16>, dim3(g), dim3(NT), 0, st, ARGS);
 #undef ARGS
   return (int)hipGetLastError();
 }
@@ -1216,9 +1216,9 @@ int pda_stem_pool(const void* y, const float* sc, const float* sh, void* out, vo
   const int g = grid_for((long long)N * Ho * Wo * (C / 8));
 #define ARGS (const void*)y, sc, sh, (void*)out, (uint8_t*)arg, N, H, W, C, Ho, Wo, make_div(C / 8), \
              make_div(Wo), make_div(Ho)
-  if (dt == DT_BF16) PDA_LAUNCH(stem_pool_kernel<DT_BF16>, dim3(g), dim3(NT), 0, st, ARGS);
-  else if (dt == DT_F32) PDA_LAUNCH(stem_pool_kernel<DT_F32>, dim3(g), dim3(NT), 0, st, ARGS);
-  else PDA_LAUNCH(stem_pool_kernel<DT_F16>, dim3(g), dim3(NT), 0, st, ARGS);
+  if (dt == DT_BF16) TRACKED_LAUNCH(stem_pool_kernel<DT_BF16>, dim3(g), dim3(NT), 0, st, ARGS);
+  else if (dt == DT_F32) TRACKED_LAUNCH(stem_pool_kernel<DT_F32>, dim3(g), dim3(NT), 0, st, ARGS);
+  else TRACKED_LAUNCH(stem_pool_kernel<DT_F16>, dim3(g), dim3(NT), 0, st, ARGS);
 #undef ARGS
   return (int)hipGetLastError();
 }
@@ -1229,9 +1229,9 @@ int pda_maxpool_bwd(const void* dout, const void* dout2, const void* arg, void* 
   const int g = grid_for((long long)N * H * W * (C / 8));
 #define ARGS (const void*)dout, (const void*)dout2, (const uint8_t*)arg, (void*)din, N, H, W, C, Ho, Wo, \
              make_div(C / 8), make_div(W), make_div(H)
-  if (dt == DT_BF16) PDA_LAUNCH(maxpool_bwd_kernel<DT_BF16>, dim3(g), dim3(NT), 0, st, ARGS);
-  else if (dt == DT_F32) PDA_LAUNCH(maxpool_bwd_kernel<DT_F32>, dim3(g), dim3(NT), 0, st, ARGS);
-  else PDA_LAUNCH(maxpool_bwd_kernel<DT_F16>, dim3(g), dim3(NT), 0, st, ARGS);
+  if (dt == DT_BF16) TRACKED_LAUNCH(maxpool_bwd_kernel<DT_BF16>, dim3(g), dim3(NT), 0, st, ARGS);
+  else if (dt == DT_F32) TRACKED_LAUNCH(maxpool_bwd_kernel<DT_F32>, dim3(g), dim3(NT), 0, st, ARGS);
+  else TRACKED_LAUNCH(maxpool_bwd_kernel<DT_F16>, dim3(g), dim3(NT), 0, st, ARGS);
 #undef ARGS
   return (int)hipGetLastError();
 }
@@ -1240,9 +1240,9 @@ int pda_tail_pool(const void* y, const float* sc, const float* sh, const void* r
                   const float* sh2, void* out, int N, int HW, int C, int mode, int dt,
                   hipStream_t st) {
 #define ARGS (const void*)y, sc, sh, (const void*)r2, sc2, sh2, (void*)out, HW, C, mode
-  if (dt == DT_BF16) PDA_LAUNCH(tail_pool_kernel<DT_BF16>, dim3(N), dim3(NT), 0, st, ARGS);
-  else if (dt == DT_F32) PDA_LAUNCH(tail_pool_kernel<DT_F32>, dim3(N), dim3(NT), 0, st, ARGS);
-  else PDA_LAUNCH(tail_pool_kernel<DT_F16>, dim3(N), dim3(NT), 0, st, ARGS);
+  if (dt == DT_BF16) TRACKED_LAUNCH(tail_pool_kernel<DT_BF16>, dim3(N), dim3(NT), 0, st, ARGS);
+  else if (dt == DT_F32) TRACKED_LAUNCH(tail_pool_kernel<DT_F32>, dim3(N), dim3(NT), 0, st, ARGS);
+  else TRACKED_LAUNCH(tail_pool_kernel<DT_F16>, dim3(N), dim3(NT), 0, st, ARGS);
 #undef ARGS
   return (int)hipGetLastError();
 }
@@ -1269,7 +1269,7 @@ static BwdArgs to_args(const BwdArgsC* c) {
 int pda_bn_bwd_reduce(const BwdArgsC* c, int G, int dt, hipStream_t st) {
   BwdArgs a = to_args(c);
   a.rows_per_block = (a.rows + G - 1) / G;
-#define K(D) PDA_LAUNCH(bn_bwd_reduce_kernel<D>, dim3(G), dim3(NT), 0, st, a)
+#define K(D) TRACKED_LAUNCH(bn_bwd_reduce_kernel<D>, dim3(G), dim3(NT), 0, st, a)
   if (dt == DT_BF16) K(DT_BF16); else if (dt == DT_F32) K(DT_F32); else K(DT_F16);
 #undef K
   return (int)hipGetLastError();
@@ -1284,7 +1284,7 @@ int pda_stem_bwd_reduce(const void* dout, const void* dout2, const void* arg, co
   if (rows * C >= (1ll << 31) || C % 8 || Ho != (H + 1) / 2 || Wo != (W + 1) / 2) return -2;
   const long long quads = (long long)N * Ho * Wo;
   const long long qpb = (quads + G - 1) / G;
-#define K(D) PDA_LAUNCH(stem_bwd_reduce_kernel<D>, dim3(G), dim3(NT), 0, st, (const void*)dout, \
+#define K(D) TRACKED_LAUNCH(stem_bwd_reduce_kernel<D>, dim3(G), dim3(NT), 0, st, (const void*)dout, \
                                 (const void*)dout2, (const uint8_t*)arg, (const void*)y, sc, sh,       \
                                 (void*)dz_out, part, quads, qpb, H, W, C, Ho, Wo, make_div(Wo),        \
                                 make_div(Ho))
@@ -1297,7 +1297,7 @@ int pda_bn_bwd_finalize(const float* part, int G, int nq, int qy, int C, float c
                         const float* gamma, const float* mean, const float* invstd, float* dgamma,
                         float* dbeta, float* k1, float* k2, float* k3, float gscale, int accumulate,
                         hipStream_t st) {
-  PDA_LAUNCH(bn_bwd_finalize_kernel, dim3((C + 15) / 16), dim3(1024), 0, st, part, G, nq, qy,
+  TRACKED_LAUNCH(bn_bwd_finalize_kernel, dim3((C + 15) / 16), dim3(1024), 0, st, part, G, nq, qy,
                      C, count, gamma, mean, invstd, dgamma, dbeta, k1, k2, k3, gscale, accumulate);
   return (int)hipGetLastError();
 }
@@ -1338,13 +1338,13 @@ int pda_bn_bwd_apply(const BwdArgsC* c, const void* dz_in, const void* ysel, con
 #undef KA
       return (int)hipGetLastError();
     }
-#define K(D) PDA_LAUNCH(bn_bwd_apply_dz_kernel<D>, dim3(g), dim3(NT), 0, st, (const void*)dz_in, \
+#define K(D) TRACKED_LAUNCH(bn_bwd_apply_dz_kernel<D>, dim3(g), dim3(NT), 0, st, (const void*)dz_in, \
                                 (const void*)ysel, k1, k2, k3, (void*)dy, n8, a.C)
     if (dt == DT_BF16) K(DT_BF16); else if (dt == DT_F32) K(DT_F32); else K(DT_F16);
 #undef K
     return (int)hipGetLastError();
   }
-#define K(D) PDA_LAUNCH(bn_bwd_apply_kernel<D>, dim3(g), dim3(NT), 0, st, a, (const void*)dz_in, \
+#define K(D) TRACKED_LAUNCH(bn_bwd_apply_kernel<D>, dim3(g), dim3(NT), 0, st, a, (const void*)dz_in, \
                                 (const void*)ysel, k1, k2, k3, (void*)dy)
   if (dt == DT_BF16) K(DT_BF16); else if (dt == DT_F32) K(DT_F32); else K(DT_F16);
 #undef K

@@ -198,7 +198,7 @@ __device__ __forceinline__ uint32_t xcd_remap(uint32_t bid, uint32_t nwg) {
 extern thread_local hipStream_t g_trk_stream;
 extern thread_local hipEvent_t g_trk_event;
 extern thread_local unsigned long long g_trk_count;   // tracked launches so far (this thread)
-#define PDA_LAUNCH(K, G, B, S, ST, ...)                                                        \
+#define TRACKED_LAUNCH(K, G, B, S, ST, ...)                                                        \
   do {                                                                                         \
     hipStream_t pda_st_ = (ST);                                                                \
     if (g_trk_event != nullptr && pda_st_ == g_trk_stream) {                                   \

@@ -1822,7 +1822,7 @@ static int launch(const ConvParams& p, dim3 grid, hipStream_t st) {
                 DT != DT_BF16 && DT != DT_F16) {
     return -1;
   } else {
-    PDA_LAUNCH((conv_gemm_kernel<PASS, DT, BM, BN, ST>), grid, dim3(conv_nt<ST>()), 0, st, p);
+    TRACKED_LAUNCH((conv_gemm_kernel<PASS, DT, BM, BN, ST>), grid, dim3(conv_nt<ST>()), 0, st, p);
     return (int)hipGetLastError();
   }
 }
@@ -2073,10 +2073,10 @@ int pda_bn_fold(const void* w, const float* k, int Cout, int Cin, void* wf, floa
   const int nG = (Cin / 16) * (Cin / 16), nB = Cin / 4, nR = (Cout * (Cin / 8) + 255) / 256;
   const dim3 grid(nG + nB + nR);
   if (dt == DT_BF16)
-    PDA_LAUNCH(bn_fold_kernel<DT_BF16>, grid, dim3(256), 0, st, (const u16*)w, k, Cout, Cin,
+    TRACKED_LAUNCH(bn_fold_kernel<DT_BF16>, grid, dim3(256), 0, st, (const u16*)w, k, Cout, Cin,
                        (u16*)wf, bias, nG, nB);
   else if (dt == DT_F16)
-    PDA_LAUNCH(bn_fold_kernel<DT_F16>, grid, dim3(256), 0, st, (const u16*)w, k, Cout, Cin,
+    TRACKED_LAUNCH(bn_fold_kernel<DT_F16>, grid, dim3(256), 0, st, (const u16*)w, k, Cout, Cin,
                        (u16*)wf, bias, nG, nB);
   else
     return -1;
@@ -2151,9 +2151,9 @@ int pda_fold_bgemm(const void* w, const float* gram, int Cout, int C, float* b, 
   if (C % 4) return -2;
   const dim3 grid((Cout * (C / 4) + 255) / 256);
   if (dt == DT_BF16)
-    PDA_LAUNCH(fold_bgemm_kernel<DT_BF16>, grid, dim3(256), 0, st, (const u16*)w, gram, Cout, C, b);
+    TRACKED_LAUNCH(fold_bgemm_kernel<DT_BF16>, grid, dim3(256), 0, st, (const u16*)w, gram, Cout, C, b);
   else if (dt == DT_F16)
-    PDA_LAUNCH(fold_bgemm_kernel<DT_F16>, grid, dim3(256), 0, st, (const u16*)w, gram, Cout, C, b);
+    TRACKED_LAUNCH(fold_bgemm_kernel<DT_F16>, grid, dim3(256), 0, st, (const u16*)w, gram, Cout, C, b);
   else
     return -1;
   return (int)hipGetLastError();
@@ -2201,7 +2201,7 @@ int pda_wgrad_reduce_batch(const RedDescC* ds, int n, hipStream_t st) {
     d.pitch = c.pitch; d.accumulate = c.accumulate; d.scale = c.scale; d.blk0 = blk;
     blk += (c.M * c.N + 63) / 64;
   }
-  PDA_LAUNCH(wgrad_reduce_batch_kernel, dim3(blk), dim3(256), 0, st, b);
+  TRACKED_LAUNCH(wgrad_reduce_batch_kernel, dim3(blk), dim3(256), 0, st, b);
   return (int)hipGetLastError();
 }
 
@@ -2215,7 +2215,7 @@ int pda_wgrad_reduce(const float* slab, float* grad, int splits, int M, int N, i
     const dim3 grid((total + epb - 1) / epb);
 #define RED_CASE(E)                                                                              \
   if (epb == E) {                                                                               \
-    PDA_LAUNCH(wgrad_reduce4_kernel<E>, grid, dim3(256), 0, st, slab, grad, splits, M, N, \
+    TRACKED_LAUNCH(wgrad_reduce4_kernel<E>, grid, dim3(256), 0, st, slab, grad, splits, M, N, \
                        cin_pad_log2, cin_real, dst_pitch, scale, accumulate, ck, cB, cs);       \
     return (int)hipGetLastError();                                                              \
   }
@@ -2224,7 +2224,7 @@ int pda_wgrad_reduce(const float* slab, float* grad, int splits, int M, int N, i
   }
   int blocks = (total + 255) / 256;
   if (blocks > 4096) blocks = 4096;
-  PDA_LAUNCH(wgrad_reduce_kernel, dim3(blocks), dim3(256), 0, st, slab, grad, splits, M, N,
+  TRACKED_LAUNCH(wgrad_reduce_kernel, dim3(blocks), dim3(256), 0, st, slab, grad, splits, M, N,
                      cin_pad_log2, cin_real, dst_pitch, scale, accumulate, ck, cB, cs);
   return (int)hipGetLastError();
 }

@@ -433,28 +433,28 @@ int pda_fork_probe(float* dst, const float* src, int n, hipEvent_t stop, hipStre
   if (stop != nullptr)
     hipExtLaunchKernelGGL(fork_probe_kernel, grid, block, 0, st, nullptr, stop, 0, dst, src, n);
   else
-    PDA_LAUNCH(fork_probe_kernel, grid, block, 0, st, dst, src, n);
+    TRACKED_LAUNCH(fork_probe_kernel, grid, block, 0, st, dst, src, n);
   return (int)hipGetLastError();
 }
 
 int pda_xent(const float* logits, int B, int K, int ld_in, const long long* labels, float* loss_rows,
              float* loss, void* dlog, int ld_out, float gscale, const float* gdev, int dt,
              int want_grad, hipStream_t st) {
-  PDA_LAUNCH(xent_kernel, dim3((B + 3) / 4), dim3(NT), 0, st, logits, B, K, ld_in, labels,
+  TRACKED_LAUNCH(xent_kernel, dim3((B + 3) / 4), dim3(NT), 0, st, logits, B, K, ld_in, labels,
                      loss_rows, dlog, ld_out, gscale, gdev, dt, want_grad);
-  if (loss) PDA_LAUNCH(mean_kernel, dim3(1), dim3(1024), 0, st, loss_rows, B, loss);
+  if (loss) TRACKED_LAUNCH(mean_kernel, dim3(1), dim3(1024), 0, st, loss_rows, B, loss);
   return (int)hipGetLastError();
 }
 
 int pda_topk(const float* logits, int B, int K, int ld, const long long* labels, float* hits,
              hipStream_t st) {
-  PDA_LAUNCH(topk_kernel, dim3((B + 3) / 4), dim3(NT), 0, st, logits, B, K, ld, labels, hits);
+  TRACKED_LAUNCH(topk_kernel, dim3((B + 3) / 4), dim3(NT), 0, st, logits, B, K, ld, labels, hits);
   return (int)hipGetLastError();
 }
 
 int pda_col_sum(const void* x, int rows, int C, int ld, float scale, float* out, int dt,
                 int accumulate, hipStream_t st) {
-  PDA_LAUNCH(col_sum_kernel, dim3((C + 63) / 64), dim3(1024), 0, st, x, rows, C, ld,
+  TRACKED_LAUNCH(col_sum_kernel, dim3((C + 63) / 64), dim3(1024), 0, st, x, rows, C, ld,
                      scale, out, dt, accumulate);
   return (int)hipGetLastError();
 }
@@ -462,19 +462,19 @@ int pda_col_sum(const void* x, int rows, int C, int ld, float scale, float* out,
 int pda_sgd_flat(float* p, float* g, float* buf, void* shadow, long long n, float lr, float momentum,
                  float wd, const float* scale, const float* found_inf, int flags, int dt,
                  hipStream_t st) {
-  PDA_LAUNCH(sgd_flat_kernel, dim3(grid_for(n / 4 + 1, 8192)), dim3(NT), 0, st, p, g, buf,
+  TRACKED_LAUNCH(sgd_flat_kernel, dim3(grid_for(n / 4 + 1, 8192)), dim3(NT), 0, st, p, g, buf,
                      (u16*)shadow, n, lr, momentum, wd, scale, found_inf, flags, dt);
   return (int)hipGetLastError();
 }
 
 int pda_cast_flat(const float* p, void* s, long long n, int dt, hipStream_t st) {
-  PDA_LAUNCH(cast_flat_kernel, dim3(grid_for(n, 8192)), dim3(NT), 0, st, p, (u16*)s, n, dt);
+  TRACKED_LAUNCH(cast_flat_kernel, dim3(grid_for(n, 8192)), dim3(NT), 0, st, p, (u16*)s, n, dt);
   return (int)hipGetLastError();
 }
 
 int pda_amp_scan(const float* g, long long n, float* found_inf, float* inv, float* scale,
                  int* tracker, int* ws, float growth, float backoff, int interval, hipStream_t st) {
-  PDA_LAUNCH(amp_scan_kernel, dim3(grid_for(n / 4 + 1, 2048)), dim3(NT), 0, st, g, n,
+  TRACKED_LAUNCH(amp_scan_kernel, dim3(grid_for(n / 4 + 1, 2048)), dim3(NT), 0, st, g, n,
                      found_inf, inv, scale, tracker, ws, growth, backoff, interval);
   return (int)hipGetLastError();
 }
@@ -482,49 +482,49 @@ int pda_amp_scan(const float* g, long long n, float* found_inf, float* inv, floa
 int pda_pack_stem(const float* src, void* dst, int Cout, int RS, int Cin, int Cpad, int Kpad, int dt,
                   hipStream_t st) {
   const int n = Cout * Kpad;
-  PDA_LAUNCH(pack_stem_kernel, dim3((n + 255) / 256), dim3(256), 0, st, src, dst, Cout,
+  TRACKED_LAUNCH(pack_stem_kernel, dim3((n + 255) / 256), dim3(256), 0, st, src, dst, Cout,
                      RS, Cin, Cpad, Kpad, dt);
   return (int)hipGetLastError();
 }
 
 int pda_synth(const long long* ids, int B, unsigned salt, int num_classes, unsigned* keys,
               long long* labels, int S, void* out, int dt, hipStream_t st) {
-  PDA_LAUNCH(synth_labels_kernel, dim3((B + 255) / 256), dim3(256), 0, st, ids, B, salt,
+  TRACKED_LAUNCH(synth_labels_kernel, dim3((B + 255) / 256), dim3(256), 0, st, ids, B, salt,
                      num_classes, keys, labels);
-  PDA_LAUNCH(synth_nhwc8_kernel, dim3(grid_for((long long)B * S * S, 8192)), dim3(NT), 0, st,
+  TRACKED_LAUNCH(synth_nhwc8_kernel, dim3(grid_for((long long)B * S * S, 8192)), dim3(NT), 0, st,
                      keys, labels, B, S, out, dt);
   return (int)hipGetLastError();
 }
 
 int pda_synth_s2d(const long long* ids, int B, unsigned salt, int num_classes, unsigned* keys,
                   long long* labels, int S, void* out, int dt, hipStream_t st) {
-  PDA_LAUNCH(synth_labels_kernel, dim3((B + 255) / 256), dim3(256), 0, st, ids, B, salt,
+  TRACKED_LAUNCH(synth_labels_kernel, dim3((B + 255) / 256), dim3(256), 0, st, ids, B, salt,
                      num_classes, keys, labels);
-  PDA_LAUNCH(synth_s2d_kernel, dim3(grid_for((long long)B * (S / 2) * (S / 2), 8192)), dim3(NT),
+  TRACKED_LAUNCH(synth_s2d_kernel, dim3(grid_for((long long)B * (S / 2) * (S / 2), 8192)), dim3(NT),
                      0, st, keys, labels, B, S, out, dt);
   return (int)hipGetLastError();
 }
 
 int pda_nchw_to_s2d(const float* x, int B, int C, int S, void* out, int dt, hipStream_t st) {
-  PDA_LAUNCH(nchw_to_s2d_kernel, dim3(grid_for((long long)B * (S / 2) * (S / 2), 8192)),
+  TRACKED_LAUNCH(nchw_to_s2d_kernel, dim3(grid_for((long long)B * (S / 2) * (S / 2), 8192)),
                      dim3(NT), 0, st, x, B, C, S, out, dt);
   return (int)hipGetLastError();
 }
 
 int pda_pack_stem_s2d(const float* src, void* dst, int Cout, int dt, hipStream_t st) {
-  PDA_LAUNCH(pack_stem_s2d_kernel, dim3((Cout * 256 + 255) / 256), dim3(256), 0, st, src,
+  TRACKED_LAUNCH(pack_stem_s2d_kernel, dim3((Cout * 256 + 255) / 256), dim3(256), 0, st, src,
                      dst, Cout, dt);
   return (int)hipGetLastError();
 }
 
 int pda_stem_s2d_grad(const float* gp, float* g, int Cout, int accumulate, hipStream_t st) {
-  PDA_LAUNCH(stem_s2d_grad_kernel, dim3((Cout * 147 + 255) / 256), dim3(256), 0, st, gp, g,
+  TRACKED_LAUNCH(stem_s2d_grad_kernel, dim3((Cout * 147 + 255) / 256), dim3(256), 0, st, gp, g,
                      Cout, accumulate);
   return (int)hipGetLastError();
 }
 
 int pda_nchw_to_nhwc8(const float* x, int B, int C, int H, int W, void* out, int dt, hipStream_t st) {
-  PDA_LAUNCH(nchw_to_nhwc8_kernel, dim3(grid_for((long long)B * H * W, 8192)), dim3(NT), 0, st,
+  TRACKED_LAUNCH(nchw_to_nhwc8_kernel, dim3(grid_for((long long)B * H * W, 8192)), dim3(NT), 0, st,
                      x, B, C, H, W, out, dt);
   return (int)hipGetLastError();
 }

@@ -203,10 +203,10 @@ int launch_stem(const void* x, const void* w, void* y, float* stats, int Nb, int
   const int tpb = (tiles + cap - 1) / cap;
   const int grid = (tiles + tpb - 1) / tpb;
   if (stats)
-    PDA_LAUNCH((stem_fwd_kernel<DT, PF, true>), dim3(grid), dim3(ST_NT), lds, st,
+    TRACKED_LAUNCH((stem_fwd_kernel<DT, PF, true>), dim3(grid), dim3(ST_NT), lds, st,
                        (const u16*)x, (const u16*)w, (u16*)y, stats, H, tiles, tpb);
   else
-    PDA_LAUNCH((stem_fwd_kernel<DT, PF, false>), dim3(grid), dim3(ST_NT), lds, st,
+    TRACKED_LAUNCH((stem_fwd_kernel<DT, PF, false>), dim3(grid), dim3(ST_NT), lds, st,
                        (const u16*)x, (const u16*)w, (u16*)y, stats, H, tiles, tpb);
   return hipGetLastError() == hipSuccess ? 0 : -3;
 }

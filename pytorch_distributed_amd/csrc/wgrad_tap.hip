@@ -308,11 +308,11 @@ int pda_wgrad_tap(const void* dy, const void* x, float* slab, const float* pro_s
   const dim3 grid(splits * p.co_tiles * p.ci_tiles);
   const bool pro = pro_sc != nullptr;
   if (dt == DT_BF16) {
-    if (pro) PDA_LAUNCH((wgrad_tap_kernel<DT_BF16, true>), grid, dim3(WT_NT), 0, st, p);
-    else PDA_LAUNCH((wgrad_tap_kernel<DT_BF16, false>), grid, dim3(WT_NT), 0, st, p);
+    if (pro) TRACKED_LAUNCH((wgrad_tap_kernel<DT_BF16, true>), grid, dim3(WT_NT), 0, st, p);
+    else TRACKED_LAUNCH((wgrad_tap_kernel<DT_BF16, false>), grid, dim3(WT_NT), 0, st, p);
   } else if (dt == DT_F16) {
-    if (pro) PDA_LAUNCH((wgrad_tap_kernel<DT_F16, true>), grid, dim3(WT_NT), 0, st, p);
-    else PDA_LAUNCH((wgrad_tap_kernel<DT_F16, false>), grid, dim3(WT_NT), 0, st, p);
+    if (pro) TRACKED_LAUNCH((wgrad_tap_kernel<DT_F16, true>), grid, dim3(WT_NT), 0, st, p);
+    else TRACKED_LAUNCH((wgrad_tap_kernel<DT_F16, false>), grid, dim3(WT_NT), 0, st, p);
   } else {
     return -1;
   }

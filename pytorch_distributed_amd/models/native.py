@@ -194,7 +194,7 @@ class NativeResNet(nn.Module):
         # _ReplicaGraph side_split): the backward leaves the batched weight-gradient kernels queued
         # (no flush, no end-of-backward join) for the capture driver to record on the second stream
         self.defer_side = False
-        # fork tracking (csrc/common.h PDA_LAUNCH): while the native forward / backward runs
+        # fork tracking (csrc/common.h TRACKED_LAUNCH): while the native forward / backward runs
         # eagerly, every kernel launch on the main stream completes one event through its own
         # dispatch, and a fork to the second stream waits on that event instead of recording a
         # marker between kernels (the marker costs ~4-5 us of main-stream bubble per fork,
