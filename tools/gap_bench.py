@@ -16,19 +16,21 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
 def summary(d):
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    from prof_summary import family
     f = glob.glob(os.path.join(d, "**", "*kernel_trace.csv"), recursive=True)[0]
     rows = sorted(csv.DictReader(open(f)), key=lambda r: int(r["Start_Timestamp"]))
     gaps = {}
     for a, b in zip(rows, rows[1:]):
         if a["Stream_Id"] != b["Stream_Id"]:
             continue
-        ka = a["Kernel_Name"].split("(")[0].split("<")[0].split()[-1]
-        kb = b["Kernel_Name"].split("(")[0].split("<")[0].split()[-1]
+        ka, kb = family(a["Kernel_Name"]), family(b["Kernel_Name"])
         g = (int(b["Start_Timestamp"]) - int(a["End_Timestamp"])) / 1e3
         gaps.setdefault((ka, kb), []).append(g)
     for (ka, kb), v in sorted(gaps.items(), key=lambda x: -len(x[1])):
         if len(v) >= 10:
-            print(f"{ka[:28]:28s} -> {kb[:28]:28s} n={len(v):4d} median gap {statistics.median(v):6.2f} us")
+            print(f"{ka[:28]:28s} -> {kb[:28]:28s} n={len(v):4d} median gap {statistics.median(v):6.2f} us"
+                  f"  mean {statistics.mean(v):6.2f}")
 
 
 def main():
