@@ -125,6 +125,13 @@ __device__ __forceinline__ void st_wt(double* q, double v) {   // write-through 
   __hip_atomic_store(q, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// tiles / slabs whose loads each lane keeps in flight together (levels 1 / 2)
+#ifndef BN_STATS_U1
+#define BN_STATS_U1 4
+#endif
+#ifndef BN_STATS_U2
+#define BN_STATS_U2 4
+#endif
 template <int KIND, int NQ, class Out>
 __global__ __launch_bounds__(256) void bn_stats_kernel(const float* __restrict__ part, int T, int C,
                                                        int bm, int M, int CG,
@@ -166,14 +173,12 @@ __global__ __launch_bounds__(256) void bn_stats_kernel(const float* __restrict__
       for (int e = 0; e < 4; ++e) a[q][e] = 0.0;
     const int t0 = (int)((long long)s * T / S), t1 = (int)((long long)(s + 1) * T / S);
     if (act) {
-#pragma unroll 4
-      for (int t = t0 + lane; t < t1; t += SL) {
-        const float* pt = part + (size_t)t * PQ * C + c;
-        f32x4 d[PQ];
-#pragma unroll
-        for (int q = 0; q < PQ; ++q) d[q] = *reinterpret_cast<const f32x4*>(pt + q * C);
+      // U1 tiles' loads issued before the first use (the compiler kept one iteration's loads in
+      // flight per lane -- a dependent round per tile, ~1.5 us each beside the weight-gradient
+      // stream); accumulated in the same t order as before: bit-identical sums
+      auto acc1 = [&](const f32x4 (&d)[PQ], int tu) __attribute__((always_inline)) {
         if constexpr (KIND == 0) {
-          const double rows = (double)min(bm, M - t * bm);
+          const double rows = (double)min(bm, M - tu * bm);
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
             const double s_ = d[2][e], x = d[0][e];
@@ -186,6 +191,25 @@ __global__ __launch_bounds__(256) void bn_stats_kernel(const float* __restrict__
 #pragma unroll
             for (int e = 0; e < 4; ++e) a[q][e] += (double)d[q][e];
         }
+      };
+      int t = t0 + lane;
+      for (; t + (BN_STATS_U1 - 1) * SL < t1; t += SL * BN_STATS_U1) {   // whole batches
+        f32x4 d[BN_STATS_U1][PQ];
+#pragma unroll
+        for (int u = 0; u < BN_STATS_U1; ++u) {
+          const float* pt = part + (size_t)(t + u * SL) * PQ * C + c;
+#pragma unroll
+          for (int q = 0; q < PQ; ++q) d[u][q] = *reinterpret_cast<const f32x4*>(pt + q * C);
+        }
+#pragma unroll
+        for (int u = 0; u < BN_STATS_U1; ++u) acc1(d[u], t + u * SL);
+      }
+      for (; t < t1; t += SL) {   // the rest, one tile at a time
+        f32x4 d[PQ];
+        const float* pt = part + (size_t)t * PQ * C + c;
+#pragma unroll
+        for (int q = 0; q < PQ; ++q) d[q] = *reinterpret_cast<const f32x4*>(pt + q * C);
+        acc1(d, t);
       }
     }
     combine(a);
@@ -194,15 +218,21 @@ __global__ __launch_bounds__(256) void bn_stats_kernel(const float* __restrict__
 #pragma unroll
       for (int q = 0; q < NQ; ++q) st_wt(slabs + ((size_t)s * NQ + q) * C + col, tot[q]);
   }
-  // arrival: this block's slab stores landed (vmcnt(0) in every wave), then ONE release-ordered
-  // arrival on the group counter (agent scope: the release fence before the add orders every
-  // store of this workgroup before it in the memory model, not only by the sc1 write-through
-  // lowering; asm vmcnt(0) between fence and add: cdna_hip_programming.md G16 pitfall 12)
+  // arrival: the slab was stored write-through (sc1, st_wt) and every wave drains its stores
+  // (vmcnt(0)) before the barrier, then ONE relaxed agent-scope arrival on the group counter --
+  // the sc1 form of the hand-off (cdna_hip_programming.md G16 / the in-launch split-K recipe): no
+  // release fence, whose buffer_wbl2 writes back the XCD L2's dirty lines -- in the step, the
+  // streaming kernels' output beside this launch (BN_STATS_RELEASE=1 restores it)
+#ifndef BN_STATS_RELEASE
+#define BN_STATS_RELEASE 0
+#endif
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (tid == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if constexpr (BN_STATS_RELEASE) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
     const int old = __hip_atomic_fetch_add(cnt + g, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     flag = old == S - 1;
   }
@@ -220,15 +250,36 @@ __global__ __launch_bounds__(256) void bn_stats_kernel(const float* __restrict__
     for (int q = 0; q < NQ; ++q)
 #pragma unroll
       for (int e = 0; e < 4; ++e) a[q][e] = 0.0;
+    constexpr int U2 = NQ > 2 ? BN_STATS_U2 / 2 : BN_STATS_U2;
     if (act)
-#pragma unroll 4
-      for (int t = lane; t < S; t += SL) {
+      {
+        auto acc2 = [&](const f64x2 (&x)[NQ][2]) __attribute__((always_inline)) {
 #pragma unroll
-        for (int q = 0; q < NQ; ++q) {
-          const double* p0 = slabs + ((size_t)t * NQ + q) * C + c;
-          const f64x2 x0 = *reinterpret_cast<const f64x2*>(p0);
-          const f64x2 x1 = *reinterpret_cast<const f64x2*>(p0 + 2);
-          a[q][0] += x0[0]; a[q][1] += x0[1]; a[q][2] += x1[0]; a[q][3] += x1[1];
+          for (int q = 0; q < NQ; ++q) {
+            a[q][0] += x[q][0][0]; a[q][1] += x[q][0][1];
+            a[q][2] += x[q][1][0]; a[q][3] += x[q][1][1];
+          }
+        };
+        auto ld2 = [&](f64x2 (&x)[NQ][2], int tu) __attribute__((always_inline)) {
+#pragma unroll
+          for (int q = 0; q < NQ; ++q) {
+            const double* p0 = slabs + ((size_t)tu * NQ + q) * C + c;
+            x[q][0] = *reinterpret_cast<const f64x2*>(p0);
+            x[q][1] = *reinterpret_cast<const f64x2*>(p0 + 2);
+          }
+        };
+        int t = lane;
+        for (; t + (U2 - 1) * SL < S; t += SL * U2) {   // whole batches of U2 slabs
+          f64x2 x[U2][NQ][2];
+#pragma unroll
+          for (int u = 0; u < U2; ++u) ld2(x[u], t + u * SL);
+#pragma unroll
+          for (int u = 0; u < U2; ++u) acc2(x[u]);
+        }
+        for (; t < S; t += SL) {
+          f64x2 x[NQ][2];
+          ld2(x, t);
+          acc2(x);
         }
       }
     combine(a);
