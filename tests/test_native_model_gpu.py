@@ -429,6 +429,38 @@ def test_forward_tail_fold_matches_apply_path():
         assert not worse, (m, worse)
 
 
+def test_fork_tracking_is_bit_exact():
+    """Fork tracking (csrc/common.h TRACKED_LAUNCH: forks to the weight-gradient stream wait on an
+    event completed by the latest main-stream launch itself) changes only how the second stream
+    waits: logits and every gradient bit-identical with it on and off, over two steps; the forks
+    really used the tracked event (the launch counter moved while armed)."""
+    from pytorch_distributed_amd.ops import ext
+    _, nm = _pair("resnet50", image=64)
+    torch.manual_seed(13)
+    x = torch.randn(32, 3, 64, 64, device=DEV)
+    y = torch.randint(0, 1000, (32,), device=DEV)
+    nm.train()
+    crit = nm.make_criterion()
+    res = {}
+    for mode in (True, False, True):
+        nm.fork_tracking = mode
+        outs = []
+        for _ in range(2):
+            nm.zero_grad_flat()
+            c0 = ext.lib().pda_track_count()
+            out = nm(x)
+            crit(out, y).backward()
+            torch.cuda.synchronize()
+            moved = ext.lib().pda_track_count() != c0
+            assert moved == mode, (mode, moved)
+            outs.append((out.detach().clone(), nm.flat_grad.detach().clone()))
+        res.setdefault(mode, []).append(outs)
+    for (l1, g1), (l2, g2) in zip(res[True][0], res[False][0]):
+        assert torch.equal(l1, l2) and torch.equal(g1, g2)
+    for (l1, g1), (l2, g2) in zip(res[True][0], res[True][1]):
+        assert torch.equal(l1, l2) and torch.equal(g1, g2)
+
+
 def test_decomposed_fold_wgrad_matches_apply_path():
     """PDA_BN_FOLD_WG: the folded tails' conv3 weight gradient in the decomposed form (forward-time
     Gram and column sums of a2 on the second stream, plain dz^T a2 combined in the split-K reduce)
