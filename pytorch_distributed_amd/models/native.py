@@ -758,6 +758,14 @@ class NativeResNet(nn.Module):
         self._trk_on = True
         self._trk_c0 = L.pda_track_count()
 
+    def __del__(self):
+        ev = getattr(self, "_trk_ev", None)
+        if ev is not None:
+            try:
+                ext.lib().pda_event_destroy(ev)
+            except Exception:   # (interpreter shutdown: the library may be gone)
+                pass
+
     def _fork(self) -> None:
         """The second stream waits for everything queued on the main stream so far: on the tracked
         event (completed by the latest native launch) when the main stream has issued a native
