@@ -553,7 +553,7 @@ def bn_epilogue(ws: "Workspace", G: int, y, scale, shift, res=None, y2=None, sca
 _WGRAD_TUNED = {
     (64, 1, 64, 1, 56): ((-64, 128), 512),      # C1
     (64, 3, 64, 1, 56): ((64, 128), 512),       # C2
-    (256, 1, 64, 1, 56): ((-128, 128), 512),    # C3
+    (256, 1, 64, 1, 56): ((-128, 64), 512),     # C3 (round 5, decomposed conv3 fold: -128x128 +0.05 ms)
     (64, 1, 256, 1, 56): ((128, 128), 512),     # C4
     (128, 1, 256, 1, 56): ((-128, 128), 512),   # C5
     (128, 3, 128, 2, 28): ((128, 64), 2048),    # C6
@@ -723,7 +723,11 @@ def conv_wgrad(dy: torch.Tensor, x: torch.Tensor, g: ConvGeom, grad: torch.Tenso
 # which 3x3 stride-1 weight gradients run the tap-reuse kernel (csrc/wgrad_tap.hip), by image width
 # ("0": none); the generic tiles re-read X per (tap, channel) column tile and dY per N-tile
 _WGRAD_TAP = {int(v) for v in os.environ.get("PDA_WGRAD_TAP", "56,28").split(",") if v.strip() not in ("", "0")}
-_WGRAD_TAP_BLOCKS = 256   # one 104 KiB block per CU: the split count is the block count
+# blocks of the tap-reuse weight gradient (one 104 KiB block per CU: the split count is the block
+# count). Alone 256 is fastest (C2 165 vs 176 us at 512); in the step fewer blocks leave the other
+# CUs to the main chain: 256 / 192 / 128 / 112 / 96 / 80 / 64 -> 96 (-0.2 ms/step vs 256;
+# profiles/ab_r5.md section 15)
+_WGRAD_TAP_BLOCKS = 96
 
 
 def wgrad_tap_ok(g: ConvGeom, dtype: torch.dtype) -> bool:
