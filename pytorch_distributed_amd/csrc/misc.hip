@@ -166,8 +166,8 @@ __global__ __launch_bounds__(NT) void cast_flat_kernel(const float* __restrict__
 // the LAST workgroup to finish (arrival counter, agent-scope acq_rel) publishes
 //   found_inf[0] = any non-finite in g,  inv[0] = 1/scale (what the SGD unscales by),
 // then applies torch._amp_update_scale_ to scale/tracker (skipped when tracker == nullptr).
-// ws[0] = OR accumulator, ws[1] = arrival counter, both reset by that last workgroup, so the
-// kernel needs no memset and replays inside a HIP graph.
+// ws[0..1] = one 64-bit word (arrivals | non-finite blocks << 32), reset by that last workgroup,
+// so the kernel needs no memset and replays inside a HIP graph.
 __global__ __launch_bounds__(NT) void amp_scan_kernel(const float* __restrict__ g, long long n,
                                                       float* __restrict__ found_inf,
                                                       float* __restrict__ inv,
@@ -187,14 +187,20 @@ __global__ __launch_bounds__(NT) void amp_scan_kernel(const float* __restrict__ 
   __syncthreads();
   if (__any(bad) && (threadIdx.x & 63) == 0) s_bad = 1;
   __syncthreads();
+  // ONE relaxed 64-bit arrival per block carries its payload: low word = arrivals, high word =
+  // blocks that saw a non-finite value. The last arriver's fetch result (+ its own add) holds every
+  // block's flag, so no release / acquire fences (each an L2 writeback / invalidate) are needed.
+  __shared__ int s_any;
   if (threadIdx.x == 0) {
-    if (s_bad) __hip_atomic_fetch_or(&ws[0], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const int prev = __hip_atomic_fetch_add(&ws[1], 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
-    s_last = prev == (int)gridDim.x - 1;
+    const unsigned long long add = 1ull + (s_bad ? (1ull << 32) : 0ull);
+    const unsigned long long prev = __hip_atomic_fetch_add(
+        reinterpret_cast<unsigned long long*>(ws), add, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    s_last = (unsigned)(prev & 0xffffffffull) == gridDim.x - 1;
+    s_any = ((prev + add) >> 32) != 0;
   }
   __syncthreads();
   if (s_last && threadIdx.x == 0) {
-    const bool f = __hip_atomic_load(&ws[0], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) != 0;
+    const bool f = s_any != 0;
     const float sc = scale[0];
     found_inf[0] = f ? 1.f : 0.f;
     inv[0] = (float)(1.0 / (double)sc);
@@ -213,8 +219,8 @@ __global__ __launch_bounds__(NT) void amp_scan_kernel(const float* __restrict__ 
         }
       }
     }
-    __hip_atomic_store(&ws[0], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store(&ws[1], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(reinterpret_cast<unsigned long long*>(ws), 0ull, __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
   }
 }
 

@@ -579,7 +579,8 @@ def test_amp_scan_matches_gradscaler_state_machine():
     s_ref, t_ref = scale.clone(), tracker.clone()
     fi, inv = torch.zeros(1, device=DEV), torch.zeros(1, device=DEV)
     ws = torch.zeros(2, dtype=torch.int32, device=DEV)
-    pattern = [0, 0, 0, 1, 0, 2, 0, 0, 0, 0, 3, 0]    # 1: inf, 2: nan, 3: -inf at the very end
+    # 1: inf, 2: nan, 3: -inf at the very end, 4: non-finite values in every workgroup
+    pattern = [0, 0, 0, 1, 0, 2, 0, 0, 0, 0, 3, 0, 4, 0, 0, 0]
     for step, kind in enumerate(pattern):
         gg = g.clone()
         if kind == 1:
@@ -588,6 +589,8 @@ def test_amp_scan_matches_gradscaler_state_machine():
             gg[n // 2] = float("nan")
         elif kind == 3:
             gg[n - 1] = float("-inf")
+        elif kind == 4:
+            gg[::997] = float("inf")
         fr = torch.zeros(1, device=DEV)
         inv_ref = s_ref.double().reciprocal().float()
         torch._amp_foreach_non_finite_check_and_unscale_([gg.clone()], fr, inv_ref)
