@@ -989,10 +989,11 @@ def bn_bwd_finish(ws: "Workspace", part, G: int, nq: int, y, mean, invstd, gamma
 
 
 # channels per block group of the statistics kernel (csrc/bn.hip stats_cg): a quad of channels gets
-# 1024 / cg lanes, so narrower groups shorten both levels' serial load chains
-# statistics-kernel geometry, measured (profiles/ab_r4.md sections 4, 8, 13): 256-channel block
-# groups (64: +0.03 ms/step), S = sqrt(0.75 T) slabs with at least 8 (1 / 4: within noise)
-_BN_CG = 256
+# 1024 / cg lanes, so narrower groups shorten both levels' serial load chains.  Measured in step
+# (profiles/ab_r5.md section 17): 64-channel groups -0.12 ms/step against 256 since the round-5
+# hand-off dropped its release fence (round 4, with the fence: 64 was +0.03), 32 -0.05; S =
+# sqrt(0.75 T) slabs with at least 8 (0.2: +0.16, 1.5 / 3.0: within noise)
+_BN_CG = 64
 _BN_SK = 0.75
 _BN_SMIN = 8
 
