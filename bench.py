@@ -1,7 +1,9 @@
 """Headline benchmark: ResNet-50 training images/sec, batch 400 per GPU, whole job.
 
-Contract (driver): ``python bench.py --gpus N --steps K --warmup W``; for N>1 it is
-launched by ``torch.distributed.run`` (one rank per GPU, RCCL over xGMI). Each
+Contract (driver): ``python bench.py --gpus N --steps K --warmup W``; for N>1 it runs one rank
+per GPU (RCCL over xGMI) -- launched by ``torch.distributed.run`` (``WORLD_SIZE`` must then equal
+N), or, started bare, it launches the N ranks itself as a child ``torch.distributed.run`` after
+checking that N GPUs are visible (fewer: a non-zero exit, never a silent smaller run). Each
 step is a full training step on synthetic data (on-device generation of the
 batch, forward, loss, backward with bucketed gradient all-reduce, fused SGD with
 momentum + weight decay), random-init ResNet-50, bf16 compute / fp32 master
@@ -104,7 +106,69 @@ def parse():
                          "own tuning for the topology")
     ap.add_argument("--nccl-proto", default="", help="NCCL_PROTO (LL, LL128, Simple; '' = RCCL's choice)")
     ap.add_argument("--nccl-algo", default="", help="NCCL_ALGO (Ring, Tree; '' = RCCL's choice)")
+    ap.add_argument("--rehearse-fold", action="store_true",
+                    help="allow more ranks than visible GPUs (several ranks share a device: launch "
+                         "rehearsals only, never a measurement)")
     return ap.parse_args()
+
+
+def _launch_ranks(args) -> int | None:
+    """``--gpus N`` means N ranks, however bench.py is started (the reference's DDP script spawns its
+    own ranks, /root/reference/restnet_ddp.py:153-155). Started by a launcher (``WORLD_SIZE`` set),
+    this process is one rank and the world must equal ``--gpus``. Started bare with ``--gpus N > 1``,
+    this process becomes the launcher: it checks -- from sysfs, no HIP call -- that N GPUs are
+    visible, starts ``torch.distributed.run`` with N ranks as a CHILD process (never an exec: the
+    child ranks own the GPUs) on a 127.0.0.1 rendezvous, lets rank 0's single JSON line through on
+    the shared stdout, and returns the launcher's exit code (non-zero when any rank failed).
+    Returns None when this process should run the benchmark itself."""
+    world_env = os.environ.get("WORLD_SIZE")
+    if args.dp:
+        return None     # one process driving --gpus devices (resnet_dp.py), never N ranks
+    if world_env is not None:
+        world = int(world_env)
+        if world != args.gpus:
+            print(f"bench: WORLD_SIZE {world} but --gpus {args.gpus}: the record would mislabel the "
+                  f"run; pass --gpus {world}", file=sys.stderr, flush=True)
+            return 2
+        return None
+    if args.gpus <= 1:
+        return None
+    if args.device == "cuda" and not args.rehearse_fold:
+        from pytorch_distributed_amd.launch import visible_gpu_count
+        n = visible_gpu_count()
+        if n < args.gpus:
+            print(f"bench: --gpus {args.gpus} needs {args.gpus} visible GPUs, this process sees {n} "
+                  f"(--rehearse-fold shares devices for launch rehearsals)", file=sys.stderr, flush=True)
+            return 2
+    import signal
+    import subprocess
+    from pytorch_distributed_amd.launch import free_port
+    env = dict(os.environ)
+    env["PDA_BENCH_LAUNCHER"] = "self"
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           "--nproc-per-node", str(args.gpus), "--master-addr", "127.0.0.1",
+           "--master-port", str(free_port()), os.path.abspath(__file__), *sys.argv[1:]]
+    child = subprocess.Popen(cmd, env=env, start_new_session=True)
+
+    def _forward(sig, _frame):
+        # a timeout of the parent must also end every rank: the launcher stops its ranks (each in
+        # a session of its own) on SIGTERM / SIGINT
+        try:
+            os.killpg(child.pid, sig)
+        except OSError:
+            pass
+    for s in (signal.SIGTERM, signal.SIGINT, signal.SIGHUP):
+        signal.signal(s, _forward)
+    try:
+        rc = child.wait()
+    finally:
+        if child.poll() is None:
+            _forward(signal.SIGTERM, None)
+            try:
+                child.wait(timeout=30)
+            except subprocess.TimeoutExpired:
+                _forward(signal.SIGKILL, None)
+    return rc if rc >= 0 else 128 - rc
 
 
 def _configure_process(args) -> dict:
@@ -149,6 +213,10 @@ class Ctx:
         self.cuda = args.device == "cuda"
         if self.cuda:
             ndev = max(torch.cuda.device_count(), 1)
+            lws = int(os.environ.get("LOCAL_WORLD_SIZE", str(self.world)))
+            if lws > ndev and not args.rehearse_fold and not args.dp:
+                raise SystemExit(f"bench: {lws} ranks on this node but {ndev} visible GPU(s); "
+                                 f"--rehearse-fold shares devices for launch rehearsals")
             self.device = torch.device("cuda", self.local_rank % ndev)  # >1 rank/GPU: rehearsals only
             torch.cuda.set_device(self.device)
         else:
@@ -464,10 +532,16 @@ def _dp_pass(ctx: Ctx, args, dtype) -> dict:
 def main():
     args = parse()
     sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    rc = _launch_ranks(args)           # before any HIP call of this process
+    if rc is not None:
+        sys.stdout.flush()
+        sys.stderr.flush()
+        sys.exit(rc)
     proc = _configure_process(args)    # before Ctx: Ctx initialises HIP (set_device)
+    proc["launcher"] = ("bench.py -> torch.distributed.run (self-launched ranks)"
+                        if os.environ.get("PDA_BENCH_LAUNCHER") == "self"
+                        else "external launcher" if "WORLD_SIZE" in os.environ else "single process")
     ctx = Ctx(args)
-    if args.gpus != ctx.world and ctx.world > 1:
-        print(f"warning: --gpus {args.gpus} but WORLD_SIZE {ctx.world}", file=sys.stderr)
     if ctx.world > 1:
         import torch.distributed as dist
         timeout = datetime.timedelta(seconds=float(os.environ.get("PDA_DIST_TIMEOUT_S", "600")))

@@ -194,6 +194,59 @@ def test_visible_gpu_count_render_nodes_and_selectors(monkeypatch, tmp_path):
     assert launch.gpu_pci_bdf(0) is None
 
 
+def _run_bare(gpus, extra_args=(), extra_env=None, tmp=None, device_args=ARGS):
+    """bench.py started the way the driver starts ``--gpus 1``: no external launcher."""
+    env = dict(os.environ)
+    env.update({"OMP_NUM_THREADS": "1", "PDA_BIND_NUMA": "0"})
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "LOCAL_WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    env.update(extra_env or {})
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", str(gpus), *device_args,
+           *extra_args]
+    return subprocess.run(cmd, cwd=tmp, env=env, capture_output=True, text=True, timeout=600)
+
+
+def test_bench_bare_gpus8_self_launches_ranks(tmp_path):
+    """``python bench.py --gpus 8`` with NO external launcher still runs 8 ranks (the parent starts
+    torch.distributed.run as a child before any HIP call) and relays ONE record from rank 0."""
+    r = _run_bare(8, ("--amp-steps", "0", "--comm-probe", "0"), tmp=tmp_path)
+    assert r.returncode == 0, r.stderr[-4000:]
+    rec = _record(r)
+    assert rec["n_gpus"] == 8 and rec["config"]["parallelism"] == "dp8"
+    assert rec["config"]["global_batch"] == 16
+    assert rec["weights_consistent"] is True
+    assert rec["launcher"].startswith("bench.py -> torch.distributed.run")
+    sp = rec["rank_time_spread"]["headline"]
+    assert 0 < sp["min_s"] <= sp["max_s"]
+
+
+def test_bench_bare_diverged_rank_exit_code_relayed(tmp_path):
+    """A failing rank under the self-launch makes the parent exit non-zero."""
+    r = _run_bare(2, ("--amp-steps", "0", "--comm-probe", "0"), {"PDA_BENCH_PERTURB_RANK": "1"},
+                  tmp=tmp_path)
+    assert r.returncode != 0
+    assert "parameters differ across ranks" in r.stderr
+
+
+def test_bench_refuses_more_gpus_than_visible(tmp_path):
+    """``--gpus 2`` where fewer GPUs are visible (none in this container) exits non-zero at once with
+    the device-count message instead of folding ranks onto one device."""
+    import time
+    t0 = time.time()
+    r = _run_bare(2, tmp=tmp_path, device_args=("--steps", "1", "--warmup", "0"),
+                  extra_env={"HIP_VISIBLE_DEVICES": "", "CUDA_VISIBLE_DEVICES": ""})
+    assert r.returncode == 2, (r.returncode, r.stderr[-2000:])
+    assert "needs 2 visible GPUs" in r.stderr
+    assert not [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert time.time() - t0 < 120
+
+
+def test_bench_refuses_world_size_mismatch(tmp_path):
+    """Started by a launcher whose world differs from --gpus: refused, not mislabelled."""
+    r = _run_bare(4, tmp=tmp_path, extra_env={"WORLD_SIZE": "2", "RANK": "0", "LOCAL_RANK": "0"})
+    assert r.returncode == 2 and "WORLD_SIZE 2 but --gpus 4" in r.stderr
+
+
 def test_bench_cpu_diverged_rank_fails(tmp_path):
     r = _run(2, {"PDA_BENCH_PERTURB_RANK": "1"}, tmp=tmp_path)
     assert r.returncode != 0

@@ -28,7 +28,7 @@ def test_bench_torchrun_two_ranks(tmp_path):
                 "HSA_ENABLE_IPC_MODE_LEGACY": "0"})
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
            "--master-addr", "127.0.0.1", "--master-port", str(_port()),
-           os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "2", "--warmup", "1",
+           os.path.join(ROOT, "bench.py"), "--gpus", "2", "--rehearse-fold", "--steps", "2", "--warmup", "1",
            "--batch", "16", "--image-size", "64"]
     r = subprocess.run(cmd, cwd=tmp_path, env=env, capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stderr[-4000:]
@@ -68,8 +68,28 @@ def test_bench_torchrun_perturbed_rank_fails(tmp_path):
                 "HSA_ENABLE_IPC_MODE_LEGACY": "0", "PDA_BENCH_PERTURB_RANK": "1"})
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
            "--master-addr", "127.0.0.1", "--master-port", str(_port()),
-           os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "1", "--warmup", "1",
+           os.path.join(ROOT, "bench.py"), "--gpus", "2", "--rehearse-fold", "--steps", "1", "--warmup", "1",
            "--batch", "8", "--image-size", "64", "--fp32-steps", "0", "--amp-steps", "0",
            "--dp-steps", "0"]
     r = subprocess.run(cmd, cwd=tmp_path, env=env, capture_output=True, text=True, timeout=300)
     assert r.returncode != 0 and "parameters differ across ranks" in r.stderr
+
+
+def test_bench_bare_gpus2_refused_on_one_gpu_box(tmp_path):
+    """The driver's invocation form, ``python bench.py --gpus 2`` with no launcher, on a box with one
+    visible GPU: a non-zero exit with the device-count message within seconds (no HIP call made),
+    never a silent one-GPU record."""
+    import time
+    from pytorch_distributed_amd.launch import visible_gpu_count
+    if visible_gpu_count() >= 2:
+        pytest.skip("more than one GPU visible")
+    env = dict(os.environ)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "LOCAL_WORLD_SIZE"):
+        env.pop(k, None)
+    t0 = time.time()
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "1",
+                        "--warmup", "0"], cwd=tmp_path, env=env, capture_output=True, text=True,
+                       timeout=120)
+    assert r.returncode == 2, (r.returncode, r.stderr[-2000:])
+    assert "needs 2 visible GPUs" in r.stderr and time.time() - t0 < 60
+    assert not [l for l in r.stdout.splitlines() if l.startswith("{")]
