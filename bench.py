@@ -399,6 +399,11 @@ def _fp32_pass(ctx: Ctx, args, mode: str = "split") -> dict:
            f"{key}_ms_per_step": round(1000.0 * el / args.fp32_steps, 3)}
     if mode == "split":
         res.update({"fp32_engine": tr.engine, "fp32_conv": "split (bf16 MFMA hi/lo, >= TF32)",
+                    "fp32_conv_note": "fp32_* = split convs (per-conv error <= TF32, "
+                                      "tests/test_f32_precision_gpu.py); fp32_exact_* = f32 MFMA. "
+                                      "TF32 is torch's cudnn.allow_tf32 default, which the reference "
+                                      "never changes; its GPU model is not stated, so whether its "
+                                      "fp32 bar ran TF32 is parity unpinned",
                     "fp32_mode": "single" if world == 1 else "per-rank local steps, no all-reduce"})
     del tr
     if ctx.cuda:
@@ -517,6 +522,9 @@ def _dp_pass(ctx: Ctx, args, dtype) -> dict:
                        "dp_gpu_util_pct": rec.get("gpu_util_pct"), "dp_vs_baseline": rec.get("vs_baseline"),
                        "dp_exposed_comm_ms": rec.get("exposed_comm_ms"),
                        "dp_segments": rec.get("dp_segments"),
+                       "dp_replay_ms_per_step": rec.get("dp_replay_ms_per_step"),
+                       "dp_replay_vs_eager": rec.get("dp_replay_vs_eager"),
+                       "dp_replay_segments": rec.get("dp_replay_segments"),
                        "dp_side_graphs": rec.get("dp_side_graphs")}
         except subprocess.TimeoutExpired:
             res = {"dp_error": f"timeout after {limit:.0f} s"}
@@ -594,6 +602,19 @@ def main():
         diag["dp_segments"] = len(rg.graphs)
         diag["dp_side_graphs"] = sum(g is not None for g in getattr(rg, "sides", []))
         nxt += 1
+    if args.dp and not getattr(tr.dp, "replicas", None) and ctx.cuda and args.steps > 0:
+        # one device: the eager step above is what torch's DataParallel does for one device; the
+        # replica-graph replay an N > 1 run takes (per-block segment graphs + weight-gradient side
+        # graphs) is timed here too, so that path has a number on every 1-GPU record
+        tr.dp.force_replay = True
+        for i in range(3):            # capture + settle
+            tr.step(nxt + i)
+        rel = _timed(ctx, tr, nxt + 3, args.steps, "dp_replay")
+        nxt += 3 + args.steps
+        diag["dp_replay_ms_per_step"] = round(1000.0 * rel / args.steps, 3)
+        diag["dp_replay_vs_eager"] = round(rel / elapsed, 4)
+        diag["dp_replay_segments"] = len(tr.dp._graphs[0].graphs)
+        tr.dp.force_replay = False
     if args.dp:   # every replica must hold bit-identical weights (the replicated fused SGD)
         try:
             tr.state_checksum()

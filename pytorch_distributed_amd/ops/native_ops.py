@@ -732,10 +732,11 @@ _WGRAD_TAP_BLOCKS = 96
 
 def wgrad_tap_ok(g: ConvGeom, dtype: torch.dtype) -> bool:
     """Whether :func:`conv_wgrad` runs the tap-reuse kernel for this conv: 3x3 / stride 1 / pad 1,
-    16-bit, channel counts in 64-column tiles, image width in the ``PDA_WGRAD_TAP`` set (<= 59)."""
+    16-bit, channel counts in 64-column tiles, image width in the ``PDA_WGRAD_TAP`` set (<= 59).
+    Cin must be a power of two: the reduce decodes a slab column's tap as ``n >> log2(Cin)``."""
     return (dtype in (torch.bfloat16, torch.float16) and g.R == 3 and g.S == 3 and g.stride == 1
             and g.pad == 1 and g.Ho == g.H and g.Wo == g.W and g.W <= 59 and g.W in _WGRAD_TAP
-            and g.Cin % 64 == 0 and g.Cout % 64 == 0
+            and g.Cin % 64 == 0 and g.Cout % 64 == 0 and (g.Cin & (g.Cin - 1)) == 0
             and getattr(ext.lib(), "pda_wgrad_tap", None) is not None)
 
 

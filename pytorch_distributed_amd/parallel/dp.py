@@ -136,6 +136,11 @@ class DataParallel(nn.Module):
         # HIP events at the end of backward and after the last gradient all-reduce of the next
         # graph-replayed step (exposed_comm_ms); diagnostics only
         self.timing = False
+        # one device: replay the replica graphs anyway (bench.py dp_replay_ms_per_step)
+        self.force_replay = os.environ.get("PDA_DP_FORCE_REPLAY", "0") == "1"
+        # host-side bound on one segment's replay enqueue per device worker (a graph launch takes
+        # ~1 ms): a worker that raises or never returns becomes an exception in the caller
+        self.replay_timeout_s = float(os.environ.get("PDA_DP_REPLAY_TIMEOUT_S", "120"))
         self._ev_bwd = self._ev_comm = None
 
     # ------------------------------------------------------------------ construction
@@ -296,11 +301,11 @@ class DataParallel(nn.Module):
     def train_step_chunks(self, xs, ys, optimizer, graph: bool = True) -> torch.Tensor:
         """:meth:`train_step` on per-replica input chunks (e.g. generated on each GPU directly,
         skipping the scatter from ``device_ids[0]``)."""
-        if graph and not self.replicas:
+        if graph and not self.replicas and not self.force_replay:
             # one device: the module's own (eager, two-stream) step, as torch's DataParallel calls
             # the module directly for a single device; replay only pays where one host thread
-            # drives several GPUs (the per-block segment graphs cost ~5 % on one device,
-            # profiles/ab_r5.md section 7)
+            # drives several GPUs. ``force_replay`` keeps the replica graphs on one device, so the
+            # path an N > 1 run takes is measurable on one (bench.py dp_replay_ms_per_step)
             graph = False
         if graph:
             from ..runtime.graphs import graphs_unsafe_warning, single_queue_graphs
@@ -417,8 +422,10 @@ class DataParallel(nn.Module):
                 # one host thread per device: hipGraphLaunch of a ~150-node segment costs ~0.5 ms
                 # of host time and CUDAGraph.replay releases the GIL, so the N replicas enqueue
                 # concurrently instead of staggering device i's start by i launches
-                list(self._pool().map(lambda a: a[0][0].replay(s, a[0][1], a[0][2], a[1]),
-                                      zip(jobs, streams)))
+                run_workers(self._pool(), [
+                    (lambda a=a: a[0][0].replay(s, a[0][1], a[0][2], a[1]))
+                    for a in zip(jobs, streams)], self.replay_timeout_s,
+                    [f"cuda:{rg.dev.index}" for rg, _, _ in jobs])
             else:
                 for (rg, x, y), st in zip(jobs, streams):
                     rg.replay(s, x, y, st)
@@ -465,6 +472,27 @@ class DataParallel(nn.Module):
             self._armed = True
             torch.autograd.Variable._execution_engine.queue_callback(self._reduce_grads)
         return g
+
+
+def run_workers(pool, fns, timeout_s: float, names=None) -> list:
+    """Run ``fns`` on the executor ``pool`` and wait at most ``timeout_s`` seconds for all of them:
+    the first worker exception is re-raised here (naming its device), and workers still running at
+    the deadline raise TimeoutError instead of hanging the step. Results in ``fns`` order."""
+    from concurrent.futures import FIRST_EXCEPTION, wait
+    names = names or [str(i) for i in range(len(fns))]
+    futs = [pool.submit(f) for f in fns]
+    done, pending = wait(futs, timeout=timeout_s, return_when=FIRST_EXCEPTION)
+    for f, n in zip(futs, names):
+        if f in done and f.exception() is not None:
+            for p in pending:
+                p.cancel()
+            raise RuntimeError(f"DataParallel replay worker for {n} failed: "
+                               f"{type(f.exception()).__name__}: {f.exception()}") from f.exception()
+    if pending:
+        late = [n for f, n in zip(futs, names) if f in pending]
+        raise TimeoutError(f"DataParallel replay worker(s) for {late} did not return within "
+                           f"{timeout_s:.0f} s")
+    return [f.result() for f in futs]
 
 
 class _ReplicaGraph:

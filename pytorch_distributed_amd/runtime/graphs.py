@@ -77,15 +77,44 @@ def native_train_step(model, opt, x: torch.Tensor, y: torch.Tensor, scaler=None)
 GRAPH_QUEUES_VAR = "DEBUG_HIP_FORCE_GRAPH_QUEUES"
 
 
+def hip_runtime_started() -> bool:
+    """Whether the HIP/HSA runtime of this process has initialised -- it then holds ``/dev/kfd``
+    open. ``torch.cuda.is_initialized()`` alone misses it: ``device_count()`` / ``is_available()``
+    start the runtime (which reads GRAPH_QUEUES_VAR once) without setting torch's flag."""
+    if torch.cuda.is_initialized():
+        return True
+    try:
+        for fd in os.listdir("/proc/self/fd"):
+            try:
+                if os.readlink(f"/proc/self/fd/{fd}") == "/dev/kfd":
+                    return True
+            except OSError:
+                continue
+    except OSError:
+        pass
+    return False
+
+
+# the variable's value as last observed while the runtime had NOT started (the value it reads at
+# its start unless changed in between); at module import, and again at every query made before
+# the runtime starts. A module imported after the runtime started keeps the import-time value.
+_QUEUES_SEEN = os.environ.get(GRAPH_QUEUES_VAR)
+
+
 def single_queue_graphs() -> bool:
-    """Whether HIP graphs launch on one queue in this process (see GRAPH_QUEUES_VAR)."""
-    return os.environ.get(GRAPH_QUEUES_VAR) == "1"
+    """Whether HIP graphs launch on one queue in this process (see GRAPH_QUEUES_VAR): the variable
+    must have been "1" before the HIP runtime started. A value set after the runtime started (by
+    then it has read the variable) is not trusted."""
+    global _QUEUES_SEEN
+    if not hip_runtime_started():
+        _QUEUES_SEEN = os.environ.get(GRAPH_QUEUES_VAR)
+    return _QUEUES_SEEN == "1"
 
 
 def request_single_queue_graphs() -> bool:
     """Ask for single-queue graph launch if HIP has not started yet in this process (an explicit
     setting is kept); returns whether graph replay is safe here (:func:`single_queue_graphs`)."""
-    if os.environ.get(GRAPH_QUEUES_VAR) is None and not torch.cuda.is_initialized():
+    if not hip_runtime_started() and os.environ.get(GRAPH_QUEUES_VAR) is None:
         os.environ[GRAPH_QUEUES_VAR] = "1"
     return single_queue_graphs()
 

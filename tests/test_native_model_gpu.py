@@ -488,3 +488,42 @@ def test_decomposed_fold_wgrad_matches_apply_path():
         if e_wg > 1.3 * e_apply + 0.01:
             bad.append((n, e_wg, e_apply))
     assert not bad, bad
+
+
+def test_fork_tracking_orders_side_stream_reads():
+    """The rule fork tracking relies on (models/native.py _fork): a fork after a TRACKED native
+    launch makes the second stream wait on the event that launch's own dispatch completes. A long
+    chain of tracked streaming launches on the main stream (each doubles the previous buffer), then
+    _fork(), then a side-stream read: the read must see the chain's final values -- a fork that did
+    not wait would copy a stale or half-written buffer. Also checks the fork took the tracked path
+    (the launch counter moved) and that an untracked fork (tracking off) orders the same read."""
+    import ctypes as C
+    from pytorch_distributed_amd.ops import ext
+    L = ext.lib()
+    _, nm = _pair("resnet18", image=32)
+    assert nm._side is not None
+    n = 32 << 20                              # 128 MiB per buffer: ~50 us per launch
+    base = torch.full((n,), 1.0, device=DEV)
+    bufs = [base.clone(), torch.empty_like(base)]
+    ms = C.c_void_p(torch.cuda.current_stream(DEV).cuda_stream)
+    for tracking in (True, False):
+        nm.fork_tracking = tracking
+        bufs[0].copy_(base)
+        torch.cuda.synchronize()
+        nm._track(True)
+        c0 = L.pda_track_count()
+        steps = 12
+        for k in range(steps):
+            src, dst = bufs[k % 2], bufs[(k + 1) % 2]
+            assert L.pda_fork_probe(C.c_void_p(dst.data_ptr()), C.c_void_p(src.data_ptr()), n, None,
+                                    ms) == 0
+        moved = L.pda_track_count() != c0
+        nm._fork()
+        with torch.cuda.stream(nm._side):
+            seen = bufs[steps % 2].clone()
+        nm._track(False)
+        torch.cuda.current_stream(DEV).wait_stream(nm._side)
+        torch.cuda.synchronize()
+        assert moved == tracking, (tracking, moved)
+        want = float(2 ** steps)
+        assert bool((seen == want).all()), (tracking, seen.min().item(), seen.max().item())
