@@ -71,7 +71,6 @@ enum Pass : int { FWD = 0, DGRAD = 1, WGRAD = 2, WGRAD_BNA = 3, DGRAD_BNF = 4, W
                   FWD_TAIL = 6 };
 
 template <int V> struct IC { static constexpr int value = V; };
-typedef unsigned int pu32x4 __attribute__((ext_vector_type(4)));
 
 struct ConvParams {
   const void* a;      // FWD: X [Nb,H,W,Cin]; DGRAD: dY [Nb,Ho,Wo,Cout]; WGRAD: dY
@@ -1387,8 +1386,6 @@ __global__ __launch_bounds__(conv_nt<st_of(STAGES_T)>(), (PASS_T == WGRAD_BNA ||
     // which bounds the prefetch registers to PD rows.
     constexpr int PD = RPTH > 4 ? 4 : RPTH;
     char* outb = reinterpret_cast<char*>(p.out);
-    const __amdgpu_buffer_rsrc_t rso = __builtin_amdgcn_make_buffer_rsrc(
-        p.out, (short)0, (int)((uint32_t)p.M * (uint32_t)p.out_pitch * (uint32_t)ES), 0x00020000);
     const int gcol = n0 + cc * EPO;
     auto row_off = [&](int i, bool& ok) __attribute__((always_inline)) -> uint32_t {
       const int grow = m0 + rg + RG * i;
@@ -1473,9 +1470,7 @@ __global__ __launch_bounds__(conv_nt<st_of(STAGES_T)>(), (PASS_T == WGRAD_BNA ||
         for (int j = 0; j < PD; ++j) {
           const int row = rg + RG * (g0 + j);   // local row of the staged half
           i32x4 v = *reinterpret_cast<const i32x4*>(ct + c_addr(row, cc) * 16);
-          if constexpr (!PERS) {
-            if (!eok[j]) continue;
-          }
+          if (!eok[j]) continue;
           if constexpr (O32) {   // one element per dword
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
@@ -1528,7 +1523,7 @@ __global__ __launch_bounds__(conv_nt<st_of(STAGES_T)>(), (PASS_T == WGRAD_BNA ||
               q1[k] += dz * yv;
               if constexpr (MODE == 2) q2[k] += dz * y2v;
             }
-          } else if (do_stats && (!PERS || eok[j])) {
+          } else if (do_stats) {
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
               const f32x2 dlt = unpack2<DT>((uint32_t)v[k]) - shv[k];
@@ -1536,13 +1531,8 @@ __global__ __launch_bounds__(conv_nt<st_of(STAGES_T)>(), (PASS_T == WGRAD_BNA ||
               q1[k] += dlt * dlt;
             }
           }
-          if constexpr (PERS) {   // branch-free: a row past M stores at OOB (dropped)
-            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(pu32x4, v), rso,
-                                                   eok[j] ? (int)(eoff[j] * ES) : (int)OOB, 0, 0);
-          } else {
-            i32x4* dst = reinterpret_cast<i32x4*>(outb + (size_t)eoff[j] * ES);
-            *dst = v;
-          }
+          i32x4* dst = reinterpret_cast<i32x4*>(outb + (size_t)eoff[j] * ES);
+          *dst = v;
         }
       }
       }
@@ -1599,27 +1589,20 @@ __global__ __launch_bounds__(conv_nt<st_of(STAGES_T)>(), (PASS_T == WGRAD_BNA ||
   };   // epilogue
 
   if constexpr (PERS) {
-    // persistent walk. LDS holds the k-tile being multiplied; the registers the NEXT one (of this
-    // tile, or the first of the block's next tile), loaded BEFORE the MFMAs and the epilogue and
-    // stored to LDS after them -- loads and the wait for them in the same iteration, so the
-    // compiler's vmcnt counts only the epilogue's (unconditional) stores issued in between
-    // instead of draining them at a loop back-edge
+    // persistent walk: tile v's MFMAs and epilogue run while the loads of tile v + gridDim.x's
+    // first k-tile are in flight (issued right after tile v's last k-tile was published to LDS)
     int v = blockIdx.x;
-    if (nk > 0) {
-      load_tile(0);
-      store_tile(0);
-      __syncthreads();
-    }
+    if (nk > 0) load_tile(0);
     for (;;) {
       const int vn = v + (int)gridDim.x;
       const bool more = vn < ntile;
       const int tmc = tm, tnc = tn, m0c = m0, n0c = n0;
       for (int kt = 0; kt < nk; ++kt) {
-        const bool last = kt + 1 == nk;
-        const bool nxt = !last || more;
-        if (!last) {
+        store_tile(0);
+        __syncthreads();
+        if (kt + 1 < nk) {
           load_tile(kt + 1);
-        } else if (more) {   // the next tile's loader offsets, then its first k-tile
+        } else if (more) {   // next tile's loader offsets, then its first k-tile
           const int tt = (int)xcd_remap(vn, ntile);
           tm = tt / tiles_n; tn = tt - tm * tiles_n; m0 = tm * BM; n0 = tn * BN;
           setup_fwd();
@@ -1628,15 +1611,8 @@ __global__ __launch_bounds__(conv_nt<st_of(STAGES_T)>(), (PASS_T == WGRAD_BNA ||
         }
         mma_tile(smem, smem + A_BYTES);
         __syncthreads();
-        if (last) {
-          epilogue();
-          __syncthreads();   // the epilogue's last LDS reads before the next staging
-        }
-        if (nxt) {
-          store_tile(0);
-          __syncthreads();
-        }
       }
+      epilogue();
       if (!more) break;
       v = vn;
       const int tt = (int)xcd_remap(v, ntile);
@@ -1645,6 +1621,7 @@ __global__ __launch_bounds__(conv_nt<st_of(STAGES_T)>(), (PASS_T == WGRAD_BNA ||
       for (int i = 0; i < MI; ++i)
 #pragma unroll
         for (int j = 0; j < NI; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+      __syncthreads();   // the epilogue's last LDS reads before the next tile's staging
     }
   } else {
     epilogue();
