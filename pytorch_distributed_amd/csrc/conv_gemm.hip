@@ -211,25 +211,14 @@ constexpr int conv_min_blocks() {
   return (STAGES == 1 && BM * BN <= 128 * 128) ? 3 : 2;
 }
 
-// STAGES_T == 0: the PERSISTENT single-stage form (FWD only): gridDim.x <= tiles blocks, each walks
-// the tiles v = blockIdx.x, + gridDim.x, ... and issues the loads of its next tile's first k-tile
-// before the MFMAs and the epilogue of the current one, so a CU keeps operand loads in flight
-// through every epilogue instead of only while another resident block happens to be loading.
-constexpr int st_of(int s) { return s == 0 ? 1 : s; }
-// resident blocks per CU of the persistent tiles: the walk keeps the next tile's operands and the
-// loop state live across the epilogue, so one block fewer than the single-stage budget (no spills)
-constexpr int conv_pers_blocks(int bm, int bn) { return bm * bn >= 128 * 128 ? 2 : 3; }
-
-template <int PASS_T, int DT, int BM, int BN, int STAGES_T>
+template <int PASS_T, int DT, int BM, int BN, int STAGES>
 // WGRAD_BNA holds the fixed column chunk's 24 BN coefficients and the y chunks: 3 blocks per CU
 // (the 16-bit WGRAD budget of 4 spilled 15 VGPRs); its 256-column tile (the stem's whole N: dz and
 // y staged and transformed once instead of once per 128-column tile) needs 246: 2 blocks per CU
 // (the 128x128 WGRAD_BNA tile of the bottleneck conv3 fold: 2 blocks, 3 spilled 89 VGPRs)
 // FWD_TAIL holds the residual chunks and both branches' BN coefficients across the MFMAs: the
 // 128x64 tile at 3 blocks per CU, 128x128 at 2 (the plain FWD budgets spill 43 / 50 VGPRs)
-__global__ __launch_bounds__(conv_nt<st_of(STAGES_T)>(), (PASS_T == WGRAD_BNA || PASS_T == WGRAD_GRAM ? (BN >= 256 || BM * BN >= 128 * 128 ? 2 : 3) : PASS_T == FWD_TAIL ? (BM * BN >= 128 * 128 ? 2 : 3) : STAGES_T == 0 ? conv_pers_blocks(BM, BN) : conv_min_blocks<DT, BM, BN, st_of(STAGES_T)>())) void conv_gemm_kernel(ConvParams p_arg) {
-  constexpr bool PERS = STAGES_T == 0;
-  constexpr int STAGES = st_of(STAGES_T);
+__global__ __launch_bounds__(conv_nt<STAGES>(), (PASS_T == WGRAD_BNA || PASS_T == WGRAD_GRAM ? (BN >= 256 || BM * BN >= 128 * 128 ? 2 : 3) : PASS_T == FWD_TAIL ? (BM * BN >= 128 * 128 ? 2 : 3) : conv_min_blocks<DT, BM, BN, STAGES>())) void conv_gemm_kernel(ConvParams p_arg) {
   constexpr int PASS = PASS_T == WGRAD_BNA || PASS_T == WGRAD_GRAM ? WGRAD
                        : PASS_T == DGRAD_BNF ? DGRAD : PASS_T == FWD_TAIL ? FWD : PASS_T;
   constexpr bool TAILP = PASS_T == FWD_TAIL;   // tail-apply prologue (a = relu(bn3(y3) + r))
@@ -247,7 +236,6 @@ __global__ __launch_bounds__(conv_nt<st_of(STAGES_T)>(), (PASS_T == WGRAD_BNA ||
   static_assert(!ABN || DT == DT_BF16 || DT == DT_F16, "WGRAD_BNA: 16-bit operands");
   static_assert(!BNF || ((DT == DT_BF16 || DT == DT_F16) && !DMA), "DGRAD_BNF: 16-bit, register-staged");
   static_assert(!TAILP || ((DT == DT_BF16 || DT == DT_F16) && STAGES == 1), "FWD_TAIL: 16-bit, single-stage");
-  static_assert(!PERS || (PASS_T == FWD && (DT == DT_BF16 || DT == DT_F16)), "persistent: 16-bit FWD");
   // DGRAD / WGRAD read the parameters in place in the kernarg segment (constant address space):
   // binding a reference to the by-value argument makes the compiler copy the whole ~1 KB block to
   // scratch once a member array is indexed dynamically (DGRAD tap tables), and costs WGRAD spills.
@@ -256,7 +244,7 @@ __global__ __launch_bounds__(conv_nt<st_of(STAGES_T)>(), (PASS_T == WGRAD_BNA ||
 #if defined(__HIP_DEVICE_COMPILE__)
   typedef const __attribute__((address_space(4))) ConvParams KParams;
   auto&& p = [&]() -> decltype(auto) {
-    if constexpr (PASS != FWD || PERS) return *(KParams*)__builtin_amdgcn_kernarg_segment_ptr();
+    if constexpr (PASS != FWD) return *(KParams*)__builtin_amdgcn_kernarg_segment_ptr();
     else return (p_arg);
   }();
 #else   // host pass of the template (never executed): the plain argument
@@ -323,8 +311,8 @@ __global__ __launch_bounds__(conv_nt<st_of(STAGES_T)>(), (PASS_T == WGRAD_BNA ||
   const int tiles_m = (p.M + BM - 1) / BM;
   const int ntile = tiles_m * tiles_n;
   const int t = (int)xcd_remap(blockIdx.x, ntile);
-  int tm = t / tiles_n, tn = t - tm * tiles_n;   // (PERS: the block's current tile)
-  int m0 = tm * BM, n0 = tn * BN;
+  const int tm = t / tiles_n, tn = t - tm * tiles_n;
+  const int m0 = tm * BM, n0 = tn * BN;
   const int split = blockIdx.y;  // WGRAD: K split; DGRAD: parity class
 
   // ---- K range --------------------------------------------------------------------
@@ -432,33 +420,6 @@ __global__ __launch_bounds__(conv_nt<st_of(STAGES_T)>(), (PASS_T == WGRAD_BNA ||
     for (int i = 0; i < BR; ++i)
       b_off[i] = col < p.N ? (uint32_t)((tid / CPR + RPI * i) * p.R * p.S * p.Cin + col) * (uint32_t)ES : OOB;
   }
-  // PERS: the FWD loader offsets above for the block's current (m0, n0), recomputed per tile
-  auto setup_fwd = [&]() __attribute__((always_inline)) {
-    if constexpr (PERS) {
-#pragma unroll
-      for (int i = 0; i < AR; ++i) {
-        const int m = m0 + (tid >> 3) + 32 * i;
-        const bool okm = m < p.M;
-        const uint32_t mm = okm ? m : 0;
-        const uint32_t img = fdiv(mm, p.dHoWo), rem = mm - img * p.dHoWo.d;
-        const uint32_t yo = fdiv(rem, p.dWo), xo = rem - yo * p.dWo.d;
-        const int y0 = (int)yo * p.stride - p.pad, x0 = (int)xo * p.stride - p.pad;
-        a_base[i] = (((int)img * p.H + y0) * p.W + x0) * p.Cin * ES;
-        uint64_t msk = 0;
-        for (int r = 0, t = 0; r < p.R; ++r) {
-          const bool yok = (unsigned)(y0 + r) < (unsigned)p.H;
-          for (int q = 0; q < p.S; ++q, ++t)
-            if (yok && (unsigned)(x0 + q) < (unsigned)p.W) msk |= 1ull << t;
-        }
-        a_mask[i] = okm ? msk : 0ull;
-      }
-#pragma unroll
-      for (int i = 0; i < BR; ++i) {
-        const int n = n0 + (tid >> 3) + 32 * i;
-        b_off[i] = n < p.N ? (uint32_t)(n * p.Kpad + (tid & 7) * EPC) * (uint32_t)ES : OOB;
-      }
-    }
-  };
   // WGRAD B gather: fixed column chunk per thread -> (tap, c)
   int wb_r = 0, wb_s = 0, wb_c = 0;
   bool wb_colok = true;
@@ -1250,7 +1211,7 @@ __global__ __launch_bounds__(conv_nt<st_of(STAGES_T)>(), (PASS_T == WGRAD_BNA ||
   if constexpr (DMA) {
     vm_wait<0>();
     __syncthreads();   // the epilogue reuses the ring
-  } else if constexpr (!PERS) {
+  } else {
     if (nk > 0) {
       load_tile(0);
       if constexpr (STAGES == 2) {
@@ -1276,7 +1237,6 @@ __global__ __launch_bounds__(conv_nt<st_of(STAGES_T)>(), (PASS_T == WGRAD_BNA ||
   }
 
   // ================================================================ epilogue
-  auto epilogue = [&]() __attribute__((always_inline)) {
   const int lr = lane & 15, lg = lane >> 4;
   // every accumulator value as (row, 4 consecutive columns) within the wave tile: the MFMA runs
   // with swapped operands (D = C^T), so a lane holds 4 consecutive C columns per 16x16 tile
@@ -1586,46 +1546,6 @@ __global__ __launch_bounds__(conv_nt<st_of(STAGES_T)>(), (PASS_T == WGRAD_BNA ||
       rows(IC<-1>{}, IC<0>{});
     }
   }
-  };   // epilogue
-
-  if constexpr (PERS) {
-    // persistent walk: tile v's MFMAs and epilogue run while the loads of tile v + gridDim.x's
-    // first k-tile are in flight (issued right after tile v's last k-tile was published to LDS)
-    int v = blockIdx.x;
-    if (nk > 0) load_tile(0);
-    for (;;) {
-      const int vn = v + (int)gridDim.x;
-      const bool more = vn < ntile;
-      const int tmc = tm, tnc = tn, m0c = m0, n0c = n0;
-      for (int kt = 0; kt < nk; ++kt) {
-        store_tile(0);
-        __syncthreads();
-        if (kt + 1 < nk) {
-          load_tile(kt + 1);
-        } else if (more) {   // next tile's loader offsets, then its first k-tile
-          const int tt = (int)xcd_remap(vn, ntile);
-          tm = tt / tiles_n; tn = tt - tm * tiles_n; m0 = tm * BM; n0 = tn * BN;
-          setup_fwd();
-          load_tile(0);
-          tm = tmc; tn = tnc; m0 = m0c; n0 = n0c;
-        }
-        mma_tile(smem, smem + A_BYTES);
-        __syncthreads();
-      }
-      epilogue();
-      if (!more) break;
-      v = vn;
-      const int tt = (int)xcd_remap(v, ntile);
-      tm = tt / tiles_n; tn = tt - tm * tiles_n; m0 = tm * BM; n0 = tn * BN;
-#pragma unroll
-      for (int i = 0; i < MI; ++i)
-#pragma unroll
-        for (int j = 0; j < NI; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-      __syncthreads();   // the epilogue's last LDS reads before the next tile's staging
-    }
-  } else {
-    epilogue();
-  }
 }
 
 // split-K slab reduction for WGRAD, with layout remap + scale, into the f32 gradient buffer:
@@ -1910,23 +1830,7 @@ static int launch(const ConvParams& p, dim3 grid, hipStream_t st) {
 // Tile codes: bm < 0 selects the single-buffer (STAGES = 1) variant of tile |bm| x bn; bm > 1000
 // the LDS-DMA 8-wave variant (STAGES = 3) of tile (bm - 1000) x bn (16-bit, no operand prologue).
 // bm > 2000: the tap-reuse (HALO) variant of (bm - 2000) x bn for 3x3 stride-1 FWD / DGRAD.
-// bm > 3000: the persistent single-stage variant (STAGES_T = 0) of (bm - 3000) x bn, FWD only.
-static int tile_bm(int bm) {
-  return bm > 3000 ? bm - 3000 : bm > 2000 ? bm - 2000 : bm > 1000 ? bm - 1000 : (bm < 0 ? -bm : bm);
-}
-// compute units of the current device (persistent grids)
-static int num_cu() {
-  static int cus[64] = {0};
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
-  if (cus[dev] == 0) {
-    int n = 0;
-    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
-      n = 256;
-    cus[dev] = n;
-  }
-  return cus[dev];
-}
+static int tile_bm(int bm) { return bm > 2000 ? bm - 2000 : bm > 1000 ? bm - 1000 : (bm < 0 ? -bm : bm); }
 static bool halo_ok(const ConvParams& p, int csz) {
   return p.R == 3 && p.S == 3 && p.stride == 1 && p.pad == 1 && p.W <= 63 && csz % 64 == 0 &&
          p.Ho == p.H && p.Wo == p.W;
@@ -1934,25 +1838,6 @@ static bool halo_ok(const ConvParams& p, int csz) {
 
 template <int PASS>
 static int dispatch(int dt, int bm, int bn, const ConvParams& p, dim3 grid, hipStream_t st) {
-  if (bm > 3000) {
-    if constexpr (PASS == FWD) {
-      // resident blocks per CU of the single-stage tile (its register budget); grid a multiple of
-      // the 8 XCDs so a block's virtual tiles v, v + G, ... stay on its XCD (xcd_remap)
-      auto pgrid = [&](int occ) {
-        int g = num_cu() * occ;
-        if ((int)grid.x < g) g = (int)grid.x;
-        if (g > 8) g &= ~7;
-        return dim3(g, 1);
-      };
-#define TILE_CASE0(D, M_, N_)                                                   \
-  if (dt == D && bm - 3000 == M_ && bn == N_)                                  \
-    return launch<PASS, D, M_, N_, 0>(p, pgrid(conv_pers_blocks(M_, N_)), st);
-      TILE_CASE0(DT_BF16, 128, 128) TILE_CASE0(DT_BF16, 128, 64)
-      TILE_CASE0(DT_F16, 128, 128) TILE_CASE0(DT_F16, 128, 64)
-#undef TILE_CASE0
-    }
-    return -1;
-  }
   if (bm > 2000) {
     if constexpr (PASS != WGRAD) {
       if (p.pro_sc != nullptr || !halo_ok(p, PASS == FWD ? p.Cin : p.Cout)) return -5;

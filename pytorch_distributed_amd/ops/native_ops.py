@@ -167,8 +167,7 @@ def tile_rows(bm: int) -> int:
     """M rows of a tile code: -bm = single-stage register-staged, bm > 1000 = the LDS-DMA 8-wave
     variant of (bm - 1000) rows, bm > 2000 = its tap-reuse form for 3x3 stride-1 fwd / dgrad
     (csrc/conv_gemm.hip dispatch)."""
-    return (bm - 3000 if bm > 3000 else bm - 2000 if bm > 2000 else bm - 1000 if bm > 1000
-            else abs(bm))
+    return bm - 2000 if bm > 2000 else bm - 1000 if bm > 1000 else abs(bm)
 
 
 def _ktile(bm: int, bn: int, kdt: int, pro: bool = False) -> Tuple[int, int]:
@@ -176,13 +175,11 @@ def _ktile(bm: int, bn: int, kdt: int, pro: bool = False) -> Tuple[int, int]:
     apply an operand prologue (the bytes never pass through registers): those launches fall back
     to the register-staged 128-row tile. The split-f32 kernels stage hi + lo tiles: single-stage
     tiles of at most 128 x 128."""
-    if bm > 3000 and kdt not in (1, 2):   # the persistent tiles: 16-bit (prologue allowed)
-        bm = -(bm - 3000)
-    elif 1000 < bm < 3000 and (kdt not in (1, 2) or pro):   # (the HALO tiles too)
+    if bm > 1000 and (kdt not in (1, 2) or pro):   # (the HALO tiles too)
         bm, bn = -128, min(bn, 128)
     if kdt != 3:
         return bm, bn
-    return -min(tile_rows(bm), 128), min(bn, _SPLIT_BN)
+    return -min(abs(bm), 128), min(bn, _SPLIT_BN)
 
 
 def pick_tile(M: int, N: int, K: Optional[int] = None, dma: bool = False) -> Tuple[int, int]:

@@ -1152,38 +1152,3 @@ def test_wgrad_reduce_batch_matches_single_reduces():
     for a, b, c in zip(single, batch, again):
         assert rel_err(b, a) < 1e-6, rel_err(b, a)
         assert torch.equal(b, c)
-
-
-@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
-@pytest.mark.parametrize("geo", [(33, 56, 64, 256, 1), (9, 56, 256, 64, 1), (25, 30, 64, 64, 3),
-                                 (40, 28, 128, 512, 1)])
-@pytest.mark.parametrize("pro", [False, True])
-def test_conv_fwd_persistent_matches_single_stage(geo, pro, dtype):
-    """The persistent forward tiles (code 3000 + bm: a grid of at most CUs x resident blocks walks
-    every tile, the next tile's first k-tile loaded during the current tile's MFMAs and epilogue)
-    compute exactly what the single-stage tile of the same shape computes: bit-identical output and
-    BatchNorm statistics partials, with and without the BN+ReLU operand prologue, on grids that loop
-    several times (more tiles than blocks), ragged last M tiles and several column tiles."""
-    K = _k()
-    torch.manual_seed(11)
-    Nb, H, Cin, Cout, k = geo
-    g = K.ConvGeom(Nb, H, H, Cin, Cout, k, k, 1, k // 2)
-    x = (torch.randn(Nb, H, H, Cin, device=DEV) + 0.1).to(dtype)
-    w = (torch.randn(Cout, k, k, Cin, device=DEV) / (8 * k)).to(dtype).view(Cout, -1)
-    pr = (torch.rand(Cin, device=DEV) + 0.5, torch.randn(Cin, device=DEV) * 0.2) if pro else None
-    bn = 64 if Cout <= 64 else 128
-    M = Nb * H * H
-    T = -(-M // 128)
-    outs = []
-    for bm in (-128, 3128):
-        y = torch.empty(Nb, H, H, Cout, device=DEV, dtype=dtype)
-        st = torch.full((T * 3 * Cout,), float("nan"), device=DEV)
-        K.conv_fwd(x, w, g, y, stats=st, tile=(bm, bn), pro=pr)
-        outs.append((y, st))
-    torch.cuda.synchronize()
-    assert torch.equal(outs[0][0], outs[1][0])
-    assert torch.equal(outs[0][1], outs[1][1])
-    ref = torch.nn.functional.conv2d(
-        (torch.relu(x.float() * pr[0] + pr[1]) if pro else x.float()).permute(0, 3, 1, 2),
-        w.float().view(Cout, k, k, Cin).permute(0, 3, 1, 2), padding=k // 2).permute(0, 2, 3, 1)
-    torch.testing.assert_close(outs[1][0].float(), ref, rtol=3e-2, atol=3e-2)
