@@ -67,21 +67,10 @@ template <int N> __device__ __forceinline__ void vm_wait() {
 // branch), formed while staging A from y3 (p.a) and r (p.pro_res) -- the tail's BN-apply pass is
 // folded into its consumer: a is written once by the blocks of the first N-tile (p.pro_out, plus the
 // ReLU bitmask p.pro_mask in mode 1) instead of written by an apply pass and read back by the conv.
-//
-// DGRAD_BNA: DGRAD of a 1x1 stride-1 conv whose dY is a BatchNorm-backward output formed while
-// staging A, dY = k1[c]*dz + k2[c]*y + k3[c] (a = dz, a2 = y, per-k-tile channel coefficients) --
-// the apply pass of that BN (read dz and y, write dY) folds into its consumer: the blocks of the
-// first N-tile also write the formed dY (p.pro_out) for the weight gradient, as FWD_TAIL writes a.
 enum Pass : int { FWD = 0, DGRAD = 1, WGRAD = 2, WGRAD_BNA = 3, DGRAD_BNF = 4, WGRAD_GRAM = 5,
-                  FWD_TAIL = 6, DGRAD_BNA = 7 };
+                  FWD_TAIL = 6 };
 
 template <int V> struct IC { static constexpr int value = V; };
-
-// resident blocks per CU of the 128x128 DGRAD_BNA tile (its dz, y and coefficient registers): 2 holds
-// it in 214 VGPRs; 3 caps it at 168 with 104 B of spills
-#ifndef CONV_DBNA_BLOCKS
-#define CONV_DBNA_BLOCKS 2
-#endif
 
 struct ConvParams {
   const void* a;      // FWD: X [Nb,H,W,Cin]; DGRAD: dY [Nb,Ho,Wo,Cout]; WGRAD: dY
@@ -229,15 +218,13 @@ template <int PASS_T, int DT, int BM, int BN, int STAGES>
 // (the 128x128 WGRAD_BNA tile of the bottleneck conv3 fold: 2 blocks, 3 spilled 89 VGPRs)
 // FWD_TAIL holds the residual chunks and both branches' BN coefficients across the MFMAs: the
 // 128x64 tile at 3 blocks per CU, 128x128 at 2 (the plain FWD budgets spill 43 / 50 VGPRs)
-__global__ __launch_bounds__(conv_nt<STAGES>(), (PASS_T == WGRAD_BNA || PASS_T == WGRAD_GRAM ? (BN >= 256 || BM * BN >= 128 * 128 ? 2 : 3) : PASS_T == FWD_TAIL ? (BM * BN >= 128 * 128 ? 2 : 3) : PASS_T == DGRAD_BNA ? (BM * BN >= 128 * 128 ? CONV_DBNA_BLOCKS : 3) : conv_min_blocks<DT, BM, BN, STAGES>())) void conv_gemm_kernel(ConvParams p_arg) {
+__global__ __launch_bounds__(conv_nt<STAGES>(), (PASS_T == WGRAD_BNA || PASS_T == WGRAD_GRAM ? (BN >= 256 || BM * BN >= 128 * 128 ? 2 : 3) : PASS_T == FWD_TAIL ? (BM * BN >= 128 * 128 ? 2 : 3) : conv_min_blocks<DT, BM, BN, STAGES>())) void conv_gemm_kernel(ConvParams p_arg) {
   constexpr int PASS = PASS_T == WGRAD_BNA || PASS_T == WGRAD_GRAM ? WGRAD
-                       : PASS_T == DGRAD_BNF || PASS_T == DGRAD_BNA ? DGRAD
-                       : PASS_T == FWD_TAIL ? FWD : PASS_T;
+                       : PASS_T == DGRAD_BNF ? DGRAD : PASS_T == FWD_TAIL ? FWD : PASS_T;
   constexpr bool TAILP = PASS_T == FWD_TAIL;   // tail-apply prologue (a = relu(bn3(y3) + r))
   constexpr bool GRAM = PASS_T == WGRAD_GRAM;   // A = relu(ak1*a + ak3); no second tensor
   constexpr bool ABN = PASS_T == WGRAD_BNA || GRAM;
   constexpr bool BNF = PASS_T == DGRAD_BNF;
-  constexpr bool DBNA = PASS_T == DGRAD_BNA;   // dY = k1*dz + k2*y + k3 formed while staging A
   constexpr bool DMA = STAGES >= 3;
   // STAGES == 4 (HALO): tap reuse for 3x3 stride-1 FWD / DGRAD -- see the HALO main loop
   constexpr bool HALO = STAGES == 4;
@@ -249,7 +236,6 @@ __global__ __launch_bounds__(conv_nt<STAGES>(), (PASS_T == WGRAD_BNA || PASS_T =
   static_assert(!ABN || DT == DT_BF16 || DT == DT_F16, "WGRAD_BNA: 16-bit operands");
   static_assert(!BNF || ((DT == DT_BF16 || DT == DT_F16) && !DMA), "DGRAD_BNF: 16-bit, register-staged");
   static_assert(!TAILP || ((DT == DT_BF16 || DT == DT_F16) && STAGES == 1), "FWD_TAIL: 16-bit, single-stage");
-  static_assert(!DBNA || ((DT == DT_BF16 || DT == DT_F16) && STAGES == 1), "DGRAD_BNA: 16-bit, single-stage");
   // DGRAD / WGRAD read the parameters in place in the kernarg segment (constant address space):
   // binding a reference to the by-value argument makes the compiler copy the whole ~1 KB block to
   // scratch once a member array is indexed dynamically (DGRAD tap tables), and costs WGRAD spills.
@@ -471,9 +457,8 @@ __global__ __launch_bounds__(conv_nt<STAGES>(), (PASS_T == WGRAD_BNA || PASS_T =
   // WGRAD_BNA: y beside dz (same geometry), its chunks and the chunks' validity (padding rows must
   // stay 0, not k3)
   const __amdgpu_buffer_rsrc_t rsa2 = __builtin_amdgcn_make_buffer_rsrc(
-      const_cast<void*>(ABN || DBNA ? p.a2 : p.a), (short)0, (int)a_bytes, 0x00020000);
-  i32x4 ray[ABN || DBNA ? AR : 1];
-  f32x2 dk1[DBNA ? 4 : 1], dk2[DBNA ? 4 : 1], dk3[DBNA ? 4 : 1];   // DGRAD_BNA: the k-tile's chunk
+      const_cast<void*>(ABN ? p.a2 : p.a), (short)0, (int)a_bytes, 0x00020000);
+  i32x4 ray[ABN ? AR : 1];
   bool av[ABN ? AR : 1];
   // DGRAD_BNF: the Gram operand (the dX-resolution tensor, xa_c channels)
   const __amdgpu_buffer_rsrc_t rsx = __builtin_amdgcn_make_buffer_rsrc(
@@ -486,8 +471,7 @@ __global__ __launch_bounds__(conv_nt<STAGES>(), (PASS_T == WGRAD_BNA || PASS_T =
   i32x4 rres[TAILP ? AR : 1];
   int st_c = 0, st_c_w = 0;     // channel base of the loaded / of the staged k-tile
   uint32_t tail_bits = 0;       // ReLU bits of the staged chunks (byte i: chunk i)
-  // the first N-tile's blocks write a (FWD_TAIL) / the formed dY (DGRAD_BNA): each A chunk once
-  const bool tail_wr = (TAILP || DBNA) && tn == 0 && p.pro_out != nullptr;
+  const bool tail_wr = TAILP && tn == 0;   // the first N-tile's blocks write a (each A chunk once)
 
   i32x4 ra[AR], rb[BR];
   i32x4 ra2[SPLIT ? AR : 1], rb2[SPLIT ? BR : 1];   // DT_F32S: elements 4..7 of each chunk
@@ -642,19 +626,6 @@ __global__ __launch_bounds__(conv_nt<STAGES>(), (PASS_T == WGRAD_BNA || PASS_T =
         for (int i = 0; i < AR; ++i) {
           const bool ok = ((uint32_t)a_mask[i] >> ti) & 1u;
           lda(i, ok ? (uint32_t)(a_base[i] + toff) : OOB);
-          if constexpr (DBNA) {   // y beside dz; padding / ragged rows must stay 0, not k3
-            ray[i] = bld(rsa2, ok ? (uint32_t)(a_base[i] + toff) : OOB);
-            pv[i] = ok;
-          }
-        }
-        if constexpr (DBNA) {   // the chunk's 8 channels (1x1: the k-tile's channel base + 8 x lane)
-          st_c = k0 - ti * p.Cout;
-#pragma unroll
-          for (int k = 0; k < 4; ++k) {
-            dk1[k] = *reinterpret_cast<const f32x2*>(p.ak1 + c + 2 * k);
-            dk2[k] = *reinterpret_cast<const f32x2*>(p.ak2 + c + 2 * k);
-            dk3[k] = *reinterpret_cast<const f32x2*>(p.ak3 + c + 2 * k);
-          }
         }
         if constexpr (BNF) xt = false;
       }
@@ -729,15 +700,6 @@ __global__ __launch_bounds__(conv_nt<STAGES>(), (PASS_T == WGRAD_BNA || PASS_T =
         if constexpr (BNF) {
           if (xt && xpro && pv[i]) pro_apply(ra[i]);
         }
-        if constexpr (DBNA) {
-          if (i == 0) st_c_w = st_c;
-          if (pv[i]) {
-#pragma unroll
-            for (int k = 0; k < 4; ++k)
-              ra[i][k] = (int)pack2<DT>(bnb_affine2(dk1[k], dk2[k], dk3[k], unpack2<DT>((uint32_t)ra[i][k]),
-                                                    unpack2<DT>((uint32_t)ray[i][k])));
-          }
-        }
         const int addr = row_addr((tid >> 3) + 32 * i, tid & 7);
         if constexpr (SPLIT) split_put(sa, addr, ra[i], ra2[i]);
         else *reinterpret_cast<i32x4*>(sa + addr) = ra[i];
@@ -804,7 +766,7 @@ __global__ __launch_bounds__(conv_nt<STAGES>(), (PASS_T == WGRAD_BNA || PASS_T =
   // global store issued before those loads would hold their vmcnt wait behind its completion (VMEM
   // counts loads and stores in order), which made the in-staging store 4x slower per launch
   auto tail_store = [&]() __attribute__((always_inline)) {
-    if constexpr (TAILP || DBNA) {
+    if constexpr (TAILP) {
       if (!tail_wr) return;
 #pragma unroll
       for (int i = 0; i < AR; ++i) {
@@ -812,9 +774,7 @@ __global__ __launch_bounds__(conv_nt<STAGES>(), (PASS_T == WGRAD_BNA || PASS_T =
         const i32x4 v = *reinterpret_cast<const i32x4*>(smem + row_addr((tid >> 3) + 32 * i, tid & 7));
         const uint32_t e = (uint32_t)(a_base[i] / ES) + (uint32_t)(st_c_w + (tid & 7) * EPC);
         *reinterpret_cast<i32x4*>(reinterpret_cast<u16*>(p.pro_out) + e) = v;
-        if constexpr (TAILP) {
-          if (p.pro_mask) p.pro_mask[e >> 3] = (uint8_t)(tail_bits >> (8 * i));
-        }
+        if (p.pro_mask) p.pro_mask[e >> 3] = (uint8_t)(tail_bits >> (8 * i));
       }
     }
   };
@@ -1858,8 +1818,7 @@ struct ConvDesc {  // mirrors pytorch_distributed_amd/ops/ext.py ConvDesc
 
 template <int PASS, int DT, int BM, int BN, int ST>
 static int launch(const ConvParams& p, dim3 grid, hipStream_t st) {
-  if constexpr ((PASS == WGRAD_BNA || PASS == DGRAD_BNF || PASS == WGRAD_GRAM || PASS == FWD_TAIL ||
-                 PASS == DGRAD_BNA) &&
+  if constexpr ((PASS == WGRAD_BNA || PASS == DGRAD_BNF || PASS == WGRAD_GRAM || PASS == FWD_TAIL) &&
                 DT != DT_BF16 && DT != DT_F16) {
     return -1;
   } else {
@@ -2103,35 +2062,6 @@ int pda_conv_dgrad_bnf(const ConvDesc* d, const void* dz, const void* wf, void* 
   BNF_CASE(DT_F16, 64, 128, 2)
 #endif
 #undef BNF_CASE
-  return -1;
-}
-
-// DGRAD of a 1x1 stride-1 conv whose dY = k1*dz + k2*y + k3 (k = [k1;k2;k3], 3 x Cout f32, the
-// BatchNorm backward of the conv's output) is formed while staging (DGRAD_BNA); dy_out (nullable)
-// receives the formed dY (for the weight gradient). Register-staged single-stage tiles (-128, 128)
-// and (-128, 64); -1 otherwise.
-int pda_conv_dgrad_bna(const ConvDesc* d, const void* dz, const void* y, const float* k1,
-                       const float* k2, const float* k3, const void* w, void* dx, const BnEpi* epi,
-                       void* dy_out, int dt, int bm, int bn, hipStream_t st) {
-  if (dt != DT_BF16 && dt != DT_F16) return -1;
-  if (d->R != 1 || d->S != 1 || d->stride != 1 || d->pad != 0 || (d->Cout % 64) || !y || !k1 ||
-      !k2 || !k3)
-    return -2;
-  if (!fits32((long long)d->Nb * d->Ho * d->Wo * d->Cout, (long long)d->Cout * d->Cin,
-              (long long)d->Nb * d->H * d->W * d->Cin, dt))
-    return -4;
-  ConvParams p{};
-  const int rc = dgrad_params(p, d, dz, w, dx, epi);
-  if (rc) return rc;
-  p.a2 = y; p.ak1 = k1; p.ak2 = k2; p.ak3 = k3; p.pro_out = dy_out;
-  const int abm = tile_bm(bm);
-  const dim3 grid(((p.M + abm - 1) / abm) * ((p.N + bn - 1) / bn), 1);
-#define DBNA_CASE(D, N_) \
-  if (dt == D && bm == -128 && bn == N_) return launch<DGRAD_BNA, D, 128, N_, 1>(p, grid, st);
-#ifndef CONV_DMA_ONLY
-  DBNA_CASE(DT_BF16, 128) DBNA_CASE(DT_BF16, 64) DBNA_CASE(DT_F16, 128) DBNA_CASE(DT_F16, 64)
-#endif
-#undef DBNA_CASE
   return -1;
 }
 

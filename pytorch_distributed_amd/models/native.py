@@ -1074,8 +1074,6 @@ class NativeResNet(nn.Module):
         dx_main = None
         prev_tail = None
         cur = torch.cuda.current_stream(self.device)
-        sync = getattr(ws, "sync_comm", None)
-        bna = None   # (dz, y, k) of the BN whose apply folds into the next (1x1) dgrad (DGRAD_BNA)
         for j in range(n - 1, -1, -1):
             u = b.units[j]
             a_in = acts[j]
@@ -1086,9 +1084,6 @@ class NativeResNet(nn.Module):
                 a_in = ys[j - 1]
                 pro = (sp_[2], sp_[3])
             bnf = None
-            wg_late = None   # a weight gradient that reads the dY this unit's dgrad writes
-            dy_cur = dy
-            bna_next = None
             if fold and j == n - 1:
                 # tail fold: (dz, k) stand for dy3 in both of conv3's gradients
                 k3 = kt[:3 * u.cout]
@@ -1109,19 +1104,13 @@ class NativeResNet(nn.Module):
                                              bna=(y3, k3), wscale=self.wgrad_scale),
                                 dz, a_in, ys[-1], kt)
             else:
-                def wg(w, u=u, g=g, dy=dy, a=a_in, pro=pro):
-                    K.conv_wgrad(dy, a, g, self.wgrad_view(u), w, accumulate=acc, pro=pro,
-                                 wscale=self.wgrad_scale)
-                if bna is None:
-                    self._wgrad(wg, dy, a_in)
-                else:   # dY is written by this unit's own dgrad (below): fork after it
-                    wg_late = wg
+                self._wgrad(lambda w, u=u, g=g, dy=dy, a=a_in, pro=pro:
+                            K.conv_wgrad(dy, a, g, self.wgrad_view(u), w, accumulate=acc, pro=pro,
+                                         wscale=self.wgrad_scale), dy, a_in)
 
-            def dgrad(out, epi=None, u=u, g=g, dy=dy, bnf=bnf, a_in=a_in, pro=pro, bna=bna):
+            def dgrad(out, epi=None, u=u, g=g, dy=dy, bnf=bnf, a_in=a_in, pro=pro):
                 if bnf is not None:
                     K.conv_dgrad_bnf(dz, bnf[0], g, out, a_in, bnf[1], xa_pro=pro, epi=epi)
-                elif bna is not None:   # dY = k1*dz + k2*y + k3 formed in staging, written to dy
-                    K.conv_dgrad(bna[0], self.w16_ohwi(u), g, out, epi=epi, bna=(bna[1], bna[2], dy))
                 else:
                     K.conv_dgrad(dy, self.w16_ohwi(u), g, out, epi=epi)
             out = self._empty(*a_in.shape)
@@ -1133,25 +1122,14 @@ class NativeResNet(nn.Module):
                 epi, part_p, nq_p = K.bn_epilogue(ws, Gp, ys[j - 1], sp[2], sp[3])
                 dgrad(out, epi)                                      # out = dz of bn_{j-1}
                 dyp = self._empty(*ys[j - 1].shape)
-                if ((sync is None or sync.world_size == 1) and not self.f32
-                        and K.dgrad_bna_ok(up.geom(Nb), Nb, ys[-1].dtype)):
-                    # bn_{j-1}'s apply folds into unit j-1's (1x1) dgrad: coefficients only here
-                    kb = torch.empty(3 * up.cout, dtype=torch.float32, device=self.device)
-                    K.bn_bwd_finish(ws, part_p, Gp, nq_p, ys[j - 1], sp[0], sp[1], self.gamma(up),
-                                    self.dgamma(up), self.dbeta(up), out, None, accumulate=acc,
-                                    k_out=kb)
-                    bna_next = (out, ys[j - 1], kb)
-                else:
-                    K.bn_bwd_finish(ws, part_p, Gp, nq_p, ys[j - 1], sp[0], sp[1], self.gamma(up),
-                                    self.dgamma(up), self.dbeta(up), out, dyp, accumulate=acc)
-                    bna_next = None
+                K.bn_bwd_finish(ws, part_p, Gp, nq_p, ys[j - 1], sp[0], sp[1], self.gamma(up),
+                                self.dgamma(up), self.dbeta(up), out, dyp, accumulate=acc)
                 dy = dyp
             elif prev is not None:
                 pb, prec = prev
                 if sc_ev is not None:
                     cur.wait_event(sc_ev)
-                Gp = K.dgrad_slabs(g, Nb, tile=K.dgrad_bna_tile(g, Nb) if bna is not None else None,
-                                   dtype=ys[-1].dtype)
+                Gp = K.dgrad_slabs(g, Nb, dtype=ys[-1].dtype)
                 epi, part_p, nq_p = K.bn_epilogue(ws, Gp, g2=shortcut_g,
                                                   **self._tail_args(pb, prec, use_mask=True))
                 dgrad(out, epi)                                      # out = dz of prev tail
@@ -1159,9 +1137,6 @@ class NativeResNet(nn.Module):
             else:
                 dgrad(out)
                 dx_main = out
-            if wg_late is not None:
-                self._wgrad(wg_late, dy_cur, a_in)
-            bna = bna_next if j > 0 else None
         if sc_ev is not None:   # the caller (next tail / stem backward) reads shortcut_g on main
             cur.wait_event(sc_ev)
         return dx_main, shortcut_g, prev_tail

@@ -83,8 +83,6 @@ _SIGS = {
     "pda_conv_fwd_tail": [C.POINTER(ConvDesc), _V, _V, _I, _V, _V, _V, _V, _V, _V, _V, _V, _V, _I, _I,
                           _I, _I, _V],
     "pda_conv_dgrad": [C.POINTER(ConvDesc), _V, _V, _V, C.POINTER(BnEpi), _I, _I, _I, _V],
-    "pda_conv_dgrad_bna": [C.POINTER(ConvDesc), _V, _V, _V, _V, _V, _V, _V, C.POINTER(BnEpi), _V,
-                           _I, _I, _I, _V],
     "pda_conv_dgrad_bnf": [C.POINTER(ConvDesc), _V, _V, _V, C.POINTER(BnEpi), _V, _V, _V, _V, _I, _I,
                            _I, _V],
     "pda_bn_fold": [_V, _V, _I, _I, _V, _V, _I, _V],

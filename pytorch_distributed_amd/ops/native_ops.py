@@ -466,55 +466,21 @@ def dgrad_slabs(g: ConvGeom, Nb: int, tile: Optional[Tuple[int, int]] = None,
 
 
 def conv_dgrad(dy: torch.Tensor, w: torch.Tensor, g: ConvGeom, dx: torch.Tensor,
-               tile: Optional[Tuple[int, int]] = None, epi: Optional[ext.BnEpi] = None,
-               bna: Optional[Tuple[torch.Tensor, torch.Tensor, Optional[torch.Tensor]]] = None
-               ) -> torch.Tensor:
+               tile: Optional[Tuple[int, int]] = None, epi: Optional[ext.BnEpi] = None) -> torch.Tensor:
     """dx[Nb,H,W,Cin] = conv_transpose(dy[Nb,Ho,Wo,Cout], w[Cout,R,S,Cin]).
 
     With ``epi`` (see :func:`bn_epilogue`) the kernel instead stores dz = dA * relu_mask (dA = the
-    transposed conv result [+ epi.g2]) and writes the BatchNorm-backward partial sums.
-    ``bna = (y, k, dy_out)`` (1x1 stride-1 convs, :func:`dgrad_bna_ok`): ``dy`` is the masked gradient
-    dz of the BatchNorm after this conv and the kernel forms dY = k1*dz + k2*y + k3 (k = [k1; k2; k3],
-    3 x Cout f32, from :func:`bn_bwd_finish` ``k_out``) while staging -- that BN's apply pass folded
-    into its consumer; ``dy_out`` (optional) receives the formed dY for the weight gradient."""
+    transposed conv result [+ epi.g2]) and writes the BatchNorm-backward partial sums."""
     Nb = dy.shape[0]
     kdt = _kdt(dy)
-    d = g.desc(Nb)
-    if bna is not None:
-        y, k, dy_out = bna
-        C_ = g.Cout
-        bm, bn = tile or dgrad_bna_tile(g, Nb)
-        rc = ext.lib().pda_conv_dgrad_bna(C.byref(d), ptr(dy), ptr(y), ptr(k[0:C_]), ptr(k[C_:2 * C_]),
-                                          ptr(k[2 * C_:3 * C_]), ptr(w), ptr(dx),
-                                          C.byref(epi) if epi is not None else None, ptr(dy_out),
-                                          kdt, bm, bn, stream(dy.device))
-        check(rc, "conv_dgrad_bna")
-        return dx
     bm, bn = tile or dgrad_tile(g, Nb, dma=kdt in (1, 2))
+    d = g.desc(Nb)
     kbm, kbn = _ktile(bm, bn, kdt)
     rc = ext.lib().pda_conv_dgrad(C.byref(d), ptr(dy), ptr(w), ptr(dx),
                                   C.byref(epi) if epi is not None else None, kdt, kbm, kbn,
                                   stream(dy.device))
     check(rc, "conv_dgrad")
     return dx
-
-
-def dgrad_bna_tile(g: ConvGeom, Nb: int) -> Tuple[int, int]:
-    """Tile of the DGRAD_BNA launch: the register-staged single-stage 128-row tiles it is built for."""
-    return -128, (64 if g.Cin <= 64 else 128)
-
-
-def dgrad_bna_ok(g: ConvGeom, Nb: int, dtype: torch.dtype) -> bool:
-    """Whether :func:`conv_dgrad` can fold the BatchNorm-backward apply of its dY into its operand
-    staging (``bna``): a 1x1 stride-1 conv without padding, 16-bit, dY channels in 64-column
-    k-tiles, enough 128-row tiles to fill the GPU (``PDA_DGRAD_BNA=0`` keeps the apply pass)."""
-    return (_DGRAD_BNA and g.R == 1 and g.S == 1 and g.stride == 1 and g.pad == 0
-            and dtype in (torch.bfloat16, torch.float16) and g.Cout % 64 == 0
-            and math.ceil(Nb * g.H * g.W / 128) * math.ceil(g.Cin / 128) >= 2 * _NUM_CU
-            and getattr(ext.lib(), "pda_conv_dgrad_bna", None) is not None)
-
-
-_DGRAD_BNA = os.environ.get("PDA_DGRAD_BNA", "1") != "0"
 
 
 def bn_fold(w: torch.Tensor, k: torch.Tensor, wf: torch.Tensor, bias: torch.Tensor,

@@ -1152,47 +1152,3 @@ def test_wgrad_reduce_batch_matches_single_reduces():
     for a, b, c in zip(single, batch, again):
         assert rel_err(b, a) < 1e-6, rel_err(b, a)
         assert torch.equal(b, c)
-
-
-@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
-@pytest.mark.parametrize("geo", [(9, 56, 256, 64), (11, 28, 512, 128), (7, 14, 1024, 256), (4, 56, 64, 64)])
-def test_conv_dgrad_bna_matches_apply_then_dgrad(geo, dtype):
-    """DGRAD_BNA (a 1x1 conv's data gradient forming dY = k1*dz + k2*y + k3 while staging, and
-    writing that dY for the weight gradient) is bit-identical to the apply pass followed by the plain
-    data gradient: same fma chain (common.h bnb_affine), same GEMM; with the fused BN-backward
-    epilogue of the previous BatchNorm too. The written dY matches the float reference."""
-    K = _k()
-    torch.manual_seed(3)
-    Nb, H, Cin, Cout = geo
-    g = K.ConvGeom(Nb, H, H, Cin, Cout, 1, 1, 1, 0)
-    dz = (torch.randn(Nb, H, H, Cout, device=DEV) * 0.5).to(dtype)
-    y = torch.randn(Nb, H, H, Cout, device=DEV).to(dtype)
-    k = torch.cat([torch.rand(Cout, device=DEV) + 0.5, torch.randn(Cout, device=DEV) * 0.1,
-                   torch.randn(Cout, device=DEV) * 0.05])
-    w = (torch.randn(Cout, 1, 1, Cin, device=DEV) / 16).to(dtype)
-    dy_out = torch.full_like(dz, float("nan"))
-    dx_b = torch.empty(Nb, H, H, Cin, device=DEV, dtype=dtype)
-    assert K.dgrad_bna_ok(g, Nb, dtype) or Nb * H * H < 128 * 512
-    K.conv_dgrad(dz, w, g, dx_b, bna=(y, k, dy_out), tile=K.dgrad_bna_tile(g, Nb))
-    dx_p = torch.empty_like(dx_b)
-    K.conv_dgrad(dy_out, w, g, dx_p, tile=K.dgrad_bna_tile(g, Nb))
-    torch.cuda.synchronize()
-    ref = (k[:Cout] * dz.float() + k[Cout:2 * Cout] * y.float() + k[2 * Cout:]).to(dtype)
-    torch.testing.assert_close(dy_out.float(), ref.float(), rtol=1e-2, atol=1e-2)
-    assert torch.equal(dx_b, dx_p)
-    # with the previous BatchNorm's fused backward epilogue (mode 0: relu(bn(y_prev)))
-    yp = torch.randn(Nb, H, H, Cin, device=DEV).to(dtype)
-    sc, sh = torch.rand(Cin, device=DEV) + 0.5, torch.randn(Cin, device=DEV) * 0.1
-    ws = K.Workspace(DEV)
-    Gp = K.dgrad_slabs(g, Nb, tile=K.dgrad_bna_tile(g, Nb), dtype=dtype)
-    outs = []
-    for bna in (True, False):
-        epi, part, nq = K.bn_epilogue(ws, Gp, yp, sc, sh)
-        o = torch.empty_like(dx_b)
-        if bna:
-            K.conv_dgrad(dz, w, g, o, epi=epi, bna=(y, k, None), tile=K.dgrad_bna_tile(g, Nb))
-        else:
-            K.conv_dgrad(dy_out, w, g, o, epi=epi, tile=K.dgrad_bna_tile(g, Nb))
-        torch.cuda.synchronize()
-        outs.append((o, part[:Gp * nq * Cin].clone()))
-    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])

@@ -527,29 +527,3 @@ def test_fork_tracking_orders_side_stream_reads():
         assert moved == tracking, (tracking, moved)
         want = float(2 ** steps)
         assert bool((seen == want).all()), (tracking, seen.min().item(), seen.max().item())
-
-
-def test_dgrad_bna_fold_is_bit_exact(monkeypatch):
-    """The bottleneck bn1 backward apply folded into conv1's data gradient (DGRAD_BNA: conv1's dgrad
-    forms dY from dz and y1 while staging and writes it for conv1's weight gradient) changes no value:
-    logits, loss and every gradient bit-identical to the apply-pass schedule over two steps."""
-    from pytorch_distributed_amd.ops import native_ops as K
-    res = {}
-    for on in (True, False):
-        monkeypatch.setattr(K, "_DGRAD_BNA", on)
-        _, nm = _pair("resnet50", image=64)
-        torch.manual_seed(21)
-        x = torch.randn(32, 3, 64, 64, device=DEV)
-        y = torch.randint(0, 1000, (32,), device=DEV)
-        nm.train()
-        crit = nm.make_criterion()
-        outs = []
-        for _ in range(2):
-            nm.zero_grad_flat()
-            out = nm(x)
-            crit(out, y).backward()
-            torch.cuda.synchronize()
-            outs.append((out.detach().clone(), nm.flat_grad.detach().clone()))
-        res[on] = outs
-    for (l1, g1), (l2, g2) in zip(res[True], res[False]):
-        assert torch.equal(l1, l2) and torch.equal(g1, g2)
