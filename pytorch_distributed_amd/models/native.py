@@ -143,8 +143,6 @@ class NativeResNet(nn.Module):
         # stem_bna = False keeps the apply-pass form for tests) and runs on the main stream, beside
         # layer1's weight gradients on the second stream (profiles/ab_r4.md section 8)
         self.stem_bna = True
-        # the fused stem backward reads y0 at the pooling argmax (stem_pool writes it) instead of y0
-        self.stem_yam = os.environ.get("PDA_STEM_YAM", "1") != "0"
         self.tail_mask = True         # tails store the ReLU bitmask the backward reads
         # a block's tail BN apply (+ residual + ReLU) runs inside the next block's conv1 forward,
         # which stages a = relu(bn3(y3) + r) from y3 and r and writes a once (FWD_TAIL); blocks whose
@@ -614,8 +612,7 @@ class NativeResNet(nn.Module):
         arg = torch.empty(Nb, ph, ph, self.stem.cout, dtype=torch.uint8, device=self.device)
         # y0 at every window's argmax: the fused stem backward reads it instead of y0 (a quarter of
         # the bytes; its ReLU mask and BN partials live at the argmax pixels only)
-        yam = (self._empty(Nb, ph, ph, self.stem.cout)
-               if save and self.fused_stem_bwd and self.stem_yam else None)
+        yam = self._empty(Nb, ph, ph, self.stem.cout) if save and self.fused_stem_bwd else None
         sc, sh = self._coeffs(self.stem, train)
         K.stem_pool(y0, sc, sh, p, arg, yam=yam)
         if self.probe is not None:
