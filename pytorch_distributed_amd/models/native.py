@@ -206,9 +206,6 @@ class NativeResNet(nn.Module):
         # diagnostics (tools/layer_times.py): called on the main stream as probe(phase, name) after
         # the stem and after each residual block, forward and backward
         self.probe: Optional[Callable[[str, str], None]] = None
-        # the NativeSGD whose update of every parameter but the stem's may start inside the backward
-        # (NativeSGD.early, armed by training loops that always step after backward)
-        self.early_opt: Optional["NativeSGD"] = None
         self.refresh_shadow()
 
     def set_wgrad_batch(self, mode: str) -> None:
@@ -900,17 +897,6 @@ class NativeResNet(nn.Module):
                 self.segment_hook(self.block_bounds[nblk - bi])
             if self.probe is not None:
                 self.probe("bwd", b.name)
-        # every gradient but the stem's is final here: an armed optimizer updates that range on the
-        # second stream (after its queued weight gradients) while the main stream runs the stem's
-        # serial backward chain, which is all that is left
-        early = self.early_opt
-        if (early is not None and early.early and red is None and self._side is not None
-                and not self.defer_side and not torch.cuda.is_current_stream_capturing()):
-            self._flush_wgrad()
-            self._flush_reduces()
-            self._fork()
-            with torch.cuda.stream(self._side):
-                early._launch_early(self.block_bounds[-2])
         # ---- stem: maxpool backward of (main + shortcut) gradients, BN backward, wgrad
         x0, y0, arg = sv["x0"], sv["y0"], sv["arg"]
         st0 = sv["stem_stats"]
@@ -1264,14 +1250,6 @@ class NativeSGD(torch.optim.Optimizer):
         self.model = model
         self.flat_mom = torch.zeros_like(model.flat_params)
         self._initialized = False
-        # early: the backward launches the update of [0, stem) itself, on its second stream once those
-        # gradients are final (fc .. layer1; the stem's are produced last, by a serial chain on the
-        # main stream), and step() then updates only the stem. Only for loops that ALWAYS step after
-        # backward (NativeTrainer, the trainer's step), with per-rank gradients (no DDP reducer) and
-        # no loss scaling (AMP's overflow check spans every gradient): off by default.
-        self.early = False
-        self._early_hi = 0
-        model.early_opt = self
         # per-parameter momentum views (torch format in state_dict)
         self._views = {}
         fp = model.flat_params
@@ -1296,24 +1274,15 @@ class NativeSGD(torch.optim.Optimizer):
                    None if m.f32 else m.flat_shadow[lo:hi], g["lr"], g["momentum"],
                    g["weight_decay"], self._initialized, inv_scale=inv_scale, found_inf=found_inf)
 
-    def _launch_early(self, hi: int) -> None:
-        """Called by the backward (its second stream) once every gradient below ``hi`` is final."""
-        self._launch_range(0, hi)
-        self._early_hi = hi
-
     def _launch(self, inv_scale=None, found_inf=None) -> None:
         g = self.param_groups[0]
         m = self.model
-        lo, self._early_hi = self._early_hi, 0
         if m._grads_zero:
             # zero_grad() and no backward since: torch 2.x's set_to_none leaves every .grad None,
             # and SGD skips parameters without a gradient -- the flat gradient still holds the
             # previous step's values (no memset), so applying it would be a stale update
             return
-        if lo and inv_scale is not None:
-            raise RuntimeError("NativeSGD.early with loss scaling: the overflow check must precede "
-                               "every update")
-        self._launch_range(lo, m.numel, inv_scale, found_inf)
+        self._launch_range(0, m.numel, inv_scale, found_inf)
         m._pack_stem()
         # (an overflow-skipped first step leaves the momentum buffer unset on the device but the
         # flag set: the next step then reads the zero-initialised buffer, m*0 + d == d)
@@ -1376,9 +1345,6 @@ class NativeTrainer:
             from ..parallel.ddp import DistributedDataParallel
             self.net = DistributedDataParallel(self.model, bucket_cap_mb=bucket_mb)
         self.opt = self.model.make_optimizer(lr=0.1, momentum=0.9, weight_decay=1e-4)
-        # step() always follows the backward: the update of all but the stem starts inside it
-        # (PDA_EARLY_SGD=0: one update after the backward)
-        self.opt.early = dtype != torch.float16 and os.environ.get("PDA_EARLY_SGD", "1") != "0"
         self.crit = self.model.make_criterion()
         self.ds = SyntheticImageNet("train", seed=0, image_size=image_size)
         self.gen = self.model.input_generator(self.ds)

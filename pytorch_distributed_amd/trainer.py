@@ -344,10 +344,6 @@ def run(cfg: RunConfig, mode: str, local_rank: int = 0, nprocs: Optional[int] = 
     if mode == "ddp_amp":
         from .amp import LossScaler
         ctx.scaler = LossScaler(enabled=(dtype == torch.float16))
-    if hasattr(optimizer, "early") and not (ctx.scaler is not None and ctx.scaler.enabled):
-        # this loop always steps after backward: the native SGD may update every parameter but
-        # the stem's inside the backward (models/native.py NativeSGD.early; DDP keeps it off)
-        optimizer.early = True
 
     best_acc, start_epoch, start_step = 0.0, 0, 0
     ckpt = load_latest(save_path)

@@ -527,28 +527,3 @@ def test_fork_tracking_orders_side_stream_reads():
         assert moved == tracking, (tracking, moved)
         want = float(2 ** steps)
         assert bool((seen == want).all()), (tracking, seen.min().item(), seen.max().item())
-
-
-def test_early_sgd_is_bit_exact():
-    """NativeSGD.early (the update of every parameter but the stem's launched inside the backward on
-    the second stream, beside the stem's backward) changes no value: after three full trainer steps
-    the weights, momentum buffers and BN buffers are bit-identical to the single post-backward
-    update, and the early update really ran (its range was recorded for the step)."""
-    from pytorch_distributed_amd.models.native import NativeTrainer
-    res = {}
-    for early in (True, False):
-        tr = NativeTrainer("resnet50", 16, torch.bfloat16, DEV, image_size=64)
-        tr.opt.early = early
-        seen = []
-        orig = tr.opt._launch_early
-        tr.opt._launch_early = lambda hi, f=orig: (seen.append(hi), f(hi))
-        for i in range(3):
-            tr.step(i)
-        torch.cuda.synchronize()
-        m = tr.model
-        assert bool(seen) == early and (not early or seen[0] == m.block_bounds[-2])
-        res[early] = [t.clone() for t in (m.flat_params, tr.opt.flat_mom, m.flat_bufstore,
-                                          m.flat_shadow)]
-        del tr
-    for a, b in zip(res[True], res[False]):
-        assert torch.equal(a, b)
