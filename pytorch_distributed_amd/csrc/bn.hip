@@ -417,17 +417,13 @@ __global__ __launch_bounds__(NT) void bn_apply_kernel(
 }
 
 // ------------------------------------------------------------------ stem: bn + relu + maxpool 3x3/2/1
-// y: [N,H,W,C], out: [N,Ho,Wo,C], arg: [N,Ho,Wo,C] uint8 window index (0..8); yam (nullable):
-// [N,Ho,Wo,C] the pre-BN y at each window's argmax -- everything the stem backward needs of y (its
-// ReLU mask and BN partials live at the argmax pixels only), so that pass reads this quarter-size
-// tensor instead of y itself
+// y: [N,H,W,C], out: [N,Ho,Wo,C], arg: [N,Ho,Wo,C] uint8 window index (0..8)
 template <int DT>
 __global__ __launch_bounds__(NT) void stem_pool_kernel(const void* __restrict__ y,
                                                        const float* __restrict__ sc,
                                                        const float* __restrict__ sh,
                                                        void* __restrict__ out,
-                                                       uint8_t* __restrict__ arg,
-                                                       void* __restrict__ yam, int N, int H,
+                                                       uint8_t* __restrict__ arg, int N, int H,
                                                        int W, int C, int Ho, int Wo, FastDiv dCK,
                                                        FastDiv dWo, FastDiv dHo) {
   const int CK = C / 8;
@@ -436,12 +432,12 @@ __global__ __launch_bounds__(NT) void stem_pool_kernel(const void* __restrict__ 
     const uint32_t pix = fdiv(i, dCK), ck = i - pix * CK;
     const uint32_t p2 = fdiv(pix, dWo), xo = pix - p2 * Wo;
     const uint32_t n = fdiv(p2, dHo), yo = p2 - n * Ho;
-    float a[8], b[8], best[8], bv[8];
+    float a[8], b[8], best[8];
     int bi[8];
     ld8f(sc + ck * 8, a);
     ld8f(sh + ck * 8, b);
 #pragma unroll
-    for (int e = 0; e < 8; ++e) { best[e] = -1.f; bi[e] = 0; bv[e] = 0.f; }
+    for (int e = 0; e < 8; ++e) { best[e] = -1.f; bi[e] = 0; }
     for (int dy = 0; dy < 3; ++dy) {
       const int yy = yo * 2 - 1 + dy;
       if ((unsigned)yy >= (unsigned)H) continue;
@@ -453,12 +449,11 @@ __global__ __launch_bounds__(NT) void stem_pool_kernel(const void* __restrict__ 
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
           const float r = fmaxf(v[e] * a[e] + b[e], 0.f);
-          if (r > best[e]) { best[e] = r; bi[e] = dy * 3 + dx; bv[e] = v[e]; }
+          if (r > best[e]) { best[e] = r; bi[e] = dy * 3 + dx; }
         }
       }
     }
     store8<DT>(out, (size_t)i * 8, best);
-    if (yam) store8<DT>(yam, (size_t)i * 8, bv);   // (bv: a DT value, stored exactly)
     uint64_t packed = 0;
 #pragma unroll
     for (int e = 0; e < 8; ++e) packed |= (uint64_t)bi[e] << (8 * e);
@@ -671,10 +666,7 @@ __global__ __launch_bounds__(NT) void bn_bwd_reduce_kernel(BwdArgs a) {
 }
 
 // Stem backward, one pass: maxpool gradient gather (as maxpool_bwd_kernel) -> ReLU mask of
-// relu(bn(y0)) -> dz stored -> per-block partials q0 = sum dz, q1 = sum dz*y0. With ``yam`` (the
-// forward's y0 at each window's argmax, stem_pool_kernel) a pixel's y0 is taken from a window that
-// selected it -- the only pixels dz can be non-zero at -- so y0 itself (4x the bytes) is not read;
-// same values, same order: bit-identical dz and partials. Replaces
+// relu(bn(y0)) -> dz stored -> per-block partials q0 = sum dz, q1 = sum dz*y0. Replaces
 // maxpool_bwd (write dA0) + bn_bwd_reduce (re-read dA0): one full read of the largest activation
 // of the network (400x112x112x64) less, and one launch less.
 // Work item = one 2x2 quad of input pixels (2yo..2yo+1, 2xo..2xo+1) x 8 channels: the pooling
@@ -684,9 +676,8 @@ __global__ __launch_bounds__(NT) void bn_bwd_reduce_kernel(BwdArgs a) {
 template <int DT>
 __global__ __launch_bounds__(NT) void stem_bwd_reduce_kernel(
     const void* __restrict__ dout, const void* __restrict__ dout2, const uint8_t* __restrict__ arg,
-    const void* __restrict__ y, const void* __restrict__ yam, const float* __restrict__ sc,
-    const float* __restrict__ sh, void* __restrict__ dz_out, float* __restrict__ part,
-    long long quads, long long quads_per_block,
+    const void* __restrict__ y, const float* __restrict__ sc, const float* __restrict__ sh,
+    void* __restrict__ dz_out, float* __restrict__ part, long long quads, long long quads_per_block,
     int H, int W, int C, int Ho, int Wo, FastDiv dWo, FastDiv dHo) {
   __shared__ float red[2][NT][8];
   const int CK = C / 8;
@@ -712,7 +703,7 @@ __global__ __launch_bounds__(NT) void stem_bwd_reduce_kernel(
         const bool y1 = (int)yo + 1 < Ho, x1 = (int)xo + 1 < Wo;
         // gather the 4 windows (w bit 1: yo+1, bit 0: xo+1); a window past the edge re-reads a
         // valid one and gets argmax bytes 0xff, which match no tap
-        Raw8<DT> dv[4], dv2[4], ym[4];
+        Raw8<DT> dv[4], dv2[4];
         uint64_t am[4];
 #pragma unroll
         for (int w = 0; w < 4; ++w) {
@@ -722,7 +713,6 @@ __global__ __launch_bounds__(NT) void stem_bwd_reduce_kernel(
           am[w] = live ? a8 : ~0ull;
           dv[w] = ldraw8<DT>(dout, (size_t)o * C + c0);
           if (dout2) dv2[w] = ldraw8<DT>(dout2, (size_t)o * C + c0);
-          if (yam) ym[w] = ldraw8<DT>(yam, (size_t)o * C + c0);
         }
         // the quad's 4 pixels (pixel bit 1: row 2yo+1, bit 0: col 2xo+1); a pixel past an odd
         // edge loads the quad's first pixel and is neither stored nor counted
@@ -734,12 +724,7 @@ __global__ __launch_bounds__(NT) void stem_bwd_reduce_kernel(
           const int yy = 2 * (int)yo + (px >> 1), x = 2 * (int)xo + (px & 1);
           pin[px] = yy < H && x < W;
           prow[px] = ((size_t)n * H + (pin[px] ? yy : 2 * (int)yo)) * W + (pin[px] ? x : 2 * (int)xo);
-          if (!yam) yr[px] = ldraw8<DT>(y, prow[px] * C + c0);
-        }
-        float ymf[4][8];
-        if (yam) {
-#pragma unroll
-          for (int w = 0; w < 4; ++w) cvt8<DT>(ym[w], ymf[w]);
+          yr[px] = ldraw8<DT>(y, prow[px] * C + c0);
         }
         float d[4][8];
 #pragma unroll
@@ -755,9 +740,9 @@ __global__ __launch_bounds__(NT) void stem_bwd_reduce_kernel(
 #pragma unroll
         for (int px = 0; px < 4; ++px) {
           const int py = px >> 1, pxx = px & 1;
-          float g[8], yv[8];
+          float g[8];
 #pragma unroll
-          for (int e = 0; e < 8; ++e) { g[e] = 0.f; yv[e] = 0.f; }
+          for (int e = 0; e < 8; ++e) g[e] = 0.f;
 #pragma unroll
           for (int w = 0; w < 4; ++w) {
             const int wy = w >> 1, wx = w & 1;
@@ -767,12 +752,10 @@ __global__ __launch_bounds__(NT) void stem_bwd_reduce_kernel(
             const int me = (py + 1 - 2 * wy) * 3 + (pxx + 1 - 2 * wx);
 #pragma unroll
             for (int e = 0; e < 8; ++e)
-              if ((int)((am[w] >> (8 * e)) & 0xff) == me) {
-                g[e] += d[w][e];
-                if (yam) yv[e] = ymf[w][e];   // every window that selected the pixel holds its y0
-              }
+              if ((int)((am[w] >> (8 * e)) & 0xff) == me) g[e] += d[w][e];
           }
-          if (!yam) cvt8<DT>(yr[px], yv);
+          float yv[8];
+          cvt8<DT>(yr[px], yv);
 #pragma unroll
           for (int e = 0; e < 8; ++e) g[e] = yv[e] * s[e] + h[e] > 0.f ? g[e] : 0.f;
           if (!pin[px]) continue;
@@ -1278,11 +1261,11 @@ int pda_bn_apply(const void* y, const float* sc, const float* sh, const void* r2
   return (int)hipGetLastError();
 }
 
-int pda_stem_pool(const void* y, const float* sc, const float* sh, void* out, void* arg, void* yam,
-                  int N, int H, int W, int C, int Ho, int Wo, int dt, hipStream_t st) {
+int pda_stem_pool(const void* y, const float* sc, const float* sh, void* out, void* arg, int N,
+                  int H, int W, int C, int Ho, int Wo, int dt, hipStream_t st) {
   if ((long long)N * H * W * (C / 8) >= (1ll << 31)) return -2;
   const int g = grid_for((long long)N * Ho * Wo * (C / 8));
-#define ARGS (const void*)y, sc, sh, (void*)out, (uint8_t*)arg, yam, N, H, W, C, Ho, Wo, make_div(C / 8), \
+#define ARGS (const void*)y, sc, sh, (void*)out, (uint8_t*)arg, N, H, W, C, Ho, Wo, make_div(C / 8), \
              make_div(Wo), make_div(Ho)
   if (dt == DT_BF16) TRACKED_LAUNCH(stem_pool_kernel<DT_BF16>, dim3(g), dim3(NT), 0, st, ARGS);
   else if (dt == DT_F32) TRACKED_LAUNCH(stem_pool_kernel<DT_F32>, dim3(g), dim3(NT), 0, st, ARGS);
@@ -1345,8 +1328,7 @@ int pda_bn_bwd_reduce(const BwdArgsC* c, int G, int dt, hipStream_t st) {
 
 // stem backward reduce (maxpool gather + ReLU mask + dz store + partials [G][2][C])
 int pda_stem_bwd_reduce(const void* dout, const void* dout2, const void* arg, const void* y,
-                        const void* yam, const float* sc, const float* sh, void* dz_out, float* part,
-                        int G, int N,
+                        const float* sc, const float* sh, void* dz_out, float* part, int G, int N,
                         int H, int W, int C, int Ho, int Wo, int dt, hipStream_t st) {
   const long long rows = (long long)N * H * W;
   // the quad decomposition assumes the 3x3/2 pad-1 pooling geometry
@@ -1354,7 +1336,7 @@ int pda_stem_bwd_reduce(const void* dout, const void* dout2, const void* arg, co
   const long long quads = (long long)N * Ho * Wo;
   const long long qpb = (quads + G - 1) / G;
 #define K(D) TRACKED_LAUNCH(stem_bwd_reduce_kernel<D>, dim3(G), dim3(NT), 0, st, (const void*)dout, \
-                                (const void*)dout2, (const uint8_t*)arg, (const void*)y, yam, sc, sh,  \
+                                (const void*)dout2, (const uint8_t*)arg, (const void*)y, sc, sh,       \
                                 (void*)dz_out, part, quads, qpb, H, W, C, Ho, Wo, make_div(Wo),        \
                                 make_div(Ho))
   if (dt == DT_BF16) K(DT_BF16); else if (dt == DT_F32) K(DT_F32); else K(DT_F16);

@@ -607,15 +607,12 @@ class NativeResNet(nn.Module):
         ph = self.pool_hw
         p = self._empty(Nb, ph, ph, self.stem.cout)
         arg = torch.empty(Nb, ph, ph, self.stem.cout, dtype=torch.uint8, device=self.device)
-        # y0 at every window's argmax: the fused stem backward reads it instead of y0 (a quarter of
-        # the bytes; its ReLU mask and BN partials live at the argmax pixels only)
-        yam = self._empty(Nb, ph, ph, self.stem.cout) if save and self.fused_stem_bwd else None
         sc, sh = self._coeffs(self.stem, train)
-        K.stem_pool(y0, sc, sh, p, arg, yam=yam)
+        K.stem_pool(y0, sc, sh, p, arg)
         if self.probe is not None:
             self.probe("fwd", "stem")
         if save:
-            saved["y0"], saved["arg"], saved["yam"] = y0, arg, yam
+            saved["y0"], saved["arg"] = y0, arg
             saved["stem_stats"] = self.stem.state
             saved["blocks"] = []
         h = p
@@ -911,7 +908,7 @@ class NativeResNet(nn.Module):
         if self.fused_stem_bwd:   # maxpool gather + ReLU mask + BN partials in one pass
             dz0 = self._empty(*y0.shape)
             part, G, nq = K.stem_bwd_reduce(ws, dx_main, arg, y0, st0[2], st0[3], dz0,
-                                            dout2=shortcut_g, yam=sv.get("yam"))
+                                            dout2=shortcut_g)
             if bna:
                 k0 = self._stem_k
                 K.bn_bwd_finish(ws, part, G, nq, y0, st0[0], st0[1], self.gamma(u), self.dgamma(u),

@@ -101,11 +101,11 @@ _SIGS = {
     "pda_slab_reduce": [_V, _I, _I, _I, _V, _V],
     "pda_bn_eval_coeffs": [_V, _V, _V, _V, _F, _I, _V, _V, _V],
     "pda_bn_apply": [_V, _V, _V, _V, _V, _V, _V, _L, _I, _I, _I, _V, _I, _V],
-    "pda_stem_pool": [_V, _V, _V, _V, _V, _V, _I, _I, _I, _I, _I, _I, _I, _V],
+    "pda_stem_pool": [_V, _V, _V, _V, _V, _I, _I, _I, _I, _I, _I, _I, _V],
     "pda_maxpool_bwd": [_V, _V, _V, _V, _I, _I, _I, _I, _I, _I, _I, _V],
     "pda_tail_pool": [_V, _V, _V, _V, _V, _V, _V, _I, _I, _I, _I, _I, _V],
     "pda_bn_bwd_reduce": [C.POINTER(BwdArgs), _I, _I, _V],
-    "pda_stem_bwd_reduce": [_V, _V, _V, _V, _V, _V, _V, _V, _V, _I, _I, _I, _I, _I, _I, _I, _I, _V],
+    "pda_stem_bwd_reduce": [_V, _V, _V, _V, _V, _V, _V, _V, _I, _I, _I, _I, _I, _I, _I, _I, _V],
     "pda_bn_bwd_finalize": [_V, _I, _I, _I, _I, _F, _V, _V, _V, _V, _V, _V, _V, _V, _F, _I, _V],
     "pda_bn_bwd_apply": [C.POINTER(BwdArgs), _V, _V, _V, _V, _V, _V, _I, _V],
     "pda_xent": [_V, _I, _I, _I, _V, _V, _V, _V, _I, _F, _V, _I, _I, _V],

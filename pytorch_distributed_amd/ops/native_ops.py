@@ -859,13 +859,11 @@ def bn_apply(y, scale, shift, out, res=None, y2=None, scale2=None, shift2=None, 
     return out
 
 
-def stem_pool(y, scale, shift, out, arg, yam=None):
-    """Stem BN + ReLU + 3x3/2 max-pool; ``arg`` receives each window's argmax and ``yam`` (optional,
-    pooled shape) the pre-BN ``y`` at it -- what :func:`stem_bwd_reduce` reads instead of ``y``."""
+def stem_pool(y, scale, shift, out, arg):
     N, H, W, C_ = y.shape
     Ho, Wo = out.shape[1], out.shape[2]
-    rc = ext.lib().pda_stem_pool(ptr(y), ptr(scale), ptr(shift), ptr(out), ptr(arg), ptr(yam), N, H,
-                                 W, C_, Ho, Wo, dt_of(y), stream(y.device))
+    rc = ext.lib().pda_stem_pool(ptr(y), ptr(scale), ptr(shift), ptr(out), ptr(arg), N, H, W, C_, Ho,
+                                 Wo, dt_of(y), stream(y.device))
     check(rc, "stem_pool")
     return out
 
@@ -889,17 +887,15 @@ def tail_pool(y, scale, shift, out, res=None, y2=None, scale2=None, shift2=None)
     return out
 
 
-def stem_bwd_reduce(ws: "Workspace", dout, arg, y, scale, shift, dz_out, dout2=None, yam=None):
+def stem_bwd_reduce(ws: "Workspace", dout, arg, y, scale, shift, dz_out, dout2=None):
     """Stem backward, one pass: max-pool gradient gather (``dout`` [+ ``dout2``] through the argmax
-    bytes) -> ReLU mask of relu(bn(y)) -> ``dz_out`` -> BatchNorm-backward partial sums. ``yam``
-    (:func:`stem_pool`): y at the windows' argmax pixels, read instead of ``y`` (bit-identical).
+    bytes) -> ReLU mask of relu(bn(y)) -> ``dz_out`` -> BatchNorm-backward partial sums.
     Returns (part, G, nq) for :func:`bn_bwd_finish`."""
     N, H, W, C_ = y.shape
     Ho, Wo = dout.shape[1], dout.shape[2]
     G = max(1, min(_STEM_G, (N * H * W) // 512))   # gather-latency bound: more blocks than a reduce
     part = ws.get("bn_part", G * 2 * C_)
-    rc = ext.lib().pda_stem_bwd_reduce(ptr(dout), ptr(dout2), ptr(arg), ptr(y), ptr(yam), ptr(scale),
-                                       ptr(shift),
+    rc = ext.lib().pda_stem_bwd_reduce(ptr(dout), ptr(dout2), ptr(arg), ptr(y), ptr(scale), ptr(shift),
                                        ptr(dz_out), ptr(part), G, N, H, W, C_, Ho, Wo, dt_of(y),
                                        stream(y.device))
     check(rc, "stem_bwd_reduce")

@@ -495,18 +495,6 @@ def test_stem_bwd_reduce_matches_unfused(with_shortcut, H):
     ref.backward(gsum.permute(0, 3, 1, 2))
     assert rel_err(db, br.grad) < 2e-2
     assert rel_err(dg, gr.grad) < 2e-2
-    # the y-at-argmax form (stem_pool yam, read instead of y): bit-identical dz and partials
-    out2 = torch.empty_like(out)
-    arg2 = torch.empty_like(arg)
-    yam = torch.full_like(out, float("nan"))
-    K.stem_pool(y, sc, sh, out2, arg2, yam=yam)
-    dz2 = torch.empty_like(y)
-    part_c = part[:G * nq * C].clone()
-    part2, G2, nq2 = K.stem_bwd_reduce(ws, g, arg2, y, sc, sh, dz2, dout2=g2, yam=yam)
-    torch.cuda.synchronize()
-    assert torch.equal(out2, out) and torch.equal(arg2, arg)
-    assert (G2, nq2) == (G, nq)
-    assert torch.equal(dz2, dz) and torch.equal(part2[:G * nq * C], part_c)
 
 
 def test_tail_pool():
