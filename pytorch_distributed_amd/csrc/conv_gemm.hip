@@ -1875,8 +1875,6 @@ static int dispatch(int dt, int bm, int bn, const ConvParams& p, dim3 grid, hipS
     // 256x64 forward (the N = 64 stem: K = 256 is 4 k-tiles, so a block's life is mostly its load
     // -> MFMA -> epilogue latency chain; twice the rows per chain)
     if constexpr (PASS == FWD) { TILE_CASE1(DT_BF16, 256, 64) TILE_CASE1(DT_F16, 256, 64) }
-    // 64x256 forward (expansion 1x1 convs, N = 4K: one A tile staged per 256 output channels)
-    if constexpr (PASS == FWD) { TILE_CASE1(DT_BF16, 64, 256) }
     TILE_CASE1(DT_F16, 128, 128) TILE_CASE1(DT_F16, 128, 64) TILE_CASE1(DT_F16, 64, 128)
     TILE_CASE1(DT_F32, 128, 128) TILE_CASE1(DT_F32, 128, 64) TILE_CASE1(DT_F32, 64, 128)
     // the split-f32 path stages hi + lo tiles: single-stage only (LDS)
