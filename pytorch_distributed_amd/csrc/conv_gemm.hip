@@ -1499,23 +1499,36 @@ __global__ __launch_bounds__(conv_nt<STAGES>(), (PASS_T == WGRAD_BNA || PASS_T =
       if (do_stats) {
         __syncthreads();
         float* red = reinterpret_cast<float*>(smem);  // [NQ][RG][BN] (+ FWD: shift row)
+        // column pair k of chunk cc sits at slot (k + cc/4 + 2*(row&1)) & 3 of the chunk's 8 floats:
+        // the 16 lanes of one ds_write_b64 group (16 chunks of a row, or 8 chunks of two rows when
+        // BN = 64) then cover all 32 banks -- the plain layout put 4 lanes on every bank pair
+        auto spos = [&](int cc_, int k_, int g_) __attribute__((always_inline)) {
+          if constexpr (EPO == 8) return cc_ * 8 + 2 * ((k_ + (cc_ >> 2) + 2 * (g_ & 1)) & 3);
+          else return cc_ * EPO + 2 * k_;
+        };
 #pragma unroll
         for (int k = 0; k < EPO / 2; ++k) {
-          *reinterpret_cast<f32x2*>(red + rg * BN + cc * EPO + 2 * k) = q0[k];
-          *reinterpret_cast<f32x2*>(red + RG * BN + rg * BN + cc * EPO + 2 * k) = q1[k];
-          if constexpr (NQ > 2) *reinterpret_cast<f32x2*>(red + 2 * RG * BN + rg * BN + cc * EPO + 2 * k) = q2[k];
+          const int sp = spos(cc, k, rg);
+          *reinterpret_cast<f32x2*>(red + rg * BN + sp) = q0[k];
+          *reinterpret_cast<f32x2*>(red + RG * BN + rg * BN + sp) = q1[k];
+          if constexpr (NQ > 2) *reinterpret_cast<f32x2*>(red + 2 * RG * BN + rg * BN + sp) = q2[k];
           if constexpr (SHIFTED) {
-            if (rg == 0) *reinterpret_cast<f32x2*>(red + 2 * RG * BN + cc * EPO + 2 * k) = shv[k];
+            if (rg == 0) *reinterpret_cast<f32x2*>(red + 2 * RG * BN + spos(cc, k, 0)) = shv[k];
           }
         }
         __syncthreads();
         if (tid < BN) {
           float a = 0.f, b = 0.f, c2 = 0.f;
+          // this thread's column in the even / odd rows of the swizzled layout
+          const int e_ = tid % EPO;
+          const int pe = spos(tid / EPO, e_ >> 1, 0) + (e_ & 1);
+          const int po = spos(tid / EPO, e_ >> 1, 1) + (e_ & 1);
 #pragma unroll 8
           for (int g = 0; g < RG; ++g) {
-            a += red[g * BN + tid];
-            b += red[RG * BN + g * BN + tid];
-            if constexpr (NQ > 2) c2 += red[2 * RG * BN + g * BN + tid];
+            const int pc = (g & 1) ? po : pe;
+            a += red[g * BN + pc];
+            b += red[RG * BN + g * BN + pc];
+            if constexpr (NQ > 2) c2 += red[2 * RG * BN + g * BN + pc];
           }
           const int col = n0 + tid;
           if (col < p.N) {
@@ -1523,7 +1536,7 @@ __global__ __launch_bounds__(conv_nt<STAGES>(), (PASS_T == WGRAD_BNA || PASS_T =
               float* dst = p.stats + (size_t)tm * 3 * p.N + col;
               dst[0] = a;
               dst[p.N] = b;
-              dst[2 * p.N] = red[2 * RG * BN + tid];
+              dst[2 * p.N] = red[2 * RG * BN + pe];
             } else {
               float* dst = p.epart;
               const size_t slab = (size_t)split * tiles_m + tm;
