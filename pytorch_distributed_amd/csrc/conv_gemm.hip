@@ -31,9 +31,7 @@ constexpr int NT = 256;
 // STAGES == 3 selects the LDS-DMA main loop: 512 threads (8 waves, one block per CU), operands
 // copied global -> LDS by buffer_load ... lds (16 B per lane, no VGPR round trip) into a 3-slot
 // ring, two k-tiles in flight across ONE barrier per k-tile (counted vmcnt, raw s_barrier).
-// STAGES == 5: the same LDS-DMA ring with 4 waves (256 threads) and a 3-slot ring, so two blocks
-// share a CU (the 8-wave block is alone on its CU: its epilogue overlaps nothing)
-template <int STAGES> constexpr int conv_nt() { return STAGES == 3 || STAGES == 4 ? 512 : NT; }
+template <int STAGES> constexpr int conv_nt() { return STAGES >= 3 ? 512 : NT; }
 
 // one LDS-DMA piece: lane l's 16 bytes at byte voff of the buffer land at lds + 16*l (lds must be
 // wave-uniform: it becomes M0). An out-of-range voff (>= the buffer's size) writes zeros.
@@ -231,8 +229,8 @@ __global__ __launch_bounds__(conv_nt<STAGES>(), (PASS_T == WGRAD_BNA || PASS_T =
   // STAGES == 4 (HALO): tap reuse for 3x3 stride-1 FWD / DGRAD -- see the HALO main loop
   constexpr bool HALO = STAGES == 4;
   constexpr int NTH = conv_nt<STAGES>();
-  // wave grid: 2x2 (256 threads); 8-wave DMA: 4x2 or 2x4 so the wave tile stays square-ish
-  constexpr int WM = NTH == 512 ? (BM >= BN ? 4 : 2) : 2;
+  // wave grid: 2x2 (256 threads); DMA: 4x2 or 2x4 so the wave tile stays square-ish
+  constexpr int WM = DMA ? (BM >= BN ? 4 : 2) : 2;
   constexpr int WN = (NTH / 64) / WM;
   static_assert(!DMA || ((DT == DT_BF16 || DT == DT_F16) && !ABN), "LDS-DMA: 16-bit");
   static_assert(!ABN || DT == DT_BF16 || DT == DT_F16, "WGRAD_BNA: 16-bit operands");
@@ -289,8 +287,7 @@ __global__ __launch_bounds__(conv_nt<STAGES>(), (PASS_T == WGRAD_BNA || PASS_T =
 #ifndef CONV_WGRAD_DMA_SLOTS
 #define CONV_WGRAD_DMA_SLOTS 0
 #endif
-  constexpr int NSLOT = STAGES == 5 ? 3
-      : DMA && !HALO
+  constexpr int NSLOT = DMA && !HALO
       ? (PASS == WGRAD && CONV_WGRAD_DMA_SLOTS > 0 ? CONV_WGRAD_DMA_SLOTS
                                                    : (4 * STAGE <= 144 * 1024 ? 4 : 3))
       : STAGES;
@@ -1846,10 +1843,7 @@ static int launch(const ConvParams& p, dim3 grid, hipStream_t st) {
 // Tile codes: bm < 0 selects the single-buffer (STAGES = 1) variant of tile |bm| x bn; bm > 1000
 // the LDS-DMA 8-wave variant (STAGES = 3) of tile (bm - 1000) x bn (16-bit, no operand prologue).
 // bm > 2000: the tap-reuse (HALO) variant of (bm - 2000) x bn for 3x3 stride-1 FWD / DGRAD.
-// bm > 4000: the 4-wave LDS-DMA variant (STAGES = 5) of (bm - 4000) x bn (16-bit, no prologue).
-static int tile_bm(int bm) {
-  return bm > 4000 ? bm - 4000 : bm > 2000 ? bm - 2000 : bm > 1000 ? bm - 1000 : (bm < 0 ? -bm : bm);
-}
+static int tile_bm(int bm) { return bm > 2000 ? bm - 2000 : bm > 1000 ? bm - 1000 : (bm < 0 ? -bm : bm); }
 static bool halo_ok(const ConvParams& p, int csz) {
   return p.R == 3 && p.S == 3 && p.stride == 1 && p.pad == 1 && p.W <= 63 && csz % 64 == 0 &&
          p.Ho == p.H && p.Wo == p.W;
@@ -1857,19 +1851,6 @@ static bool halo_ok(const ConvParams& p, int csz) {
 
 template <int PASS>
 static int dispatch(int dt, int bm, int bn, const ConvParams& p, dim3 grid, hipStream_t st) {
-  if (bm > 4000) {
-    if (p.pro_sc != nullptr) return -5;   // the operand prologue needs register staging
-#define TILE_CASE5(D, M_, N_)                                                   \
-  if (dt == D && bm - 4000 == M_ && bn == N_) return launch<PASS, D, M_, N_, 5>(p, grid, st);
-    if constexpr (PASS != WGRAD) {
-      TILE_CASE5(DT_BF16, 128, 64) TILE_CASE5(DT_BF16, 64, 128) TILE_CASE5(DT_BF16, 128, 128)
-#ifndef CONV_DMA_ONLY
-      TILE_CASE5(DT_F16, 128, 64) TILE_CASE5(DT_F16, 64, 128) TILE_CASE5(DT_F16, 128, 128)
-#endif
-    }
-#undef TILE_CASE5
-    return -1;
-  }
   if (bm > 2000) {
     if constexpr (PASS != WGRAD) {
       if (p.pro_sc != nullptr || !halo_ok(p, PASS == FWD ? p.Cin : p.Cout)) return -5;

@@ -167,8 +167,7 @@ def tile_rows(bm: int) -> int:
     """M rows of a tile code: -bm = single-stage register-staged, bm > 1000 = the LDS-DMA 8-wave
     variant of (bm - 1000) rows, bm > 2000 = its tap-reuse form for 3x3 stride-1 fwd / dgrad
     (csrc/conv_gemm.hip dispatch)."""
-    return (bm - 4000 if bm > 4000 else bm - 2000 if bm > 2000 else bm - 1000 if bm > 1000
-            else abs(bm))
+    return bm - 2000 if bm > 2000 else bm - 1000 if bm > 1000 else abs(bm)
 
 
 def _ktile(bm: int, bn: int, kdt: int, pro: bool = False) -> Tuple[int, int]:

@@ -25,8 +25,7 @@ COUNT = {"C1": 1, "C2": 3, "C3": 4, "C4": 2, "C5": 1, "C6": 1, "C7": 4, "C8": 1,
          "C11": 1, "C12": 1, "C13": 6, "C14": 1, "C15": 5, "C16": 5, "C17": 1, "C18": 1, "C19": 3,
          "C20": 1, "C21": 2, "C22": 2}
 TILES = [(128, 128), (128, 64), (64, 128), (64, 64), (-128, 128), (-128, 64), (-64, 128), (-256, 128),
-         (1256, 128), (1128, 256), (1128, 128), (2256, 128), (2256, 64), (4128, 64), (4064, 128),
-         (4128, 128)]
+         (1256, 128), (1128, 256), (1128, 128), (2256, 128), (2256, 64)]
 # -bm: 1-stage; the -256 tile is compiled for wgrad only (other passes report n/a);
 # 1000 + bm: the LDS-DMA 8-wave tiles; 2000 + bm: their tap-reuse form (3x3 stride-1 fwd / dgrad)
 
