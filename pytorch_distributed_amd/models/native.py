@@ -194,6 +194,9 @@ class NativeResNet(nn.Module):
         # _ReplicaGraph side_split): the backward leaves the batched weight-gradient kernels queued
         # (no flush, no end-of-backward join) for the capture driver to record on the second stream
         self.defer_side = False
+        # with defer_side: called right after each weight gradient is queued (its inputs are the
+        # main-stream work issued so far), so a capture driver can end the main segment there
+        self.wgrad_hook: Optional[Callable[[], None]] = None
         # fork tracking (csrc/common.h TRACKED_LAUNCH): while the native forward / backward runs
         # eagerly, every kernel launch on the main stream completes one event through its own
         # dispatch, and a fork to the second stream waits on that event instead of recording a
@@ -790,6 +793,8 @@ class NativeResNet(nn.Module):
         if self._wbatch is not None:
             self._wbatch.append(fn)
             self._keep.extend(keep)
+            if self.defer_side and self.wgrad_hook is not None:
+                self.wgrad_hook()   # (DataParallel capture: a side graph per weight gradient)
             return
         self._fork()
         with torch.cuda.stream(self._side):

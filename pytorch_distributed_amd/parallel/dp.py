@@ -516,8 +516,13 @@ class _ReplicaGraph:
         self.dev = m.device
         self.gscale = 1.0 / global_batch
         self.splits = list(splits)
-        self.side_split = (getattr(m, "_side", None) is not None
-                           and os.environ.get("PDA_DP_SIDE", "1") != "0")
+        side = os.environ.get("PDA_DP_SIDE", "conv")
+        if side not in ("conv", "1", "0"):
+            raise ValueError(f"PDA_DP_SIDE={side!r}: expected conv, 1 or 0")
+        self.side_split = getattr(m, "_side", None) is not None and side != "0"
+        # "conv": a side graph per weight gradient (the main segment ends where its inputs are
+        # complete, so it starts as early as in the eager schedule); "1": one per residual block
+        self.side_per_conv = self.side_split and side == "conv"
         with torch.cuda.device(self.dev):
             self.x = torch.empty(shape, dtype=m.dtype, device=self.dev)
             self.y = torch.empty(shape[0], dtype=torch.int64, device=self.dev)
@@ -555,6 +560,19 @@ class _ReplicaGraph:
         self.sides.append(self._capture_side() if self.side_split else None)
         self.seg_reduce.append(upto)
 
+    def _split_conv(self) -> None:
+        """NativeResNet.wgrad_hook (side_per_conv): end the main segment after the work a weight
+        gradient just queued depends on and record that weight gradient as a side graph."""
+        if not self._capturing:
+            return
+        # (second-stream work forked inside the segment -- the shortcut branch's data gradient --
+        # joins it: a capture cannot end with an unjoined fork)
+        torch.cuda.current_stream(self.dev).wait_stream(self.m._side)
+        self._end_segment(None)
+        g = torch.cuda.CUDAGraph()
+        g.capture_begin(pool=self._pool_h)
+        self.graphs.append(g)
+
     def _split(self, upto: int) -> None:
         """NativeResNet.segment_hook, after each residual block's backward."""
         if self.side_split and self._capturing:
@@ -586,11 +604,13 @@ class _ReplicaGraph:
         m._grads_zero = True          # every step overwrites the flat gradient
         m.segment_hook = self._split if (self.splits or self.side_split) else None
         m.defer_side = self.side_split and self._capturing
+        m.wgrad_hook = self._split_conv if self.side_per_conv else None
         try:
             m.native_backward(dlog16)
         finally:
             m.segment_hook = None
             m.defer_side = False
+            m.wgrad_hook = None
         self.loss = loss
 
     def join_side(self, stream: torch.cuda.Stream) -> None:

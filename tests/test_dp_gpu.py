@@ -43,7 +43,7 @@ def test_native_dataparallel_matches_single_model():
     assert torch.equal(dp.module.flat_params, dp.replicas[0].flat_params)
 
 
-@pytest.mark.parametrize("side", ["1", "0"])
+@pytest.mark.parametrize("side", ["conv", "1", "0"])
 @pytest.mark.parametrize("segments", ["stage", "0"])
 def test_native_dataparallel_graph_step_matches_eager(segments, side, monkeypatch):
     """train_step replayed from per-replica HIP graphs == the same schedule launched eagerly (bit
@@ -51,8 +51,9 @@ def test_native_dataparallel_graph_step_matches_eager(segments, side, monkeypatc
     ATen's cross-entropy: equal up to the 16-bit rounding of dlogits). ``stage``: the completed
     gradient slice after layer4 / layer3 / layer2 is reduced on a comm stream while the next
     segments replay (4 reductions). ``side`` (PDA_DP_SIDE): the weight gradients are recorded as
-    graphs of their own, one per residual block, replayed on the second stream beside the next
-    block's main chain (one main segment per block + the stem's)."""
+    graphs of their own -- one per weight gradient ("conv", the main chain split where each one's
+    inputs are complete) or one per residual block ("1") -- replayed on the second stream beside
+    the following main-chain segment."""
     monkeypatch.setenv("PDA_DP_SEGMENTS", segments)
     monkeypatch.setenv("PDA_DP_SIDE", side)
     from pytorch_distributed_amd.data import SyntheticImageNet
@@ -96,9 +97,14 @@ def test_native_dataparallel_graph_step_matches_eager(segments, side, monkeypatc
     assert graphed._graphs[0].graph is not None and eager._graphs[0].graph is None
     rg = graphed._graphs[0]
     nblk = len(graphed.module.blocks)
-    assert len(rg.graphs) == (nblk + 1 if side == "1" else (4 if segments == "stage" else 1))
+    nside = sum(g is not None for g in rg.sides)
+    if side == "conv":   # one side graph per weight gradient (every conv + the fc), after its segment
+        nconv = sum(len(b.units) + (b.ds is not None) for b in graphed.module.blocks) + 2
+        assert nside == nconv and len(rg.graphs) >= nconv + nblk, (nside, nconv, len(rg.graphs))
+    else:
+        assert len(rg.graphs) == (nblk + 1 if side == "1" else (4 if segments == "stage" else 1))
+        assert (nside > nblk // 2) == (side == "1")
     assert len(rg.sides) == len(rg.graphs)
-    assert (sum(g is not None for g in rg.sides) > nblk // 2) == (side == "1")
     assert [u for u in rg.seg_reduce if u is not None] == rg.splits + [graphed.module.numel]
     assert len(rg.splits) == (3 if segments == "stage" else 0)
     ex = graphed.exposed_comm_ms()
