@@ -219,7 +219,7 @@ class NativeResNet(nn.Module):
         self._wbatch = [] if self._side is not None and mode != "0" else None
 
     @contextlib.contextmanager
-    def graph_schedule(self):
+    def graph_schedule(self, concurrent_side: bool = False):
         """Schedule for HIP-graph capture, for the duration of the block only: fork the wgrad
         stream once per stage (unless PDA_WGRAD_BATCH says otherwise): replayed 29.16-29.23 ms vs
         29.50-29.63 per block and 29.85-30.00 per conv (profiles/ab_r2_inlaunch_bn.md section 10).
@@ -238,7 +238,10 @@ class NativeResNet(nn.Module):
         # 29.03 -> 28.85 ms/step, profiles/ab_r3_dma.md section 18). Per model: another model
         # running eagerly meanwhile keeps its own plans.
         prev_scale = self.wgrad_scale
-        if "PDA_WGRAD_SCALE" not in os.environ:
+        # (concurrent_side: the capture records the weight gradients as graphs of their own that
+        # replay on the second stream beside the main chain, as the eager step runs them: they keep
+        # the eager step's targets -- DataParallel replay 27.03-27.09 vs 27.12-27.24 ms at x1.0)
+        if "PDA_WGRAD_SCALE" not in os.environ and not concurrent_side:
             self.wgrad_scale = 1.0
         try:
             yield

@@ -657,7 +657,7 @@ class _ReplicaGraph:
             cur = torch.cuda.current_stream(self.dev)
             side = torch.cuda.Stream(self.dev)
             side.wait_stream(cur)
-            with self.m.graph_schedule():
+            with self.m.graph_schedule(concurrent_side=self.side_split):
                 with torch.cuda.stream(side):
                     self._body()               # the real step for this batch (also sizes workspaces)
                 cur.wait_stream(side)
