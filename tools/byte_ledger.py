@@ -42,6 +42,11 @@ class Ledger:
         self.tensors[name] = T(h, c, es)
         return name
 
+    def wg(self, phase, kernel, reads, slab_mb):
+        """A split-K weight gradient (side stream): its f32 slab written, then read by the reduce."""
+        self.k(phase, "side", kernel, reads, (), extra_w=slab_mb)
+        self.k(phase, "side", kernel.split(" ")[0] + " wgrad_reduce", (), (), extra_r=slab_mb)
+
     def k(self, phase, stream, kernel, reads=(), writes=(), extra_r=0.0, extra_w=0.0):
         r = {n: self.tensors[n] for n in reads}
         w = {n: self.tensors[n] for n in writes}
@@ -151,8 +156,7 @@ def build():
                 L.k("bwd", "main", f"{n}.tail finish + apply2", [dz, f"{n}.y3", f"{n}.yd"],
                     [f"{n}.dy3", f"{n}.dyd"])
             L.k("bwd", "side", f"{n}.ds dgrad", [f"{n}.dyd"], [f"{n}.scg"])
-            L.k("bwd", "side", f"{n}.ds wgrad", [f"{n}.dyd", b["xin"]], [],
-                extra_w=wslab(b["cin"], out, 1, ho) * 2)
+            L.wg("bwd", f"{n}.ds wgrad", [f"{n}.dyd", b["xin"]], wslab(b["cin"], out, 1, ho))
         elif not fold:
             L.t(f"{n}.dy3", ho, out)
             L.k("bwd", "main", f"{n}.tail finish + apply", [dz, f"{n}.y3"], [f"{n}.dy3"])
@@ -161,24 +165,20 @@ def build():
         L.t(f"{n}.dy2", ho, mid)
         if fold:
             L.k("bwd", "main", f"{n}.conv3 DGRAD_BNF", [dz, f"{n}.y2"], [f"{n}.dz2"])
-            L.k("bwd", "side", f"{n}.conv3 wgrad (dz^T a2)", [dz, f"{n}.y2"], [],
-                extra_w=wslab(mid, out, 1, ho) * 2)
+            L.wg("bwd", f"{n}.conv3 wgrad (dz^T a2)", [dz, f"{n}.y2"], wslab(mid, out, 1, ho))
         else:
             L.k("bwd", "main", f"{n}.conv3 dgrad", [f"{n}.dy3", f"{n}.y2"], [f"{n}.dz2"])
-            L.k("bwd", "side", f"{n}.conv3 wgrad", [f"{n}.dy3", f"{n}.y2"], [],
-                extra_w=wslab(mid, out, 1, ho) * 2)
+            L.wg("bwd", f"{n}.conv3 wgrad", [f"{n}.dy3", f"{n}.y2"], wslab(mid, out, 1, ho))
         L.k("bwd", "main", f"{n}.bn2 finish + apply", [f"{n}.dz2", f"{n}.y2"], [f"{n}.dy2"])
         # conv2 (3x3): dgrad -> dz1 (epilogue on y1), wgrad (tap-reuse at 56/28, else generic)
         L.t(f"{n}.dz1", hi, mid)
         L.t(f"{n}.dy1", hi, mid)
         L.k("bwd", "main", f"{n}.conv2 dgrad", [f"{n}.dy2", f"{n}.y1"], [f"{n}.dz1"])
         a1 = b["a1"] or f"{n}.y1"
-        L.k("bwd", "side", f"{n}.conv2 wgrad", [f"{n}.dy2", a1], [],
-            extra_w=wslab(mid, mid, 9, ho) * 2)
+        L.wg("bwd", f"{n}.conv2 wgrad", [f"{n}.dy2", a1], wslab(mid, mid, 9, ho))
         L.k("bwd", "main", f"{n}.bn1 finish + apply", [f"{n}.dz1", f"{n}.y1"], [f"{n}.dy1"])
         # conv1 (1x1): wgrad; dgrad whose epilogue forms the PREVIOUS tail's dz (+ shortcut grad)
-        L.k("bwd", "side", f"{n}.conv1 wgrad", [f"{n}.dy1", b["xin"]], [],
-            extra_w=wslab(b["cin"], mid, 1, hi) * 2)
+        L.wg("bwd", f"{n}.conv1 wgrad", [f"{n}.dy1", b["xin"]], wslab(b["cin"], mid, 1, hi))
         sc = f"{n}.scg" if b["ds"] else dz
         if i > 0:
             pb = blocks[i - 1]
@@ -196,7 +196,8 @@ def build():
     # stem: fused maxpool gather + relu mask + partials (writes dz0), finish (k only), wgrad BNA
     L.t("dz0", 112, 64)
     L.k("bwd", "main", "stem_bwd_reduce", ["dp", stem_sc, "arg", "y0"], ["dz0"])
-    L.k("bwd", "main", "stem wgrad BNA", ["dz0", "y0", "x0"], [], extra_w=wslab(16, 64, 16, 112) * 2)
+    L.k("bwd", "main", "stem wgrad BNA", ["dz0", "y0", "x0"], [], extra_w=wslab(16, 64, 16, 112))
+    L.k("bwd", "main", "stem wgrad_reduce", (), (), extra_r=wslab(16, 64, 16, 112))
     return L
 
 
@@ -219,8 +220,8 @@ def report(L: Ledger, md: bool):
     out.append("# Analytic byte ledger of the native ResNet-50 bf16 step (bs 400, 224 px)\n")
     out.append("Generated by `tools/byte_ledger.py` from the default schedule of `models/native.py`. "
                "Activation / gradient bytes per kernel launch (MB = 1e6 B); every tensor charged once "
-               "per kernel that touches it; f32 split-K slabs as '(slab/partials)' (written + read by "
-               "the reduce).\n")
+               "per kernel that touches it; f32 split-K slabs as '(slab/partials)' (written by the "
+               "weight gradient, read by its reduce; slab sizes estimated from the split targets).\n")
     out.append("| phase | stream | read GB | write GB |\n|---|---|---|---|")
     for ph in ("fwd", "bwd"):
         for s in ("main", "side"):
