@@ -785,18 +785,20 @@ class NativeResNet(nn.Module):
         else:
             self._side.wait_stream(cur)
 
-    def _wgrad(self, fn: Callable, *keep: torch.Tensor) -> None:
+    def _wgrad(self, fn: Callable, *keep: torch.Tensor, split: bool = True) -> None:
         """Enqueue ``fn(workspace)`` (weight-gradient kernels) on the wgrad stream, ordered after
         everything queued so far on the main stream. Tensors the side stream reads are kept alive
         until the end-of-backward join, so the caching allocator cannot hand their memory to a
-        main-stream allocation while the side stream may still be reading it."""
+        main-stream allocation while the side stream may still be reading it. ``split=False``: the
+        next weight gradient follows with no main-stream launch in between (a DataParallel capture
+        records both in one side graph instead of ending an empty main segment)."""
         if self._side is None:
             fn(self.ws)
             return
         if self._wbatch is not None:
             self._wbatch.append(fn)
             self._keep.extend(keep)
-            if self.defer_side and self.wgrad_hook is not None:
+            if split and self.defer_side and self.wgrad_hook is not None:
                 self.wgrad_hook()   # (DataParallel capture: a side graph per weight gradient)
             return
         self._fork()
@@ -943,14 +945,14 @@ class NativeResNet(nn.Module):
                 # drains layer1's weight gradients: the stem's runs beside them instead of after
                 stem_wgrad(ws)
             else:
-                self._wgrad(stem_wgrad, dz0, y0, x0, k0)
+                self._wgrad(stem_wgrad, dz0, y0, x0, k0, split=False)   # (the last: no main work follows)
         else:
             def stem_wgrad(w):
                 rb, w.reduce_batch = w.reduce_batch, None
                 K.conv_wgrad(dy0, x0, g0, self.stem_wgrad, w, wscale=self.wgrad_scale)
                 w.reduce_batch = rb
                 K.stem_s2d_grad(self.stem_wgrad, self.wgrad_view(u), accumulate=acc)
-            self._wgrad(stem_wgrad, dy0, x0)
+            self._wgrad(stem_wgrad, dy0, x0, split=False)
         if not self.defer_side:
             self._flush_wgrad()
             self._flush_reduces()
@@ -1074,7 +1076,7 @@ class NativeResNet(nn.Module):
             self._wgrad(lambda w, u=b.ds, g=g, dyd=dyd: K.conv_wgrad(dyd, x, g, self.wgrad_view(u),
                                                                     w, accumulate=acc,
                                                                     wscale=self.wgrad_scale),
-                        dyd, x)
+                        dyd, x, split=fold)   # (fold: bn_fold launches before conv3's wgrad)
         else:
             K.bn_bwd_finish(ws, part, G, nq, ys[-1], sl[0], sl[1], self.gamma(ul), self.dgamma(ul),
                             self.dbeta(ul), dz, dy, accumulate=acc, k_out=kt)

@@ -576,6 +576,8 @@ class _ReplicaGraph:
     def _split(self, upto: int) -> None:
         """NativeResNet.segment_hook, after each residual block's backward."""
         if self.side_split and self._capturing:
+            if self.side_per_conv and upto not in self.splits:
+                return   # every weight gradient already ended a segment: no block boundary needed
             self._end_segment(upto if upto in self.splits else None)
             g = torch.cuda.CUDAGraph()
             g.capture_begin(pool=self._pool_h)

@@ -1,5 +1,7 @@
 """Native DataParallel semantics on one GPU: two replicas sharing cuda:0 (plain-copy sync path)
 must produce the same update as one model on the concatenated batch."""
+import warnings
+
 import pytest
 import torch
 
@@ -82,7 +84,11 @@ def test_native_dataparallel_graph_step_matches_eager(segments, side, monkeypatc
         x, y = gen(torch.arange(16) + 16 * step)
         graphed.timing = step == 3
         le = eager.train_step(x, y, oe, graph=False)
-        lg = graphed.train_step(x, y, og)
+        with warnings.catch_warnings(record=True) as caught:
+            warnings.simplefilter("always")
+            lg = graphed.train_step(x, y, og)
+        # (conv mode: a block boundary right after a weight gradient's split records nothing)
+        assert not [w for w in caught if "Graph is empty" in str(w.message)], step
         torch.cuda.synchronize()
         if step == 0:
             assert abs(la.item() - lg.item()) < 1e-4 * abs(la.item())
@@ -99,8 +105,13 @@ def test_native_dataparallel_graph_step_matches_eager(segments, side, monkeypatc
     nblk = len(graphed.module.blocks)
     nside = sum(g is not None for g in rg.sides)
     if side == "conv":   # one side graph per weight gradient (every conv + the fc), after its segment
-        nconv = sum(len(b.units) + (b.ds is not None) for b in graphed.module.blocks) + 2
-        assert nside == nconv and len(rg.graphs) >= nconv + nblk, (nside, nconv, len(rg.graphs))
+        # (the shortcut's weight gradient shares conv_n's side graph unless a tail fold's
+        # bn_fold launch separates them)
+        m = graphed.module
+        nconv = sum(len(b.units) + (b.ds is not None and bool(m._tail_fold_ok(b, 8)))
+                    for b in m.blocks) + 2
+        assert nside == nconv and nconv <= len(rg.graphs) <= nconv + len(rg.splits) + 1, \
+            (nside, nconv, len(rg.graphs))
     else:
         assert len(rg.graphs) == (nblk + 1 if side == "1" else (4 if segments == "stage" else 1))
         assert (nside > nblk // 2) == (side == "1")
