@@ -1301,6 +1301,29 @@ __global__ __launch_bounds__(conv_nt<STAGES>(), (PASS_T == WGRAD_BNA || PASS_T =
     // row; one packed 8-byte store (4 columns) per item per lane (f32: one 16-B store).
     constexpr int CPR = BN / EPO;
     auto c_addr = [&](int row, int chunk) { return row * CPR + (chunk ^ (row & (CPR - 1))); };
+    // 16-bit C tile with BN <= 128: 8-byte pieces (4 columns) XOR-swizzled by cswz(row) instead of
+    // 16-byte chunks. The MFMA layout writes one piece per lane and a ds_write_b64 lane group is 16
+    // rows of ONE piece: 16-B chunks give them only 8 distinct bank quads (2-way conflicts on every
+    // C-tile write -- the bulk of the 21-35 % LDS conflicts of the layer-1/2 launches,
+    // profiles/pmc_r5_step.md); pieces give 16, i.e. all 32 banks. The reader loads its chunk as two
+    // ds_read_b64 (same LDS cycles as one b128): conflict-free when rows 2 apart (BN = 64, 128-B
+    // rows) or 1 apart (BN = 128) differ in the swizzle's parity.
+    constexpr bool PIECE = !O32 && BN <= 128;
+    auto cswz = [&](int row) __attribute__((always_inline)) {
+      if constexpr (BN == 64) return (row & 12) | ((row & 1) << 1) | ((row >> 1) & 1);
+      else return row & 15;
+    };
+    auto ld_c = [&](int row, int chunk) __attribute__((always_inline)) -> i32x4 {
+      if constexpr (PIECE) {
+        const char* rb = smem + row * (BN * ES);
+        const int o = ((2 * chunk) ^ cswz(row)) << 3;
+        const uint2 a = *reinterpret_cast<const uint2*>(rb + o);
+        const uint2 b = *reinterpret_cast<const uint2*>(rb + (o ^ 8));
+        return i32x4{(int)a.x, (int)a.y, (int)b.x, (int)b.y};
+      } else {
+        return *reinterpret_cast<const i32x4*>(smem + c_addr(row, chunk) * 16);
+      }
+    };
     // f32: the waves of wave-row h write their tiles to local rows [0, BM/2) of the LDS image
     auto stage_f32 = [&](int h) __attribute__((always_inline)) {
       if (wr != h) return;
@@ -1319,7 +1342,8 @@ __global__ __launch_bounds__(conv_nt<STAGES>(), (PASS_T == WGRAD_BNA || PASS_T =
         }
         if (relu) v = __builtin_elementwise_max(v, (f32x4){0.f, 0.f, 0.f, 0.f});
         // row & (CPR-1) == lr & (CPR-1) for CPR <= 16 (folded); BN = 256 needs the full row
-        const int cbyte = (((col >> 3) ^ (row & (CPR - 1))) << 4) + ((col & 4) << 1);
+        const int cbyte = PIECE ? (((col >> 2) ^ cswz(row)) << 3)
+                                : (((col >> 3) ^ (row & (CPR - 1))) << 4) + ((col & 4) << 1);
         uint2 pk;
         pk.x = pack2<DT>(f32x2{v[0], v[1]});
         pk.y = pack2<DT>(f32x2{v[2], v[3]});
@@ -1414,7 +1438,7 @@ __global__ __launch_bounds__(conv_nt<STAGES>(), (PASS_T == WGRAD_BNA || PASS_T =
       prefetch(h * RPTH);
       __syncthreads();
       if (SHIFTED && h == 0 && do_stats) {   // shift = the tile's first row (always a valid row)
-        const i32x4 v0 = *reinterpret_cast<const i32x4*>(ct + c_addr(0, cc) * 16);
+        const i32x4 v0 = ld_c(0, cc);
         if constexpr (O32) {
 #pragma unroll
           for (int e = 0; e < 4; ++e) shv[e >> 1][e & 1] = __int_as_float(v0[e]);
@@ -1429,7 +1453,7 @@ __global__ __launch_bounds__(conv_nt<STAGES>(), (PASS_T == WGRAD_BNA || PASS_T =
 #pragma unroll
         for (int j = 0; j < PD; ++j) {
           const int row = rg + RG * (g0 + j);   // local row of the staged half
-          i32x4 v = *reinterpret_cast<const i32x4*>(ct + c_addr(row, cc) * 16);
+          i32x4 v = ld_c(row, cc);
           if (!eok[j]) continue;
           if constexpr (O32) {   // one element per dword
 #pragma unroll
