@@ -278,7 +278,10 @@ __global__ __launch_bounds__(conv_nt<STAGES>(), (PASS_T == WGRAD_BNA || PASS_T =
   constexpr int NH = O32 ? 2 : 1;
   constexpr int C_BYTES = BM / NH * BN * ES;
   // HALO: two input-slab slots of BM + 128 rows (any W <= 63: BM + 2W + 2 rows), three weight-tile
-  // slots and one zero row (the fragment source of a tap that falls outside the image)
+  // slots and one zero row (the fragment source of a tap that falls outside the image; a masked
+  // lane's broadcast read of it shares a bank quad with an unmasked lane: the ~22 % LDS conflicts
+  // of these launches -- a per-lane zero address removes them but costs 34 VGPRs and spills,
+  // profiles/ab_r6.md section 10)
   constexpr int SLAB_ROWS = BM + 128, SLAB_BYTES = SLAB_ROWS * 128;
   constexpr int ZOFF = 2 * SLAB_BYTES + 3 * B_BYTES;
   // LDS-DMA ring slots: 4 when they fit in 144 KiB (three tiles in flight), else 3
