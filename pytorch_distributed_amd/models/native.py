@@ -663,7 +663,9 @@ class NativeResNet(nn.Module):
                 if j < len(b.units) - 1:
                     sc, sh = self._coeffs(u, train)
                     if gram_side and j == len(b.units) - 2:
-                        rec["gram"] = self._fold_gram(b.units[-1], y, sc, sh)
+                        gB, gs, forked = self._fold_gram(b.units[-1], y, sc, sh)
+                        rec["gram"] = (gB, gs)
+                        gram_pending = gram_pending or forked
                     if self._fuse_into(b.units[j + 1]):
                         # the next conv applies BN+ReLU while staging its tiles
                         a, pro = y, (sc, sh)
@@ -722,7 +724,6 @@ class NativeResNet(nn.Module):
             if save:
                 rec["ys"], rec["acts"], rec["yd"] = ys, acts, yd
                 saved["blocks"].append(rec)
-                gram_pending = gram_pending or "gram" in rec
             h = out
             if self.probe is not None:
                 self.probe("fwd", b.name)
@@ -1016,15 +1017,30 @@ class NativeResNet(nn.Module):
 
     def _fold_gram(self, ul: ConvBN, y2, sc, sh):
         """Forward-time half of the decomposed conv3 weight gradient, on the second stream beside
-        conv3's forward: Gram(a2), the column sums s of a2 = relu(bn2(y2)), and B = W3 Gram(a2)."""
+        conv3's forward: Gram(a2), the column sums s of a2 = relu(bn2(y2)), and B = W3 Gram(a2).
+        Returns (B, s, forked): under a DataParallel capture with per-weight-gradient side graphs
+        (``wgrad_hook``) the work is queued like a weight gradient and recorded as a side graph
+        (forked = False: nothing for the forward to join)."""
         C_ = y2.shape[-1]
+        if self.defer_side and self.wgrad_hook is not None and self._wbatch is not None:
+            gram = torch.empty(C_ + 1, C_, dtype=torch.float32, device=self.device)
+            B = torch.empty(ul.cout, C_, dtype=torch.float32, device=self.device)
+            w16 = self.w16(ul)
+
+            def fn(w, y2=y2, sc=sc, sh=sh, gram=gram, B=B, w16=w16):
+                K.conv_wgrad_gram(y2, sc, sh, gram, w)
+                K.fold_bgemm(w16, gram[:C_], B)
+            self._wbatch.append(fn)
+            self._keep.extend([y2, sc, sh, gram, B, w16])
+            self.wgrad_hook()
+            return B, gram[C_], False
         self._fork()
         with torch.cuda.stream(self._side):
             gram = torch.empty(C_ + 1, C_, dtype=torch.float32, device=self.device)
             K.conv_wgrad_gram(y2, sc, sh, gram, self.ws_w)   # Gram rows, then the column sums
             B = torch.empty(ul.cout, C_, dtype=torch.float32, device=self.device)
             K.fold_bgemm(self.w16(ul), gram[:C_], B)
-        return B, gram[C_]
+        return B, gram[C_], True
 
     def _block_backward(self, b: Block, rec, tail, prev, acc):
         """Returns (dx_main, shortcut_grad, prev_tail) -- the last is the fused reduction of the

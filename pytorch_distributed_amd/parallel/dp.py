@@ -598,16 +598,19 @@ class _ReplicaGraph:
         from ..ops import native_ops as K
         m = self.m
         B = self.x.shape[0]
-        logits = m.native_forward(self.x, train=True, save=True)
-        loss = torch.empty((), dtype=torch.float32, device=self.dev)
-        rows = torch.empty(B, dtype=torch.float32, device=self.dev)
-        dlog16 = torch.empty(B, m.fc_rows, dtype=m.dtype, device=self.dev)
-        K.xent(logits, self.y, rows, loss, dlog=dlog16, gscale=self.gscale)
-        m._grads_zero = True          # every step overwrites the flat gradient
-        m.segment_hook = self._split if (self.splits or self.side_split) else None
+        # (set before the forward: conv mode also records the forward-time Gram work of the tail
+        # folds as side graphs -- forked inside a segment graph, the runtime replayed it on the
+        # main queue: ~0.8 ms/step of Gram / B-GEMM / reduce launches serialised into the chain)
         m.defer_side = self.side_split and self._capturing
         m.wgrad_hook = self._split_conv if self.side_per_conv else None
         try:
+            logits = m.native_forward(self.x, train=True, save=True)
+            loss = torch.empty((), dtype=torch.float32, device=self.dev)
+            rows = torch.empty(B, dtype=torch.float32, device=self.dev)
+            dlog16 = torch.empty(B, m.fc_rows, dtype=m.dtype, device=self.dev)
+            K.xent(logits, self.y, rows, loss, dlog=dlog16, gscale=self.gscale)
+            m._grads_zero = True          # every step overwrites the flat gradient
+            m.segment_hook = self._split if (self.splits or self.side_split) else None
             m.native_backward(dlog16)
         finally:
             m.segment_hook = None

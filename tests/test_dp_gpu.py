@@ -122,6 +122,49 @@ def test_native_dataparallel_graph_step_matches_eager(segments, side, monkeypatc
     assert ex is not None and 0.0 <= ex < 1000.0, ex
 
 
+def test_native_dataparallel_bottleneck_replay_records_grams_as_side_graphs(monkeypatch):
+    """Bottleneck replicas (ResNet-50 at 64 px) in conv mode: the forward-time Gram work of every
+    tail fold is recorded as a side graph of its own (forked inside a segment graph, the runtime
+    replayed it on the main queue), and the replayed step stays bit-identical to the eager one."""
+    monkeypatch.setenv("PDA_DP_SEGMENTS", "0")
+    monkeypatch.setenv("PDA_DP_SIDE", "conv")
+    from pytorch_distributed_amd.data import SyntheticImageNet
+    from pytorch_distributed_amd.models import build_model
+    from pytorch_distributed_amd.models.native import NativeResNet
+    from pytorch_distributed_amd.parallel import DataParallel
+    torch.manual_seed(0)
+    sd = build_model("resnet50").state_dict()
+    dps = []
+    for _ in range(2):
+        r = build_model("resnet50")
+        r.load_state_dict(sd)
+        dps.append(DataParallel(NativeResNet(r, device=DEV, image_size=64), device_ids=[0, 0]))
+    eager, graphed = dps
+    m = graphed.module
+    nfold = sum(1 for b in m.blocks if len(b.units) == 3 and m._tail_fold_ok(b, 8)) \
+        if m.bn_fold_wg else 0
+    assert nfold > 0
+    gen = eager.module.input_generator(SyntheticImageNet("train", image_size=64))
+    oe = eager.make_optimizer(lr=0.05, momentum=0.9, weight_decay=1e-4)
+    og = graphed.make_optimizer(lr=0.05, momentum=0.9, weight_decay=1e-4)
+    for step in range(3):
+        x, y = gen(torch.arange(16) + 16 * step)
+        le = eager.train_step(x, y, oe, graph=False)
+        with warnings.catch_warnings(record=True) as caught:
+            warnings.simplefilter("always")
+            lg = graphed.train_step(x, y, og)
+        assert not [w for w in caught if "Graph is empty" in str(w.message)], step
+        torch.cuda.synchronize()
+        assert le.item() == lg.item(), (step, le.item(), lg.item())
+        assert torch.equal(eager.module.flat_grad, graphed.module.flat_grad), step
+        assert torch.equal(eager.module.flat_params, graphed.module.flat_params), step
+    rg = graphed._graphs[0]
+    nside = sum(g is not None for g in rg.sides)
+    nconv = sum(len(b.units) + (b.ds is not None and bool(m._tail_fold_ok(b, 8)))
+                for b in m.blocks) + 2
+    assert nside == nconv + nfold, (nside, nconv, nfold)
+
+
 def test_native_dataparallel_segment_mismatch_falls_back(monkeypatch):
     """The first segmented replay verifies that every replica holds the same summed gradient; a
     mismatch (forced here: the checksum reports a different value for one replica) must not break
