@@ -15,6 +15,8 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
 def main() -> None:
+    from pytorch_distributed_amd.runtime.graphs import request_single_queue_graphs
+    request_single_queue_graphs()   # (before HIP starts: the replica graphs need it)
     from pytorch_distributed_amd.bench_step import _DPTrainer
     steps = int(sys.argv[1]) if len(sys.argv) > 1 else 10
     tr = _DPTrainer("resnet50", 400, torch.bfloat16, [0], 224)
