@@ -17,9 +17,6 @@
 //   maxpool_bwd     : deterministic gather of max-pool gradients through the argmax bytes
 #include "common.h"
 
-#include <cstdlib>
-#include <cstring>
-
 namespace {
 
 constexpr int NT = 256;
@@ -457,88 +454,6 @@ __global__ __launch_bounds__(NT) void stem_pool_kernel(const void* __restrict__ 
       }
     }
     store8<DT>(out, (size_t)i * 8, best);
-    uint64_t packed = 0;
-#pragma unroll
-    for (int e = 0; e < 8; ++e) packed |= (uint64_t)bi[e] << (8 * e);
-    reinterpret_cast<uint64_t*>(arg)[i] = packed;
-  }
-}
-
-// Row-staged form (16-bit y, 3 * W * C * 2 B of LDS <= 48 KiB; the ResNet stem: 3 x 112 x 64 x 2 B
-// = 42 KiB): one block per output row (n, yo) copies input rows 2yo-1 .. 2yo+1 into LDS with
-// contiguous 16-B loads, then every (xo, 8-channel chunk) item takes its nine taps from LDS. The
-// flat kernel above gathers each y element ~2.25 times through the caches with per-lane 16-B
-// requests at a 256-B stride (4.4 TB/s); here every row is one streaming copy. Same compare order
-// and arithmetic as the flat kernel: bitwise the same output and argmax bytes.
-template <int DT>
-__global__ __launch_bounds__(NT) void stem_pool_rows_kernel(const void* __restrict__ y,
-                                                            const float* __restrict__ sc,
-                                                            const float* __restrict__ sh,
-                                                            void* __restrict__ out,
-                                                            uint8_t* __restrict__ arg, int H, int W,
-                                                            int C, int Ho, int Wo, int ck_log2) {
-  extern __shared__ __attribute__((aligned(16))) char rows_lds[];
-  i32x4* rows = reinterpret_cast<i32x4*>(rows_lds);
-  const int CK = 1 << ck_log2;                  // 8-channel chunks per pixel (a power of two)
-  const int rowc = W * CK;                      // 16-B chunks per input row
-  const int n = blockIdx.x / Ho, yo = blockIdx.x - n * Ho;
-  const int y0 = 2 * yo - 1;
-  const i32x4* src = reinterpret_cast<const i32x4*>(y);
-  // chunk (x, c) of a row sits at x*CK + (c ^ ((x >> 1) & (CK - 1))): the nine-tap reads of a
-  // wave (8 consecutive xo x 8 chunks, x = 2xo - 1 + dx) then spread over all bank quads
-  auto slot = [&](int o) { return o ^ ((o >> (ck_log2 + 1)) & (CK - 1)); };
-  // all three rows' loads in flight before their LDS writes, 4 per row per thread per round
-  for (int o0 = 0; o0 < rowc; o0 += 4 * NT) {
-    i32x4 t[3][4];
-#pragma unroll
-    for (int r = 0; r < 3; ++r) {
-      const int yy = y0 + r;
-      const i32x4* s_ = src + ((size_t)n * H + (yy < 0 ? 0 : yy)) * rowc;
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const int o = o0 + k * NT + threadIdx.x;
-        if (o < rowc && (unsigned)yy < (unsigned)H) t[r][k] = s_[o];
-      }
-    }
-#pragma unroll
-    for (int r = 0; r < 3; ++r) {
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const int o = o0 + k * NT + threadIdx.x;
-        if (o < rowc && (unsigned)(y0 + r) < (unsigned)H) rows[r * rowc + slot(o)] = t[r][k];
-      }
-    }
-  }
-  __syncthreads();
-  const int items = Wo * CK;
-  for (int it = threadIdx.x; it < items; it += NT) {
-    const int xo = it >> ck_log2, ck = it & (CK - 1);
-    float a[8], b[8], best[8];
-    int bi[8];
-    ld8f(sc + ck * 8, a);
-    ld8f(sh + ck * 8, b);
-#pragma unroll
-    for (int e = 0; e < 8; ++e) { best[e] = -1.f; bi[e] = 0; }
-#pragma unroll
-    for (int dy = 0; dy < 3; ++dy) {
-      if ((unsigned)(y0 + dy) >= (unsigned)H) continue;
-#pragma unroll
-      for (int dx = 0; dx < 3; ++dx) {
-        const int xx = xo * 2 - 1 + dx;
-        if ((unsigned)xx >= (unsigned)W) continue;
-        Raw8<DT> rv;
-        rv.v = rows[dy * rowc + slot(xx * CK + ck)];
-        float v[8];
-        cvt8<DT>(rv, v);
-#pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          const float r = fmaxf(v[e] * a[e] + b[e], 0.f);
-          if (r > best[e]) { best[e] = r; bi[e] = dy * 3 + dx; }
-        }
-      }
-    }
-    const size_t i = ((size_t)blockIdx.x * Wo + xo) * CK + ck;
-    store8<DT>(out, i * 8, best);
     uint64_t packed = 0;
 #pragma unroll
     for (int e = 0; e < 8; ++e) packed |= (uint64_t)bi[e] << (8 * e);
@@ -1349,23 +1264,6 @@ int pda_bn_apply(const void* y, const float* sc, const float* sh, const void* r2
 int pda_stem_pool(const void* y, const float* sc, const float* sh, void* out, void* arg, int N,
                   int H, int W, int C, int Ho, int Wo, int dt, hipStream_t st) {
   if ((long long)N * H * W * (C / 8) >= (1ll << 31)) return -2;
-  // PDA_STEM_POOL=flat: the gather kernel (A/B); default: row-staged where its LDS image fits
-  // (read per call: the kernel test switches it between calls)
-  const char* pe = getenv("PDA_STEM_POOL");
-  const bool rows_ok = !(pe && strcmp(pe, "flat") == 0);
-  const size_t lds = 3ull * W * C * 2;
-  const int ck = C / 8;
-  if (rows_ok && (dt == DT_BF16 || dt == DT_F16) && C % 8 == 0 && (ck & (ck - 1)) == 0 && lds <= 48 * 1024 &&
-      Ho == (H + 1) / 2 && Wo == (W + 1) / 2 && (long long)N * Ho < (1ll << 31)) {
-    const dim3 grid((unsigned)(N * Ho));
-    int l2 = 0;
-    while ((1 << l2) < ck) ++l2;
-#define RARGS (const void*)y, sc, sh, (void*)out, (uint8_t*)arg, H, W, C, Ho, Wo, l2
-    if (dt == DT_BF16) TRACKED_LAUNCH(stem_pool_rows_kernel<DT_BF16>, grid, dim3(NT), lds, st, RARGS);
-    else TRACKED_LAUNCH(stem_pool_rows_kernel<DT_F16>, grid, dim3(NT), lds, st, RARGS);
-#undef RARGS
-    return (int)hipGetLastError();
-  }
   const int g = grid_for((long long)N * Ho * Wo * (C / 8));
 #define ARGS (const void*)y, sc, sh, (void*)out, (uint8_t*)arg, N, H, W, C, Ho, Wo, make_div(C / 8), \
              make_div(Wo), make_div(Ho)

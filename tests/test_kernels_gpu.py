@@ -447,33 +447,6 @@ def test_stem_pool_and_backward():
                                rtol=2e-2, atol=2e-1)
 
 
-@pytest.mark.parametrize("H", [12, 15, 112])
-def test_stem_pool_rows_matches_flat(H, monkeypatch):
-    """The row-staged stem pool (input rows through LDS, one block per output row) == the flat
-    gather kernel bit for bit: pooled values AND argmax bytes (the backward routes by them)."""
-    K = _k()
-    dtype = torch.bfloat16
-    N, C = 2, 64
-    torch.manual_seed(3)
-    y = torch.randn(N, H, H, C, device=DEV).to(dtype)
-    y[0, :3, :3] = 0   # ties among relu zeros: the first tap must win in both kernels
-    sc = torch.rand(C, device=DEV) + 0.5
-    sh = torch.randn(C, device=DEV) * 0.1
-    Ho = (H + 2 - 3) // 2 + 1
-    outs = []
-    for mode in ("rows", "flat"):
-        monkeypatch.setenv("PDA_STEM_POOL", mode)
-        out = torch.full((N, Ho, Ho, C), 7.0, device=DEV, dtype=dtype)
-        arg = torch.full((N, Ho, Ho, C), 77, device=DEV, dtype=torch.uint8)
-        K.stem_pool(y, sc, sh, out, arg)
-        torch.cuda.synchronize()
-        outs.append((out, arg))
-    assert torch.equal(outs[0][0], outs[1][0])
-    assert torch.equal(outs[0][1], outs[1][1])
-    ref = F.max_pool2d(torch.relu(y.float() * sc + sh).permute(0, 3, 1, 2), 3, 2, 1)
-    assert rel_err(outs[0][0], ref.permute(0, 2, 3, 1)) < 1e-2
-
-
 @pytest.mark.parametrize("H", [14, 15])
 @pytest.mark.parametrize("with_shortcut", [False, True])
 def test_stem_bwd_reduce_matches_unfused(with_shortcut, H):
