@@ -607,10 +607,11 @@ def main():
         # replica-graph replay an N > 1 run takes (per-block segment graphs + weight-gradient side
         # graphs) is timed here too, so that path has a number on every 1-GPU record
         tr.dp.force_replay = True
-        for i in range(3):            # capture + settle
+        nw = 1 + max(2, args.warmup)  # the capture step, then as many warm replays as the headline
+        for i in range(nw):
             tr.step(nxt + i)
-        rel = _timed(ctx, tr, nxt + 3, args.steps, "dp_replay")
-        nxt += 3 + args.steps
+        rel = _timed(ctx, tr, nxt + nw, args.steps, "dp_replay")
+        nxt += nw + args.steps
         diag["dp_replay_ms_per_step"] = round(1000.0 * rel / args.steps, 3)
         diag["dp_replay_vs_eager"] = round(rel / elapsed, 4)
         diag["dp_replay_segments"] = len(tr.dp._graphs[0].graphs)
