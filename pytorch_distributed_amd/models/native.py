@@ -177,13 +177,6 @@ class NativeResNet(nn.Module):
         self._side = (torch.cuda.Stream(device) if os.environ.get("PDA_WGRAD_STREAM", "1") != "0"
                       else None)
         self.ws_w = Workspace(device) if self._side is not None else self.ws
-        # the tail folds' forward-time Gram work on a third stream (PDA_GRAM_STREAM=0: on the second
-        # one): queued on the second stream it sat ahead of the next downsampling block's shortcut
-        # conv, and that block's join made the main chain wait for it (48 / 71 us of main-stream
-        # idle before layer2.0 / layer3.0's tails, profiles/rocprof_r6_final.md)
-        self._gram_side = (torch.cuda.Stream(device) if self._side is not None
-                           and os.environ.get("PDA_GRAM_STREAM", "1") != "0" else None)
-        self.ws_g = Workspace(device) if self._gram_side is not None else self.ws_w
         # When the wgrad stream forks: "0" once per conv (eager default: each weight gradient
         # starts as soon as its inputs exist), "block" queues a residual block's weight-gradient
         # kernels and forks ONCE per block, "stage" once per stage (graph-capture default: in a
@@ -739,8 +732,7 @@ class NativeResNet(nn.Module):
             # per block stalled the main chain 20-55 us whenever a Gram was still running
             # (graph captures need every fork joined; the backward's weight gradients follow the
             # Grams on that stream anyway)
-            torch.cuda.current_stream(self.device).wait_stream(
-                self._gram_side if self._gram_side is not None else self._side)
+            torch.cuda.current_stream(self.device).wait_stream(self._side)
         logits = torch.empty(Nb, self.num_classes, dtype=torch.float32, device=self.device)
         g = ConvGeom(Nb, 1, 1, self.feat_dim, self.num_classes, 1, 1, 1, 0)
         K.conv_fwd(feat, self.fc_w16, g, logits, tile=self._fc_tile(),
@@ -781,19 +773,18 @@ class NativeResNet(nn.Module):
             except Exception:   # (interpreter shutdown: the library may be gone)
                 pass
 
-    def _fork(self, stream: Optional[torch.cuda.Stream] = None) -> None:
-        """The second stream (or ``stream``) waits for everything queued on the main stream so far:
-        on the tracked event (completed by the latest native launch) when the main stream has
-        issued a native launch since tracking was armed -- the forward / backward issue nothing
-        else on it between forks -- else with a regular event record."""
-        st = stream if stream is not None else self._side
+    def _fork(self) -> None:
+        """The second stream waits for everything queued on the main stream so far: on the tracked
+        event (completed by the latest native launch) when the main stream has issued a native
+        launch since tracking was armed -- the forward / backward issue nothing else on it between
+        forks -- else with a regular event record."""
         cur = torch.cuda.current_stream(self.device)
         L = ext.lib()
         if self._trk_on and L.pda_track_count() != self._trk_c0:
-            K.check(L.pda_stream_wait_event(C.c_void_p(st.cuda_stream), self._trk_ev),
+            K.check(L.pda_stream_wait_event(C.c_void_p(self._side.cuda_stream), self._trk_ev),
                     "pda_stream_wait_event")
         else:
-            st.wait_stream(cur)
+            self._side.wait_stream(cur)
 
     def _wgrad(self, fn: Callable, *keep: torch.Tensor, split: bool = True) -> None:
         """Enqueue ``fn(workspace)`` (weight-gradient kernels) on the wgrad stream, ordered after
@@ -1032,7 +1023,7 @@ class NativeResNet(nn.Module):
         return (64, 64) if self.dtype in (torch.bfloat16, torch.float16) else None
 
     def _fold_gram(self, ul: ConvBN, y2, sc, sh):
-        """Forward-time half of the decomposed conv3 weight gradient, on a stream of its own beside
+        """Forward-time half of the decomposed conv3 weight gradient, on the second stream beside
         conv3's forward: Gram(a2), the column sums s of a2 = relu(bn2(y2)), and B = W3 Gram(a2).
         Returns (B, s, forked): under a DataParallel capture with per-weight-gradient side graphs
         (``wgrad_hook``) the work is queued like a weight gradient and recorded as a side graph
@@ -1050,11 +1041,10 @@ class NativeResNet(nn.Module):
             self._keep.extend([y2, sc, sh, gram, B, w16])
             self.wgrad_hook()
             return B, gram[C_], False
-        st = self._gram_side if self._gram_side is not None else self._side
-        self._fork(st)
-        with torch.cuda.stream(st):
+        self._fork()
+        with torch.cuda.stream(self._side):
             gram = torch.empty(C_ + 1, C_, dtype=torch.float32, device=self.device)
-            K.conv_wgrad_gram(y2, sc, sh, gram, self.ws_g)   # Gram rows, then the column sums
+            K.conv_wgrad_gram(y2, sc, sh, gram, self.ws_w)   # Gram rows, then the column sums
             B = torch.empty(ul.cout, C_, dtype=torch.float32, device=self.device)
             K.fold_bgemm(self.w16(ul), gram[:C_], B)
         return B, gram[C_], True
