@@ -138,8 +138,9 @@ class DataParallel(nn.Module):
         self.timing = False
         # one device: replay the replica graphs anyway (bench.py dp_replay_ms_per_step)
         self.force_replay = os.environ.get("PDA_DP_FORCE_REPLAY", "0") == "1"
-        # host-side bound on one segment's replay enqueue per device worker (a graph launch takes
-        # ~1 ms): a worker that raises or never returns becomes an exception in the caller
+        # host-side bound on one reduce interval's replay enqueue per device worker (its segments'
+        # graph launches, ~ms): a worker that raises or never returns becomes an exception in the
+        # caller
         self.replay_timeout_s = float(os.environ.get("PDA_DP_REPLAY_TIMEOUT_S", "120"))
         self._ev_bwd = self._ev_comm = None
 
@@ -417,24 +418,35 @@ class DataParallel(nn.Module):
                     and len(set(self.device_ids)) == len(self.device_ids))
         timing = self.timing
         lo = 0
-        for s in range(nseg):
+        s = 0
+        while s < nseg:
+            # the segments up to the next all-reduce point (or the last): with a side graph per
+            # weight gradient a step has ~65 segments but only 4 reduce points, and one worker task
+            # per device per reduce interval keeps the host's per-segment dispatch cost out of the
+            # N-device enqueue
+            e = s
+            while e < nseg - 1 and ends[e] is None:
+                e += 1
             if threaded:
-                # one host thread per device: hipGraphLaunch of a ~150-node segment costs ~0.5 ms
-                # of host time and CUDAGraph.replay releases the GIL, so the N replicas enqueue
-                # concurrently instead of staggering device i's start by i launches
+                # one host thread per device: hipGraphLaunch of a segment costs host time and
+                # CUDAGraph.replay releases the GIL, so the N replicas enqueue concurrently instead
+                # of staggering device i's start by i launches
                 run_workers(self._pool(), [
-                    (lambda a=a: a[0][0].replay(s, a[0][1], a[0][2], a[1]))
+                    (lambda a=a, s0=s, s1=e: [a[0][0].replay(k, a[0][1], a[0][2], a[1])
+                                             for k in range(s0, s1 + 1)])
                     for a in zip(jobs, streams)], self.replay_timeout_s,
                     [f"cuda:{rg.dev.index}" for rg, _, _ in jobs])
             else:
-                for (rg, x, y), st in zip(jobs, streams):
-                    rg.replay(s, x, y, st)
-            if timing and s == nseg - 1:
+                for k in range(s, e + 1):
+                    for (rg, x, y), st in zip(jobs, streams):
+                        rg.replay(k, x, y, st)
+            if timing and e == nseg - 1:
                 self._ev_bwd = [torch.cuda.Event(enable_timing=True) for _ in streams]
-                for e, st, (rg, _, _) in zip(self._ev_bwd, streams, jobs):
+                for ev, st, (rg, _, _) in zip(self._ev_bwd, streams, jobs):
                     rg.join_side(st)
-                    e.record(st)
-            hi = ends[s]
+                    ev.record(st)
+            hi = ends[e]
+            s = e + 1
             if hi is None:
                 continue
             for c, st, (rg, _, _) in zip(cs, streams, jobs):
