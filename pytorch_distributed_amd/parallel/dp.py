@@ -432,8 +432,7 @@ class DataParallel(nn.Module):
                 # CUDAGraph.replay releases the GIL, so the N replicas enqueue concurrently instead
                 # of staggering device i's start by i launches
                 run_workers(self._pool(), [
-                    (lambda a=a, s0=s, s1=e: [a[0][0].replay(k, a[0][1], a[0][2], a[1])
-                                             for k in range(s0, s1 + 1)])
+                    (lambda a=a, s0=s, s1=e: a[0][0].replay_range(s0, s1, a[0][1], a[0][2], a[1]))
                     for a in zip(jobs, streams)], self.replay_timeout_s,
                     [f"cuda:{rg.dev.index}" for rg, _, _ in jobs])
             else:
@@ -640,18 +639,26 @@ class _ReplicaGraph:
         """Replay segment ``s`` on ``stream`` (the caller's current stream on this device: a
         worker thread's own current stream is the default stream), then its weight-gradient graph
         on the second stream after it; segment 0 first takes the inputs."""
+        self.replay_range(s, s, x, y, stream)
+
+    def replay_range(self, s0: int, s1: int, x: torch.Tensor, y: torch.Tensor,
+                     stream: Optional[torch.cuda.Stream] = None) -> None:
+        """:meth:`replay` of segments ``s0 .. s1`` under one device context (host cost per segment:
+        a main-graph launch, and for a side graph one event hand-off + its launch)."""
         with torch.cuda.device(self.dev):
             st = stream or torch.cuda.current_stream(self.dev)
-            with torch.cuda.stream(st):
-                if s == 0:
-                    self.x.copy_(x, non_blocking=True)
-                    self.y.copy_(y, non_blocking=True)
-                self.graphs[s].replay()
-            side = self.sides[s] if s < len(self.sides) else None
-            if side is not None:
-                self.m._side.wait_stream(st)
-                with torch.cuda.stream(self.m._side):
-                    side.replay()
+            side_st = self.m._side
+            for s in range(s0, s1 + 1):
+                with torch.cuda.stream(st):
+                    if s == 0:
+                        self.x.copy_(x, non_blocking=True)
+                        self.y.copy_(y, non_blocking=True)
+                    self.graphs[s].replay()
+                side = self.sides[s] if s < len(self.sides) else None
+                if side is not None:
+                    side_st.wait_stream(st)
+                    with torch.cuda.stream(side_st):
+                        side.replay()
             self.loss = self._graph_loss
 
     def run(self, x: torch.Tensor, y: torch.Tensor, graph: bool = True,
@@ -660,8 +667,7 @@ class _ReplicaGraph:
         time -- eagerly for this batch and then captured for the next replays."""
         if graph and self.graphs:
             st = stream or torch.cuda.current_stream(self.dev)
-            for s in range(len(self.graphs)):
-                self.replay(s, x, y, st)
+            self.replay_range(0, len(self.graphs) - 1, x, y, st)
             self.join_side(st)
             return
         with torch.cuda.device(self.dev), torch.cuda.stream(stream or torch.cuda.current_stream(self.dev)):

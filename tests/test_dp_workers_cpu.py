@@ -63,6 +63,10 @@ class _FakeReplica:
     def replay(self, s, x, y, st):
         self.log.append(("replay", self.i, s, threading.current_thread().name))
 
+    def replay_range(self, s0, s1, x, y, st):
+        for s in range(s0, s1 + 1):
+            self.replay(s, x, y, st)
+
     def join_side(self, st):
         pass
 
