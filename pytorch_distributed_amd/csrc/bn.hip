@@ -17,6 +17,9 @@
 //   maxpool_bwd     : deterministic gather of max-pool gradients through the argmax bytes
 #include "common.h"
 
+#include <cstdlib>
+#include <cstring>
+
 namespace {
 
 constexpr int NT = 256;
@@ -425,10 +428,13 @@ __global__ __launch_bounds__(NT) void stem_pool_kernel(const void* __restrict__ 
                                                        void* __restrict__ out,
                                                        uint8_t* __restrict__ arg, int N, int H,
                                                        int W, int C, int Ho, int Wo, FastDiv dCK,
-                                                       FastDiv dWo, FastDiv dHo) {
+                                                       FastDiv dWo, FastDiv dHo, int rev) {
   const int CK = C / 8;
   const int total = N * Ho * Wo * CK;
-  for (int i = blockIdx.x * NT + threadIdx.x; i < total; i += gridDim.x * NT) {
+  for (int i0 = blockIdx.x * NT + threadIdx.x; i0 < total; i0 += gridDim.x * NT) {
+    // rev: last rows first -- the stem conv wrote them last, so up to the Infinity Cache's 256 MiB
+    // of y are still cached when the pool starts
+    const int i = rev ? total - 1 - i0 : i0;
     const uint32_t pix = fdiv(i, dCK), ck = i - pix * CK;
     const uint32_t p2 = fdiv(pix, dWo), xo = pix - p2 * Wo;
     const uint32_t n = fdiv(p2, dHo), yo = p2 - n * Ho;
@@ -1265,8 +1271,10 @@ int pda_stem_pool(const void* y, const float* sc, const float* sh, void* out, vo
                   int H, int W, int C, int Ho, int Wo, int dt, hipStream_t st) {
   if ((long long)N * H * W * (C / 8) >= (1ll << 31)) return -2;
   const int g = grid_for((long long)N * Ho * Wo * (C / 8));
+  const char* rv = pda_reverse_env();
+  const int rev = (rv && strstr(rv, "stem_pool")) ? 1 : 0;
 #define ARGS (const void*)y, sc, sh, (void*)out, (uint8_t*)arg, N, H, W, C, Ho, Wo, make_div(C / 8), \
-             make_div(Wo), make_div(Ho)
+             make_div(Wo), make_div(Ho), rev
   if (dt == DT_BF16) TRACKED_LAUNCH(stem_pool_kernel<DT_BF16>, dim3(g), dim3(NT), 0, st, ARGS);
   else if (dt == DT_F32) TRACKED_LAUNCH(stem_pool_kernel<DT_F32>, dim3(g), dim3(NT), 0, st, ARGS);
   else TRACKED_LAUNCH(stem_pool_kernel<DT_F16>, dim3(g), dim3(NT), 0, st, ARGS);

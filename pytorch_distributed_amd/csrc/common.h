@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 #include <hip/hip_ext.h>
 #include <stdint.h>
+#include <cstdlib>
 
 typedef short s16x8 __attribute__((ext_vector_type(8)));
 typedef short s16x4 __attribute__((ext_vector_type(4)));
@@ -187,6 +188,23 @@ __device__ __forceinline__ uint32_t xcd_remap(uint32_t bid, uint32_t nwg) {
   const uint32_t q = nwg >> 3, r = nwg & 7, x = bid & 7;
   const uint32_t base = x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q;
   return base + (bid >> 3);
+}
+// Launches that walk their tiles / items from the end (xcd_remap_rev, the stem pool's reversed
+// grid-stride loop): PDA_REVERSE lists them ("fwd_tail", "bnf", "stem_pool"; "none": none); default
+// all three -- their producers (conv3, the tail-epilogue data gradient, the stem conv) ran just
+// before and wrote those tiles last, so up to 256 MiB of their reads hit the Infinity Cache
+// (profiles/ab_r6.md section 13: -0.08 ms/step)
+inline const char* pda_reverse_env() {
+  const char* e = getenv("PDA_REVERSE");
+  return e ? e : "fwd_tail+bnf+stem_pool";
+}
+// the same XCD chunks, each walked from its end: a consumer launched right after a producer of the
+// same chunking reads first what the producer wrote last (still in the 256 MiB Infinity Cache)
+__device__ __forceinline__ uint32_t xcd_remap_rev(uint32_t bid, uint32_t nwg) {
+  const uint32_t q = nwg >> 3, r = nwg & 7, x = bid & 7;
+  const uint32_t base = x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q;
+  const uint32_t len = x < r ? q + 1 : q;
+  return base + (len - 1 - (bid >> 3));
 }
 
 // ---------------------------------------------------------------------------------------------

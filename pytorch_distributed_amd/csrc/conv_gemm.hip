@@ -24,6 +24,9 @@
 // partial sum / sum-of-squares (BatchNorm statistics) per M-tile -- no extra pass over Y.
 #include "common.h"
 
+#include <cstdlib>
+#include <cstring>
+
 namespace {
 
 constexpr int NT = 256;
@@ -119,6 +122,7 @@ struct ConvParams {
   // and the epilogue bias b[N]
   const void* xa; const float* xa_sc; const float* xa_sh; const float* dbias;
   int xa_c;
+  int rev;   // walk each XCD's tile chunk from its end (xcd_remap_rev; PDA_REVERSE experiments)
   // FWD BatchNorm statistics (stats != nullptr) are per-M-tile SHIFTED partials
   // stats[tile][3][N] = (sum(y - s), sum((y - s)^2), s), s = the tile's first row (no f32
   // cancellation when |mean| >> std); bn.hip bn_fwd_stats combines and finalizes them.
@@ -313,7 +317,7 @@ __global__ __launch_bounds__(conv_nt<STAGES>(), (PASS_T == WGRAD_BNA || PASS_T =
   const int tiles_n = (p.N + BN - 1) / BN;
   const int tiles_m = (p.M + BM - 1) / BM;
   const int ntile = tiles_m * tiles_n;
-  const int t = (int)xcd_remap(blockIdx.x, ntile);
+  const int t = (int)(p.rev ? xcd_remap_rev(blockIdx.x, ntile) : xcd_remap(blockIdx.x, ntile));
   const int tm = t / tiles_n, tn = t - tm * tiles_n;
   const int m0 = tm * BM, n0 = tn * BN;
   const int split = blockIdx.y;  // WGRAD: K split; DGRAD: parity class
@@ -2001,6 +2005,7 @@ int pda_conv_fwd_tail(const ConvDesc* d, const void* y3, const void* w, int Kpad
   p.a = y3; p.b = w; p.out = y; p.stats = stats; p.bias = nullptr;
   p.M = d->Nb * d->Ho * d->Wo; p.N = d->Cout; p.Kpad = Kpad; p.K = Kpad;
   p.out_f32 = 0; p.relu = 0; p.out_pitch = d->Cout;
+  { const char* rv = pda_reverse_env(); p.rev = (rv && strstr(rv, "fwd_tail")) ? 1 : 0; }
   const int tiles = ((p.M + 127) / 128) * ((p.N + bn - 1) / bn);
 #define TAIL_CASE(D, N_) \
   if (dt == D && bm == -128 && bn == N_) return launch<FWD_TAIL, D, 128, N_, 1>(p, dim3(tiles, 1), st);
@@ -2091,6 +2096,7 @@ int pda_conv_dgrad_bnf(const ConvDesc* d, const void* dz, const void* wf, void* 
   const int rc = dgrad_params(p, d, dz, wf, dx, epi);
   if (rc) return rc;
   p.xa = xa; p.xa_sc = xa_sc; p.xa_sh = xa_sh; p.dbias = dbias; p.xa_c = xa_c;
+  { const char* rv = pda_reverse_env(); p.rev = (rv && strstr(rv, "bnf")) ? 1 : 0; }
   const int abm = tile_bm(bm);
   const dim3 grid(((p.M + abm - 1) / abm) * ((p.N + bn - 1) / bn), d->stride * d->stride);
 #define BNF_CASE(D, M_, N_, S_) \

@@ -461,6 +461,36 @@ def test_fork_tracking_is_bit_exact():
         assert torch.equal(l1, l2) and torch.equal(g1, g2)
 
 
+def test_reversed_tile_walks_are_bit_exact(monkeypatch):
+    """PDA_REVERSE (csrc/common.h pda_reverse_env): FWD_TAIL, DGRAD_BNF and the stem pool walk
+    their tiles from the end of each XCD chunk by default (Infinity-Cache reuse of what their
+    producers wrote last) -- only the order changes: logits and every gradient bit-identical to the
+    forward walk, over two steps (running statistics included)."""
+    _, nm = _pair("resnet50", image=64)
+    torch.manual_seed(17)
+    x = torch.randn(32, 3, 64, 64, device=DEV)
+    y = torch.randint(0, 1000, (32,), device=DEV)
+    nm.train()
+    crit = nm.make_criterion()
+    buf0 = nm.flat_bufstore.detach().clone()
+    res = {}
+    for mode in ("none", "fwd_tail+bnf+stem_pool"):
+        monkeypatch.setenv("PDA_REVERSE", mode)
+        with torch.no_grad():
+            nm.flat_bufstore.copy_(buf0)
+        outs = []
+        for _ in range(2):
+            nm.zero_grad_flat()
+            out = nm(x)
+            crit(out, y).backward()
+            torch.cuda.synchronize()
+            outs.append((out.detach().clone(), nm.flat_grad.detach().clone(),
+                         nm.flat_bufstore.detach().clone()))
+        res[mode] = outs
+    for a, b in zip(res["none"], res["fwd_tail+bnf+stem_pool"]):
+        assert all(torch.equal(u, v) for u, v in zip(a, b))
+
+
 def test_decomposed_fold_wgrad_matches_apply_path():
     """PDA_BN_FOLD_WG: the folded tails' conv3 weight gradient in the decomposed form (forward-time
     Gram and column sums of a2 on the second stream, plain dz^T a2 combined in the split-K reduce)
