@@ -933,18 +933,14 @@ __global__ __launch_bounds__(NT) void bn_bwd_apply_dz_u_kernel(const void* __res
                                                                const float* __restrict__ k1,
                                                                const float* __restrict__ k2,
                                                                const float* __restrict__ k3,
-                                                               void* __restrict__ dy, int n8, int C,
-                                                               int rev) {
+                                                               void* __restrict__ dy, int n8, int C) {
   const int C8 = C >> 3;
   const int stride = gridDim.x * NT;
   int i = blockIdx.x * NT + threadIdx.x;
   if (i >= n8) return;
-  // rev: chunk n8-1-i instead of i (the walk from the end: see csrc/common.h pda_reverse_env); a
-  // thread's channel is fixed either way (C8 divides the stride and n8)
-  auto ix = [&](int j) __attribute__((always_inline)) { return rev ? n8 - 1 - j : j; };
   f32x2 A[4], B[4], K3[4];
   {
-    const int c0 = (ix(i) % C8) * 8;
+    const int c0 = (i % C8) * 8;
     ld8p<DT>(k1 + c0, A);
     ld8p<DT>(k2 + c0, B);
     ld8p<DT>(k3 + c0, K3);
@@ -957,8 +953,8 @@ __global__ __launch_bounds__(NT) void bn_bwd_apply_dz_u_kernel(const void* __res
     i32x4 dz[U], yv[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      dz[u] = ldnt<NTM & 1>(dzp + ix(i + u * stride));
-      yv[u] = ldnt<NTM & 1>(yp + ix(i + u * stride));
+      dz[u] = ldnt<NTM & 1>(dzp + i + u * stride);
+      yv[u] = ldnt<NTM & 1>(yp + i + u * stride);
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
@@ -967,18 +963,17 @@ __global__ __launch_bounds__(NT) void bn_bwd_apply_dz_u_kernel(const void* __res
       for (int k = 0; k < 4; ++k)
         o[k] = (int)pack2<DT>(bnb_affine2(A[k], B[k], K3[k], unpack2<DT>((uint32_t)dz[u][k]),
                                           unpack2<DT>((uint32_t)yv[u][k])));
-      st_out<NTM>(op, rs, ix(i + u * stride), o);
+      st_out<NTM>(op, rs, i + u * stride, o);
     }
   }
   for (; i < n8; i += stride) {
-    const int j = ix(i);
-    const i32x4 dz = dzp[j], yv = yp[j];
+    const i32x4 dz = dzp[i], yv = yp[i];
     i32x4 o;
 #pragma unroll
     for (int k = 0; k < 4; ++k)
       o[k] = (int)pack2<DT>(bnb_affine2(A[k], B[k], K3[k], unpack2<DT>((uint32_t)dz[k]),
                                         unpack2<DT>((uint32_t)yv[k])));
-    op[j] = o;
+    op[i] = o;
   }
 }
 
@@ -991,16 +986,14 @@ __global__ __launch_bounds__(NT) void bn_bwd_apply_dz2_u_kernel(const void* __re
                                                                 const void* __restrict__ y2sel,
                                                                 const float* __restrict__ k,
                                                                 void* __restrict__ dy,
-                                                                void* __restrict__ dy2, int n8, int C,
-                                                                int rev) {
+                                                                void* __restrict__ dy2, int n8, int C) {
   const int C8 = C >> 3;
   const int stride = gridDim.x * NT;
   int i = blockIdx.x * NT + threadIdx.x;
   if (i >= n8) return;
-  auto ix = [&](int j) __attribute__((always_inline)) { return rev ? n8 - 1 - j : j; };
   f32x2 A[4], B[4], K3[4], A2[4], B2[4], K32[4];
   {
-    const int c0 = (ix(i) % C8) * 8;
+    const int c0 = (i % C8) * 8;
     ld8p<DT>(k + c0, A);
     ld8p<DT>(k + C + c0, B);
     ld8p<DT>(k + 2 * C + c0, K3);
@@ -1029,17 +1022,14 @@ __global__ __launch_bounds__(NT) void bn_bwd_apply_dz2_u_kernel(const void* __re
     i32x4 dz[U], yv[U], y2v[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      dz[u] = ldnt<NTM & 1>(dzp + ix(i + u * stride));
-      yv[u] = ldnt<NTM & 1>(yp + ix(i + u * stride));
-      y2v[u] = ldnt<NTM & 1>(y2p + ix(i + u * stride));
+      dz[u] = ldnt<NTM & 1>(dzp + i + u * stride);
+      yv[u] = ldnt<NTM & 1>(yp + i + u * stride);
+      y2v[u] = ldnt<NTM & 1>(y2p + i + u * stride);
     }
 #pragma unroll
-    for (int u = 0; u < U; ++u) one(dz[u], yv[u], y2v[u], ix(i + u * stride));
+    for (int u = 0; u < U; ++u) one(dz[u], yv[u], y2v[u], i + u * stride);
   }
-  for (; i < n8; i += stride) {
-    const int j = ix(i);
-    one(dzp[j], yp[j], y2p[j], j);
-  }
+  for (; i < n8; i += stride) one(dzp[i], yp[i], y2p[i], i);
 }
 
 // bn_apply_kernel's 16-bit path with U chunks per trip (see bn_bwd_apply_dz_u_kernel).
@@ -1386,9 +1376,7 @@ int pda_bn_bwd_apply2(const void* dz, const void* y, const void* y2, const float
     u = 1;
     m = 0;
   }
-  const char* rv = pda_reverse_env();
-  const int rev = (rv && strstr(rv, "apply")) ? 1 : 0;
-#define KA dz, y, y2, k, dy, dy2, n8, C, rev
+#define KA dz, y, y2, k, dy, dy2, n8, C
   if (dt == DT_BF16) STREAM_DISPATCH_UM(bn_bwd_apply_dz2_u_kernel, DT_BF16, gs, st, u, m, KA);
   else STREAM_DISPATCH_UM(bn_bwd_apply_dz2_u_kernel, DT_F16, gs, st, u, m, KA);
 #undef KA
@@ -1403,9 +1391,7 @@ int pda_bn_bwd_apply(const BwdArgsC* c, const void* dz_in, const void* ysel, con
     const int n8 = (int)(a.rows * (a.C / 8));
     const int gs = dt != DT_F32 ? stream_grid(n8, a.C) : 0;
     if (gs > 0) {
-      const char* rv = pda_reverse_env();
-      const int rev = (rv && strstr(rv, "apply")) ? 1 : 0;
-#define KA (const void*)dz_in, (const void*)ysel, k1, k2, k3, (void*)dy, n8, a.C, rev
+#define KA (const void*)dz_in, (const void*)ysel, k1, k2, k3, (void*)dy, n8, a.C
       if (dt == DT_BF16) STREAM_DISPATCH(bn_bwd_apply_dz_u_kernel, DT_BF16, gs, st, KA);
       else STREAM_DISPATCH(bn_bwd_apply_dz_u_kernel, DT_F16, gs, st, KA);
 #undef KA

@@ -320,8 +320,7 @@ __global__ __launch_bounds__(conv_nt<STAGES>(), (PASS_T == WGRAD_BNA || PASS_T =
   const int t = (int)(p.rev ? xcd_remap_rev(blockIdx.x, ntile) : xcd_remap(blockIdx.x, ntile));
   const int tm = t / tiles_n, tn = t - tm * tiles_n;
   const int m0 = tm * BM, n0 = tn * BN;
-  // WGRAD: K split (p.rev: the last splits first); DGRAD: parity class
-  const int split = (PASS == WGRAD && p.rev) ? (int)gridDim.y - 1 - (int)blockIdx.y : (int)blockIdx.y;
+  const int split = blockIdx.y;  // WGRAD: K split; DGRAD: parity class
 
   // ---- K range --------------------------------------------------------------------
   int kbeg = 0, kend = p.K;
@@ -2148,7 +2147,6 @@ int pda_conv_wgrad_bna(const ConvDesc* d, const void* dz, const void* y, const f
   p.M = d->Cout; p.N = d->R * d->S * d->Cin;
   p.K = d->Nb * d->Ho * d->Wo;
   p.k_chunk = k_chunk;
-  { const char* rv = pda_reverse_env(); p.rev = (rv && strstr(rv, "bna")) ? 1 : 0; }
   const int abm = bm < 0 ? -bm : bm;
   const dim3 grid(((p.M + abm - 1) / abm) * ((p.N + bn - 1) / bn), splits);
 #define BNA_CASE(D, M_, N_, S_) \

@@ -462,10 +462,10 @@ def test_fork_tracking_is_bit_exact():
 
 
 def test_reversed_tile_walks_are_bit_exact(monkeypatch):
-    """PDA_REVERSE (csrc/common.h pda_reverse_env): launches that walk their tiles / items from the
-    end (Infinity-Cache reuse of what their producers wrote last; every reversible launch kind here)
-    -- only the order changes: logits and every gradient bit-identical to the forward walk, over
-    two steps (running statistics included)."""
+    """PDA_REVERSE (csrc/common.h pda_reverse_env): FWD_TAIL, DGRAD_BNF and the stem pool walk
+    their tiles from the end of each XCD chunk by default (Infinity-Cache reuse of what their
+    producers wrote last) -- only the order changes: logits and every gradient bit-identical to the
+    forward walk, over two steps (running statistics included)."""
     _, nm = _pair("resnet50", image=64)
     torch.manual_seed(17)
     x = torch.randn(32, 3, 64, 64, device=DEV)
@@ -474,7 +474,7 @@ def test_reversed_tile_walks_are_bit_exact(monkeypatch):
     crit = nm.make_criterion()
     buf0 = nm.flat_bufstore.detach().clone()
     res = {}
-    for mode in ("none", "fwd_tail+bnf+stem_pool+bna+apply"):
+    for mode in ("none", "fwd_tail+bnf+stem_pool"):
         monkeypatch.setenv("PDA_REVERSE", mode)
         with torch.no_grad():
             nm.flat_bufstore.copy_(buf0)
@@ -487,7 +487,7 @@ def test_reversed_tile_walks_are_bit_exact(monkeypatch):
             outs.append((out.detach().clone(), nm.flat_grad.detach().clone(),
                          nm.flat_bufstore.detach().clone()))
         res[mode] = outs
-    for a, b in zip(res["none"], res["fwd_tail+bnf+stem_pool+bna+apply"]):
+    for a, b in zip(res["none"], res["fwd_tail+bnf+stem_pool"]):
         assert all(torch.equal(u, v) for u, v in zip(a, b))
 
 
