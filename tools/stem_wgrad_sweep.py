@@ -24,8 +24,10 @@ def main():
     k = torch.randn(3 * 64, device=dev) * 0.1
     ws = K.Workspace(dev)
     out = torch.empty(64 * 256, device=dev)
-    targets = [((-64, 128), 1536), ((-64, 256), 512), ((-64, 256), 768), ((-64, 256), 1024),
-               ((-64, 256), 1536)]
+    # (round 6 also timed a double-buffered 64x256 build: 440-446 us at 512-1536 blocks vs
+    # 395-397 us single-stage -- not built; profiles/ab_r6.md section 14)
+    targets = [((-64, 256), 1024), ((-64, 128), 1536), ((-64, 256), 512), ((-64, 256), 768),
+               ((-64, 256), 1536), ((64, 128), 1024), ((64, 128), 2048)]
     res = {}
     for tb in targets:
         K.conv_wgrad(dz, x, g, out, ws, bna=(y, k), tile=tb[0], target_blocks=tb[1])
