@@ -268,6 +268,237 @@ __global__ __launch_bounds__(WT_NT, 1) void wgrad_tap_kernel(WtParams p_arg) {
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// The stem's weight gradient in the tap-reuse form (the stem conv = a 4x4 stride-1 conv with pad
+// 2 on the 2x2 space-to-depth image: 16 input channels, 64 output channels, 112 x 112), with the
+// stem BatchNorm's backward formed in LDS (dY = k1*dz + k2*y + k3, WGRAD_BNA's operand):
+//
+//   dW[co][r][s][ci] = sum over output pixels p of dY[p][co] * X[p + (r - 2, s - 2)][ci]
+//
+// Padded index space: output rows q = (n, oy, ox) over an Hp x Wp = (H + 3) x (W + 3) grid (real
+// outputs oy, ox < H, W; the rest are padding rows with dY = 0) and X rows q' = (n, yp, xp) with
+// X[q'] = x[n][yp - 2][xp - 2] (zero outside). Tap (r, s) is the constant FORWARD row shift
+// d = r Wp + s for every q (the forward halo is 3 Wp + 3 rows, none backward).
+//
+// Block = 512 threads (8 waves: wr = co half, wc = 4 taps = 64 of the 256 columns), one block per
+// CU, its padded-row range [q0, q0 + KB) in steps of 64 rows. LDS: X in a 1024-row ring of 32-B
+// rows (16 channels), dz and y in NS + 1 tile slots [64 rows][64 co] each; all by LDS-DMA, NS = 4
+// steps ahead. X rows sit in 16-row blocks at slot (j & 8) | ((j & 7) ^ 4 (j >> 3)): the transposed
+// fragment reads of a wave touch rows L .. L+3 and L+8 .. L+11 (32 B each) in one lane group, and
+// the slot map puts them in 8 distinct 32-B bank windows for any row offset L. dY of step s+1 is
+// formed in place in its dz slot during step s (its DMA has landed; nothing in step s reads it).
+constexpr int SW_RING = 1024;                      // X ring rows (power of two, 16-row blocks)
+constexpr int SW_XROW = 32;                        // 16 channels x 2 B
+constexpr int SW_XBYTES = SW_RING * SW_XROW;
+constexpr int SW_ATILE = 64 * 128;                 // dz / y tile [64 rows][64 co]
+constexpr int SW_COEF = 3 * 64 * 4;
+constexpr int SW_LDS = SW_XBYTES + 2 * (WT_NS + 1) * SW_ATILE + SW_COEF;
+
+struct SwParams {
+  const void* dz;      // [Nb, H, W, 64] 16-bit, the stem BN's masked gradient
+  const void* y;       // [Nb, H, W, 64] 16-bit, the BN input
+  const float* k;      // [3][64]: dY = k[0] dz + k[1] y + k[2]
+  const void* x;       // [Nb, H, W, 16] 16-bit (the space-to-depth image)
+  float* slab;         // [splits][64][16 taps x 16]
+  int Nb, H, W;
+  int Hp, Wp, Kp;
+  int kb, nsteps, fhalo;   // fhalo = 3 Wp + 3
+  FastDiv dHpWp, dWp;
+};
+
+__device__ __forceinline__ int sw_slot(int j) { return (j & 8) | ((j & 7) ^ ((j >> 3) << 2)); }
+// ring byte offset of X row r
+__device__ __forceinline__ int sw_xaddr(int r) {
+  const int rr = r & (SW_RING - 1);
+  return ((rr & ~15) + sw_slot(rr & 15)) * SW_XROW;
+}
+
+template <int DT>
+__global__ __launch_bounds__(WT_NT, 1) void wgrad_stem_tap_kernel(SwParams p_arg) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  typedef const __attribute__((address_space(4))) SwParams KP;
+  KP& p = *(KP*)__builtin_amdgcn_kernarg_segment_ptr();
+#else
+  const SwParams& p = p_arg;
+#endif
+  __shared__ __attribute__((aligned(16))) char smem[SW_LDS];
+  char* xr = smem;
+  char* tz = smem + SW_XBYTES;                               // dz slots (dY after the transform)
+  char* ty = tz + (WT_NS + 1) * SW_ATILE;                   // y slots
+  float* coef = reinterpret_cast<float*>(ty + (WT_NS + 1) * SW_ATILE);   // [3][64]
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = wid & 1, wc = wid >> 1;
+  const int split = (int)xcd_remap(blockIdx.x, gridDim.x);
+  const FastDiv dHpWp = p.dHpWp, dWp = p.dWp;
+  const int Kp = p.Kp, H = p.H, W = p.W;
+  // padded output row q -> byte offset of its 64-channel pixel (+ c elems), OOB for padding rows
+  auto out_pix = [&](int q, int c_elems) __attribute__((always_inline)) -> uint32_t {
+    if (q < 0 || q >= Kp) return WT_OOB;
+    const uint32_t n = fdiv((uint32_t)q, dHpWp), rem = (uint32_t)q - n * dHpWp.d;
+    const uint32_t oy = fdiv(rem, dWp), ox = rem - oy * dWp.d;
+    if (oy >= (uint32_t)H || ox >= (uint32_t)W) return WT_OOB;
+    return ((((n * H + oy) * W + ox) * 64u) + (uint32_t)c_elems) * 2u;
+  };
+  // padded X row q' -> byte offset of its 16-channel pixel (+ c elems), OOB outside the image
+  auto x_pix = [&](int q, int c_elems) __attribute__((always_inline)) -> uint32_t {
+    if (q < 0 || q >= Kp) return WT_OOB;
+    const uint32_t n = fdiv((uint32_t)q, dHpWp), rem = (uint32_t)q - n * dHpWp.d;
+    const uint32_t yp = fdiv(rem, dWp), xp = rem - yp * dWp.d;
+    if (yp < 2 || yp >= (uint32_t)H + 2 || xp < 2 || xp >= (uint32_t)W + 2) return WT_OOB;
+    return ((((n * H + yp - 2) * W + xp - 2) * 16u) + (uint32_t)c_elems) * 2u;
+  };
+  const int q0 = split * p.kb;
+  const int q_end = min(q0 + p.kb, Kp);
+  const int ns = p.nsteps;
+  const uint32_t npix = (uint32_t)p.Nb * p.H * p.W;
+  const __amdgpu_buffer_rsrc_t rdz = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<void*>(p.dz), (short)0, (int)(npix * 128u), 0x00020000);
+  const __amdgpu_buffer_rsrc_t ry = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<void*>(p.y), (short)0, (int)(npix * 128u), 0x00020000);
+  const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<void*>(p.x), (short)0, (int)(npix * 32u), 0x00020000);
+
+  // X rows: step s reads [q0 + 64 s, q0 + 64 s + 64 + fhalo); pieces of 32 rows from the
+  // 32-aligned base b0; fr(s) = first row not needed by steps <= s (32-aligned)
+  const int b0 = q0 & ~31;
+  auto fr = [&](int s) { return (q0 + 64 * (s + 1) + p.fhalo + 31) & ~31; };
+  // one 32-row X piece at row r (32-aligned): lane -> slot lane/2 of the piece, channel half lane&1
+  auto x_piece = [&](int r, bool live) __attribute__((always_inline)) {
+    const int b = lane >> 5, sl = (lane >> 1) & 15;
+    const int row = r + 16 * b + sw_slot(sl);            // (sw_slot is an involution)
+    wt_dma16(rx, xr + (r & (SW_RING - 1)) * SW_XROW, live ? x_pix(row, (lane & 1) * 8) : WT_OOB);
+  };
+  // the dz / y tiles of step s, piece w: rows q0 + 64 s + 8 w + lane/8 (rows past the range: zero)
+  const int lrow = lane >> 3, lch = lane & 7;
+  auto a_pieces = [&](int s, int w) __attribute__((always_inline)) {
+    const int rl = 8 * w + lrow;
+    const int q = q0 + 64 * s + rl;
+    const int lc = lch ^ wt_swz(rl);
+    const uint32_t off = q < q_end ? out_pix(q, lc * 8) : WT_OOB;
+    const int slot = (s % (WT_NS + 1)) * SW_ATILE + 8 * w * 128;
+    wt_dma16(rdz, tz + slot, off);
+    wt_dma16(ry, ty + slot, off);
+  };
+  // per step: waves 0, 1 add the step's two X pieces (3 DMAs), every wave its dz + y pieces (2)
+  const bool xw = wid < 2;
+  // prologue: steps 0 .. NS-1 in order (step 0 also carries X rows [b0, fr(0)))
+  for (int r = b0 + 32 * wid; r < fr(0); r += 256) x_piece(r, true);
+  a_pieces(0, wid);
+#pragma unroll
+  for (int s = 1; s < WT_NS; ++s) {
+    if (xw) x_piece(fr(s - 1) + 32 * wid, s < ns);
+    a_pieces(s, wid);
+  }
+  if (tid < 192) coef[tid] = p.k[tid];
+  // dY = k1 dz + k2 y + k3 in place of step s's dz slot: one 16-B chunk per thread; padding and
+  // out-of-range rows stay 0
+  auto form_dy = [&](int s) __attribute__((always_inline)) {
+    const int rl = tid >> 3, pc = tid & 7;
+    const int lc = pc ^ wt_swz(rl);
+    const int q = q0 + 64 * s + rl;
+    const bool ok = q < q_end && out_pix(q, 0) != WT_OOB;
+    const int off = (s % (WT_NS + 1)) * SW_ATILE + rl * 128 + pc * 16;
+    i32x4* zp = reinterpret_cast<i32x4*>(tz + off);
+    const i32x4 z = *zp, yv = *reinterpret_cast<const i32x4*>(ty + off);
+    i32x4 o;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const f32x2 k1 = *reinterpret_cast<const f32x2*>(coef + lc * 8 + 2 * k);
+      const f32x2 k2 = *reinterpret_cast<const f32x2*>(coef + 64 + lc * 8 + 2 * k);
+      const f32x2 k3 = *reinterpret_cast<const f32x2*>(coef + 128 + lc * 8 + 2 * k);
+      const f32x2 d = unpack2<DT>((uint32_t)z[k]), u = unpack2<DT>((uint32_t)yv[k]);
+      const f32x2 f = f32x2{__builtin_fmaf(k1.x, d.x, __builtin_fmaf(k2.x, u.x, k3.x)),
+                            __builtin_fmaf(k1.y, d.y, __builtin_fmaf(k2.y, u.y, k3.y))};
+      o[k] = ok ? (int)pack2<DT>(f) : 0;
+    }
+    *zp = o;
+  };
+  // step 0's operands: landed (every wave's step-0 group), formed before the loop's first barrier
+  if (xw) wt_vm_wait<3 * (WT_NS - 1)>(); else wt_vm_wait<2 * (WT_NS - 1)>();
+  __syncthreads();
+  form_dy(0);
+
+  f32x4 acc[2][4];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int g = lane >> 4, fi = lane & 15, fq = fi >> 2, fp = fi & 3;
+  const int L0 = 8 * g + fq;
+  const int half = (fp & 1) << 3;
+  // X fragment addresses at s = s2 = 0 for the wave's 4 taps (t = 4 wc + j: shift r Wp + s), rows
+  // L0 / L0 + 4; a 32-row substep / 64-row step advances them by 1 / 2 KiB (32 = 0 mod 16 keeps
+  // the slot map), wrapped at the ring
+  int xa[4][2];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int t = 4 * wc + j;
+    const int dsh = (t >> 2) * p.Wp + (t & 3);
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+      xa[j][h] = sw_xaddr(q0 + dsh + L0 + 4 * h) + ((fp >> 1) << 4) + half;
+  }
+  int aa[2][2][2];   // dY tile: byte offset of substep s2, co tile i, row L0 / L0 + 4
+#pragma unroll
+  for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int k = s2 * 32 + L0 + 4 * h;
+        const int chunk = (wr * 32 + 16 * i) / 8 + (fp >> 1);
+        aa[s2][i][h] = k * 128 + ((chunk ^ wt_swz(k)) << 4) + half;
+      }
+
+  for (int s = 0; s < ns; ++s) {
+    // steps s and s+1 have landed (s+1 is formed now)
+    if (xw) wt_vm_wait<3 * (WT_NS - 2)>(); else wt_vm_wait<2 * (WT_NS - 2)>();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    // the operands of step s + NS (past the range: out-of-bounds no-ops -- the per-step count
+    // stays fixed); their slots were last read in step s - 1
+    if (xw) x_piece(fr(s + WT_NS - 1) + 32 * wid, s + WT_NS < ns);
+    a_pieces(s + WT_NS, wid);
+    if (s + 1 < ns) form_dy(s + 1);
+    const char* sa = tz + (s % (WT_NS + 1)) * SW_ATILE;
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2) {
+      s16x8 fa[2], fb[4];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const s16x4 v0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(s16x4, sa + aa[s2][i][0]));
+        const s16x4 v1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(s16x4, sa + aa[s2][i][1]));
+        fa[i] = s16x8{v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
+      }
+      const int roff = (64 * s + 32 * s2) * SW_XROW;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int a0 = (xa[j][0] + roff) & (SW_XBYTES - 1);
+        const int a1 = (xa[j][1] + roff) & (SW_XBYTES - 1);
+        const s16x4 v0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(s16x4, xr + a0));
+        const s16x4 v1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(s16x4, xr + a1));
+        fb[j] = s16x8{v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
+      }
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = mfma16<DT>(fb[j], fa[i], acc[i][j]);
+    }
+  }
+  wt_vm_wait<0>();   // the trailing no-op DMAs, before the block can exit
+
+  // slab[split][co][t * 16 + ci]: lane = co row (lane & 15) of tile i, 4 consecutive channels
+  float* out = p.slab + (size_t)split * 64 * 256;
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int co = wr * 32 + 16 * i + fi;
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      *reinterpret_cast<f32x4*>(out + (size_t)co * 256 + (4 * wc + j) * 16 + 4 * g) = acc[i][j];
+  }
+}
+
 FastDiv wt_div(uint32_t d) {
   FastDiv f;
   f.d = d;
@@ -318,5 +549,32 @@ int pda_wgrad_tap(const void* dy, const void* x, float* slab, const float* pro_s
   }
   return (int)hipGetLastError();
 }
+
+// The stem's weight-gradient slabs in the tap-reuse form (wgrad_stem_tap_kernel): slab
+// [splits][64][16 taps x 16] (f32), summed by pda_wgrad_reduce as the generic kernel's. dz, y
+// [Nb,H,W,64], x [Nb,H,W,16] 16-bit, k [3][64]. kb: padded rows per split (multiple of 64);
+// splits = ceil(Nb (H+3)(W+3) / kb). W + 3 <= 122 (the X ring holds 4 steps + the forward halo).
+int pda_wgrad_stem_tap(const void* dz, const void* y, const float* k, const void* x, float* slab,
+                       int Nb, int H, int W, int kb, int splits, int dt, hipStream_t st) {
+  if (kb <= 0 || (kb % 64) || H <= 0 || W <= 0 || W + 3 > 122 || !dz || !y || !k || !x || !slab)
+    return -2;
+  SwParams p{};
+  p.dz = dz; p.y = y; p.k = k; p.x = x; p.slab = slab;
+  p.Nb = Nb; p.H = H; p.W = W;
+  p.Hp = H + 3; p.Wp = W + 3;
+  const long long kp = (long long)Nb * p.Hp * p.Wp;
+  if (kp >= (1ll << 30) || (long long)Nb * H * W * 128 >= 0x7fffffffll) return -4;
+  p.Kp = (int)kp;
+  p.kb = kb; p.nsteps = kb / 64; p.fhalo = 3 * p.Wp + 3;
+  if ((long long)splits * kb < kp || (long long)(splits - 1) * kb >= kp) return -3;
+  p.dHpWp = wt_div((uint32_t)(p.Hp * p.Wp));
+  p.dWp = wt_div((uint32_t)p.Wp);
+  const dim3 grid(splits);
+  if (dt == DT_BF16) TRACKED_LAUNCH((wgrad_stem_tap_kernel<DT_BF16>), grid, dim3(WT_NT), 0, st, p);
+  else if (dt == DT_F16) TRACKED_LAUNCH((wgrad_stem_tap_kernel<DT_F16>), grid, dim3(WT_NT), 0, st, p);
+  else return -1;
+  return (int)hipGetLastError();
+}
+
 
 }  // extern "C"

@@ -87,6 +87,7 @@ _SIGS = {
                            _I, _V],
     "pda_bn_fold": [_V, _V, _I, _I, _V, _V, _I, _V],
     "pda_wgrad_tap": [_V, _V, _V, _V, _V, _I, _I, _I, _I, _I, _I, _I, _I, _V],
+    "pda_wgrad_stem_tap": [_V, _V, _V, _V, _V, _I, _I, _I, _I, _I, _I, _V],
     "pda_stem_fwd": [_V, _V, _V, _V, _I, _I, _I, _I, _I, _V],
     "pda_conv_wgrad": [C.POINTER(ConvDesc), _V, _V, _V, _I, _I, _V, _V, _I, _I, _I, _V],
     "pda_conv_wgrad_bna": [C.POINTER(ConvDesc), _V, _V, _V, _V, _V, _V, _V, _I, _I, _V, _V, _I, _I, _I,

@@ -680,6 +680,9 @@ def conv_wgrad(dy: torch.Tensor, x: torch.Tensor, g: ConvGeom, grad: torch.Tenso
     if (tile is None and target_blocks is None and bna is None and combine is None
             and cin_real is None and wgrad_tap_ok(g, dy.dtype)):
         return conv_wgrad_tap(dy, x, g, grad, ws, scale, accumulate, pro)
+    if (tile is None and target_blocks is None and bna is not None and combine is None
+            and cin_real is None and pro is None and stem_wgrad_tap_ok(g, dy.dtype)):
+        return conv_wgrad_stem_tap(dy, bna[0], bna[1], x, g, grad, ws, scale, accumulate)
     bm, bn, splits, k_chunk = wgrad_plan(g, Nb, tile, target_blocks, f32=dy.dtype == torch.float32,
                                          dma=dy.dtype != torch.float32 and pro is None and bna is None,
                                          wscale=wscale, bna=bna is not None)
@@ -771,6 +774,48 @@ def conv_wgrad_tap(dy: torch.Tensor, x: torch.Tensor, g: ConvGeom, grad: torch.T
         return grad
     check(L.pda_wgrad_reduce(ptr(slab), ptr(grad), splits, M, N, int(math.log2(g.Cin)), g.Cin, N,
                              float(scale), int(accumulate), None, None, None, st), "wgrad_reduce")
+    return grad
+
+
+# the stem's weight gradient (WGRAD_BNA operand) on the tap-reuse kernel (csrc/wgrad_tap.hip
+# wgrad_stem_tap_kernel); PDA_STEM_WGRAD=generic: the implicit-GEMM WGRAD_BNA tile. Blocks = splits
+# (one 113 KiB block per CU)
+_STEM_WGRAD = os.environ.get("PDA_STEM_WGRAD", "tap")
+_STEM_TAP_BLOCKS = int(os.environ.get("PDA_STEM_TAP_BLOCKS", "512"))
+
+
+def stem_wgrad_tap_ok(g: ConvGeom, dtype: torch.dtype) -> bool:
+    """The space-to-depth stem conv (4x4, stride 1, pad 2, 16 -> 64 channels, same-size output) in
+    16 bit, with the tap-reuse stem kernel built."""
+    return (_STEM_WGRAD == "tap" and dtype in (torch.bfloat16, torch.float16) and g.R == 4
+            and g.S == 4 and g.stride == 1 and g.pad == 2 and g.Cin == 16 and g.Cout == 64
+            and g.Ho == g.H and g.Wo == g.W and g.W + 3 <= 122
+            and getattr(ext.lib(), "pda_wgrad_stem_tap", None) is not None)
+
+
+def conv_wgrad_stem_tap(dz: torch.Tensor, y: torch.Tensor, k: torch.Tensor, x: torch.Tensor,
+                        g: ConvGeom, grad: torch.Tensor, ws: "Workspace", scale: float = 1.0,
+                        accumulate: bool = False, blocks: Optional[int] = None) -> torch.Tensor:
+    """grad (f32 [64][16 taps x 16]) = scale * dW of the stem conv with dY = k1*dz + k2*y + k3
+    formed in LDS (:func:`conv_wgrad` ``bna``): each block loads its pixel range of dz, y and the
+    input once for all 16 taps; split-K slabs reduced by the same fixed-order launch."""
+    Nb = dz.shape[0]
+    kp = Nb * (g.H + 3) * (g.W + 3)
+    nb = blocks or _STEM_TAP_BLOCKS
+    kb = max(64, math.ceil(kp / nb / 64) * 64)
+    splits = math.ceil(kp / kb)
+    M, N = 64, 256
+    rb = ws.reduce_batch
+    slab = rb.slab(splits * M * N) if rb is not None else ws.get("wgrad_slab", splits * M * N)
+    st = stream(dz.device)
+    L = ext.lib()
+    check(L.pda_wgrad_stem_tap(ptr(dz), ptr(y), ptr(k), ptr(x), ptr(slab), Nb, g.H, g.W, kb, splits,
+                               _kdt(dz), st), "wgrad_stem_tap")
+    if rb is not None:
+        rb.add(slab, grad, splits, M, N, 4, 16, N, scale, accumulate)
+        return grad
+    check(L.pda_wgrad_reduce(ptr(slab), ptr(grad), splits, M, N, 4, 16, N, float(scale),
+                             int(accumulate), None, None, None, st), "wgrad_reduce")
     return grad
 
 

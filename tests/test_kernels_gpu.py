@@ -1065,6 +1065,46 @@ def test_conv_fwd_tail_matches_apply_then_conv(geo, mode, dtype):
 
 
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("Nb,H", [(2, 11), (3, 20), (2, 112)])
+def test_wgrad_stem_tap_matches_fp32_and_bna(Nb, H, dtype):
+    """csrc/wgrad_tap.hip wgrad_stem_tap_kernel: the stem's weight gradient (4x4 / stride 1 / pad
+    2 on the 16-channel space-to-depth image, output cropped to H x H) with dY = k1*dz + k2*y + k3
+    formed in LDS, all 16 taps per block, against the fp32 reference of the same dY and against the
+    implicit-GEMM WGRAD_BNA tile; several split counts (ragged last split); deterministic."""
+    K = _k()
+    torch.manual_seed(Nb * H)
+    g = K.stem_s2d_geom(Nb, 2 * H)
+    if not K.stem_wgrad_tap_ok(g, dtype):
+        pytest.skip("stem tap kernel not selected")
+    x = torch.randn(Nb, H, H, 16, device=DEV).to(dtype)
+    dz = torch.randn(Nb, H, H, 64, device=DEV).to(dtype)
+    y = (torch.randn(Nb, H, H, 64, device=DEV) * 2 + 1).to(dtype)
+    kk = torch.randn(3 * 64, device=DEV)
+    dy = (kk[:64].double() * dz.double() + (kk[64:128].double() * y.double()
+                                            + kk[128:].double()).float().double()).float().to(dtype)
+    dyp = torch.zeros(Nb, 64, H + 1, H + 1, device=DEV)
+    dyp[:, :, :H, :H] = dy.float().permute(0, 3, 1, 2)
+    ref = torch.nn.grad.conv2d_weight(x.float().permute(0, 3, 1, 2), (64, 16, 4, 4), dyp, padding=2)
+    ref = ref.permute(0, 2, 3, 1).contiguous()          # OHWI
+    ws = K.Workspace(torch.device(DEV))
+    gen = torch.zeros(64 * 256, device=DEV)
+    K.conv_wgrad(dz, x, g, gen, ws, bna=(y, kk), tile=(-64, 256))   # the generic WGRAD_BNA tile
+    outs = []
+    for blocks in (5, 64, 512):
+        gw = torch.full((64 * 256,), float("nan"), device=DEV)
+        K.conv_wgrad_stem_tap(dz, y, kk, x, g, gw, ws, blocks=blocks)
+        outs.append(gw.clone())
+    again = torch.full_like(outs[-1], float("nan"))
+    K.conv_wgrad(dz, x, g, again, ws, bna=(y, kk))          # the dispatch picks the tap kernel
+    torch.cuda.synchronize()
+    e_gen = rel_err(gen.view_as(ref), ref)
+    for o in outs:
+        e = rel_err(o.view_as(ref), ref)
+        assert e < 2 * e_gen + 1e-5, (e, e_gen)
+    assert torch.equal(again, outs[-1])
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
 @pytest.mark.parametrize("geo", [(2, 56, 64, 64, False), (2, 56, 64, 64, True), (3, 28, 128, 128, False),
                                  (2, 28, 64, 128, True), (3, 14, 256, 256, False), (5, 7, 128, 64, True)])
 def test_wgrad_tap_matches_fp32_and_generic(geo, dtype):

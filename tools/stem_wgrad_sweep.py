@@ -26,11 +26,20 @@ def main():
     out = torch.empty(64 * 256, device=dev)
     # (round 6 also timed a double-buffered 64x256 build: 440-446 us at 512-1536 blocks vs
     # 395-397 us single-stage -- not built; profiles/ab_r6.md section 14)
+    # (("tap", n): the tap-reuse stem kernel with n blocks, csrc/wgrad_tap.hip)
     targets = [((-64, 256), 1024), ((-64, 128), 1536), ((-64, 256), 512), ((-64, 256), 768),
-               ((-64, 256), 1536), ((64, 128), 1024), ((64, 128), 2048)]
+               ((64, 128), 1024)]
+    if K.stem_wgrad_tap_ok(g, torch.bfloat16):
+        targets += [("tap", 256), ("tap", 384), ("tap", 512), ("tap", 768), ("tap", 1024)]
+
+    def run(tb):
+        if tb[0] == "tap":
+            K.conv_wgrad_stem_tap(dz, y, k, x, g, out, ws, blocks=tb[1])
+        else:
+            K.conv_wgrad(dz, x, g, out, ws, bna=(y, k), tile=tb[0], target_blocks=tb[1])
     res = {}
     for tb in targets:
-        K.conv_wgrad(dz, x, g, out, ws, bna=(y, k), tile=tb[0], target_blocks=tb[1])
+        run(tb)
         torch.cuda.synchronize()
         res[tb] = out.clone()
     ref = res[targets[0]]
@@ -40,14 +49,14 @@ def main():
         for tb in targets:
             st.record()
             for _ in range(3):
-                K.conv_wgrad(dz, x, g, out, ws, bna=(y, k), tile=tb[0], target_blocks=tb[1])
+                run(tb)
             en.record()
             en.synchronize()
             times[tb].append(st.elapsed_time(en) / 3 * 1e3)
     for tb in targets:
-        plan = K.wgrad_plan(g, B, tile=tb[0], target_blocks=tb[1])
+        plan = "-" if tb[0] == "tap" else K.wgrad_plan(g, B, tile=tb[0], target_blocks=tb[1])
         err = ((res[tb] - ref).norm() / ref.norm()).item()
-        print(f"tile {tb[0]} target {tb[1]:5d} plan {plan}: {statistics.median(times[tb]):8.1f} us  "
+        print(f"tile {str(tb[0]):>10} target {tb[1]:5d} plan {plan}: {statistics.median(times[tb]):8.1f} us  "
               f"rel diff vs the first: {err:.2e}")
 
 
