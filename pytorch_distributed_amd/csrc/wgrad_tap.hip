@@ -51,9 +51,25 @@ struct WtParams {
   FastDiv dHpWp, dWp;
 };
 
-__device__ __forceinline__ void wt_dma16(__amdgpu_buffer_rsrc_t r, char* lds, uint32_t voff) {
-  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)lds, 16,
-                                           (int)voff, 0, 0, 0);
+// Buffer descriptor (base, num_records bytes; out-of-range offsets read 0) in SGPRs.
+typedef int wt_rsrc_t __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ wt_rsrc_t wt_rsrc(const void* base, uint32_t bytes) {
+  const uint64_t b = (uint64_t)(uintptr_t)base;
+  return wt_rsrc_t{(int)(uint32_t)b, (int)(uint32_t)(b >> 32), (int)bytes, 0x00020000};
+}
+// One 16-B-per-lane LDS-DMA (64 lanes -> 1 KiB at lds, lane-linear), written in asm: the
+// builtin's DMA is tracked by hipcc as a pending LDS store, and in these loops (a BN prologue or
+// a second operand stream beside it) hipcc then waits vmcnt(0) before the first transposed read
+// of every step -- which drains the whole NS-step pipeline each step. The asm DMA is invisible to
+// that bookkeeping; the kernels count their DMAs themselves (wt_vm_wait). M0 is saved/restored
+// in the statement (compiler-reserved); s_nop 4: the descriptor may come fresh from a VALU.
+__device__ __forceinline__ void wt_dma16(wt_rsrc_t r, char* lds, uint32_t voff) {
+  const uint32_t l = __builtin_amdgcn_readfirstlane(
+      (uint32_t)(uintptr_t)(__attribute__((address_space(3))) char*)lds);
+  uint32_t keep;
+  asm volatile("s_nop 4\n\ts_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\t"
+               "buffer_load_dwordx4 %1, %2, 0 offen lds\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep) : "v"(voff), "s"(r), "s"(l) : "memory");
 }
 template <int N> __device__ __forceinline__ void wt_vm_wait() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
@@ -98,10 +114,8 @@ __global__ __launch_bounds__(WT_NT, 1) void wgrad_tap_kernel(WtParams p_arg) {
   const int q0 = split * p.kb;
   const int q_end = min(q0 + p.kb, p.Kp);
   const int ns = p.nsteps;
-  const __amdgpu_buffer_rsrc_t rdy = __builtin_amdgcn_make_buffer_rsrc(
-      const_cast<void*>(p.dy), (short)0, (int)((uint32_t)p.Nb * p.H * p.W * p.Cout * 2u), 0x00020000);
-  const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc(
-      const_cast<void*>(p.x), (short)0, (int)((uint32_t)p.Nb * p.H * p.W * p.Cin * 2u), 0x00020000);
+  const wt_rsrc_t rdy = wt_rsrc(p.dy, (int)((uint32_t)p.Nb * p.H * p.W * p.Cout * 2u));
+  const wt_rsrc_t rx = wt_rsrc(p.x, (int)((uint32_t)p.Nb * p.H * p.W * p.Cin * 2u));
 
   // X rows: step s reads [q0 + 64 s - halo, q0 + 64 s + 64 + halo); rows are issued in 8-row
   // pieces from the 8-aligned base b0; fr(s) = first row not needed by steps <= s (8-aligned)
@@ -287,12 +301,16 @@ __global__ __launch_bounds__(WT_NT, 1) void wgrad_tap_kernel(WtParams p_arg) {
 // fragment reads of a wave touch rows L .. L+3 and L+8 .. L+11 (32 B each) in one lane group, and
 // the slot map puts them in 8 distinct 32-B bank windows for any row offset L. dY of step s+1 is
 // formed in place in its dz slot during step s (its DMA has landed; nothing in step s reads it).
+#ifndef PDA_SW_NS
+#define PDA_SW_NS 4
+#endif
+constexpr int SW_NS = PDA_SW_NS;                  // steps in flight
 constexpr int SW_RING = 1024;                      // X ring rows (power of two, 16-row blocks)
 constexpr int SW_XROW = 32;                        // 16 channels x 2 B
 constexpr int SW_XBYTES = SW_RING * SW_XROW;
 constexpr int SW_ATILE = 64 * 128;                 // dz / y tile [64 rows][64 co]
 constexpr int SW_COEF = 3 * 64 * 4;
-constexpr int SW_LDS = SW_XBYTES + 2 * (WT_NS + 1) * SW_ATILE + SW_COEF;
+constexpr int SW_LDS = SW_XBYTES + 2 * (SW_NS + 1) * SW_ATILE + SW_COEF;
 
 struct SwParams {
   const void* dz;      // [Nb, H, W, 64] 16-bit, the stem BN's masked gradient
@@ -324,8 +342,8 @@ __global__ __launch_bounds__(WT_NT, 1) void wgrad_stem_tap_kernel(SwParams p_arg
   __shared__ __attribute__((aligned(16))) char smem[SW_LDS];
   char* xr = smem;
   char* tz = smem + SW_XBYTES;                               // dz slots (dY after the transform)
-  char* ty = tz + (WT_NS + 1) * SW_ATILE;                   // y slots
-  float* coef = reinterpret_cast<float*>(ty + (WT_NS + 1) * SW_ATILE);   // [3][64]
+  char* ty = tz + (SW_NS + 1) * SW_ATILE;                   // y slots
+  float* coef = reinterpret_cast<float*>(ty + (SW_NS + 1) * SW_ATILE);   // [3][64]
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wr = wid & 1, wc = wid >> 1;
@@ -352,12 +370,9 @@ __global__ __launch_bounds__(WT_NT, 1) void wgrad_stem_tap_kernel(SwParams p_arg
   const int q_end = min(q0 + p.kb, Kp);
   const int ns = p.nsteps;
   const uint32_t npix = (uint32_t)p.Nb * p.H * p.W;
-  const __amdgpu_buffer_rsrc_t rdz = __builtin_amdgcn_make_buffer_rsrc(
-      const_cast<void*>(p.dz), (short)0, (int)(npix * 128u), 0x00020000);
-  const __amdgpu_buffer_rsrc_t ry = __builtin_amdgcn_make_buffer_rsrc(
-      const_cast<void*>(p.y), (short)0, (int)(npix * 128u), 0x00020000);
-  const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc(
-      const_cast<void*>(p.x), (short)0, (int)(npix * 32u), 0x00020000);
+  const wt_rsrc_t rdz = wt_rsrc(p.dz, (int)(npix * 128u));
+  const wt_rsrc_t ry = wt_rsrc(p.y, (int)(npix * 128u));
+  const wt_rsrc_t rx = wt_rsrc(p.x, (int)(npix * 32u));
 
   // X rows: step s reads [q0 + 64 s, q0 + 64 s + 64 + fhalo); pieces of 32 rows from the
   // 32-aligned base b0; fr(s) = first row not needed by steps <= s (32-aligned)
@@ -376,7 +391,7 @@ __global__ __launch_bounds__(WT_NT, 1) void wgrad_stem_tap_kernel(SwParams p_arg
     const int q = q0 + 64 * s + rl;
     const int lc = lch ^ wt_swz(rl);
     const uint32_t off = q < q_end ? out_pix(q, lc * 8) : WT_OOB;
-    const int slot = (s % (WT_NS + 1)) * SW_ATILE + 8 * w * 128;
+    const int slot = (s % (SW_NS + 1)) * SW_ATILE + 8 * w * 128;
     wt_dma16(rdz, tz + slot, off);
     wt_dma16(ry, ty + slot, off);
   };
@@ -386,7 +401,7 @@ __global__ __launch_bounds__(WT_NT, 1) void wgrad_stem_tap_kernel(SwParams p_arg
   for (int r = b0 + 32 * wid; r < fr(0); r += 256) x_piece(r, true);
   a_pieces(0, wid);
 #pragma unroll
-  for (int s = 1; s < WT_NS; ++s) {
+  for (int s = 1; s < SW_NS; ++s) {
     if (xw) x_piece(fr(s - 1) + 32 * wid, s < ns);
     a_pieces(s, wid);
   }
@@ -398,7 +413,7 @@ __global__ __launch_bounds__(WT_NT, 1) void wgrad_stem_tap_kernel(SwParams p_arg
     const int lc = pc ^ wt_swz(rl);
     const int q = q0 + 64 * s + rl;
     const bool ok = q < q_end && out_pix(q, 0) != WT_OOB;
-    const int off = (s % (WT_NS + 1)) * SW_ATILE + rl * 128 + pc * 16;
+    const int off = (s % (SW_NS + 1)) * SW_ATILE + rl * 128 + pc * 16;
     i32x4* zp = reinterpret_cast<i32x4*>(tz + off);
     const i32x4 z = *zp, yv = *reinterpret_cast<const i32x4*>(ty + off);
     i32x4 o;
@@ -415,7 +430,7 @@ __global__ __launch_bounds__(WT_NT, 1) void wgrad_stem_tap_kernel(SwParams p_arg
     *zp = o;
   };
   // step 0's operands: landed (every wave's step-0 group), formed before the loop's first barrier
-  if (xw) wt_vm_wait<3 * (WT_NS - 1)>(); else wt_vm_wait<2 * (WT_NS - 1)>();
+  if (xw) wt_vm_wait<3 * (SW_NS - 1)>(); else wt_vm_wait<2 * (SW_NS - 1)>();
   __syncthreads();
   form_dy(0);
 
@@ -453,15 +468,15 @@ __global__ __launch_bounds__(WT_NT, 1) void wgrad_stem_tap_kernel(SwParams p_arg
 
   for (int s = 0; s < ns; ++s) {
     // steps s and s+1 have landed (s+1 is formed now)
-    if (xw) wt_vm_wait<3 * (WT_NS - 2)>(); else wt_vm_wait<2 * (WT_NS - 2)>();
+    if (xw) wt_vm_wait<3 * (SW_NS - 2)>(); else wt_vm_wait<2 * (SW_NS - 2)>();
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     // the operands of step s + NS (past the range: out-of-bounds no-ops -- the per-step count
     // stays fixed); their slots were last read in step s - 1
-    if (xw) x_piece(fr(s + WT_NS - 1) + 32 * wid, s + WT_NS < ns);
-    a_pieces(s + WT_NS, wid);
+    if (xw) x_piece(fr(s + SW_NS - 1) + 32 * wid, s + SW_NS < ns);
+    a_pieces(s + SW_NS, wid);
     if (s + 1 < ns) form_dy(s + 1);
-    const char* sa = tz + (s % (WT_NS + 1)) * SW_ATILE;
+    const char* sa = tz + (s % (SW_NS + 1)) * SW_ATILE;
 #pragma unroll
     for (int s2 = 0; s2 < 2; ++s2) {
       s16x8 fa[2], fb[4];
