@@ -14,6 +14,28 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef double f64x2 __attribute__((ext_vector_type(2)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef int i32x4 __attribute__((ext_vector_type(4)));
+
+// LDS-DMA (buffer_load_dwordx4 ... lds): buffer descriptor (base, num_records bytes; offsets past
+// it read 0) in SGPRs, and one 16-B-per-lane piece (64 lanes -> 1 KiB at lds, lane-linear; lds
+// wave-uniform: it becomes M0). Written in asm: hipcc tracks the builtin's DMA as a pending LDS
+// store and, in loops with transposed (ds_read_b64_tr_b16) reads, waits vmcnt(0) before the first
+// such read of every step -- draining every tile the loop keeps in flight. The asm DMA is invisible
+// to that bookkeeping; the kernels count their DMAs themselves (counted s_waitcnt vmcnt). M0 is
+// compiler-reserved: saved and restored in the statement. s_nop 4: the descriptor may come fresh
+// from a VALU (readfirstlane).
+typedef int dma_rsrc_t __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ dma_rsrc_t dma_rsrc(const void* base, uint32_t bytes) {
+  const uint64_t b = (uint64_t)(uintptr_t)base;
+  return dma_rsrc_t{(int)(uint32_t)b, (int)(uint32_t)(b >> 32), (int)bytes, 0x00020000};
+}
+__device__ __forceinline__ void dma16_asm(dma_rsrc_t r, char* lds, uint32_t voff) {
+  const uint32_t l = __builtin_amdgcn_readfirstlane(
+      (uint32_t)(uintptr_t)(__attribute__((address_space(3))) char*)lds);
+  uint32_t keep;
+  asm volatile("s_nop 4\n\ts_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\t"
+               "buffer_load_dwordx4 %1, %2, 0 offen lds\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep) : "v"(voff), "s"(r), "s"(l) : "memory");
+}
 typedef unsigned short u16;
 
 #define LDS_PTR(T, p) ((__attribute__((address_space(3))) T*)(p))

@@ -51,26 +51,9 @@ struct WtParams {
   FastDiv dHpWp, dWp;
 };
 
-// Buffer descriptor (base, num_records bytes; out-of-range offsets read 0) in SGPRs.
-typedef int wt_rsrc_t __attribute__((ext_vector_type(4)));
-__device__ __forceinline__ wt_rsrc_t wt_rsrc(const void* base, uint32_t bytes) {
-  const uint64_t b = (uint64_t)(uintptr_t)base;
-  return wt_rsrc_t{(int)(uint32_t)b, (int)(uint32_t)(b >> 32), (int)bytes, 0x00020000};
-}
-// One 16-B-per-lane LDS-DMA (64 lanes -> 1 KiB at lds, lane-linear), written in asm: the
-// builtin's DMA is tracked by hipcc as a pending LDS store, and in these loops (a BN prologue or
-// a second operand stream beside it) hipcc then waits vmcnt(0) before the first transposed read
-// of every step -- which drains the whole NS-step pipeline each step. The asm DMA is invisible to
-// that bookkeeping; the kernels count their DMAs themselves (wt_vm_wait). M0 is saved/restored
-// in the statement (compiler-reserved); s_nop 4: the descriptor may come fresh from a VALU.
-__device__ __forceinline__ void wt_dma16(wt_rsrc_t r, char* lds, uint32_t voff) {
-  const uint32_t l = __builtin_amdgcn_readfirstlane(
-      (uint32_t)(uintptr_t)(__attribute__((address_space(3))) char*)lds);
-  uint32_t keep;
-  asm volatile("s_nop 4\n\ts_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\t"
-               "buffer_load_dwordx4 %1, %2, 0 offen lds\n\ts_mov_b32 m0, %0"
-               : "=&s"(keep) : "v"(voff), "s"(r), "s"(l) : "memory");
-}
+typedef dma_rsrc_t wt_rsrc_t;
+__device__ __forceinline__ wt_rsrc_t wt_rsrc(const void* base, uint32_t bytes) { return dma_rsrc(base, bytes); }
+__device__ __forceinline__ void wt_dma16(wt_rsrc_t r, char* lds, uint32_t voff) { dma16_asm(r, lds, voff); }
 template <int N> __device__ __forceinline__ void wt_vm_wait() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
