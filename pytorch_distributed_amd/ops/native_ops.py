@@ -777,17 +777,18 @@ def conv_wgrad_tap(dy: torch.Tensor, x: torch.Tensor, g: ConvGeom, grad: torch.T
     return grad
 
 
-# the stem's weight gradient (WGRAD_BNA operand) on the tap-reuse kernel (csrc/wgrad_tap.hip
-# wgrad_stem_tap_kernel); PDA_STEM_WGRAD=generic: the implicit-GEMM WGRAD_BNA tile. Blocks = splits
-# (one 113 KiB block per CU)
-_STEM_WGRAD = os.environ.get("PDA_STEM_WGRAD", "tap")
+# PDA_STEM_WGRAD=tap: the stem's weight gradient (WGRAD_BNA operand) on the tap-reuse kernel
+# (csrc/wgrad_tap.hip wgrad_stem_tap_kernel) instead of the implicit-GEMM WGRAD_BNA 64x256 tile.
+# Off by default: 435-440 us vs 384-393 us alone at batch 400, step time unchanged within noise
+# (profiles/ab_r6.md section 15). Blocks = splits (one 113 KiB block per CU)
+_STEM_WGRAD = os.environ.get("PDA_STEM_WGRAD", "generic")
 _STEM_TAP_BLOCKS = int(os.environ.get("PDA_STEM_TAP_BLOCKS", "512"))
 
 
-def stem_wgrad_tap_ok(g: ConvGeom, dtype: torch.dtype) -> bool:
+def stem_wgrad_tap_ok(g: ConvGeom, dtype: torch.dtype, force: bool = False) -> bool:
     """The space-to-depth stem conv (4x4, stride 1, pad 2, 16 -> 64 channels, same-size output) in
-    16 bit, with the tap-reuse stem kernel built."""
-    return (_STEM_WGRAD == "tap" and dtype in (torch.bfloat16, torch.float16) and g.R == 4
+    16 bit, with the tap-reuse stem kernel built (and selected, unless ``force``)."""
+    return ((force or _STEM_WGRAD == "tap") and dtype in (torch.bfloat16, torch.float16) and g.R == 4
             and g.S == 4 and g.stride == 1 and g.pad == 2 and g.Cin == 16 and g.Cout == 64
             and g.Ho == g.H and g.Wo == g.W and g.W + 3 <= 122
             and getattr(ext.lib(), "pda_wgrad_stem_tap", None) is not None)

@@ -29,7 +29,7 @@ def main():
     # (("tap", n): the tap-reuse stem kernel with n blocks, csrc/wgrad_tap.hip)
     targets = [((-64, 256), 1024), ((-64, 128), 1536), ((-64, 256), 512), ((-64, 256), 768),
                ((64, 128), 1024)]
-    if K.stem_wgrad_tap_ok(g, torch.bfloat16):
+    if K.stem_wgrad_tap_ok(g, torch.bfloat16, force=True):
         targets += [("tap", 256), ("tap", 384), ("tap", 512), ("tap", 768), ("tap", 1024)]
 
     def run(tb):
