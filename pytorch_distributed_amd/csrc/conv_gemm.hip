@@ -38,8 +38,14 @@ template <int STAGES> constexpr int conv_nt() { return STAGES >= 3 ? 512 : NT; }
 
 // one LDS-DMA piece: lane l's 16 bytes at byte voff of the buffer land at lds + 16*l (lds must be
 // wave-uniform: it becomes M0). An out-of-range voff (>= the buffer's size) writes zeros.
-// (common.h dma16_asm: why not the builtin)
-__device__ __forceinline__ void dma16(dma_rsrc_t r, char* lds, uint32_t voff) { dma16_asm(r, lds, voff); }
+// The builtin, not common.h dma16_asm: with it hipcc drains the HALO data gradient's pipeline
+// before each tap's transposed reads (vmcnt(0)), and the asm form makes that launch 9 % faster
+// alone -- but the step 0.04-0.08 ms slower (the overlapped side-stream weight gradients lose
+// more than the chain gains; profiles/ab_r6.md section 15).
+__device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t r, char* lds, uint32_t voff) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)lds, 16,
+                                           (int)voff, 0, 0, 0);
+}
 template <int N> __device__ __forceinline__ void vm_wait() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
@@ -456,8 +462,6 @@ __global__ __launch_bounds__(conv_nt<STAGES>(), (PASS_T == WGRAD_BNA || PASS_T =
                                                                          (int)a_bytes, 0x00020000);
   const __amdgpu_buffer_rsrc_t rsb = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p.b), (short)0,
                                                                          (int)b_bytes, 0x00020000);
-  // the same two buffers as LDS-DMA descriptors
-  const dma_rsrc_t dsa = dma_rsrc(p.a, a_bytes), dsb = dma_rsrc(p.b, b_bytes);
   auto bld = [&](const __amdgpu_buffer_rsrc_t& r, uint32_t off) __attribute__((always_inline)) -> i32x4 {
     return __builtin_bit_cast(i32x4, __builtin_amdgcn_raw_buffer_load_b128(r, (int)off, 0, 0));
   };
@@ -952,8 +956,8 @@ __global__ __launch_bounds__(conv_nt<STAGES>(), (PASS_T == WGRAD_BNA || PASS_T =
   // piece i of the thread into ring slot `slot`
   auto dma_piece = [&](int i, int slot, const uint32_t* voff) __attribute__((always_inline)) {
     char* sa = smem + slot * STAGE;
-    if (i < GA) dma16(dsa, sa + (wid * GA + i) * 1024, voff[i]);
-    else dma16(dsb, sa + A_BYTES + (wid * GB + i - GA) * 1024, voff[i]);
+    if (i < GA) dma16(rsa, sa + (wid * GA + i) * 1024, voff[i]);
+    else dma16(rsb, sa + A_BYTES + (wid * GB + i - GA) * 1024, voff[i]);
   };
   auto issue_dma = [&](int kt, int slot) __attribute__((always_inline)) {
     uint32_t voff[GP];
@@ -1072,7 +1076,7 @@ __global__ __launch_bounds__(conv_nt<STAGES>(), (PASS_T == WGRAD_BNA || PASS_T =
     const int Wd = p.W;
     if (tid < 8) *reinterpret_cast<i32x4*>(smem + ZOFF + tid * 16) = i32x4{0, 0, 0, 0};
     auto a_piece = [&](int cc, int j) __attribute__((always_inline)) {
-      dma16(dsa, smem + (cc & 1) * SLAB_BYTES + (j * 8 + wid) * 1024,
+      dma16(rsa, smem + (cc & 1) * SLAB_BYTES + (j * 8 + wid) * 1024,
             cc < nch ? ha_off[j] + (uint32_t)(cc * 64 * ES) : OOB);
     };
     auto b_offsets = [&](int cc, int t, uint32_t* voff) __attribute__((always_inline)) {
@@ -1082,7 +1086,7 @@ __global__ __launch_bounds__(conv_nt<STAGES>(), (PASS_T == WGRAD_BNA || PASS_T =
       for (int j = 0; j < GB; ++j) voff[j] = cc < nch ? db_off[j] + k : OOB;
     };
     auto b_piece = [&](int slot, int j, const uint32_t* voff) __attribute__((always_inline)) {
-      dma16(dsb, smem + 2 * SLAB_BYTES + slot * B_BYTES + (wid * GB + j) * 1024, voff[j]);
+      dma16(rsb, smem + 2 * SLAB_BYTES + slot * B_BYTES + (wid * GB + j) * 1024, voff[j]);
     };
     {
 #pragma unroll
