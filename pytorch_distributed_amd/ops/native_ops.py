@@ -730,7 +730,7 @@ _WGRAD_TAP = {int(v) for v in os.environ.get("PDA_WGRAD_TAP", "56,28").split(","
 # count). Alone 256 is fastest (C2 165 vs 176 us at 512); in the step fewer blocks leave the other
 # CUs to the main chain: 256 / 192 / 128 / 112 / 96 / 80 / 64 -> 96 (-0.2 ms/step vs 256;
 # profiles/ab_r5.md section 15)
-_WGRAD_TAP_BLOCKS = 96
+_WGRAD_TAP_BLOCKS = int(os.environ.get("PDA_WGRAD_TAP_BLOCKS", "96"))
 
 
 def wgrad_tap_ok(g: ConvGeom, dtype: torch.dtype) -> bool:
