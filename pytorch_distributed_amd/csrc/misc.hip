@@ -430,6 +430,10 @@ int pda_track(hipStream_t st, hipEvent_t ev) {
 }
 unsigned long long pda_track_count() { return g_trk_count; }
 int pda_event_create(hipEvent_t* ev) { return (int)hipEventCreateWithFlags(ev, hipEventDisableTiming); }
+// flags: hipEventDisableTiming | optionally hipEventDisableSystemFence (the fork events are only
+// waited on by a stream of the same device: an agent-scope release is enough)
+int pda_event_create_flags(hipEvent_t* ev, unsigned flags) { return (int)hipEventCreateWithFlags(ev, flags); }
+int pda_event_record(hipEvent_t ev, hipStream_t st) { return (int)hipEventRecord(ev, st); }
 int pda_event_destroy(hipEvent_t ev) { return (int)hipEventDestroy(ev); }
 int pda_stream_wait_event(hipStream_t st, hipEvent_t ev) { return (int)hipStreamWaitEvent(st, ev, 0); }
 

@@ -758,9 +758,7 @@ class NativeResNet(nn.Module):
                 or getattr(L, "pda_track", None) is None):
             return
         if self._trk_ev is None:
-            ev = C.c_void_p()
-            K.check(L.pda_event_create(C.byref(ev)), "pda_event_create")
-            self._trk_ev = ev
+            self._trk_ev = K.fork_event_create()
         L.pda_track(C.c_void_p(torch.cuda.current_stream(self.device).cuda_stream), self._trk_ev)
         self._trk_on = True
         self._trk_c0 = L.pda_track_count()

@@ -127,6 +127,8 @@ _SIGS = {
     "pda_track": [_V, _V],
     "pda_track_count": [],
     "pda_event_create": [_V],
+    "pda_event_create_flags": [_V, _U],
+    "pda_event_record": [_V, _V],
     "pda_event_destroy": [_V],
     "pda_stream_wait_event": [_V, _V],
     "pda_bn_bwd_apply2": [_V, _V, _V, _V, _V, _V, _L, _I, _I, _V],

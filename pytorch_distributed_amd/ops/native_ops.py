@@ -785,6 +785,23 @@ _STEM_WGRAD = os.environ.get("PDA_STEM_WGRAD", "generic")
 _STEM_TAP_BLOCKS = int(os.environ.get("PDA_STEM_TAP_BLOCKS", "512"))
 
 
+# Events that order the second stream after the main one (fork tracking's per-launch completion
+# event, the DataParallel replay's side-graph hand-offs). PDA_EVENT_SYSFENCE=1: HIP's default event,
+# whose completion carries a SYSTEM-scope release (a full L2 write-back, for host / peer
+# visibility); 0: hipEventDisableSystemFence -- only a stream of the same device waits on these,
+# for which the agent-scope release of the kernel's own completion is enough.
+_EVENT_SYSFENCE = os.environ.get("PDA_EVENT_SYSFENCE", "1") == "1"
+
+
+def fork_event_create():
+    """A ``hipEvent_t`` (ctypes void pointer) for same-device stream ordering: timing disabled,
+    system-scope fence per PDA_EVENT_SYSFENCE."""
+    ev = C.c_void_p()
+    flags = 0x2 | (0 if _EVENT_SYSFENCE else 0x20000000)   # hipEventDisableTiming | ...SystemFence
+    check(ext.lib().pda_event_create_flags(C.byref(ev), flags), "pda_event_create_flags")
+    return ev
+
+
 def stem_wgrad_tap_ok(g: ConvGeom, dtype: torch.dtype, force: bool = False) -> bool:
     """The space-to-depth stem conv (4x4, stride 1, pad 2, 16 -> 64 channels, same-size output) in
     16 bit, with the tap-reuse stem kernel built (and selected, unless ``force``)."""

@@ -534,6 +534,7 @@ class _ReplicaGraph:
         # "conv": a side graph per weight gradient (the main segment ends where its inputs are
         # complete, so it starts as early as in the eager schedule); "1": one per residual block
         self.side_per_conv = self.side_split and side == "conv"
+        self._fork_ev = None   # main -> side hand-off event of the replay (native_ops.fork_event_create)
         with torch.cuda.device(self.dev):
             self.x = torch.empty(shape, dtype=m.dtype, device=self.dev)
             self.y = torch.empty(shape[0], dtype=torch.int64, device=self.dev)
@@ -656,7 +657,15 @@ class _ReplicaGraph:
                     self.graphs[s].replay()
                 side = self.sides[s] if s < len(self.sides) else None
                 if side is not None:
-                    side_st.wait_stream(st)
+                    import ctypes as C
+                    from ..ops import ext, native_ops as K
+                    if self._fork_ev is None:
+                        self._fork_ev = K.fork_event_create()
+                    L = ext.lib()
+                    K.check(L.pda_event_record(self._fork_ev, C.c_void_p(st.cuda_stream)),
+                            "pda_event_record")
+                    K.check(L.pda_stream_wait_event(C.c_void_p(side_st.cuda_stream), self._fork_ev),
+                            "pda_stream_wait_event")
                     with torch.cuda.stream(side_st):
                         side.replay()
             self.loss = self._graph_loss
