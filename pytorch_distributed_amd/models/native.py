@@ -143,6 +143,12 @@ class NativeResNet(nn.Module):
         # stem_bna = False keeps the apply-pass form for tests) and runs on the main stream, beside
         # layer1's weight gradients on the second stream (profiles/ab_r4.md section 8)
         self.stem_bna = True
+        # PDA_STEM_SPLIT=1: the stem weight gradient in decomposed form, dW = k1 (dz^T X) +
+        # k2 (y^T X) + k3 colsum(X) -- y^T X and the tap column sums of X run on the second stream
+        # in the FORWARD (y0 and x0 are known there), so the backward's exposed tail reads dz and X
+        # only (not dz and y); combined in the split-K reduce (eager world-1 steps; a DataParallel
+        # capture and SyncBatchNorm keep WGRAD_BNA)
+        self.stem_split = os.environ.get("PDA_STEM_SPLIT", "0") == "1"
         self.tail_mask = True         # tails store the ReLU bitmask the backward reads
         # a block's tail BN apply (+ residual + ReLU) runs inside the next block's conv1 forward,
         # which stages a = relu(bn3(y3) + r) from y3 and r and writes a once (FWD_TAIL); blocks whose
@@ -617,14 +623,17 @@ class NativeResNet(nn.Module):
         K.stem_pool(y0, sc, sh, p, arg)
         if self.probe is not None:
             self.probe("fwd", "stem")
+        gram_pending = False
         if save:
             saved["y0"], saved["arg"] = y0, arg
             saved["stem_stats"] = self.stem.state
             saved["blocks"] = []
+            if self._stem_split_ok(Nb, y0):
+                saved["stem_gram"] = self._stem_gram(x, y0)
+                gram_pending = True
         h = p
         feat = None
         nblk = len(self.blocks)
-        gram_pending = False
         tail_in = None   # (y3, (sc, sh), TailIn): the previous tail, folded into this block's conv1
         for bi, b in enumerate(self.blocks):
             last = bi == nblk - 1
@@ -933,10 +942,17 @@ class NativeResNet(nn.Module):
             K.bn_bwd(ws, y0, st0[0], st0[1], self.gamma(u), st0[2], st0[3], self.dgamma(u),
                      self.dbeta(u), dy0, g1=dA0, accumulate=acc)
         if bna:
+            sg = sv.get("stem_gram")
+
             def stem_wgrad(w):
                 # (stem_s2d_grad reads the reduced gradient at once: its reduce runs unbatched)
                 rb, w.reduce_batch = w.reduce_batch, None
-                K.conv_wgrad(dz0, x0, g0, self.stem_wgrad, w, bna=(y0, k0), wscale=self.wgrad_scale)
+                if sg is not None:   # decomposed: plain dz^T X, combined with k in the reduce
+                    K.conv_wgrad(dz0, x0, g0, self.stem_wgrad, w, combine=(k0, sg[0], sg[1]),
+                                 wscale=self.wgrad_scale)
+                else:
+                    K.conv_wgrad(dz0, x0, g0, self.stem_wgrad, w, bna=(y0, k0),
+                                 wscale=self.wgrad_scale)
                 w.reduce_batch = rb
                 K.stem_s2d_grad(self.stem_wgrad, self.wgrad_view(u), accumulate=acc)
             if self._side is not None and not self.defer_side:
@@ -1019,6 +1035,27 @@ class NativeResNet(nn.Module):
         batch 400 (tools/fc_probe.py, bit-identical logits). 16-bit only (the split-f32 engine has no
         double-buffered 64x64 tile)."""
         return (64, 64) if self.dtype in (torch.bfloat16, torch.float16) else None
+
+    def _stem_split_ok(self, Nb: int, y0: torch.Tensor) -> bool:
+        """Whether this training forward precomputes the stem weight gradient's y / colsum terms
+        (``stem_split``): eager, a second stream, the fused WGRAD_BNA conditions."""
+        sync = getattr(self.ws, "sync_comm", None)
+        return (self.stem_split and self._side is not None and not self.defer_side
+                and self.fused_stem_bwd and self.stem_bna and (sync is None or sync.world_size == 1)
+                and y0.dtype in (torch.bfloat16, torch.float16)
+                and K.wgrad_bna_ok(self.stem.geom(Nb), Nb, y0.dtype))
+
+    def _stem_gram(self, x0: torch.Tensor, y0: torch.Tensor):
+        """Forward-time terms of the decomposed stem weight gradient on the second stream:
+        B = y0^T X (the stem's weight-gradient GEMM with dY := y0) and the per-tap column sums s
+        of X; the forward joins the stream once after the last block."""
+        g0 = self.stem.geom(x0.shape[0])
+        self._fork()
+        with torch.cuda.stream(self._side):
+            B = torch.empty(g0.Cout * 16 * g0.Cin, dtype=torch.float32, device=self.device)
+            K.conv_wgrad(y0, x0, g0, B, self.ws_w)
+            s = K.stem_tap_colsum(x0, g0)
+        return B, s
 
     def _fold_gram(self, ul: ConvBN, y2, sc, sh):
         """Forward-time half of the decomposed conv3 weight gradient, on the second stream beside

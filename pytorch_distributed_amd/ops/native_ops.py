@@ -15,7 +15,7 @@ import ctypes as C
 import math
 import os
 from dataclasses import dataclass
-from typing import Optional, Tuple
+from typing import Dict, Optional, Tuple
 
 import torch
 
@@ -835,6 +835,42 @@ def conv_wgrad_stem_tap(dz: torch.Tensor, y: torch.Tensor, k: torch.Tensor, x: t
     check(L.pda_wgrad_reduce(ptr(slab), ptr(grad), splits, M, N, 4, 16, N, float(scale),
                              int(accumulate), None, None, None, st), "wgrad_reduce")
     return grad
+
+
+_TAP_MASKS: Dict = {}
+
+
+def stem_tap_colsum(x: torch.Tensor, g: ConvGeom) -> torch.Tensor:
+    """f32 [R*S*Cin] (column t*Cin + ci, t = r*S + s): the sum over every valid output pixel of
+    the stem conv's tap-(r, s) input, X[n][oy + r - pad][ox + s - pad][ci] (zero outside) -- the
+    k3 term of the decomposed stem weight gradient. Tap r sees input rows [r - pad, H - 1 + r - pad]
+    clipped to the image, so each tap's sum is the image total minus its excluded border rows /
+    columns (the first R-1-pad, the last pad) plus their corners: a few small reductions of x
+    (slices only: no index tensors, no host copies after the first call), not a pass per tap."""
+    Nb, H, W, Cin = x.shape
+    R, S, pad = g.R, g.S, g.pad
+    assert g.stride == 1 and g.Ho == H and g.Wo == W and H > 2 * R and W > 2 * S and pad < R
+    nt, nb = R - 1 - pad, pad            # excluded top / bottom rows (and left / right columns)
+    key = (H, W, R, S, pad, x.device)
+    if key not in _TAP_MASKS:
+        rows = list(range(nt)) + list(range(H - nb, H))
+        cols = list(range(nt)) + list(range(W - nb, W))
+        mr = [[0.0 if r - pad <= y <= H - 1 + r - pad else 1.0 for y in rows] for r in range(R)]
+        mc = [[0.0 if q - pad <= c <= W - 1 + q - pad else 1.0 for c in cols] for q in range(S)]
+        _TAP_MASKS[key] = (torch.tensor(mr, device=x.device), torch.tensor(mc, device=x.device))
+    mr, mc = _TAP_MASKS[key]
+    f32 = torch.float32
+    tot = x.sum(dim=(0, 1, 2), dtype=f32)                                            # [Cin]
+    rs = torch.cat([x[:, :nt].sum(dim=(0, 2), dtype=f32),
+                    x[:, H - nb:].sum(dim=(0, 2), dtype=f32)])                       # [nr, Cin]
+    cs = torch.cat([x[:, :, :nt].sum(dim=(0, 1), dtype=f32),
+                    x[:, :, W - nb:].sum(dim=(0, 1), dtype=f32)])                    # [nc, Cin]
+    q = torch.cat([torch.cat([x[:, :nt, :nt].sum(0, dtype=f32), x[:, :nt, W - nb:].sum(0, dtype=f32)], 1),
+                   torch.cat([x[:, H - nb:, :nt].sum(0, dtype=f32),
+                              x[:, H - nb:, W - nb:].sum(0, dtype=f32)], 1)])        # [nr, nc, Cin]
+    out = (tot[None, None] - (mr @ rs)[:, None] - (mc @ cs)[None, :]
+           + torch.einsum("ra,sb,abc->rsc", mr, mc, q))
+    return out.reshape(-1).contiguous()
 
 
 def conv_wgrad_gram(y: torch.Tensor, sc: torch.Tensor, sh: torch.Tensor, gram: torch.Tensor,

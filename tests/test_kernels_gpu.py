@@ -1064,6 +1064,40 @@ def test_conv_fwd_tail_matches_apply_then_conv(geo, mode, dtype):
     assert torch.equal(st, st_ref)
 
 
+@pytest.mark.parametrize("Nb,H", [(2, 11), (3, 20), (2, 56)])
+def test_stem_wgrad_decomposed_matches_bna(Nb, H):
+    """The decomposed stem weight gradient (models/native.py stem_split): B = y^T X by the plain
+    weight-gradient GEMM, s = per-tap column sums of X (stem_tap_colsum), then plain dz^T X with
+    k1 * . + k2 * B + k3 * s in the split-K reduce -- against the fp32 weight gradient of
+    dY = k1 dz + k2 y + k3 and against WGRAD_BNA (which rounds dY to bf16: the decomposed form
+    is at least as close)."""
+    K = _k()
+    dtype = torch.bfloat16
+    torch.manual_seed(Nb * H + 1)
+    g = K.stem_s2d_geom(Nb, 2 * H)
+    x = torch.randn(Nb, H, H, 16, device=DEV).to(dtype)
+    dz = torch.randn(Nb, H, H, 64, device=DEV).to(dtype)
+    y = (torch.randn(Nb, H, H, 64, device=DEV) * 2 + 1).to(dtype)
+    kk = torch.randn(3 * 64, device=DEV)
+    dy = (kk[:64].double() * dz.double() + kk[64:128].double() * y.double() + kk[128:].double())
+    dyp = torch.zeros(Nb, 64, H + 1, H + 1, device=DEV, dtype=torch.float64)
+    dyp[:, :, :H, :H] = dy.permute(0, 3, 1, 2)
+    ref = torch.nn.grad.conv2d_weight(x.double().permute(0, 3, 1, 2), (64, 16, 4, 4), dyp, padding=2)
+    ref = ref.permute(0, 2, 3, 1).reshape(-1).float()
+    ws = K.Workspace(torch.device(DEV))
+    B = torch.empty(64 * 256, device=DEV)
+    K.conv_wgrad(y, x, g, B, ws)
+    s = K.stem_tap_colsum(x, g)
+    dec = torch.full((64 * 256,), float("nan"), device=DEV)
+    K.conv_wgrad(dz, x, g, dec, ws, combine=(kk, B, s))
+    bna = torch.zeros(64 * 256, device=DEV)
+    K.conv_wgrad(dz, x, g, bna, ws, bna=(y, kk))
+    torch.cuda.synchronize()
+    e_dec, e_bna = rel_err(dec, ref), rel_err(bna, ref)
+    assert e_dec < e_bna + 1e-4, (e_dec, e_bna)
+    assert e_dec < 1e-3, e_dec
+
+
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
 @pytest.mark.parametrize("Nb,H", [(2, 11), (3, 20), (2, 112)])
 def test_wgrad_stem_tap_matches_fp32_and_bna(Nb, H, dtype):

@@ -520,6 +520,38 @@ def test_decomposed_fold_wgrad_matches_apply_path():
     assert not bad, bad
 
 
+def test_stem_split_wgrad_matches_bna_path():
+    """PDA_STEM_SPLIT: the stem weight gradient decomposed (y0^T X and the tap column sums of X on
+    the second stream in the forward, plain dz^T X combined with the BN-backward coefficients in
+    the split-K reduce) -- the stem's gradient as close to the fp32 reference as WGRAD_BNA's, every
+    other gradient unchanged."""
+    tm, nm = _pair("resnet50", image=64)
+    torch.manual_seed(21)
+    x = torch.randn(16, 3, 64, 64, device=DEV).to(torch.bfloat16).float()
+    y = torch.randint(0, 1000, (16,), device=DEV)
+    nm.train()
+    tm.train()
+    F.cross_entropy(tm(x), y).backward()
+    crit = nm.make_criterion()
+    grads = {}
+    for mode in (False, True):
+        nm.stem_split = mode
+        nm.zero_grad_flat()
+        crit(nm(x), y).backward()
+        torch.cuda.synchronize()
+        grads[mode] = dict((n, p.grad.detach().float().clone()) for n, p in nm.named_parameters())
+    nm.stem_split = False
+    tp = dict(tm.named_parameters())
+    stem = [n for n in grads[True] if n.startswith("conv1.")]
+    assert stem
+    for n in grads[True]:
+        if n in stem:
+            e_s, e_b = rel_err(grads[True][n], tp[n].grad), rel_err(grads[False][n], tp[n].grad)
+            assert e_s < 1.3 * e_b + 0.01, (n, e_s, e_b)
+        else:
+            assert torch.equal(grads[True][n], grads[False][n]), n
+
+
 def test_fork_tracking_orders_side_stream_reads():
     """The rule fork tracking relies on (models/native.py _fork): a fork after a TRACKED native
     launch makes the second stream wait on the event that launch's own dispatch completes. A long
