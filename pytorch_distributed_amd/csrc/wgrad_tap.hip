@@ -333,14 +333,6 @@ __global__ __launch_bounds__(WT_NT, 1) void wgrad_stem_tap_kernel(SwParams p_arg
   const int split = (int)xcd_remap(blockIdx.x, gridDim.x);
   const FastDiv dHpWp = p.dHpWp, dWp = p.dWp;
   const int Kp = p.Kp, H = p.H, W = p.W;
-  // padded output row q -> byte offset of its 64-channel pixel (+ c elems), OOB for padding rows
-  auto out_pix = [&](int q, int c_elems) __attribute__((always_inline)) -> uint32_t {
-    if (q < 0 || q >= Kp) return WT_OOB;
-    const uint32_t n = fdiv((uint32_t)q, dHpWp), rem = (uint32_t)q - n * dHpWp.d;
-    const uint32_t oy = fdiv(rem, dWp), ox = rem - oy * dWp.d;
-    if (oy >= (uint32_t)H || ox >= (uint32_t)W) return WT_OOB;
-    return ((((n * H + oy) * W + ox) * 64u) + (uint32_t)c_elems) * 2u;
-  };
   // padded X row q' -> byte offset of its 16-channel pixel (+ c elems), OOB outside the image
   auto x_pix = [&](int q, int c_elems) __attribute__((always_inline)) -> uint32_t {
     if (q < 0 || q >= Kp) return WT_OOB;
@@ -357,26 +349,57 @@ __global__ __launch_bounds__(WT_NT, 1) void wgrad_stem_tap_kernel(SwParams p_arg
   const wt_rsrc_t ry = wt_rsrc(p.y, (int)(npix * 128u));
   const wt_rsrc_t rx = wt_rsrc(p.x, (int)(npix * 32u));
 
+  // Every stream of rows below advances by exactly 64 padded rows per call: its (image, y, x)
+  // coordinates are tracked incrementally (one fdiv pair at the start, then adds and compares)
+  // instead of two fdivs per row per step.
+  struct Trk { uint32_t n, y, x; };
+  const uint32_t Hp = (uint32_t)p.Hp, Wp = (uint32_t)p.Wp;
+  auto trk = [&](int q) __attribute__((always_inline)) -> Trk {
+    const uint32_t qq = (uint32_t)max(q, 0);
+    const uint32_t n = fdiv(qq, dHpWp), rem = qq - n * dHpWp.d;
+    const uint32_t y = fdiv(rem, dWp);
+    return Trk{n, y, rem - y * dWp.d};
+  };
+  auto adv = [&](Trk& t) __attribute__((always_inline)) {
+    t.x += 64;
+    while (t.x >= Wp) { t.x -= Wp; ++t.y; }
+    while (t.y >= Hp) { t.y -= Hp; ++t.n; }
+  };
+
   // X rows: step s reads [q0 + 64 s, q0 + 64 s + 64 + fhalo); pieces of 32 rows from the
   // 32-aligned base b0; fr(s) = first row not needed by steps <= s (32-aligned)
   const int b0 = q0 & ~31;
   auto fr = [&](int s) { return (q0 + 64 * (s + 1) + p.fhalo + 31) & ~31; };
   // one 32-row X piece at row r (32-aligned): lane -> slot lane/2 of the piece, channel half lane&1
+  const int xb = lane >> 5, xsl = (lane >> 1) & 15;
   auto x_piece = [&](int r, bool live) __attribute__((always_inline)) {
-    const int b = lane >> 5, sl = (lane >> 1) & 15;
-    const int row = r + 16 * b + sw_slot(sl);            // (sw_slot is an involution)
+    const int row = r + 16 * xb + sw_slot(xsl);            // (sw_slot is an involution)
     wt_dma16(rx, xr + (r & (SW_RING - 1)) * SW_XROW, live ? x_pix(row, (lane & 1) * 8) : WT_OOB);
+  };
+  // the pieces after the prologue's bulk: rows fr(0) + 32 wid + ..., 64 further per call
+  int xq = fr(0) + 32 * wid + 16 * xb + sw_slot(xsl);
+  Trk tx = trk(xq);
+  auto x_next = [&](int r, bool live) __attribute__((always_inline)) {
+    const bool in = live && xq < Kp && tx.y >= 2 && tx.y < (uint32_t)H + 2 && tx.x >= 2 &&
+                    tx.x < (uint32_t)W + 2;
+    const uint32_t off = in ? ((((tx.n * H + tx.y - 2) * W + tx.x - 2) * 16u) + (lane & 1) * 8u) * 2u
+                            : WT_OOB;
+    wt_dma16(rx, xr + (r & (SW_RING - 1)) * SW_XROW, off);
+    xq += 64;
+    adv(tx);
   };
   // the dz / y tiles of step s, piece w: rows q0 + 64 s + 8 w + lane/8 (rows past the range: zero)
   const int lrow = lane >> 3, lch = lane & 7;
+  const int arl = 8 * wid + lrow, alc = lch ^ wt_swz(arl);
+  Trk ta = trk(q0 + arl);
   auto a_pieces = [&](int s, int w) __attribute__((always_inline)) {
-    const int rl = 8 * w + lrow;
-    const int q = q0 + 64 * s + rl;
-    const int lc = lch ^ wt_swz(rl);
-    const uint32_t off = q < q_end ? out_pix(q, lc * 8) : WT_OOB;
+    const int q = q0 + 64 * s + arl;
+    const uint32_t off = q < q_end && ta.y < (uint32_t)H && ta.x < (uint32_t)W
+                             ? ((((ta.n * H + ta.y) * W + ta.x) * 64u) + alc * 8u) * 2u : WT_OOB;
     const int slot = (s % (SW_NS + 1)) * SW_ATILE + 8 * w * 128;
     wt_dma16(rdz, tz + slot, off);
     wt_dma16(ry, ty + slot, off);
+    adv(ta);
   };
   // per step: waves 0, 1 add the step's two X pieces (3 DMAs), every wave its dz + y pieces (2)
   const bool xw = wid < 2;
@@ -385,29 +408,28 @@ __global__ __launch_bounds__(WT_NT, 1) void wgrad_stem_tap_kernel(SwParams p_arg
   a_pieces(0, wid);
 #pragma unroll
   for (int s = 1; s < SW_NS; ++s) {
-    if (xw) x_piece(fr(s - 1) + 32 * wid, s < ns);
+    if (xw) x_next(fr(s - 1) + 32 * wid, s < ns);
     a_pieces(s, wid);
   }
   if (tid < 192) coef[tid] = p.k[tid];
-  // dY = k1 dz + k2 y + k3 in place of step s's dz slot: one 16-B chunk per thread; padding and
-  // out-of-range rows stay 0
+  // dY = k1 dz + k2 y + k3 in place of step s's dz slot: one 16-B chunk per thread (the same
+  // 8 channels at every step: coefficients in registers); padding and out-of-range rows stay 0
+  const int frl = tid >> 3, fpc = tid & 7, flc = fpc ^ wt_swz(frl);
+  Trk tf = trk(q0 + frl);
+  f32x2 K1[4], K2[4], K3[4];
   auto form_dy = [&](int s) __attribute__((always_inline)) {
-    const int rl = tid >> 3, pc = tid & 7;
-    const int lc = pc ^ wt_swz(rl);
-    const int q = q0 + 64 * s + rl;
-    const bool ok = q < q_end && out_pix(q, 0) != WT_OOB;
-    const int off = (s % (SW_NS + 1)) * SW_ATILE + rl * 128 + pc * 16;
+    const int q = q0 + 64 * s + frl;
+    const bool ok = q < q_end && tf.y < (uint32_t)H && tf.x < (uint32_t)W;
+    adv(tf);
+    const int off = (s % (SW_NS + 1)) * SW_ATILE + frl * 128 + fpc * 16;
     i32x4* zp = reinterpret_cast<i32x4*>(tz + off);
     const i32x4 z = *zp, yv = *reinterpret_cast<const i32x4*>(ty + off);
     i32x4 o;
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
-      const f32x2 k1 = *reinterpret_cast<const f32x2*>(coef + lc * 8 + 2 * k);
-      const f32x2 k2 = *reinterpret_cast<const f32x2*>(coef + 64 + lc * 8 + 2 * k);
-      const f32x2 k3 = *reinterpret_cast<const f32x2*>(coef + 128 + lc * 8 + 2 * k);
       const f32x2 d = unpack2<DT>((uint32_t)z[k]), u = unpack2<DT>((uint32_t)yv[k]);
-      const f32x2 f = f32x2{__builtin_fmaf(k1.x, d.x, __builtin_fmaf(k2.x, u.x, k3.x)),
-                            __builtin_fmaf(k1.y, d.y, __builtin_fmaf(k2.y, u.y, k3.y))};
+      const f32x2 f = f32x2{__builtin_fmaf(K1[k].x, d.x, __builtin_fmaf(K2[k].x, u.x, K3[k].x)),
+                            __builtin_fmaf(K1[k].y, d.y, __builtin_fmaf(K2[k].y, u.y, K3[k].y))};
       o[k] = ok ? (int)pack2<DT>(f) : 0;
     }
     *zp = o;
@@ -415,6 +437,12 @@ __global__ __launch_bounds__(WT_NT, 1) void wgrad_stem_tap_kernel(SwParams p_arg
   // step 0's operands: landed (every wave's step-0 group), formed before the loop's first barrier
   if (xw) wt_vm_wait<3 * (SW_NS - 1)>(); else wt_vm_wait<2 * (SW_NS - 1)>();
   __syncthreads();
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    K1[k] = *reinterpret_cast<const f32x2*>(coef + flc * 8 + 2 * k);
+    K2[k] = *reinterpret_cast<const f32x2*>(coef + 64 + flc * 8 + 2 * k);
+    K3[k] = *reinterpret_cast<const f32x2*>(coef + 128 + flc * 8 + 2 * k);
+  }
   form_dy(0);
 
   f32x4 acc[2][4];
@@ -456,7 +484,7 @@ __global__ __launch_bounds__(WT_NT, 1) void wgrad_stem_tap_kernel(SwParams p_arg
     __builtin_amdgcn_s_barrier();
     // the operands of step s + NS (past the range: out-of-bounds no-ops -- the per-step count
     // stays fixed); their slots were last read in step s - 1
-    if (xw) x_piece(fr(s + SW_NS - 1) + 32 * wid, s + SW_NS < ns);
+    if (xw) x_next(fr(s + SW_NS - 1) + 32 * wid, s + SW_NS < ns);
     a_pieces(s + SW_NS, wid);
     if (s + 1 < ns) form_dy(s + 1);
     const char* sa = tz + (s % (SW_NS + 1)) * SW_ATILE;
