@@ -360,10 +360,20 @@ __global__ __launch_bounds__(WT_NT, 1) void wgrad_stem_tap_kernel(SwParams p_arg
     const uint32_t y = fdiv(rem, dWp);
     return Trk{n, y, rem - y * dWp.d};
   };
+  const bool wide = Wp > 64;   // (the stem: Wp = 115) at most one wrap per 64 rows: branch-free
   auto adv = [&](Trk& t) __attribute__((always_inline)) {
     t.x += 64;
-    while (t.x >= Wp) { t.x -= Wp; ++t.y; }
-    while (t.y >= Hp) { t.y -= Hp; ++t.n; }
+    if (wide) {
+      const bool wx = t.x >= Wp;
+      t.x -= wx ? Wp : 0u;
+      t.y += wx;
+      const bool wy = t.y >= Hp;
+      t.y -= wy ? Hp : 0u;
+      t.n += wy;
+    } else {
+      while (t.x >= Wp) { t.x -= Wp; ++t.y; }
+      while (t.y >= Hp) { t.y -= Hp; ++t.n; }
+    }
   };
 
   // X rows: step s reads [q0 + 64 s, q0 + 64 s + 64 + fhalo); pieces of 32 rows from the
