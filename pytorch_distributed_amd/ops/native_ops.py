@@ -779,7 +779,7 @@ def conv_wgrad_tap(dy: torch.Tensor, x: torch.Tensor, g: ConvGeom, grad: torch.T
 
 # PDA_STEM_WGRAD=tap: the stem's weight gradient (WGRAD_BNA operand) on the tap-reuse kernel
 # (csrc/wgrad_tap.hip wgrad_stem_tap_kernel) instead of the implicit-GEMM WGRAD_BNA 64x256 tile.
-# Off by default: 435-440 us vs 384-393 us alone at batch 400, step time unchanged within noise
+# Off by default: 368-381 us vs 375-380 us alone at batch 400, step time unchanged within noise
 # (profiles/ab_r6.md section 15). Blocks = splits (one 113 KiB block per CU)
 _STEM_WGRAD = os.environ.get("PDA_STEM_WGRAD", "generic")
 _STEM_TAP_BLOCKS = int(os.environ.get("PDA_STEM_TAP_BLOCKS", "512"))
