@@ -725,7 +725,8 @@ def conv_wgrad(dy: torch.Tensor, x: torch.Tensor, g: ConvGeom, grad: torch.Tenso
 
 # which 3x3 stride-1 weight gradients run the tap-reuse kernel (csrc/wgrad_tap.hip), by image width
 # ("0": none); the generic tiles re-read X per (tap, channel) column tile and dY per N-tile
-_WGRAD_TAP = {int(v) for v in os.environ.get("PDA_WGRAD_TAP", "56,28").split(",") if v.strip() not in ("", "0")}
+_WGRAD_TAP = {int(v) for v in os.environ.get("PDA_WGRAD_TAP", "56,28").replace("+", ",").split(",")
+              if v.strip() not in ("", "0")}
 # blocks of the tap-reuse weight gradient (one 104 KiB block per CU: the split count is the block
 # count). Alone 256 is fastest (C2 165 vs 176 us at 512); in the step fewer blocks leave the other
 # CUs to the main chain: 256 / 192 / 128 / 112 / 96 / 80 / 64 -> 96 (-0.2 ms/step vs 256;
