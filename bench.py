@@ -615,6 +615,7 @@ def main():
         diag["dp_replay_ms_per_step"] = round(1000.0 * rel / args.steps, 3)
         diag["dp_replay_vs_eager"] = round(rel / elapsed, 4)
         diag["dp_replay_segments"] = len(tr.dp._graphs[0].graphs)
+        diag["dp_side_graphs"] = sum(g is not None for g in getattr(tr.dp._graphs[0], "sides", []))
         tr.dp.force_replay = False
     if args.dp:   # every replica must hold bit-identical weights (the replicated fused SGD)
         try:
